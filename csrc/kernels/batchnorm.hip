@@ -1,0 +1,440 @@
+// BatchNorm (+ residual add) (+ ReLU) for NHWC bf16 activations, fp32 params.
+// SURVEY §2.6 K8 (ResNet-50: 53 BN layers).  x is viewed as [M = N*H*W, C].
+//
+// Forward (train):  stats_partial -> finalize -> apply     (3 launches)
+//   apply: y = act(x*scale[c] + shift[c] (+ res))
+// Backward:         bwd_partial   -> bwd_finalize -> bwd_apply
+//   dz  = dy * (y > 0)            (ReLU mask taken from the saved OUTPUT y)
+//   dx  = a[c]*dz + b[c]*x + k[c] (BN backward folded into 3 per-channel coefs)
+//   dres = dz                      (residual branch gradient, same pass)
+//
+// Memory-bound: every pass streams rows with 16-B/lane loads; each thread owns
+// a fixed group of 8 channels so per-channel coefficients live in registers.
+// Row sums use a per-channel pivot (x[0][c]) to avoid E[x^2]-E[x]^2
+// cancellation; cross-block partials are combined in fp64.
+#include "common.h"
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int kSlots = 64;  // atomic accumulation slots (see combine2)
+
+struct Geom {
+  int tpr;     // threads per row (each owns 8 channels per channel-group step)
+  int rpi;     // rows per block iteration
+  int gx;      // row blocks
+  long chunk;  // rows per block (multiple of rpi)
+};
+
+Geom geom(long M, int C, int max_blocks) {
+  Geom g;
+  int cv = C / 8;
+  g.tpr = cv < NT ? cv : NT;
+  g.rpi = NT / g.tpr;
+  long want = (M + (long)g.rpi * 8 - 1) / ((long)g.rpi * 8);
+  long gx = want < max_blocks ? want : max_blocks;
+  if (gx < 1) gx = 1;
+  long chunk = (M + gx - 1) / gx;
+  chunk = (chunk + g.rpi - 1) / g.rpi * g.rpi;
+  g.chunk = chunk;
+  g.gx = (int)((M + chunk - 1) / chunk);
+  return g;
+}
+
+__device__ __forceinline__ uint4 ld16(const bf16_t* p) { return *reinterpret_cast<const uint4*>(p); }
+
+// ------------------------------------------------------------------ forward stats
+// block sums -> slot accumulators [kSlots][2][C] (shifted sum, shifted sum of squares)
+__global__ __launch_bounds__(NT) void bn_stats_partial(const bf16_t* __restrict__ x, float* __restrict__ part,
+                                                        long M, int C, long chunk, int tpr, int rpi) {
+  __shared__ float sh[2][NT * 8];
+  const int t = threadIdx.x;
+  const int cg = t % tpr, r0 = t / tpr;
+  const bool active = r0 < rpi;
+  const int cv = C / 8;
+  const long rb = (long)blockIdx.x * chunk;
+  const long re = rb + chunk < M ? rb + chunk : M;
+  for (int g0 = 0; g0 < cv; g0 += tpr) {
+    const int c0 = (g0 + cg) * 8;
+    float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (active && g0 + cg < cv) {
+      float K[8];
+      unpack8(ld16(x + c0), K);
+      long r = rb + r0;
+      for (; r + 3L * rpi < re; r += 4L * rpi) {
+        uint4 v0 = ld16(x + r * C + c0), v1 = ld16(x + (r + rpi) * C + c0);
+        uint4 v2 = ld16(x + (r + 2L * rpi) * C + c0), v3 = ld16(x + (r + 3L * rpi) * C + c0);
+        float f[8];
+        unpack8(v0, f);
+#pragma unroll
+        for (int j = 0; j < 8; j++) { float d = f[j] - K[j]; s1[j] += d; s2[j] += d * d; }
+        unpack8(v1, f);
+#pragma unroll
+        for (int j = 0; j < 8; j++) { float d = f[j] - K[j]; s1[j] += d; s2[j] += d * d; }
+        unpack8(v2, f);
+#pragma unroll
+        for (int j = 0; j < 8; j++) { float d = f[j] - K[j]; s1[j] += d; s2[j] += d * d; }
+        unpack8(v3, f);
+#pragma unroll
+        for (int j = 0; j < 8; j++) { float d = f[j] - K[j]; s1[j] += d; s2[j] += d * d; }
+      }
+      for (; r < re; r += rpi) {
+        float f[8];
+        unpack8(ld16(x + r * C + c0), f);
+#pragma unroll
+        for (int j = 0; j < 8; j++) { float d = f[j] - K[j]; s1[j] += d; s2[j] += d * d; }
+      }
+    }
+    if (active) {
+#pragma unroll
+      for (int j = 0; j < 8; j++) { sh[0][r0 * tpr * 8 + cg * 8 + j] = s1[j]; sh[1][r0 * tpr * 8 + cg * 8 + j] = s2[j]; }
+    }
+    __syncthreads();
+    const int width = tpr * 8;
+    for (int idx = t; idx < 2 * width; idx += NT) {
+      const int a = idx / width, c = idx % width;
+      if (g0 * 8 + c < C) {
+        float acc = 0.f;
+        for (int rr = 0; rr < rpi; rr++) acc += sh[a][rr * width + c];
+        atomicAdd(&part[((long)(blockIdx.x % kSlots) * 2 + a) * C + g0 * 8 + c], acc);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Cross-block combine: partial kernels atomically add their block sums into
+// kSlots slot rows ([kSlots][2][C], slot = block % kSlots, so each address
+// sees gx/kSlots adds); finalize sums the slots in fp64 and ZEROES them again,
+// leaving the workspace clean for the next BN layer on the stream.
+__device__ __forceinline__ void combine2(float* __restrict__ part, int C, int c, double& a, double& b) {
+  a = 0.0;
+  b = 0.0;
+#pragma unroll 8
+  for (int i = 0; i < kSlots; i++) {
+    float* pa = part + ((long)i * 2) * C + c;
+    float* pb = pa + C;
+    a += (double)*pa;
+    b += (double)*pb;
+    *pa = 0.f;
+    *pb = 0.f;
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_finalize(const bf16_t* __restrict__ x, float* __restrict__ part, int gx, long M, int C,
+                            const float* __restrict__ gamma, const float* __restrict__ beta,
+                            float* __restrict__ rmean, float* __restrict__ rvar, float* __restrict__ save_mean,
+                            float* __restrict__ save_invstd, float* __restrict__ scale, float* __restrict__ shift,
+                            float eps, float momentum) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double a, b;
+  combine2(part, C, c, a, b);
+  const double K = (double)bf2f(x[c]);
+  const double m1 = a / (double)M;
+  double var = b / (double)M - m1 * m1;
+  if (var < 0.0) var = 0.0;
+  const double mean = K + m1;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  save_mean[c] = (float)mean;
+  save_invstd[c] = invstd;
+  const float g = gamma ? gamma[c] : 1.f;
+  const float bt = beta ? beta[c] : 0.f;
+  scale[c] = g * invstd;
+  shift[c] = bt - (float)mean * g * invstd;
+  if (rmean) {
+    const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
+    rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mean;
+    rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unbiased;
+  }
+}
+
+__global__ void bn_finalize_eval(const float* __restrict__ gamma, const float* __restrict__ beta,
+                                 const float* __restrict__ rmean, const float* __restrict__ rvar, int C, float eps,
+                                 float* __restrict__ scale, float* __restrict__ shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float inv = rsqrtf(rvar[c] + eps);
+  const float g = gamma ? gamma[c] : 1.f;
+  scale[c] = g * inv;
+  shift[c] = (beta ? beta[c] : 0.f) - rmean[c] * g * inv;
+}
+
+// ------------------------------------------------------------------ forward apply
+template <bool RELU, bool RES>
+__global__ __launch_bounds__(NT) void bn_apply(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
+                                               bf16_t* __restrict__ y, const float* __restrict__ scale,
+                                               const float* __restrict__ shift, long M, int C, long chunk, int tpr,
+                                               int rpi) {
+  const int t = threadIdx.x;
+  const int cg = t % tpr, r0 = t / tpr;
+  if (r0 >= rpi) return;
+  const int cv = C / 8;
+  const long rb = (long)blockIdx.x * chunk;
+  const long re = rb + chunk < M ? rb + chunk : M;
+  for (int g = cg; g < cv; g += tpr) {
+    const int c0 = g * 8;
+    float sc[8], sf[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) { sc[j] = scale[c0 + j]; sf[j] = shift[c0 + j]; }
+    long r = rb + r0;
+    for (; r + rpi < re; r += 2L * rpi) {
+      const long o0 = r * C + c0, o1 = (r + rpi) * C + c0;
+      uint4 v0 = ld16(x + o0), v1 = ld16(x + o1);
+      uint4 q0, q1;
+      if (RES) { q0 = ld16(res + o0); q1 = ld16(res + o1); }
+      float f[8], q[8];
+      unpack8(v0, f);
+      if (RES) unpack8(q0, q);
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        float z = fmaf(f[j], sc[j], sf[j]);
+        if (RES) z += q[j];
+        f[j] = RELU ? fmaxf(z, 0.f) : z;
+      }
+      *reinterpret_cast<uint4*>(y + o0) = pack8(f);
+      unpack8(v1, f);
+      if (RES) unpack8(q1, q);
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        float z = fmaf(f[j], sc[j], sf[j]);
+        if (RES) z += q[j];
+        f[j] = RELU ? fmaxf(z, 0.f) : z;
+      }
+      *reinterpret_cast<uint4*>(y + o1) = pack8(f);
+    }
+    for (; r < re; r += rpi) {
+      const long o = r * C + c0;
+      float f[8], q[8];
+      unpack8(ld16(x + o), f);
+      if (RES) unpack8(ld16(res + o), q);
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        float z = fmaf(f[j], sc[j], sf[j]);
+        if (RES) z += q[j];
+        f[j] = RELU ? fmaxf(z, 0.f) : z;
+      }
+      *reinterpret_cast<uint4*>(y + o) = pack8(f);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ backward
+template <bool RELU>
+__device__ __forceinline__ void masked_dy(const uint4 dv, const uint4 yv, float dz[8]) {
+  unpack8(dv, dz);
+  if (RELU) {
+    float yy[8];
+    unpack8(yv, yy);
+#pragma unroll
+    for (int j = 0; j < 8; j++) dz[j] = yy[j] > 0.f ? dz[j] : 0.f;
+  }
+}
+
+// block sums -> slot accumulators [kSlots][2][C]: sum(dz), sum(dz*(x-mean))
+template <bool RELU>
+__global__ __launch_bounds__(NT) void bn_bwd_partial(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                                                     const bf16_t* __restrict__ y, const float* __restrict__ mean,
+                                                     float* __restrict__ part, long M, int C, long chunk, int tpr,
+                                                     int rpi) {
+  __shared__ float sh[2][NT * 8];
+  const int t = threadIdx.x;
+  const int cg = t % tpr, r0 = t / tpr;
+  const bool active = r0 < rpi;
+  const int cv = C / 8;
+  const long rb = (long)blockIdx.x * chunk;
+  const long re = rb + chunk < M ? rb + chunk : M;
+  for (int g0 = 0; g0 < cv; g0 += tpr) {
+    const int c0 = (g0 + cg) * 8;
+    float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (active && g0 + cg < cv) {
+      float mu[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) mu[j] = mean[c0 + j];
+      long r = rb + r0;
+      for (; r + rpi < re; r += 2L * rpi) {
+        const long o0 = r * C + c0, o1 = (r + rpi) * C + c0;
+        uint4 d0 = ld16(dy + o0), d1 = ld16(dy + o1);
+        uint4 x0 = ld16(x + o0), x1 = ld16(x + o1);
+        uint4 y0 = make_uint4(0, 0, 0, 0), y1 = y0;
+        if (RELU) { y0 = ld16(y + o0); y1 = ld16(y + o1); }
+        float dz[8], xf[8];
+        masked_dy<RELU>(d0, y0, dz);
+        unpack8(x0, xf);
+#pragma unroll
+        for (int j = 0; j < 8; j++) { s1[j] += dz[j]; s2[j] += dz[j] * (xf[j] - mu[j]); }
+        masked_dy<RELU>(d1, y1, dz);
+        unpack8(x1, xf);
+#pragma unroll
+        for (int j = 0; j < 8; j++) { s1[j] += dz[j]; s2[j] += dz[j] * (xf[j] - mu[j]); }
+      }
+      for (; r < re; r += rpi) {
+        const long o = r * C + c0;
+        uint4 yv = make_uint4(0, 0, 0, 0);
+        if (RELU) yv = ld16(y + o);
+        float dz[8], xf[8];
+        masked_dy<RELU>(ld16(dy + o), yv, dz);
+        unpack8(ld16(x + o), xf);
+#pragma unroll
+        for (int j = 0; j < 8; j++) { s1[j] += dz[j]; s2[j] += dz[j] * (xf[j] - mu[j]); }
+      }
+    }
+    if (active) {
+#pragma unroll
+      for (int j = 0; j < 8; j++) { sh[0][r0 * tpr * 8 + cg * 8 + j] = s1[j]; sh[1][r0 * tpr * 8 + cg * 8 + j] = s2[j]; }
+    }
+    __syncthreads();
+    const int width = tpr * 8;
+    for (int idx = t; idx < 2 * width; idx += NT) {
+      const int a = idx / width, c = idx % width;
+      if (g0 * 8 + c < C) {
+        float acc = 0.f;
+        for (int rr = 0; rr < rpi; rr++) acc += sh[a][rr * width + c];
+        atomicAdd(&part[((long)(blockIdx.x % kSlots) * 2 + a) * C + g0 * 8 + c], acc);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// coef layout: [3][C] = a, b, k   ;  dx = a*dz + b*x + k
+__global__ __launch_bounds__(256) void bn_bwd_finalize(float* __restrict__ part, int gx, long M, int C, const float* __restrict__ gamma,
+                                const float* __restrict__ mean, const float* __restrict__ invstd,
+                                float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ coef,
+                                int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double sdy, sdx;
+  combine2(part, C, c, sdy, sdx);
+  const float inv = invstd[c];
+  const float g = gamma ? gamma[c] : 1.f;
+  const float dg = (float)sdx * inv;  // sum(dz * xhat)
+  // accumulate: the outputs are views into the flat gradient bucket (+=)
+  if (dgamma) dgamma[c] = accumulate ? dgamma[c] + dg : dg;
+  if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)sdy : (float)sdy;
+  const float a = g * inv;
+  const float b = -g * inv * inv * inv * (float)(sdx / (double)M);
+  const float k = -a * (float)(sdy / (double)M) - b * mean[c];
+  coef[c] = a;
+  coef[C + c] = b;
+  coef[2 * C + c] = k;
+}
+
+template <bool RELU, bool DRES>
+__global__ __launch_bounds__(NT) void bn_bwd_apply(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                                                   const bf16_t* __restrict__ y, const float* __restrict__ coef,
+                                                   bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long M, int C,
+                                                   long chunk, int tpr, int rpi) {
+  const int t = threadIdx.x;
+  const int cg = t % tpr, r0 = t / tpr;
+  if (r0 >= rpi) return;
+  const int cv = C / 8;
+  const long rb = (long)blockIdx.x * chunk;
+  const long re = rb + chunk < M ? rb + chunk : M;
+  for (int g = cg; g < cv; g += tpr) {
+    const int c0 = g * 8;
+    float ca[8], cb[8], ck[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) { ca[j] = coef[c0 + j]; cb[j] = coef[C + c0 + j]; ck[j] = coef[2 * C + c0 + j]; }
+    for (long r = rb + r0; r < re; r += rpi) {
+      const long o = r * C + c0;
+      uint4 yv = make_uint4(0, 0, 0, 0);
+      if (RELU) yv = ld16(y + o);
+      const uint4 dv = ld16(dy + o);
+      const uint4 xv = ld16(x + o);
+      float dz[8], xf[8], out[8];
+      masked_dy<RELU>(dv, yv, dz);
+      unpack8(xv, xf);
+#pragma unroll
+      for (int j = 0; j < 8; j++) out[j] = fmaf(ca[j], dz[j], fmaf(cb[j], xf[j], ck[j]));
+      *reinterpret_cast<uint4*>(dx + o) = pack8(out);
+      if (DRES) *reinterpret_cast<uint4*>(dres + o) = pack8(dz);
+    }
+  }
+}
+
+}  // namespace
+
+// ====================================================================== C ABI
+// cap row blocks so each partial array stays <= 1M floats (finalize reads it all)
+static int max_row_blocks(int C) {
+  int m = (1 << 20) / C;
+  return m > 2048 ? 2048 : (m < 64 ? 64 : m);
+}
+
+KFA_API long kfa_bn_workspace_floats(long M, int C) {
+  Geom g = geom(M, C, max_row_blocks(C));
+  return 2L * kSlots * C + 3L * C;
+}
+
+static bool bn_shape_ok(long M, int C) { return M > 0 && C >= 8 && (C % 8) == 0; }
+
+// ws: >= kfa_bn_workspace_floats(M, C) floats, ZERO-initialised once by the
+// caller (the slot accumulators are re-zeroed by every finalize).
+KFA_API int kfa_bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* gamma, const float* beta,
+                             float* rmean, float* rvar, float* save_mean, float* save_invstd, float* ws, long M, int C,
+                             float eps, float momentum, int relu, hipStream_t s) {
+  if (!bn_shape_ok(M, C)) return -1;
+  Geom g = geom(M, C, max_row_blocks(C));
+  float* part = ws;
+  float* scale = ws + 2L * kSlots * C;
+  float* shift = scale + C;
+  hipLaunchKernelGGL(bn_stats_partial, dim3(g.gx), dim3(NT), 0, s, x, part, M, C, g.chunk, g.tpr, g.rpi);
+  hipLaunchKernelGGL(bn_finalize, dim3(kfa_ceil_div(C, 64)), dim3(64), 0, s, x, part, g.gx, M, C, gamma, beta, rmean,
+                     rvar, save_mean, save_invstd, scale, shift, eps, momentum);
+  if (relu && res)
+    hipLaunchKernelGGL((bn_apply<true, true>), dim3(g.gx), dim3(NT), 0, s, x, res, y, scale, shift, M, C, g.chunk, g.tpr, g.rpi);
+  else if (relu)
+    hipLaunchKernelGGL((bn_apply<true, false>), dim3(g.gx), dim3(NT), 0, s, x, res, y, scale, shift, M, C, g.chunk, g.tpr, g.rpi);
+  else if (res)
+    hipLaunchKernelGGL((bn_apply<false, true>), dim3(g.gx), dim3(NT), 0, s, x, res, y, scale, shift, M, C, g.chunk, g.tpr, g.rpi);
+  else
+    hipLaunchKernelGGL((bn_apply<false, false>), dim3(g.gx), dim3(NT), 0, s, x, res, y, scale, shift, M, C, g.chunk, g.tpr, g.rpi);
+  return kfa_status();
+}
+
+KFA_API int kfa_bn_fwd_eval(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* gamma, const float* beta,
+                            const float* rmean, const float* rvar, float* ws, long M, int C, float eps, int relu,
+                            hipStream_t s) {
+  if (!bn_shape_ok(M, C)) return -1;
+  Geom g = geom(M, C, max_row_blocks(C));
+  float* scale = ws;
+  float* shift = ws + C;
+  hipLaunchKernelGGL(bn_finalize_eval, dim3(kfa_ceil_div(C, 256)), dim3(256), 0, s, gamma, beta, rmean, rvar, C, eps,
+                     scale, shift);
+  if (relu && res)
+    hipLaunchKernelGGL((bn_apply<true, true>), dim3(g.gx), dim3(NT), 0, s, x, res, y, scale, shift, M, C, g.chunk, g.tpr, g.rpi);
+  else if (relu)
+    hipLaunchKernelGGL((bn_apply<true, false>), dim3(g.gx), dim3(NT), 0, s, x, res, y, scale, shift, M, C, g.chunk, g.tpr, g.rpi);
+  else if (res)
+    hipLaunchKernelGGL((bn_apply<false, true>), dim3(g.gx), dim3(NT), 0, s, x, res, y, scale, shift, M, C, g.chunk, g.tpr, g.rpi);
+  else
+    hipLaunchKernelGGL((bn_apply<false, false>), dim3(g.gx), dim3(NT), 0, s, x, res, y, scale, shift, M, C, g.chunk, g.tpr, g.rpi);
+  return kfa_status();
+}
+
+// y is the forward OUTPUT (ReLU mask source); required when relu != 0.
+KFA_API int kfa_bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const float* gamma, const float* save_mean,
+                       const float* save_invstd, bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta, float* ws,
+                       long M, int C, int relu, int accumulate, hipStream_t s) {
+  if (!bn_shape_ok(M, C)) return -1;
+  if (relu && !y) return -2;
+  Geom g = geom(M, C, max_row_blocks(C));
+  float* part = ws;
+  float* coef = ws + 2L * kSlots * C;
+  if (relu)
+    hipLaunchKernelGGL(bn_bwd_partial<true>, dim3(g.gx), dim3(NT), 0, s, dy, x, y, save_mean, part, M, C, g.chunk, g.tpr, g.rpi);
+  else
+    hipLaunchKernelGGL(bn_bwd_partial<false>, dim3(g.gx), dim3(NT), 0, s, dy, x, y, save_mean, part, M, C, g.chunk, g.tpr, g.rpi);
+  hipLaunchKernelGGL(bn_bwd_finalize, dim3(kfa_ceil_div(C, 64)), dim3(64), 0, s, part, g.gx, M, C, gamma, save_mean,
+                     save_invstd, dgamma, dbeta, coef, accumulate);
+  if (relu && dres)
+    hipLaunchKernelGGL((bn_bwd_apply<true, true>), dim3(g.gx), dim3(NT), 0, s, dy, x, y, coef, dx, dres, M, C, g.chunk, g.tpr, g.rpi);
+  else if (relu)
+    hipLaunchKernelGGL((bn_bwd_apply<true, false>), dim3(g.gx), dim3(NT), 0, s, dy, x, y, coef, dx, dres, M, C, g.chunk, g.tpr, g.rpi);
+  else if (dres)
+    hipLaunchKernelGGL((bn_bwd_apply<false, true>), dim3(g.gx), dim3(NT), 0, s, dy, x, y, coef, dx, dres, M, C, g.chunk, g.tpr, g.rpi);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply<false, false>), dim3(g.gx), dim3(NT), 0, s, dy, x, y, coef, dx, dres, M, C, g.chunk, g.tpr, g.rpi);
+  return kfa_status();
+}

@@ -1,0 +1,53 @@
+// Shared helpers for the CDNA4 (gfx950) kernels of kubeflow_controller_amd.
+// bf16 is carried as raw uint16 bits so every kernel controls its own
+// vector width (16 B per lane loads, cdna_hip_programming.md Guideline 13).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define KFA_API extern "C" __attribute__((visibility("default")))
+
+typedef uint16_t bf16_t;
+typedef __attribute__((ext_vector_type(8))) short short8;   // 8 x bf16 MFMA operand
+typedef __attribute__((ext_vector_type(4))) float floatx4;
+typedef __attribute__((ext_vector_type(16))) float floatx16;
+
+__device__ __forceinline__ float bf2f(uint32_t b) { return __uint_as_float(b << 16); }
+
+// round-to-nearest-even float -> bf16 (NaN kept quiet)
+__device__ __forceinline__ uint32_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (u >> 16) | 0x40u;
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return u >> 16;
+}
+
+__device__ __forceinline__ uint32_t pack2(float lo, float hi) { return f2bf(lo) | (f2bf(hi) << 16); }
+
+// unpack a 16-byte vector of 8 bf16 into floats
+__device__ __forceinline__ void unpack8(const uint4 v, float f[8]) {
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
+  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
+}
+
+__device__ __forceinline__ uint4 pack8(const float f[8]) {
+  return make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+static inline int kfa_status() { return (int)hipGetLastError(); }
+
+static inline int kfa_ceil_div(long a, long b) { return (int)((a + b - 1) / b); }

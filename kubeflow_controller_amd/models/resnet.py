@@ -1,0 +1,83 @@
+"""ResNet-50 (v1.5: stride on the 3x3) in NHWC bf16 — the headline benchmark model.
+
+BASELINE.json configs "ResNet-50 synthetic ImageNet ..." (SURVEY §2.6 K7/K8/K9/K1/K2).
+Every BatchNorm is a fused ``BatchNorm2dAct`` (BN + optional residual add +
+ReLU in one HIP kernel chain); the residual add and the block's final ReLU are
+folded into ``bn3``.  Convolutions go through ``ops.conv.Conv2d`` (NHWC).
+The last BN of each block is zero-initialised (standard large-batch recipe).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+
+from ..ops.batchnorm import BatchNorm2dAct
+from ..ops.conv import Conv2d
+from ..ops.linear import Linear
+from ..ops.pool import MaxPool2d, global_avg_pool
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, cin: int, mid: int, stride: int):
+        super().__init__()
+        cout = mid * self.expansion
+        self.conv1 = Conv2d(cin, mid, 1)
+        self.bn1 = BatchNorm2dAct(mid, relu=True)
+        self.conv2 = Conv2d(mid, mid, 3, stride=stride, padding=1)
+        self.bn2 = BatchNorm2dAct(mid, relu=True)
+        self.conv3 = Conv2d(mid, cout, 1)
+        self.bn3 = BatchNorm2dAct(cout, relu=True, zero_init=True)  # + residual, fused
+        self.downsample = None
+        if stride != 1 or cin != cout:
+            self.downsample = nn.ModuleDict({"conv": Conv2d(cin, cout, 1, stride=stride),
+                                             "bn": BatchNorm2dAct(cout, relu=False)})
+
+    def forward(self, x):
+        idn = x if self.downsample is None else self.downsample["bn"](self.downsample["conv"](x))
+        y = self.bn1(self.conv1(x))
+        y = self.bn2(self.conv2(y))
+        return self.bn3(self.conv3(y), residual=idn)
+
+
+class ResNet(nn.Module):
+    def __init__(self, layers=(3, 4, 6, 3), num_classes: int = 1000, width: int = 64):
+        super().__init__()
+        self.conv1 = Conv2d(3, width, 7, stride=2, padding=3)
+        self.bn1 = BatchNorm2dAct(width, relu=True)
+        self.maxpool = MaxPool2d(3, 2, 1)
+        blocks = []
+        cin = width
+        for i, n in enumerate(layers):
+            mid = width * (2 ** i)
+            for j in range(n):
+                blocks.append(Bottleneck(cin, mid, (1 if i == 0 else 2) if j == 0 else 1))
+                cin = mid * Bottleneck.expansion
+        self.layers = nn.Sequential(*blocks)
+        self.fc = Linear(cin, num_classes)
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        for m in self.modules():
+            if isinstance(m, Conv2d):
+                fan_out = m.out_channels * m.kernel_size * m.kernel_size
+                nn.init.normal_(m.weight, 0.0, math.sqrt(2.0 / fan_out))
+        nn.init.normal_(self.fc.weight, 0.0, 0.01)
+        nn.init.zeros_(self.fc.bias)
+
+    def forward(self, x):
+        x = self.maxpool(self.bn1(self.conv1(x)))
+        x = self.layers(x)
+        return self.fc(global_avg_pool(x))
+
+
+def resnet50(num_classes: int = 1000) -> ResNet:
+    return ResNet((3, 4, 6, 3), num_classes)
+
+
+def resnet_tiny(num_classes: int = 10) -> ResNet:
+    """Same code path, toy width — for CPU plumbing tests and smoke()."""
+    return ResNet((1, 1, 1, 1), num_classes, width=8)

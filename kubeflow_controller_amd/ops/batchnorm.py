@@ -1,0 +1,145 @@
+"""Fused BatchNorm(+residual)(+ReLU) for NHWC bf16 — HIP kernel ``csrc/kernels/batchnorm.hip``.
+
+SURVEY §2.6 K8.  On a stock PyTorch-ROCm ResNet-50 step the channels-last BN
+kernels plus the separate ReLU/add elementwise kernels cost 57 of 74 ms
+(``profiles/r0_stock_torch_resnet50_bs256.md``); this op replaces all of them
+with 3 streaming passes forward and 3 backward.
+
+Layout contract: ``x`` is a 4-D bf16 tensor in channels_last memory format (or
+any tensor whose memory is ``[M, C]`` row-major with C innermost); params are
+fp32.  The ReLU mask in backward is read from the saved OUTPUT, so no extra
+mask tensor is stored.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+from ..parallel.flat import direct_grad_view, notify_grad_ready
+
+
+def _as_rows(t: torch.Tensor) -> torch.Tensor:
+    """Check that ``t``'s memory is [M, C] with C innermost (NHWC / 2-D)."""
+    if t.dim() == 4:
+        if not t.is_contiguous(memory_format=torch.channels_last):
+            t = t.contiguous(memory_format=torch.channels_last)
+    elif not t.is_contiguous():
+        t = t.contiguous()
+    return t
+
+
+def _mc(t: torch.Tensor):
+    C = t.shape[1] if t.dim() == 4 else t.shape[-1]
+    return t.numel() // C, C
+
+
+class _BNActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, residual, training, momentum, eps, relu):
+        x = _as_rows(x)
+        M, C = _mc(x)
+        if x.dtype != torch.bfloat16:
+            raise TypeError("bn_act: bf16 activations required")
+        res = _as_rows(residual) if residual is not None else None
+        if res is not None and (res.shape != x.shape or res.dtype != x.dtype):
+            raise ValueError(f"bn_act: residual {tuple(res.shape)} does not match input {tuple(x.shape)}")
+        y = torch.empty_like(x)
+        nws = _lib.lib().kfa_bn_workspace_floats(M, C) * 4
+        ws = _lib.workspace(nws, x.device, "bn")
+        s = _lib.stream()
+        if training:
+            mean = torch.empty(C, dtype=torch.float32, device=x.device)
+            invstd = torch.empty_like(mean)
+            _lib.call("kfa_bn_fwd_train", _lib.ptr(x), _lib.ptr(res), _lib.ptr(y), _lib.ptr(weight), _lib.ptr(bias),
+                      _lib.ptr(running_mean), _lib.ptr(running_var), _lib.ptr(mean), _lib.ptr(invstd),
+                      _lib.ptr(ws), M, C, eps, momentum, int(relu), s)
+        else:
+            _lib.call("kfa_bn_fwd_eval", _lib.ptr(x), _lib.ptr(res), _lib.ptr(y), _lib.ptr(weight), _lib.ptr(bias),
+                      _lib.ptr(running_mean), _lib.ptr(running_var), _lib.ptr(ws), M, C, eps, int(relu), s)
+            var = running_var
+            mean = running_mean.clone()
+            invstd = torch.rsqrt(var + eps)
+        ctx.save_for_backward(x, y if relu else None, weight, mean, invstd)
+        ctx.relu = relu
+        ctx.has_res = residual is not None
+        ctx.params = (weight, bias)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, weight, mean, invstd = ctx.saved_tensors
+        dy = _as_rows(dy)
+        M, C = _mc(x)
+        dx = torch.empty_like(x)
+        dres = torch.empty_like(x) if ctx.has_res else None
+        need_w = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
+        direct = False
+        dgamma = dbeta = None
+        if need_w:
+            gv, bv = ctx.params
+            wv, bvv = direct_grad_view(gv), direct_grad_view(bv)
+            if wv is not None and bvv is not None and wv.dtype == torch.float32 and bvv.dtype == torch.float32:
+                dgamma, dbeta, direct = wv, bvv, True  # += straight into the flat grad bucket
+            else:
+                dgamma = torch.empty(C, dtype=torch.float32, device=x.device)
+                dbeta = torch.empty(C, dtype=torch.float32, device=x.device)
+        nws = _lib.lib().kfa_bn_workspace_floats(M, C) * 4
+        ws = _lib.workspace(nws, x.device, "bn")
+        _lib.call("kfa_bn_bwd", _lib.ptr(dy), _lib.ptr(x), _lib.ptr(y), _lib.ptr(weight), _lib.ptr(mean),
+                  _lib.ptr(invstd), _lib.ptr(dx), _lib.ptr(dres), _lib.ptr(dgamma), _lib.ptr(dbeta), _lib.ptr(ws),
+                  M, C, int(ctx.relu), int(direct), _lib.stream())
+        if direct:
+            notify_grad_ready(ctx.params[0])
+            notify_grad_ready(ctx.params[1])
+            return dx, None, None, None, None, dres, None, None, None, None
+        if dgamma is not None and weight is not None and weight.dtype != torch.float32:
+            dgamma, dbeta = dgamma.to(weight.dtype), dbeta.to(weight.dtype)
+        return dx, dgamma, dbeta, None, None, dres, None, None, None, None
+
+
+def bn_act(x, weight, bias, running_mean, running_var, residual=None, training=True, momentum=0.1, eps=1e-5,
+           relu=True):
+    return _BNActFn.apply(x, weight, bias, running_mean, running_var, residual, training, momentum, eps, relu)
+
+
+def bn_act_reference(x, weight, bias, running_mean, running_var, residual=None, training=True, momentum=0.1,
+                     eps=1e-5, relu=True):
+    """Plain PyTorch fp32 reference of the same op (used by the numerics tests)."""
+    xf = x.float()
+    y = torch.nn.functional.batch_norm(xf, running_mean, running_var, weight, bias, training, momentum, eps)
+    if residual is not None:
+        y = y + residual.float()
+    if relu:
+        y = torch.relu(y)
+    return y
+
+
+class BatchNorm2dAct(nn.Module):
+    """``BatchNorm2d`` with an optional fused residual add and ReLU (NHWC bf16)."""
+
+    def __init__(self, num_features: int, relu: bool = True, eps: float = 1e-5, momentum: float = 0.1,
+                 zero_init: bool = False):
+        super().__init__()
+        self.num_features = num_features
+        self.relu = relu
+        self.eps = eps
+        self.momentum = momentum
+        self.weight = nn.Parameter(torch.zeros(num_features) if zero_init else torch.ones(num_features))
+        self.bias = nn.Parameter(torch.zeros(num_features))
+        self.register_buffer("running_mean", torch.zeros(num_features))
+        self.register_buffer("running_var", torch.ones(num_features))
+
+    def forward(self, x, residual=None):
+        if x.is_cuda:
+            return bn_act(x, self.weight, self.bias, self.running_mean, self.running_var, residual,
+                          self.training, self.momentum, self.eps, self.relu)
+        # CPU path (plumbing tests / CPU-only MNIST-style jobs): plain PyTorch.
+        y = torch.nn.functional.batch_norm(x, self.running_mean, self.running_var, self.weight.to(x.dtype),
+                                           self.bias.to(x.dtype), self.training, self.momentum, self.eps)
+        if residual is not None:
+            y = y + residual
+        return torch.relu(y) if self.relu else y
+
+    def extra_repr(self) -> str:
+        return f"{self.num_features}, relu={self.relu}, eps={self.eps}, momentum={self.momentum}"

@@ -1,0 +1,63 @@
+"""Softmax cross-entropy (fwd+bwd fused) and argmax/accuracy — ``csrc/kernels/loss.hip``.
+
+SURVEY §2.6 K2/K3: replaces ``softmax`` + clip + log + reduce_sum of
+``mnist_replica.py:167-168`` and ``softmax_cross_entropy_with_logits`` of
+``mnist_softmax.py:57-58``; at ResNet/BERT scale the gradient is produced in
+the same kernel as the loss so backward launches nothing.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+_lib.register("kfa_softmax_xent", [_lib.P, _lib.I, _lib.P, _lib.P, _lib.P, _lib.L, _lib.I, _lib.F, _lib.F, _lib.P])
+_lib.register("kfa_argmax", [_lib.P, _lib.I, _lib.P, _lib.L, _lib.I, _lib.P])
+
+
+class _XentFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels, smoothing):
+        z = logits.contiguous()
+        rows, V = z.numel() // z.shape[-1], z.shape[-1]
+        lab = labels.reshape(-1).to(torch.int64).contiguous()
+        if lab.numel() != rows:
+            raise ValueError(f"cross_entropy: {lab.numel()} labels for {rows} rows")
+        row_loss = torch.empty(rows, dtype=torch.float32, device=z.device)
+        dz = torch.empty_like(z) if logits.requires_grad else None
+        valid = max(int(rows), 1)
+        _lib.call("kfa_softmax_xent", _lib.ptr(z), int(z.dtype == torch.bfloat16), _lib.ptr(lab), _lib.ptr(row_loss),
+                  _lib.ptr(dz), rows, V, 1.0 / valid, float(smoothing), _lib.stream())
+        ctx.save_for_backward(dz)
+        return row_loss.sum() / valid
+
+    @staticmethod
+    def backward(ctx, g):
+        (dz,) = ctx.saved_tensors
+        return dz * g.to(dz.dtype), None, None
+
+
+def cross_entropy(logits: torch.Tensor, labels: torch.Tensor, label_smoothing: float = 0.0) -> torch.Tensor:
+    """Mean softmax cross-entropy over rows; fp32 scalar loss."""
+    if not logits.is_cuda:
+        return torch.nn.functional.cross_entropy(logits.float(), labels, label_smoothing=label_smoothing)
+    if logits.dtype not in (torch.bfloat16, torch.float32):
+        logits = logits.float()
+    return _XentFn.apply(logits, labels, label_smoothing)
+
+
+def argmax(logits: torch.Tensor) -> torch.Tensor:
+    if not logits.is_cuda:
+        return logits.argmax(-1)
+    z = logits.contiguous()
+    if z.dtype not in (torch.bfloat16, torch.float32):
+        z = z.float()
+    rows, V = z.numel() // z.shape[-1], z.shape[-1]
+    out = torch.empty(rows, dtype=torch.int64, device=z.device)
+    _lib.call("kfa_argmax", _lib.ptr(z), int(z.dtype == torch.bfloat16), _lib.ptr(out), rows, V, _lib.stream())
+    return out.view(z.shape[:-1])
+
+
+def accuracy(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+    """``mean(argmax(z) == y)`` (``mnist_softmax.py:70-71``)."""
+    return (argmax(logits) == labels.reshape(argmax(logits).shape)).float().mean()

@@ -178,6 +178,8 @@ class ObjectStore:
         return d
 
     def _admit(self, obj: Model) -> None:
+        if obj.kind == "Pod" and not obj.status.phase:
+            obj.status.phase = "Pending"  # apiserver default for a new pod
         if isinstance(obj, v1alpha1.TFJob):
             set_defaults(obj)
             try:
