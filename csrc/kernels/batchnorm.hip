@@ -96,7 +96,8 @@ __global__ __launch_bounds__(NT) void bn_stats_partial(const bf16_t* __restrict_
       if (g0 * 8 + c < C) {
         float acc = 0.f;
         for (int rr = 0; rr < rpi; rr++) acc += sh[a][rr * width + c];
-        atomicAdd(&part[((long)(blockIdx.x % kSlots) * 2 + a) * C + g0 * 8 + c], acc);
+        __hip_atomic_fetch_add(&part[((long)(blockIdx.x % kSlots) * 2 + a) * C + g0 * 8 + c], acc,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     __syncthreads();
@@ -114,10 +115,10 @@ __device__ __forceinline__ void combine2(float* __restrict__ part, int C, int c,
   for (int i = 0; i < kSlots; i++) {
     float* pa = part + ((long)i * 2) * C + c;
     float* pb = pa + C;
-    a += (double)*pa;
-    b += (double)*pb;
-    *pa = 0.f;
-    *pb = 0.f;
+    // read-and-zero at the coherence point: the adds came from other XCDs'
+    // workgroups, so plain loads could hit a stale line of THIS XCD's L2
+    a += (double)__hip_atomic_exchange(pa, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    b += (double)__hip_atomic_exchange(pb, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -290,7 +291,8 @@ __global__ __launch_bounds__(NT) void bn_bwd_partial(const bf16_t* __restrict__ 
       if (g0 * 8 + c < C) {
         float acc = 0.f;
         for (int rr = 0; rr < rpi; rr++) acc += sh[a][rr * width + c];
-        atomicAdd(&part[((long)(blockIdx.x % kSlots) * 2 + a) * C + g0 * 8 + c], acc);
+        __hip_atomic_fetch_add(&part[((long)(blockIdx.x % kSlots) * 2 + a) * C + g0 * 8 + c], acc,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     __syncthreads();
@@ -362,22 +364,21 @@ static int max_row_blocks(int C) {
   return m > 2048 ? 2048 : (m < 64 ? 64 : m);
 }
 
-KFA_API long kfa_bn_workspace_floats(long M, int C) {
-  Geom g = geom(M, C, max_row_blocks(C));
-  return 2L * kSlots * C + 3L * C;
-}
+// Two workspaces: `slots` (kfa_bn_slot_floats, ZERO-initialised once, kept
+// clean by every finalize) and `coef` (kfa_bn_coef_floats, scratch).  They
+// must not alias: the slot region's layout depends on C.
+KFA_API long kfa_bn_slot_floats(int C) { return 2L * kSlots * C; }
+KFA_API long kfa_bn_coef_floats(int C) { return 3L * C; }
 
 static bool bn_shape_ok(long M, int C) { return M > 0 && C >= 8 && (C % 8) == 0; }
 
-// ws: >= kfa_bn_workspace_floats(M, C) floats, ZERO-initialised once by the
-// caller (the slot accumulators are re-zeroed by every finalize).
 KFA_API int kfa_bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* gamma, const float* beta,
-                             float* rmean, float* rvar, float* save_mean, float* save_invstd, float* ws, long M, int C,
-                             float eps, float momentum, int relu, hipStream_t s) {
+                             float* rmean, float* rvar, float* save_mean, float* save_invstd, float* slots,
+                             float* coefws, long M, int C, float eps, float momentum, int relu, hipStream_t s) {
   if (!bn_shape_ok(M, C)) return -1;
   Geom g = geom(M, C, max_row_blocks(C));
-  float* part = ws;
-  float* scale = ws + 2L * kSlots * C;
+  float* part = slots;
+  float* scale = coefws;
   float* shift = scale + C;
   hipLaunchKernelGGL(bn_stats_partial, dim3(g.gx), dim3(NT), 0, s, x, part, M, C, g.chunk, g.tpr, g.rpi);
   hipLaunchKernelGGL(bn_finalize, dim3(kfa_ceil_div(C, 64)), dim3(64), 0, s, x, part, g.gx, M, C, gamma, beta, rmean,
@@ -415,13 +416,13 @@ KFA_API int kfa_bn_fwd_eval(const bf16_t* x, const bf16_t* res, bf16_t* y, const
 
 // y is the forward OUTPUT (ReLU mask source); required when relu != 0.
 KFA_API int kfa_bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const float* gamma, const float* save_mean,
-                       const float* save_invstd, bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta, float* ws,
-                       long M, int C, int relu, int accumulate, hipStream_t s) {
+                       const float* save_invstd, bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta, float* slots,
+                       float* coefws, long M, int C, int relu, int accumulate, hipStream_t s) {
   if (!bn_shape_ok(M, C)) return -1;
   if (relu && !y) return -2;
   Geom g = geom(M, C, max_row_blocks(C));
-  float* part = ws;
-  float* coef = ws + 2L * kSlots * C;
+  float* part = slots;
+  float* coef = coefws;
   if (relu)
     hipLaunchKernelGGL(bn_bwd_partial<true>, dim3(g.gx), dim3(NT), 0, s, dy, x, y, save_mean, part, M, C, g.chunk, g.tpr, g.rpi);
   else

@@ -28,12 +28,13 @@ F = ctypes.c_float
 
 # name -> argtypes (restype is int status unless listed in _RESTYPE)
 _SIGS = {
-    "kfa_bn_workspace_floats": [L, I],
-    "kfa_bn_fwd_train": [P, P, P, P, P, P, P, P, P, P, L, I, F, F, I, P],
+    "kfa_bn_slot_floats": [I],
+    "kfa_bn_coef_floats": [I],
+    "kfa_bn_fwd_train": [P, P, P, P, P, P, P, P, P, P, P, L, I, F, F, I, P],
     "kfa_bn_fwd_eval": [P, P, P, P, P, P, P, P, L, I, F, I, P],
-    "kfa_bn_bwd": [P, P, P, P, P, P, P, P, P, P, P, L, I, I, I, P],
+    "kfa_bn_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, L, I, I, I, P],
 }
-_RESTYPE = {"kfa_bn_workspace_floats": L}
+_RESTYPE = {"kfa_bn_slot_floats": L, "kfa_bn_coef_floats": L}
 
 
 def register(name: str, argtypes, restype=I) -> None:

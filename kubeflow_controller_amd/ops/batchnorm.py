@@ -34,6 +34,13 @@ def _mc(t: torch.Tensor):
     return t.numel() // C, C
 
 
+def _workspaces(C: int, device):
+    L = _lib.lib()
+    slots = _lib.workspace(L.kfa_bn_slot_floats(C) * 4, device, "bn_slots")  # zero-init, self-cleaning
+    coef = _lib.workspace(L.kfa_bn_coef_floats(C) * 4, device, "bn_coef")
+    return slots, coef
+
+
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, residual, training, momentum, eps, relu):
@@ -45,18 +52,17 @@ class _BNActFn(torch.autograd.Function):
         if res is not None and (res.shape != x.shape or res.dtype != x.dtype):
             raise ValueError(f"bn_act: residual {tuple(res.shape)} does not match input {tuple(x.shape)}")
         y = torch.empty_like(x)
-        nws = _lib.lib().kfa_bn_workspace_floats(M, C) * 4
-        ws = _lib.workspace(nws, x.device, "bn")
+        slots, coef = _workspaces(C, x.device)
         s = _lib.stream()
         if training:
             mean = torch.empty(C, dtype=torch.float32, device=x.device)
             invstd = torch.empty_like(mean)
             _lib.call("kfa_bn_fwd_train", _lib.ptr(x), _lib.ptr(res), _lib.ptr(y), _lib.ptr(weight), _lib.ptr(bias),
                       _lib.ptr(running_mean), _lib.ptr(running_var), _lib.ptr(mean), _lib.ptr(invstd),
-                      _lib.ptr(ws), M, C, eps, momentum, int(relu), s)
+                      _lib.ptr(slots), _lib.ptr(coef), M, C, eps, momentum, int(relu), s)
         else:
             _lib.call("kfa_bn_fwd_eval", _lib.ptr(x), _lib.ptr(res), _lib.ptr(y), _lib.ptr(weight), _lib.ptr(bias),
-                      _lib.ptr(running_mean), _lib.ptr(running_var), _lib.ptr(ws), M, C, eps, int(relu), s)
+                      _lib.ptr(running_mean), _lib.ptr(running_var), _lib.ptr(coef), M, C, eps, int(relu), s)
             var = running_var
             mean = running_mean.clone()
             invstd = torch.rsqrt(var + eps)
@@ -84,10 +90,10 @@ class _BNActFn(torch.autograd.Function):
             else:
                 dgamma = torch.empty(C, dtype=torch.float32, device=x.device)
                 dbeta = torch.empty(C, dtype=torch.float32, device=x.device)
-        nws = _lib.lib().kfa_bn_workspace_floats(M, C) * 4
-        ws = _lib.workspace(nws, x.device, "bn")
+        slots, coef = _workspaces(C, x.device)
         _lib.call("kfa_bn_bwd", _lib.ptr(dy), _lib.ptr(x), _lib.ptr(y), _lib.ptr(weight), _lib.ptr(mean),
-                  _lib.ptr(invstd), _lib.ptr(dx), _lib.ptr(dres), _lib.ptr(dgamma), _lib.ptr(dbeta), _lib.ptr(ws),
+                  _lib.ptr(invstd), _lib.ptr(dx), _lib.ptr(dres), _lib.ptr(dgamma), _lib.ptr(dbeta), _lib.ptr(slots),
+                  _lib.ptr(coef),
                   M, C, int(ctx.relu), int(direct), _lib.stream())
         if direct:
             notify_grad_ready(ctx.params[0])

@@ -8,8 +8,8 @@ import torch.nn.functional as F
 
 from . import _lib
 
-_lib.register("kfa_maxpool_fwd", [_lib.P, _lib.P, _lib.P] + [_lib.I] * 10 + [_lib.P])
-_lib.register("kfa_maxpool_bwd", [_lib.P, _lib.P, _lib.P] + [_lib.I] * 10 + [_lib.P])
+_lib.register("kfa_maxpool_fwd", [_lib.P, _lib.P, _lib.P] + [_lib.I] * 9 + [_lib.P])
+_lib.register("kfa_maxpool_bwd", [_lib.P, _lib.P, _lib.P] + [_lib.I] * 9 + [_lib.P])
 
 
 class _MaxPoolFn(torch.autograd.Function):
