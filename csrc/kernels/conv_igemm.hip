@@ -1,0 +1,349 @@
+// Implicit-GEMM convolution on MFMA (bf16 in, fp32 accumulate), NHWC.
+// SURVEY §2.6 K7 (ResNet-50 conv2d fwd + dgrad) and K1 (plain GEMM = 1x1 conv).
+//
+// One kernel computes  D[m][n] = sum_k A[m][k] * B[n][k]  (+ E[m][n])  where
+//   A = implicit im2col of an NHWC tensor T[Nb][H][W][C]:
+//         m = (nb, p, q) in [Nb][P][Q],  k = (r, s, c) in [R][S][C]
+//         A[m][k] = T[nb][p*sa + r*ra + oa][q*sa + s*ra + ob][c]   (0 outside)
+//   B = [N][K] row-major bf16 (K contiguous) — conv weights in [Cout][R][S][Cin]
+//   D = bf16 rows, row m written at pixel (nb, p*os + oph, q*os + opw) of an
+//       [Nb][OH][OW][ldd] tensor.
+// Forward conv:   sa = stride, ra = +1, oa = -pad, os = 1.
+// Dgrad stride 1: T = dY, ra = -1, oa = +pad, B = W transposed to [Cin][R][S][Cout].
+// Dgrad stride 2: one launch per output parity class (ph, pw) over its tap subset
+//                 (os = 2), B = the class's tap-subset weights (see conv.py).
+//
+// Tiling for CDNA4: 256 threads = 4 waves, each wave owns a 64x64 output tile
+// (4x4 MFMA 16x16x32 bf16 tiles, 64 fp32 accumulator VGPRs).  Block tiles
+// 128x128 (2x2 waves) or 256x64 (4x1, for Cout = 64 layers).  BK = 64 = one
+// (r, s) tap slice (C % 64 == 0).  Global->register prefetch of tile k+1 is
+// issued before the MFMAs of tile k (T14) — across tile boundaries too: the
+// blocks are persistent (2 per CU) and sweep an XCD-local tile range, so the
+// next tile's first slice loads under the current tile's last MFMAs and
+// epilogue.  LDS is double-buffered (one barrier
+// per k-tile) and XOR-swizzled (chunk ^= (row>>1)&7) so the 16-lane groups of
+// each ds_read_b128 hit 16 distinct 16-B slots.  Operand roles are chosen so
+// each lane's 4 accumulator rows are 4 CONSECUTIVE output channels (8-B stores).
+#include "common.h"
+
+namespace {
+
+constexpr int BK = 64;
+
+struct Geo {
+  int Nb, H, W, C;   // gathered tensor T
+  int P, Q;          // GEMM row space (m = nb*P*Q + p*Q + q)
+  int R, S;          // taps
+  int sa, ra, oa, ob;  // gather: ih = p*sa + r*ra + oa, iw = q*sa + s*ra + ob
+  int M, N, K;       // GEMM sizes (K = R*S*C)
+  int OH, OW, os, oph, opw, ldd;  // output pixel mapping / row stride (elements)
+  unsigned t_bytes, b_bytes, d_bytes;  // buffer extents: out-of-range lanes read 0 / drop stores
+};
+
+// Buffer-resource loads/stores (T8): the hardware range check turns padding
+// taps and tile tails into zero loads / dropped stores with NO branch, so hipcc
+// can keep counted vmcnt waits instead of draining to vmcnt(0) around each
+// guarded load (cdna_hip_programming.md §5 'Three .s-level traps' (c)).
+constexpr unsigned kOOB = 0x80000000u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ uint4 bload16(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+  return *reinterpret_cast<uint4*>(&v);
+}
+
+// x / d for 0 <= x < 2^24 via an fp32 reciprocal + one correction step
+// (hipcc's int32 division is a ~40-instruction sequence; these run per row).
+__device__ __forceinline__ int fdiv(int x, int d, float rcp) {
+  int q = (int)((float)x * rcp);
+  const int r = x - q * d;
+  q += (r >= d) - (r < 0);
+  return q;
+}
+
+// Workgroup barrier for LDS hand-off only.  __syncthreads() is a workgroup
+// release fence too, which makes hipcc drain vmcnt(0) for the epilogue's
+// global stores — and with them the prefetch loads in flight.  Nothing in this
+// kernel needs global-memory ordering between waves, only LDS.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+__device__ __forceinline__ int swz(int row, int chunk) { return row * BK + ((chunk ^ ((row >> 1) & 7)) << 3); }
+
+// WM x WN waves, each owning TM x TN MFMA 16x16 tiles (wave tile 16TM x 16TN)
+template <int WM, int WN, int TM, int TN>
+__global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const bf16_t* __restrict__ T, const bf16_t* __restrict__ B,
+                                                            bf16_t* __restrict__ D, const bf16_t* __restrict__ E,
+                                                            const bf16_t* __restrict__ Z, Geo g) {
+  constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
+  constexpr int AR = BM / 32, BR = BN / 32;  // 16-B chunks per thread per k-tile
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  bf16_t* As = smem;                  // [2][BM][BK]
+  bf16_t* Bs = smem + 2 * BM * BK;    // [2][BN][BK]
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  const int ntn = (g.N + BN - 1) / BN;
+  const int ntiles = ((g.M + BM - 1) / BM) * ntn;
+
+  // Persistent blocks.  XCD-aware assignment (T1): the blocks that share an
+  // XCD (b % 8) sweep one contiguous range of tiles, so tiles in flight on an
+  // XCD share A/B panels in its L2.
+  const int nwg = gridDim.x;
+  const int G = nwg < 8 ? nwg : 8;                        // XCD groups that have blocks
+  const int xcd = blockIdx.x % G, slot = blockIdx.x / G;
+  const int nslot = (nwg - xcd + G - 1) / G;               // blocks in this group
+  const int t_lo = (int)((long)ntiles * xcd / G), t_hi = (int)((long)ntiles * (xcd + 1) / G);
+  const int my_tiles = t_hi - t_lo > slot ? (t_hi - t_lo - slot + nslot - 1) / nslot : 0;
+  auto tile_of = [&](int i) { return t_lo + slot + i * nslot; };
+
+  const int kc = tid & 7;
+  const int rbase = tid >> 3;  // 0..31
+  const int PQ = g.P * g.Q;
+  const float rPQ = 1.f / (float)PQ, rQ = 1.f / (float)g.Q;
+  // pointwise fast paths: A row m is T[m] (1x1 / stride 1 / no pad) and/or D row m is D[m]
+  const bool lin_a = g.R == 1 && g.S == 1 && g.sa == 1 && g.oa == 0 && g.ob == 0 && g.H == g.P && g.W == g.Q;
+  const bool lin_d = g.os == 1 && g.oph == 0 && g.opw == 0 && g.OH == g.P && g.OW == g.Q;
+  int a_hb[AR], a_wb[AR], a_base[AR];  // element offsets fit in 32 bits (checked on the host)
+  unsigned b_off[BR];
+  const __amdgpu_buffer_rsrc_t rT = rsrc(T, g.t_bytes), rB = rsrc(B, g.b_bytes), rD = rsrc(D, g.d_bytes);
+  const __amdgpu_buffer_rsrc_t rE = rsrc(E ? E : D, E ? g.d_bytes : 0u);
+  auto setup = [&](int tile) {
+    const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
+#pragma unroll
+    for (int i = 0; i < AR; i++) {
+      const int m = m0 + rbase + 32 * i;
+      if (m < g.M && lin_a) {
+        a_hb[i] = 0;
+        a_wb[i] = 0;
+        a_base[i] = m * g.C;
+      } else if (m < g.M) {
+        const int nb = fdiv(m, PQ, rPQ), rem = m - nb * PQ;
+        const int p = fdiv(rem, g.Q, rQ), q = rem - p * g.Q;
+        a_hb[i] = p * g.sa + g.oa;
+        a_wb[i] = q * g.sa + g.ob;
+        a_base[i] = nb * g.H * g.W * g.C;
+      } else {
+        a_hb[i] = -(1 << 28);  // forces out-of-range
+        a_wb[i] = 0;
+        a_base[i] = 0;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BR; i++) {
+      const int n = n0 + rbase + 32 * i;
+      b_off[i] = n < g.N ? (unsigned)(n * g.K + kc * 8) * 2u : kOOB;
+    }
+  };
+
+  // Operand staging: LDS-DMA (global_load_lds_dwordx4).  Each wave-instruction
+  // writes 1 KiB = 8 tile rows lane-linearly; the XOR swizzle is applied on the
+  // per-lane SOURCE address (rule 21), padding taps / tails read a zero page.
+  // No staging VGPRs, no ds_write pass; waits are counted by hand.
+  const int nk = g.K / BK;
+  const int total = my_tiles * nk;
+  int setup_tile = -1;
+  const int l8 = lane >> 3, pos = lane & 7;
+  auto issue = [&](int st, int buf) {
+    const int ti = st / nk, kt = st - ti * nk;
+    if (ti != setup_tile) { setup(tile_of(ti)); setup_tile = ti; }
+    const int k0 = kt * BK;
+    const int tap = k0 / g.C, c0 = k0 - tap * g.C;
+    const int r = tap / g.S, s = tap - r * g.S;
+    const int dh = r * g.ra, dw = s * g.ra;
+#pragma unroll
+    for (int i = 0; i < AR; i++) {
+      const int row = i * 32 + wave * 8 + l8;
+      const int c = pos ^ ((row >> 1) & 7);
+      const int ih = a_hb[i] + dh, iw = a_wb[i] + dw;
+      const bool ok = (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+      const bf16_t* src = ok ? T + (unsigned)(a_base[i] + (ih * g.W + iw) * g.C + c0 + c * 8) : Z;
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(As + buf * BM * BK + (i * 32 + wave * 8) * BK),
+                                       16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < BR; i++) {
+      const int row = i * 32 + wave * 8 + l8;
+      const int c = pos ^ ((row >> 1) & 7);
+      const bf16_t* src = b_off[i] == kOOB ? Z : B + b_off[i] / 2 + k0 + (c - pos) * 8;
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(Bs + buf * BN * BK + (i * 32 + wave * 8) * BK),
+                                       16, 0, 0);
+    }
+  };
+
+  floatx4 acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; i++)
+#pragma unroll
+    for (int j = 0; j < TM; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  auto compute = [&](int buf) {
+    const bf16_t* Ab = As + buf * BM * BK;
+    const bf16_t* Bb = Bs + buf * BN * BK;
+#pragma unroll
+    for (int ks = 0; ks < 2; ks++) {
+      short8 af[TM], bf[TN];
+#pragma unroll
+      for (int i = 0; i < TM; i++)
+        af[i] = *reinterpret_cast<const short8*>(Ab + swz(wm * TM * 16 + i * 16 + fr, ks * 4 + fq));
+#pragma unroll
+      for (int i = 0; i < TN; i++)
+        bf[i] = *reinterpret_cast<const short8*>(Bb + swz(wn * TN * 16 + i * 16 + fr, ks * 4 + fq));
+#pragma unroll
+      for (int ni = 0; ni < TN; ni++)
+#pragma unroll
+        for (int mi = 0; mi < TM; mi++)
+          acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[ni], af[mi], acc[ni][mi], 0, 0, 0);
+    }
+  };
+  auto epilogue = [&](int tile) {
+    // lane holds D[n = n0 + wn*16TN + ni*16 + fq*4 + j][m = m0 + wm*16TM + mi*16 + fr]
+    const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
+#pragma unroll
+    for (int mi = 0; mi < TM; mi++) {
+      const int m = m0 + wm * TM * 16 + mi * 16 + fr;
+      unsigned orow;  // byte offset of output row m (kOOB when m is a tail row)
+      if (lin_d) {
+        orow = (unsigned)m * (unsigned)g.ldd * 2u;
+      } else {
+        const int nb = fdiv(m, PQ, rPQ), rem = m - nb * PQ;
+        const int p = fdiv(rem, g.Q, rQ), q = rem - p * g.Q;
+        orow = (unsigned)((nb * g.OH + p * g.os + g.oph) * g.OW + (q * g.os + g.opw)) * (unsigned)g.ldd * 2u;
+      }
+      orow = m < g.M ? orow : kOOB;
+#pragma unroll
+      for (int ni = 0; ni < TN; ni++) {
+        const int n = n0 + wn * TN * 16 + ni * 16 + fq * 4;
+        const unsigned off = (orow == kOOB || n >= g.N) ? kOOB : orow + (unsigned)n * 2u;
+        float v0 = acc[ni][mi][0], v1 = acc[ni][mi][1], v2 = acc[ni][mi][2], v3 = acc[ni][mi][3];
+        if (E) {  // wave-uniform branch
+          auto ev = __builtin_amdgcn_raw_buffer_load_b64(rE, off, 0, 0);
+          const uint2 e = *reinterpret_cast<uint2*>(&ev);
+          v0 += bf2f(e.x & 0xffff); v1 += bf2f(e.x >> 16); v2 += bf2f(e.y & 0xffff); v3 += bf2f(e.y >> 16);
+        }
+        uint2 o = make_uint2(pack2(v0, v1), pack2(v2, v3));
+        __builtin_amdgcn_raw_buffer_store_b64(*reinterpret_cast<decltype(__builtin_amdgcn_raw_buffer_load_b64(rD, 0, 0, 0))*>(&o), rD, off, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < TN; i++)
+#pragma unroll
+      for (int j = 0; j < TM; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  };
+
+  if (nk == 0) {  // no taps reach these outputs (strided dgrad parity class): D = 0 (+ E)
+    for (int i = 0; i < my_tiles; i++) epilogue(tile_of(i));
+    return;
+  }
+  issue(0, 0);
+  for (int st = 0; st < total; st++) {
+    const int buf = st & 1;
+    if (st + 1 < total) {
+      issue(st + 1, buf ^ 1);
+      // slice st landed (and older stores retired); slice st+1 stays in flight
+      if constexpr (AR + BR == 8) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+      else if constexpr (AR + BR == 6) asm volatile("s_waitcnt vmcnt(6)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    compute(buf);
+    if ((st + 1) % nk == 0) epilogue(tile_of(st / nk));
+    lds_barrier();  // every wave is done reading `buf` before slice st+2 is DMA'd into it
+  }
+}
+
+// zero-fill D rows of the output pixel mapping that the GEMM does not cover
+__global__ void zero_bf16(bf16_t* __restrict__ p, long n8) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x)
+    reinterpret_cast<uint4*>(p)[i] = make_uint4(0, 0, 0, 0);
+}
+
+// W[Cout][R][S][Cin] -> Wt[Cin][Rs][Ss][Cout] over the tap subset r = r0 + dr*i, s = s0 + ds*j
+__global__ void weight_transpose(const bf16_t* __restrict__ W, bf16_t* __restrict__ Wt, int Cout, int R, int S,
+                                 int Cin, int r0, int dr, int Rs, int s0, int ds, int Ss) {
+  __shared__ bf16_t tile[32][33];
+  const int tap = blockIdx.z;
+  const int ri = tap / Ss, si = tap - ri * Ss;
+  const int r = r0 + dr * ri, s = s0 + ds * si;
+  const int co0 = blockIdx.y * 32, ci0 = blockIdx.x * 32;
+  for (int y = threadIdx.y; y < 32; y += blockDim.y) {
+    const int co = co0 + y, ci = ci0 + threadIdx.x;
+    tile[y][threadIdx.x] = (co < Cout && ci < Cin) ? W[(((long)co * R + r) * S + s) * Cin + ci] : (bf16_t)0;
+  }
+  __syncthreads();
+  for (int y = threadIdx.y; y < 32; y += blockDim.y) {
+    const int ci = ci0 + y, co = co0 + threadIdx.x;
+    if (ci < Cin && co < Cout) Wt[(((long)ci * Rs + ri) * Ss + si) * Cout + co] = tile[threadIdx.x][y];
+  }
+}
+
+}  // namespace
+
+static const bf16_t* zero_page() {
+  static bf16_t* z = nullptr;
+  if (!z) {
+    if (hipMalloc(&z, 256) != hipSuccess) return nullptr;
+    (void)hipMemset(z, 0, 256);
+    (void)hipDeviceSynchronize();
+  }
+  return z;
+}
+
+// variant: 0 = 128x128 tile, 1 = 128x64 tile (N <= 64)
+KFA_API int kfa_conv_igemm(const bf16_t* T, const bf16_t* B, bf16_t* D, const bf16_t* E, int Nb, int H, int W, int C,
+                           int P, int Q, int R, int S, int sa, int ra, int oa, int ob, int N, int OH, int OW, int os,
+                           int oph, int opw, int ldd, int variant, hipStream_t st) {
+  if (C % BK != 0 || N % 8 != 0 || ldd % 8 != 0) return -1;
+  Geo g{Nb, H, W, C, P, Q, R, S, sa, ra, oa, ob, Nb * P * Q, N, R * S * C, OH, OW, os, oph, opw, ldd, 0, 0, 0};
+  if (g.K == 0) g.R = g.S = 1;  // keep index math defined; nk == 0 -> zero/addend-only epilogue
+  const long tb = (long)Nb * H * W * C * 2, bb = (long)N * R * S * C * 2, db = (long)Nb * OH * OW * ldd * 2;
+  if (tb >= (long)kOOB || bb >= (long)kOOB || db >= (long)kOOB) return -2;  // 32-bit buffer offsets
+  g.t_bytes = (unsigned)tb;
+  g.b_bytes = (unsigned)bb;
+  g.d_bytes = (unsigned)db;
+  if (g.M <= 0) return 0;
+  int cus = 256;
+  {
+    static int cached = 0;
+    if (!cached) {
+      int dev = 0;
+      hipGetDevice(&dev);
+      hipDeviceGetAttribute(&cached, hipDeviceAttributeMultiprocessorCount, dev);
+      if (cached <= 0) cached = 256;
+    }
+    cus = cached;
+  }
+  const int slots = 2 * cus;  // 2 resident blocks per CU (64 KB LDS, <=256 VGPR/2 waves)
+  auto pgrid = [&](long tiles) { return (int)(tiles < slots ? tiles : slots); };
+  if (variant == 1) {  // 128 x 64 tile (Cout <= 64): 4 waves of 32x64
+    const long tiles = (long)kfa_ceil_div(g.M, 128) * kfa_ceil_div(N, 64);
+    const int grid = (int)(tiles < 3L * cus ? tiles : 3L * cus);  // 160 VGPR, 48 KB LDS: 3 blocks / CU
+    hipLaunchKernelGGL((conv_igemm_kernel<4, 1, 2, 4>), dim3(grid), dim3(256), 2 * (128 + 64) * BK * 2, st, T, B, D,
+                       E, zero_page(), g);
+  } else {  // 128 x 128 tile: 2x2 waves of 64x64
+    const int grid = pgrid((long)kfa_ceil_div(g.M, 128) * kfa_ceil_div(N, 128));
+    hipLaunchKernelGGL((conv_igemm_kernel<2, 2, 4, 4>), dim3(grid), dim3(256), 2 * (128 + 128) * BK * 2, st, T, B, D,
+                       E, zero_page(), g);
+  }
+  return kfa_status();
+}
+
+KFA_API int kfa_zero_bf16(bf16_t* p, long n, hipStream_t st) {
+  if (n % 8) return -1;
+  long n8 = n / 8;
+  long b = (n8 + 255) / 256;
+  hipLaunchKernelGGL(zero_bf16, dim3(b < 4096 ? (b < 1 ? 1 : b) : 4096), dim3(256), 0, st, p, n8);
+  return kfa_status();
+}
+
+KFA_API int kfa_weight_transpose(const bf16_t* W, bf16_t* Wt, int Cout, int R, int S, int Cin, int r0, int dr, int Rs,
+                                 int s0, int ds, int Ss, hipStream_t st) {
+  dim3 grid(kfa_ceil_div(Cin, 32), kfa_ceil_div(Cout, 32), Rs * Ss);
+  hipLaunchKernelGGL(weight_transpose, grid, dim3(32, 8), 0, st, W, Wt, Cout, R, S, Cin, r0, dr, Rs, s0, ds, Ss);
+  return kfa_status();
+}

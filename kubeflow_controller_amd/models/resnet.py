@@ -14,7 +14,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.batchnorm import BatchNorm2dAct
-from ..ops.conv import Conv2d
+from ..ops.conv import Conv2d, GradJoin
 from ..ops.linear import Linear
 from ..ops.pool import MaxPool2d, global_avg_pool
 
@@ -37,8 +37,15 @@ class Bottleneck(nn.Module):
                                              "bn": BatchNorm2dAct(cout, relu=False)})
 
     def forward(self, x):
-        idn = x if self.downsample is None else self.downsample["bn"](self.downsample["conv"](x))
-        y = self.bn1(self.conv1(x))
+        # x feeds two branches; its gradient sum is fused into a dgrad epilogue
+        # (ops.conv.GradJoin) instead of a separate add kernel.
+        join = GradJoin()
+        if self.downsample is None:
+            y = self.bn1(self.conv1(x, join=join))
+            y = self.bn2(self.conv2(y))
+            return self.bn3(self.conv3(y), residual=join.branch(x))
+        idn = self.downsample["bn"](self.downsample["conv"](x, join=join))
+        y = self.bn1(self.conv1(join.branch(x)))
         y = self.bn2(self.conv2(y))
         return self.bn3(self.conv3(y), residual=idn)
 

@@ -1,16 +1,192 @@
-"""NHWC bf16 2-D convolution.
+"""NHWC bf16 2-D convolution on the hand-written MFMA implicit GEMM
+(``csrc/kernels/conv_igemm.hip``) — SURVEY §2.6 K7.
 
-The weight is stored ``[Cout, Cin, kh, kw]`` in channels_last memory, i.e.
-physically ``[Cout][kh][kw][Cin]`` — the K-contiguous "B^T" layout an implicit
-GEMM over NHWC activations consumes directly.
+* forward: implicit GEMM over the NHWC input (``sa = stride, ra = +1, oa = -pad``);
+* dgrad, stride 1: implicit GEMM over dY with flipped taps (``ra = -1, oa = +pad``)
+  against the weight transposed to ``[Cin][R][S][Cout]``;
+* dgrad, stride 2: split by output parity class (ph, pw); each class is a
+  stride-1 implicit GEMM over its tap subset, writing every other pixel
+  (``os = 2``); classes with no taps are zero-filled;
+* dgrad can take the residual branch's gradient as an epilogue addend
+  (``D = A.B^T + E``) — used where a tensor feeds both a conv and a skip path;
+* wgrad: vendor path for now (``aten.convolution_backward``).
+
+The weight lives as ``[Cout, Cin, kh, kw]`` in channels_last memory, i.e.
+physically ``[Cout][kh][kw][Cin]`` — exactly the K-contiguous B operand.
+Layers the kernel does not cover (the 3-channel stem) use ``F.conv2d``.
 """
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+from . import _lib
+
+P, I = _lib.P, _lib.I
+_lib.register("kfa_conv_igemm", [P, P, P, P] + [I] * 20 + [P])
+_lib.register("kfa_zero_bf16", [P, _lib.L, P])
+_lib.register("kfa_weight_transpose", [P, P] + [I] * 10 + [P])
+
+# Runtime switch (tests compare against the vendor path); env KFA_CONV_IGEMM=0 disables.
+ENABLED = os.environ.get("KFA_CONV_IGEMM", "1") != "0"
+
+
+def igemm_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+    return (ENABLED and x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and x.dim() == 4 and x.shape[1] % 64 == 0 and w.shape[0] % 8 == 0 and w.shape[2] == w.shape[3])
+
+
+def _variant(M: int, N: int) -> int:
+    return 1 if N <= 64 else 0
+
+
+def _cl(t: torch.Tensor) -> torch.Tensor:
+    return t if t.is_contiguous(memory_format=torch.channels_last) else t.contiguous(memory_format=torch.channels_last)
+
+
+def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int) -> torch.Tensor:
+    x, w = _cl(x), _cl(w)
+    Nb, C, H, W = x.shape
+    Co, _, R, S = w.shape
+    Po = (H + 2 * pad - R) // stride + 1
+    Qo = (W + 2 * pad - S) // stride + 1
+    y = torch.empty((Nb, Co, Po, Qo), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+    _lib.call("kfa_conv_igemm", _lib.ptr(x), _lib.ptr(w), _lib.ptr(y), None, Nb, H, W, C, Po, Qo, R, S, stride, 1,
+              -pad, -pad, Co, Po, Qo, 1, 0, 0, Co, _variant(Nb * Po * Qo, Co), _lib.stream())
+    return y
+
+
+def _transposed_weight(w: torch.Tensor, r0: int, dr: int, Rs: int, s0: int, ds: int, Ss: int) -> torch.Tensor:
+    Co, Ci, R, S = w.shape
+    wt = torch.empty((Ci, Rs, Ss, Co), dtype=w.dtype, device=w.device)
+    if Rs * Ss:
+        _lib.call("kfa_weight_transpose", _lib.ptr(w), _lib.ptr(wt), Co, R, S, Ci, r0, dr, Rs, s0, ds, Ss,
+                  _lib.stream())
+    return wt
+
+
+def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride: int, pad: int, addend=None) -> torch.Tensor:
+    dy, w = _cl(dy), _cl(w)
+    Nb, Co, Po, Qo = dy.shape
+    _, Ci, R, S = w.shape
+    H, W = x_shape[2], x_shape[3]
+    dx = torch.empty((Nb, Ci, H, W), dtype=dy.dtype, device=dy.device, memory_format=torch.channels_last)
+    E = None if addend is None else _cl(addend)
+    st = _lib.stream()
+    if stride == 1:
+        wt = _transposed_weight(w, 0, 1, R, 0, 1, S)
+        _lib.call("kfa_conv_igemm", _lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), _lib.ptr(E), Nb, Po, Qo, Co, H, W, R, S,
+                  1, -1, pad, pad, Ci, H, W, 1, 0, 0, Ci, _variant(Nb * H * W, Ci), st)
+        return dx
+    # stride s: output parity classes.  For class (ph, pw) the rows h = s*i + ph
+    # receive taps r with (ph + pad - r) % s == 0, from dY row i + (ph + pad - r)/s.
+    for ph in range(stride):
+        r0 = (ph + pad) % stride
+        Rs = len(range(r0, R, stride))
+        Hc = len(range(ph, H, stride))
+        for pw in range(stride):
+            s0 = (pw + pad) % stride
+            Ss = len(range(s0, S, stride))
+            Wc = len(range(pw, W, stride))
+            if Hc == 0 or Wc == 0:
+                continue
+            # a class no tap reaches (1x1/s2: 3 of 4) runs with K = 0: the kernel
+            # writes zeros (or the addend) through the same strided output mapping
+            wt = _transposed_weight(w, r0, stride, Rs, s0, stride, Ss) if Rs * Ss else w
+            oa_h = (ph + pad - r0) // stride
+            oa_w = (pw + pad - s0) // stride
+            _lib.call("kfa_conv_igemm", _lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), _lib.ptr(E), Nb, Po, Qo, Co, Hc, Wc,
+                      Rs, Ss, 1, -1, oa_h, oa_w, Ci, H, W, stride, ph, pw, Ci, _variant(Nb * Hc * Wc, Ci), st)
+    return dx
+
+
+def conv_wgrad(x: torch.Tensor, dy: torch.Tensor, w: torch.Tensor, stride: int, pad: int) -> torch.Tensor:
+    _, gw, _ = torch.ops.aten.convolution_backward(dy, x, w, None, [stride, stride], [pad, pad], [1, 1],
+                                                   False, [0, 0], 1, [False, True, False])
+    return gw
+
+
+class GradJoin:
+    """Fuses the gradient SUM of a tensor that feeds two branches into a conv's dgrad.
+
+    ``xb = join.branch(x)`` is an alias of ``x`` whose gradient is *deposited*
+    here instead of flowing back to ``x``; the conv built with
+    ``conv2d(x, w, ..., join=join)`` then computes ``dx = dgrad(dy) + deposit``
+    in its epilogue (``E`` operand of ``kfa_conv_igemm``), so autograd never runs
+    the separate add kernel.  Autograd's ready-queue order (latest-created node
+    first) runs the branch's backward before the conv's; if it ever does not,
+    the branch simply returns its gradient to autograd (correct, just unfused).
+    """
+
+    __slots__ = ("grad", "state", "fused")
+
+    def __init__(self):
+        self.grad = None
+        self.state = "empty"  # empty -> deposited -> empty | consumer-first
+        self.fused = False    # set by the consuming conv's forward (HIP path only)
+
+    def branch(self, x):
+        if not (torch.is_grad_enabled() and x.requires_grad and self.fused):
+            return x
+        return _Branch.apply(x, self)
+
+
+class _Branch(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, join):
+        ctx.join = join
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        j = ctx.join
+        if j.state == "consumer-first":
+            j.state = "empty"
+            return g, None
+        j.grad, j.state = g, "deposited"
+        return None, None
+
+
+class _ConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, stride, pad, join):
+        ctx.save_for_backward(x, w)
+        ctx.stride, ctx.pad, ctx.join = stride, pad, join
+        return conv_fwd(x, w, stride, pad)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            addend = None
+            j = ctx.join
+            if j is not None:
+                if j.state == "deposited":
+                    addend, j.grad, j.state = j.grad, None, "empty"
+                else:
+                    j.state = "consumer-first"
+            if w.shape[0] % 64 == 0 and w.shape[1] % 8 == 0:
+                dx = conv_dgrad(dy, w, x.shape, ctx.stride, ctx.pad, addend)
+            else:
+                dx = torch.nn.grad.conv2d_input(x.shape, w, dy, ctx.stride, ctx.pad)
+                if addend is not None:
+                    dx = dx + addend
+        if ctx.needs_input_grad[1]:
+            dw = conv_wgrad(x, dy, w, ctx.stride, ctx.pad)
+        return dx, dw, None, None, None
+
+
+def conv2d(x, w, stride: int = 1, pad: int = 0, join: "GradJoin | None" = None):
+    if igemm_ok(x, w):
+        if join is not None:
+            join.fused = True
+        return _ConvFn.apply(x, w, stride, pad, join)
+    return F.conv2d(x, w, None, stride, pad)  # unfused: join.branch() is a no-op alias
 
 
 class Conv2d(nn.Module):
@@ -27,10 +203,12 @@ class Conv2d(nn.Module):
         self.weight = nn.Parameter(w.contiguous(memory_format=torch.channels_last))
         self.bias = nn.Parameter(torch.zeros(out_channels)) if bias else None
 
-    def forward(self, x):
+    def forward(self, x, join: "GradJoin | None" = None):
         w = self.weight if self.weight.dtype == x.dtype else self.weight.to(x.dtype)
-        b = None if self.bias is None else self.bias.to(x.dtype)
-        return F.conv2d(x, w, b, self.stride, self.padding)
+        y = conv2d(x, w, self.stride, self.padding, join)
+        if self.bias is not None:
+            y = y + self.bias.to(y.dtype).view(1, -1, 1, 1)
+        return y
 
     def extra_repr(self) -> str:
         return (f"{self.in_channels}, {self.out_channels}, k={self.kernel_size}, s={self.stride}, "
