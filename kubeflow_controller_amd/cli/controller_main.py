@@ -99,7 +99,8 @@ class Node:
             self.endpoints = EndpointController(self.kube_client, kinf.services())
             self.supervisor = Supervisor(self.kube_client, kinf.pods(), kinf.services(),
                                          root_dir or os.path.expanduser("~/.kfa/pods"), num_gpus=num_gpus,
-                                         gpu_policy=gpu_policy, backoff_base=kubelet_backoff, extra_env=extra_env)
+                                         gpu_policy=gpu_policy, backoff_base=kubelet_backoff, extra_env=extra_env,
+                                         tfjob_informer=kinf.tfjobs())
         self.stop = threading.Event()
         self._threads: List[threading.Thread] = []
 

@@ -163,7 +163,7 @@ class Controller:
 
         if job_needs_sync and tfjob.metadata.deletionTimestamp is None:
             self.manage_tfjob(active_worker, active_ps, worker_svcs, ps_svcs, succeeded, tfjob,
-                              succeeded_indices(worker_pods))
+                              succeeded_indices(worker_pods), succeeded_indices(ps_pods))
 
         if local:
             updater = LocalUpdater(tfjob, succeeded, worker_pods)
@@ -177,7 +177,7 @@ class Controller:
         log.debug("Sync TFJob: %s", key)
 
     def manage_tfjob(self, active_worker, active_ps, worker_svcs, ps_svcs, succeeded: int,
-                     tfjob: v1alpha1.TFJob, succeeded_idx=None):
+                     tfjob: v1alpha1.TFJob, succeeded_idx=None, succeeded_ps_idx=None):
         key = key_of(tfjob)
         log.debug("Manage the TFJob %s, active workers: %d, active parameter servers: %d",
                   tfjob.metadata.name, len(active_worker), len(active_ps))
@@ -192,7 +192,8 @@ class Controller:
                     self.expectations.creation_observed(key)
                     raise
             return 1, 0
-        dj = DistributedJob(tfjob, active_worker, active_ps, worker_svcs, ps_svcs, succeeded, succeeded_idx)
+        dj = DistributedJob(tfjob, active_worker, active_ps, worker_svcs, ps_svcs, succeeded, succeeded_idx,
+                            succeeded_ps_idx)
         events = dj.action()
         n_w = n_p = 0
         first_err: Optional[Exception] = None

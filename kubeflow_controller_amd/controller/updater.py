@@ -25,9 +25,24 @@ from __future__ import annotations
 from typing import Dict, List, Optional
 
 from ..api import v1alpha1
-from ..api.core import POD_FAILED, RESTART_NEVER, Pod
+from ..api.core import POD_FAILED, POD_SUCCEEDED, RESTART_NEVER, Pod
+from ..api.meta import now_rfc3339
 from ..api.model import to_json
 from ..planner.local import EXPECTED_LOCAL_WORKER_NUMBER
+
+
+def set_condition(st: v1alpha1.TFJobStatus, ctype: str, status: str, reason: str) -> None:
+    """Upsert a condition; lastTransitionTime changes only when status flips."""
+    conds = st.conditions or []
+    for c in conds:
+        if c.type == ctype:
+            if c.status != status:
+                c.status, c.lastTransitionTime = status, now_rfc3339()
+            c.reason = reason
+            st.conditions = conds
+            return
+    conds.append(v1alpha1.TFJobCondition(type=ctype, status=status, reason=reason, lastTransitionTime=now_rfc3339()))
+    st.conditions = conds
 
 
 def _histogram(pods: List[Pod]) -> Dict[str, int]:
@@ -115,6 +130,11 @@ class DistributedUpdater:
             st.phase = v1alpha1.PHASE_RUNNING
         update_tf_replica_statuses(self.tfjob, self.worker_pods, v1alpha1.WORKER)
         update_tf_replica_statuses(self.tfjob, self.ps_pods, v1alpha1.PS)
+        if st.phase == v1alpha1.PHASE_SUCCEEDED and self.ps_pods:
+            # TFJobRecycling (types.go:153-155): workers done, PS replicas being reclaimed
+            recycling = any(p.status.phase not in (POD_SUCCEEDED, POD_FAILED) for p in self.ps_pods)
+            set_condition(st, v1alpha1.COND_RECYCLING, "True" if recycling else "False",
+                          "WorkersSucceeded" if recycling else "PSRecycled")
         return to_json(st) != before
 
 

@@ -88,15 +88,17 @@ class _Proc:
     state: str = "starting"  # starting | running | backoff | done
     log_path: str = ""
     term_sent: float = 0.0
+    recycled: bool = False  # terminated because its job finished (PS recycling)
 
 
 class Supervisor:
     def __init__(self, clientset, pod_informer, service_informer, root_dir: str, *, num_gpus: Optional[int] = None,
                  gpu_policy: str = "auto", backoff_base: float = 1.0, backoff_max: float = 60.0,
-                 grace_period: float = 10.0, extra_env: Optional[Dict[str, str]] = None):
+                 grace_period: float = 10.0, extra_env: Optional[Dict[str, str]] = None, tfjob_informer=None):
         self.client = clientset
         self.pods = pod_informer.lister()
         self.services = service_informer.lister()
+        self.tfjobs = tfjob_informer.lister() if tfjob_informer is not None else None
         self.root = os.path.abspath(root_dir)
         os.makedirs(self.root, exist_ok=True)
         self.num_gpus = detect_gpus() if num_gpus is None else num_gpus
@@ -312,6 +314,30 @@ class Supervisor:
             except errors.NotFound:
                 return
 
+    # ------------------------------------------------------------------ PS recycling
+    def _job_finished(self, pod: Pod) -> bool:
+        """Owner TFJob already Succeeded/Failed (TFJobRecycling, ``types.go:153-155``)."""
+        if self.tfjobs is None:
+            return False
+        name = pod.metadata.labels.get("tf_job_name")
+        if not name:
+            return False
+        try:
+            job = self.tfjobs.get(pod.metadata.namespace, name)
+        except errors.NotFound:
+            return False
+        if job.status.phase in (v1alpha1.PHASE_SUCCEEDED, v1alpha1.PHASE_FAILED):
+            return True
+        # the controller may not have written the phase yet: look at the workers directly
+        want = next((s.replicas for s in job.spec.specs if s.tfReplicaType == v1alpha1.WORKER), None)
+        if not want:
+            return False
+        done = [p for p in self.pods.list(pod.metadata.namespace)
+                if p.metadata.labels.get("tf_job_name") == name and p.metadata.labels.get("job_type") == v1alpha1.WORKER
+                and p.metadata.labels.get("runtime_id") == pod.metadata.labels.get("runtime_id")
+                and p.status.phase == POD_SUCCEEDED]
+        return len(done) >= want
+
     # ------------------------------------------------------------------ main loop
     def tick(self) -> None:
         now = time.monotonic()
@@ -328,7 +354,11 @@ class Supervisor:
                     res = self.rt.poll(p.pid)
                     if res is not None:
                         self._release(p)
-                        self._procs.pop(key, None)
+                        if p.recycled and pod is not None:
+                            p.state = "done"
+                            self._set_status(pod, POD_SUCCEEDED, exit_code=0, reason="Recycled")
+                        else:
+                            self._procs.pop(key, None)
                     elif now - p.term_sent > self.grace:
                         self.rt.kill_group(p.pid, signal.SIGKILL)
                     continue
@@ -345,11 +375,19 @@ class Supervisor:
                 if p.state != "running":
                     continue
                 res = self.rt.poll(p.pid)
+                finished = pod.metadata.labels.get("job_type") == v1alpha1.PS and self._job_finished(pod)
                 if res is None:
+                    if finished:  # PS replicas never exit on their own in TF: recycle them
+                        log.info("recycling PS pod %s: job finished", key)
+                        self.rt.kill_group(p.pid, signal.SIGTERM)
+                        p.term_sent = now
+                        p.state = "terminating"
+                        p.recycled = True
                     continue
                 code, sig = res
                 policy = pod.spec.restartPolicy or RESTART_ALWAYS
-                restart = policy == RESTART_ALWAYS or (policy == RESTART_ON_FAILURE and code != 0)
+                restart = (policy == RESTART_ALWAYS or (policy == RESTART_ON_FAILURE and code != 0)) and not (
+                    finished or (code == 0 and self._job_finished(pod)))
                 log.info("pod %s pid=%d exited code=%d (policy %s%s)", key, p.pid, code, policy,
                          ", restarting" if restart else "")
                 if restart:

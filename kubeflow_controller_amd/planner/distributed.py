@@ -54,7 +54,8 @@ def _index_of(obj) -> Optional[int]:
 class DistributedJob:
     def __init__(self, tfjob: v1alpha1.TFJob, active_worker_pods: List[Pod], active_ps_pods: List[Pod],
                  worker_services: List[Service], ps_services: List[Service], succeeded_worker_pods: int,
-                 succeeded_worker_indices: Optional[List[int]] = None):
+                 succeeded_worker_indices: Optional[List[int]] = None,
+                 succeeded_ps_indices: Optional[List[int]] = None):
         self.tfjob = tfjob
         self.active_worker_pods = active_worker_pods
         self.active_ps_pods = active_ps_pods
@@ -62,6 +63,7 @@ class DistributedJob:
         self.ps_services = ps_services
         self.succeeded_worker_pods = succeeded_worker_pods
         self.succeeded_worker_indices = set(succeeded_worker_indices or [])
+        self.succeeded_ps_indices = set(succeeded_ps_indices or [])
         # logical service name (<job>-<type>-<i>) -> generated object name
         self.service_names: Dict[str, str] = {}
         for typ, svcs in ((v1alpha1.WORKER, worker_services), (v1alpha1.PS, ps_services)):
@@ -96,7 +98,11 @@ class DistributedJob:
         n_worker = self.replicas(v1alpha1.WORKER)
         n_ps = self.replicas(v1alpha1.PS)
         expected_worker = n_worker - self.succeeded_worker_pods
-        expected_ps = n_ps
+        if n_worker and expected_worker <= 0:
+            # every worker succeeded: the job is complete, PS replicas are being
+            # recycled (TFJobRecycling) — never re-create anything for it
+            return [Event(Action.Nothing)]
+        expected_ps = n_ps - len(self.succeeded_ps_indices)
 
         have_wsvc = {_index_of(s) for s in self.worker_services}
         miss_wsvc = [i for i in range(n_worker) if i not in have_wsvc]
@@ -123,7 +129,8 @@ class DistributedJob:
         active_p = {_index_of(p) for p in self.active_ps_pods}
         if len(self.active_ps_pods) < expected_ps:
             self.compose()
-            missing = [i for i in range(n_ps) if i not in active_p][:expected_ps - len(self.active_ps_pods)]
+            missing = [i for i in range(n_ps) if i not in active_p and i not in self.succeeded_ps_indices]
+            missing = missing[:expected_ps - len(self.active_ps_pods)]
             events.append(Event(Action.ShouldAddPS, len(missing), missing))
         return events
 

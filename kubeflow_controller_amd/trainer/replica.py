@@ -1,0 +1,301 @@
+"""The TFJob replica runtime: what every Worker / PS / Local process runs.
+
+MI355X-native replacement of the reference's TensorFlow-1.x workload scripts
+(``examples/workdir/mnist_replica.py``, ``mnist_softmax.py``) — same CLI flags,
+same roles, same log lines, PyTorch-ROCm + hand-written HIP kernels + RCCL inside:
+
+  python -m kubeflow_controller_amd.trainer.replica --model mnist_mlp \\
+      --worker_hosts=... --ps_hosts=... --job_name=worker --task_index=0 \\
+      [--train_steps 200 --batch_size 100 --learning_rate 0.01 --sync_replicas]
+
+Roles (``mnist_replica.py:107-122``):
+* ``local`` — single process, no collectives (the Local TFJob).
+* ``worker`` — joins the worker collective (RCCL on a GPU, gloo on CPU) via
+  the chief's endpoint; trains; reports to the coordination store.
+* ``ps`` — coordinator: attaches to the chief's store, tracks the global step
+  and exits 0 once every worker reported done.  The reference's PS
+  ``server.join()``s forever; here the job completes.
+  Parameter shards are owned by worker ranks (``parallel/ps.py``).
+
+Update semantics: with PS replicas the step is push (reduce-scatter) ->
+owner-side fused optimizer -> pull (all-gather); without PS, bucketed
+all-reduce.  Both are synchronous.  ``--sync_replicas`` off (the reference's
+async default) keeps the reference's step ACCOUNTING — every worker's push
+advances the global step, so ``train_steps`` global steps take
+``ceil(train_steps / workers)`` local steps — but the update itself is
+synchronous (strictly stronger consistency than async PS).
+"""
+from __future__ import annotations
+
+import argparse
+import datetime
+import json
+import math
+import os
+import sys
+import time
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from .cluster import ClusterSpec, add_cluster_flags, parse_cluster
+
+STEP_KEY = "kfa/global_step"
+DONE_KEY = "kfa/workers_done"
+
+
+def _log(msg: str) -> None:
+    print(msg, flush=True)
+
+
+def _use_gpu(args) -> bool:
+    if args.device == "cpu":
+        return False
+    vis = os.environ.get("HIP_VISIBLE_DEVICES")
+    if vis is not None and vis.strip() == "":
+        return False  # the supervisor bound no GPU to this replica
+    return torch.cuda.is_available()
+
+
+def _store(spec: ClusterSpec, is_master: bool, timeout: float = 300.0):
+    host, port = spec.rendezvous()
+    return dist.TCPStore(host, port, spec.num_workers if is_master else None, is_master,
+                         timeout=datetime.timedelta(seconds=timeout), wait_for_workers=False)
+
+
+# ------------------------------------------------------------------ models
+def build(args, device):
+    from ..models import mnist
+    from ..ops.loss import cross_entropy
+    name = args.model
+    if name == "mnist_softmax":
+        data = mnist.SyntheticMNIST(seed=args.seed)
+        return mnist.MnistSoftmax(), data, lambda m, x, y: cross_entropy(m(x).float(), y)
+    if name == "mnist_mlp":
+        data = mnist.SyntheticMNIST(seed=args.seed)
+        return mnist.MnistMLP(args.hidden_units), data, lambda m, x, y: cross_entropy(m(x).float(), y)
+    if name in ("resnet50", "resnet_tiny"):
+        from ..models.resnet import resnet50, resnet_tiny
+        model = resnet50() if name == "resnet50" else resnet_tiny(10)
+        return model, None, lambda m, x, y: cross_entropy(m(x), y)
+    if name in ("bert_base", "bert_tiny"):
+        from ..models.bert import BertConfig, BertForPreTraining, bert_loss
+        cfg = BertConfig.base() if name == "bert_base" else BertConfig.tiny()
+        return BertForPreTraining(cfg), None, bert_loss
+    if name in ("wide_deep", "wide_deep_tiny"):
+        from ..models.wide_deep import WideDeep, WideDeepConfig, wide_deep_loss
+        cfg = WideDeepConfig() if name == "wide_deep" else WideDeepConfig.tiny()
+        return WideDeep(cfg), None, wide_deep_loss
+    raise SystemExit(f"unknown --model {name}")
+
+
+def synthetic_batch(args, model, device, rank: int):
+    g = torch.Generator(device="cpu").manual_seed(args.seed + 1000 * rank)
+    B = args.batch_size
+    if args.model.startswith("resnet"):
+        s = 224 if args.model == "resnet50" else 32
+        x = torch.randn(B, 3, s, s, generator=g).to(device)
+        x = x.to(torch.bfloat16 if device.type == "cuda" else torch.float32)
+        x = x.contiguous(memory_format=torch.channels_last)
+        y = torch.randint(0, 1000 if args.model == "resnet50" else 10, (B,), generator=g).to(device)
+        return (x, y)
+    if args.model.startswith("bert"):
+        from ..models.bert import synthetic_mlm_batch
+        return synthetic_mlm_batch(model.cfg, B, args.seq_len, g, device)
+    if args.model.startswith("wide_deep"):
+        from ..models.wide_deep import synthetic_batch as wd_batch
+        return wd_batch(model.cfg, B, g, device)
+    raise ValueError(args.model)
+
+
+# ------------------------------------------------------------------ roles
+def run_ps(spec: ClusterSpec, args) -> int:
+    """PS coordinator: follow the global step until every worker is done."""
+    _log(f"PS {spec.task_index}: joining job with {spec.num_workers} workers at "
+         f"{'%s:%d' % spec.rendezvous()}")
+    t0 = time.time()
+    store = None
+    while store is None:
+        try:
+            store = _store(spec, False, timeout=args.ps_connect_timeout)
+        except Exception as e:  # chief not up yet
+            if time.time() - t0 > args.ps_connect_timeout:
+                _log(f"PS {spec.task_index}: chief unreachable ({e}); exiting")
+                return 1
+            time.sleep(0.5)
+    last = -1
+    while True:
+        try:
+            done = int(store.add(DONE_KEY, 0))
+            step = int(store.add(STEP_KEY, 0))
+        except Exception:
+            # the chief's store is gone: the job finished (workers exit after reporting)
+            _log(f"PS {spec.task_index}: store closed at global step {last}; done")
+            return 0
+        if step != last and step % max(1, args.log_every) == 0:
+            _log(f"PS {spec.task_index}: global step {step}")
+        last = step
+        if done >= spec.num_workers:
+            _log(f"PS {spec.task_index}: all {done} workers done at global step {step}; exiting")
+            return 0
+        time.sleep(0.2)
+
+
+def run_worker(spec: ClusterSpec, args) -> int:
+    from ..ops.loss import accuracy, cross_entropy
+    from ..ops.optim import FusedAdam, FusedSGD
+    from ..parallel.ddp import GradSync, broadcast_params
+    from ..parallel.flat import split_params
+    from ..parallel.ps import ShardedGradSync, ps_assignment
+
+    use_gpu = _use_gpu(args)
+    device = torch.device("cuda", 0) if use_gpu else torch.device("cpu")
+    if not use_gpu and not spec.is_local and not os.environ.get("OMP_NUM_THREADS"):
+        # CPU replicas of one job share the node: don't oversubscribe the cores
+        torch.set_num_threads(max(1, (os.cpu_count() or 1) // (spec.num_workers + len(spec.ps))))
+    if use_gpu:
+        torch.cuda.set_device(0)
+    world = 1 if spec.is_local else spec.num_workers
+    rank = 0 if spec.is_local else spec.task_index
+    store = None
+    if not spec.is_local:
+        store = _store(spec, spec.is_chief)
+        dist.init_process_group("nccl" if use_gpu else "gloo", store=store, rank=rank, world_size=world,
+                                **({"device_id": device} if use_gpu else {}))
+    torch.manual_seed(args.seed)  # identical init everywhere (+ broadcast below)
+    model, data, loss_fn = build(args, device)
+    model = model.to(device)
+    if model.__class__.__name__ == "ResNet":
+        model = model.to(memory_format=torch.channels_last)
+    num_ps = len(spec.ps)
+    world_pad = 8 * max(world, 1)
+    groups = split_params(model, torch.bfloat16 if (use_gpu and args.bf16) else None, pad_to=world_pad)
+    if args.optimizer == "adam":
+        opt = FusedAdam(groups, lr=args.learning_rate, weight_decay=args.weight_decay)
+    else:
+        opt = FusedSGD(groups, lr=args.learning_rate, momentum=args.momentum, weight_decay=args.weight_decay)
+    broadcast_params(groups)
+    sharded = num_ps > 0 and world > 1
+    if sharded:
+        sync = ShardedGradSync(groups)
+        sync.configure(opt)
+        placement = ps_assignment(list(model.named_parameters()), num_ps)
+        if spec.is_chief:
+            counts = [sum(1 for v in placement.values() if v == p) for p in range(num_ps)]
+            _log(f"PS placement (round-robin over {num_ps} PS tasks): tensors per PS = {counts}; "
+                 f"shards owned by worker ranks 0..{world - 1}")
+    else:
+        sync = GradSync(groups, bucket_mb=args.bucket_mb)
+
+    steps_per_worker = args.train_steps if (args.sync_replicas or spec.is_local) else \
+        math.ceil(args.train_steps / world)
+    inc = 1 if (args.sync_replicas or spec.is_local) else world
+    fixed = None if data is not None else synthetic_batch(args, model, device, rank)
+    _log(f"Worker {rank}: {'local' if spec.is_local else f'{world} workers, {num_ps} ps'}, device {device}, "
+         f"model {args.model}, {sum(p.numel() for p in model.parameters())} params, "
+         f"{'sharded push/pull' if sharded else 'all-reduce'}")
+    t_begin = time.time()
+    _log(f"Training begins @ {t_begin:f}")
+    global_step = 0
+    t_first = None
+    loss = None
+    for local_step in range(steps_per_worker):
+        if data is not None:
+            xb, yb = data.next_batch(args.batch_size)
+            batch = (xb.to(device), yb.to(device))
+        else:
+            batch = fixed
+        for g in groups:
+            g.zero_grad()
+        loss = loss_fn(model, *batch)
+        loss.backward()
+        if sharded:
+            scale = sync.push()
+            opt.step(grad_scale=scale)
+            sync.pull()
+        else:
+            scale = sync.finish()
+            opt.step(grad_scale=scale)
+        global_step += inc
+        if store is not None and spec.is_chief:
+            store.add(STEP_KEY, inc)
+        if t_first is None:
+            t_first = time.time()
+        if args.log_every and (local_step % args.log_every == 0 or local_step == steps_per_worker - 1):
+            if spec.is_local:
+                _log(f"step: {local_step}")
+            else:
+                _log(f"{time.time():f}: Worker {rank}: training step {local_step + 1} done "
+                     f"(global step: {global_step})")
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+    t_end = time.time()
+    _log(f"Training ends @ {t_end:f}")
+    _log(f"Training elapsed time: {t_end - t_begin:f} s")
+    if t_first is not None and steps_per_worker > 1:
+        sps = (steps_per_worker - 1) / max(t_end - t_first, 1e-9)
+        _log(f"Steady-state: {sps:.1f} steps/s/worker, {sps * args.batch_size * world:.1f} examples/s (job)")
+    if data is not None:
+        with torch.no_grad():
+            model.eval()
+            vx, vy = data.validation
+            z = model(vx.to(device)).float()
+            ce = float(cross_entropy(z, vy.to(device))) * vx.shape[0]
+            _log(f"After {global_step} training step(s), validation cross entropy = {ce:g}")
+            tx, ty = data.test
+            acc = float(accuracy(model(tx.to(device)).float(), ty.to(device)))
+            _log(f"Test accuracy: {acc:.4f}")
+    elif loss is not None:
+        _log(f"Final loss: {float(loss):.5f}")
+    if args.model_dir and spec.is_chief:
+        os.makedirs(args.model_dir, exist_ok=True)
+        torch.save({k: v.detach().cpu() for k, v in model.state_dict().items()},
+                   os.path.join(args.model_dir, f"model.step{global_step}.pt"))
+        with open(os.path.join(args.model_dir, "manifest.json"), "w") as f:
+            json.dump({"global_step": global_step, "model": args.model, "world": world, "ps": num_ps}, f)
+    if store is not None:
+        store.add(DONE_KEY, 1)
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+def build_parser() -> argparse.ArgumentParser:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    add_cluster_flags(ap)
+    ap.add_argument("--model", default="mnist_mlp",
+                    help="mnist_softmax | mnist_mlp | resnet50 | resnet_tiny | bert_base | bert_tiny | "
+                         "wide_deep | wide_deep_tiny")
+    ap.add_argument("--train_steps", type=int, default=200)
+    ap.add_argument("--batch_size", type=int, default=100)
+    ap.add_argument("--learning_rate", type=float, default=0.01)
+    ap.add_argument("--optimizer", default="adam", choices=["adam", "sgd"])
+    ap.add_argument("--momentum", type=float, default=0.0)
+    ap.add_argument("--weight_decay", type=float, default=0.0)
+    ap.add_argument("--hidden_units", type=int, default=100)
+    ap.add_argument("--seq_len", type=int, default=128)
+    ap.add_argument("--sync_replicas", action="store_true")
+    ap.add_argument("--replicas_to_aggregate", type=int, default=None, help="accepted; = #workers")
+    ap.add_argument("--num_gpus", type=int, default=1, help="accepted (one GPU per replica)")
+    ap.add_argument("--data_dir", default="", help="accepted (synthetic data; no network)")
+    ap.add_argument("--model_dir", default="")
+    ap.add_argument("--device", default="auto", choices=["auto", "cpu", "gpu"])
+    ap.add_argument("--bf16", type=int, default=1)
+    ap.add_argument("--bucket_mb", type=float, default=16.0)
+    ap.add_argument("--log_every", type=int, default=1)
+    ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--ps_connect_timeout", type=float, default=300.0)
+    return ap
+
+
+def main(argv: Optional[list] = None) -> int:
+    args = build_parser().parse_args(argv)
+    spec = parse_cluster(args)
+    if spec.is_ps:
+        return run_ps(spec, args)
+    return run_worker(spec, args)
+
+
+if __name__ == "__main__":
+    sys.exit(main())
