@@ -143,6 +143,11 @@ class Controller:
             self.expectations.delete_expectations(key)
             return
         original = deep_copy(tfjob)
+        if not tfjob.spec.runtimeID:
+            # Mint the (UID-derived) runtime ID BEFORE claiming children: a retried
+            # sync whose spec write was lost must select the replicas it created.
+            from ..planner.util import generate_runtime_id
+            tfjob.spec.runtimeID = generate_runtime_id(tfjob.metadata.uid)
 
         worker_pods: List = []
         ps_pods: List = []

@@ -1,13 +1,20 @@
 """Helper: create children with a controller ref and claim existing ones.
 
-Reference ``pkg/controller/helper.go:42-179``.  The claim selector is the 4
-labels WITHOUT ``index`` (``helper.go:112-119``); before adopting orphans a
+Reference ``pkg/controller/helper.go:42-179``.  Before adopting orphans a
 fresh (uncached) GET of the TFJob must still show the same uid and no
 deletionTimestamp (``RecheckDeletionTimestamp``).
+
+Fix: the reference claims with the 4-label selector INCLUDING ``job_type``
+(``helper.go:112-119``), so ``GetPodsForTFJob(job, PS)`` sees the job's own
+Worker pods as "owned but not matching" and RELEASES them (orphans that the
+next Worker claim re-adopts, and that the owner's cascade delete misses).
+Here the claim uses the job-level labels (``kubeflow.caicloud.io``,
+``runtime_id``, ``tf_job_name``) and the replica type is a filter applied to
+the claimed set.
 """
 from __future__ import annotations
 
-from typing import List
+from typing import List, Optional
 
 from ..api import v1alpha1
 from ..api.core import Pod, PodTemplateSpec, Service
@@ -16,13 +23,16 @@ from .ref import PodControllerRefManager, ServiceControllerRefManager, recheck_d
 from .util import new_controller_ref
 
 
-def claim_selector(tfjob: v1alpha1.TFJob, typ: str) -> Selector:
-    return Selector.from_match_labels({
-        "kubeflow.caicloud.io": "true",
-        "job_type": typ,
-        "runtime_id": tfjob.spec.runtimeID,
-        "tf_job_name": tfjob.metadata.name,
-    })
+def claim_selector(tfjob: v1alpha1.TFJob, typ: Optional[str] = None) -> Selector:
+    labels = {"kubeflow.caicloud.io": "true", "runtime_id": tfjob.spec.runtimeID,
+              "tf_job_name": tfjob.metadata.name}
+    if typ is not None:
+        labels["job_type"] = typ
+    return Selector.from_match_labels(labels)
+
+
+def _of_type(typ: str):
+    return lambda o: o.metadata.labels.get("job_type") == typ
 
 
 class Helper:
@@ -52,12 +62,12 @@ class Helper:
 
     def get_pods_for_tfjob(self, tfjob: v1alpha1.TFJob, typ: str) -> List[Pod]:
         pods = self.pod_lister.list(tfjob.metadata.namespace)
-        cm = PodControllerRefManager(self.pod_control, tfjob, claim_selector(tfjob, typ), v1alpha1.TFJOB_KIND,
+        cm = PodControllerRefManager(self.pod_control, tfjob, claim_selector(tfjob), v1alpha1.TFJOB_KIND,
                                      v1alpha1.API_VERSION, self._can_adopt(tfjob))
-        return cm.claim_pods(pods)
+        return [p for p in cm.claim_pods(pods) if _of_type(typ)(p)]
 
     def get_services_for_tfjob(self, tfjob: v1alpha1.TFJob, typ: str) -> List[Service]:
         svcs = self.service_lister.list(tfjob.metadata.namespace)
-        cm = ServiceControllerRefManager(self.service_control, tfjob, claim_selector(tfjob, typ),
+        cm = ServiceControllerRefManager(self.service_control, tfjob, claim_selector(tfjob),
                                          v1alpha1.TFJOB_KIND, v1alpha1.API_VERSION, self._can_adopt(tfjob))
-        return cm.claim_services(svcs)
+        return [s for s in cm.claim_services(svcs) if _of_type(typ)(s)]

@@ -292,7 +292,8 @@ class Supervisor:
             st.message = message
             st.hostIP = st.podIP = "127.0.0.1"
             st.startTime = st.startTime or now_rfc3339()
-            st.gpus = list(p.gpus) if p else []
+            if p and p.gpus:  # keep the last binding visible after the replica exits
+                st.gpus = list(p.gpus)
             cs = st.containerStatuses[0] if st.containerStatuses else ContainerStatus(
                 name=cur.spec.containers[0].name or "main")
             cs.restartCount = p.restarts if p else 0
@@ -368,6 +369,12 @@ class Supervisor:
                     else:
                         self._release(p)
                         self._procs.pop(key, None)
+                    continue
+                if p.state == "backoff" and now >= p.next_start and p.restarts and self._job_finished(pod):
+                    # a replica that exited cleanly while its job was finishing is not restarted
+                    p.state = "done"
+                    self._release(p)
+                    self._set_status(pod, POD_SUCCEEDED, exit_code=0, reason="Completed")
                     continue
                 if p.state == "starting" or (p.state == "backoff" and now >= p.next_start):
                     self._start(p, pod)

@@ -137,7 +137,7 @@ class DistributedJob:
     def compose(self) -> None:
         """Stamp runtime ID (once) + labels on the Worker/PS templates (``distributed.go:210-219``)."""
         if not self.tfjob.spec.runtimeID:
-            self.tfjob.spec.runtimeID = generate_runtime_id()
+            self.tfjob.spec.runtimeID = generate_runtime_id(self.tfjob.metadata.uid)
         self.get_worker_spec().template.metadata.labels = self.get_labels(v1alpha1.WORKER)
         ps = self.get_ps_spec()
         if ps is not None:

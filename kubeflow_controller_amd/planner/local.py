@@ -54,7 +54,7 @@ class LocalJob:
 
     def compose(self) -> None:
         if not self.tfjob.spec.runtimeID:
-            self.tfjob.spec.runtimeID = generate_runtime_id()
+            self.tfjob.spec.runtimeID = generate_runtime_id(self.tfjob.metadata.uid)
         self.tfjob.spec.specs[0].template.metadata.labels = self.labels()
 
     def labels(self) -> Dict[str, str]:

@@ -220,6 +220,11 @@ class ObjectStore:
             key = (obj.kind, meta.namespace, meta.name)
             if key in self._objs:
                 raise errors.AlreadyExists(f'{obj.kind} "{meta.name}" already exists')
+            for ref in meta.ownerReferences:
+                # the GC would collect a dependent of a vanished owner at once; refuse it up front
+                # (closes the stale-cache race of a sync that outlives its TFJob's deletion)
+                if ref.controller and not any(o.metadata.uid == ref.uid for o in self._objs.values()):
+                    raise errors.NotFound(f'owner {ref.kind} "{ref.name}" (uid {ref.uid}) not found')
             meta.uid = str(uuid.uuid4())
             meta.creationTimestamp = now_rfc3339()
             meta.resourceVersion = self._next_rv()

@@ -1,0 +1,190 @@
+"""End-to-end on CPU: controller + kubelet spawn real replica processes.
+
+BASELINE config "examples/tfjob MNIST local TFJob, 1 worker + 0 PS on CPU (plumbing)"
+plus a small PS/worker job, restart policies, deletion cascade and the CLI.
+"""
+import os
+import signal
+import subprocess
+import sys
+import textwrap
+import time
+
+import pytest
+
+from kubeflow_controller_amd.api import serde, v1alpha1
+from kubeflow_controller_amd.cli.controller_main import Node
+from kubeflow_controller_amd.cli.kfctl import describe_tfjob, wait_for_phase
+from kubeflow_controller_amd.store import ObjectStore
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ENV = {"KUBEFLOW_HOSTPATH": os.path.join(ROOT, "examples", "workdir")}
+
+
+@pytest.fixture
+def node(tmp_path):
+    st = ObjectStore()
+    n = Node(st, kubelet=True, root_dir=str(tmp_path / "pods"), num_gpus=0, resync=30, kubelet_backoff=0.2,
+             extra_env={"OMP_NUM_THREADS": "1"}).start()
+    yield st, n, tmp_path / "pods"
+    n.shutdown()
+
+
+def _job(name, replicas_spec, restart="OnFailure", cmd=None):
+    specs = []
+    for typ, n, c in replicas_spec:
+        specs.append({"replicas": n, "tfReplicaType": typ, "template": {"spec": {
+            "containers": [{"name": "main", "command": c or cmd}],
+            **({"restartPolicy": restart} if restart and typ != "PS" else {})}}})
+    return v1alpha1.TFJob.from_json({"apiVersion": v1alpha1.API_VERSION, "kind": "TFJob",
+                                     "metadata": {"name": name}, "spec": {"tfReplicaSpec": specs}})
+
+
+def _logs(root, pod):
+    d = os.path.join(root, f"default_{pod.metadata.name}")
+    return "".join(open(os.path.join(d, f)).read() for f in os.listdir(d) if f.endswith(".log"))
+
+
+@pytest.mark.slow
+def test_local_mnist_tfjob_succeeds(node):
+    st, n, root = node
+    job = serde.load_file(os.path.join(ROOT, "examples", "tfjob", "local.yml"), env=ENV)[0]
+    st.create(job)
+    j = wait_for_phase(st, "default", "local-training-job", {"Succeeded", "Failed"}, 120)
+    assert j.status.phase == "Succeeded"
+    assert j.status.tfReplicaStatuses[0].type == "Local"
+    assert j.status.tfReplicaStatuses[0].tfReplicasStates == {"Succeeded": 1}
+    (p,) = st.list("Pod")
+    out = _logs(root, p)
+    assert "Test accuracy:" in out and "step: 0" in out
+    acc = float(out.split("Test accuracy:")[1].split()[0])
+    assert acc > 0.8
+    desc = describe_tfjob(st, "default", "local-training-job")
+    assert "Created pod: " + p.metadata.name in desc
+
+
+@pytest.mark.slow
+def test_dist_ps_worker_job_wiring_and_recycling(node):
+    st, n, root = node
+    job = serde.load_file(os.path.join(ROOT, "examples", "tfjob", "dist.yml"), env=ENV)[0]
+    job.spec.specs[0].replicas = 1
+    job.spec.specs[1].replicas = 2
+    st.create(job)
+    j = wait_for_phase(st, "default", "dist-training-job", {"Succeeded", "Failed"}, 180)
+    assert j.status.phase == "Succeeded"
+    deadline = time.time() + 30
+    while time.time() < deadline:  # PS replicas are recycled once the workers are done
+        j = st.get(v1alpha1.TFJOB_KIND, "default", "dist-training-job")
+        st_map = {s.type: s.tfReplicasStates for s in j.status.tfReplicaStatuses}
+        if st_map.get("PS") == {"Succeeded": 1}:
+            break
+        time.sleep(0.2)
+    assert st_map == {"Worker": {"Succeeded": 2}, "PS": {"Succeeded": 1}}, describe_tfjob(st, "default", "dist-training-job")
+    pods = st.list("Pod")
+    assert len(pods) == 3
+    svcs = st.list("Service")
+    assert len(svcs) == 3 and all(s.spec.ports[0].nodePort and s.spec.clusterIP == "127.0.0.1" for s in svcs)
+    w0 = next(p for p in pods if p.metadata.labels["job_type"] == "Worker" and p.metadata.labels["index"] == "0")
+    args = w0.spec.containers[0].args
+    assert args[0].startswith("--worker_hosts=dist-training-job-worker-0-") and args[2] == "--job_name=worker"
+    out = _logs(root, w0)
+    assert "training step" in out and "validation cross entropy" in out
+    assert "2 workers, 1 ps" in out
+
+
+def test_restart_policies(node):
+    st, n, root = node
+    flag = str(root) + "_flag"
+    script = textwrap.dedent(f"""
+        import os, sys
+        p = {flag!r}
+        if not os.path.exists(p):
+            open(p, "w").close(); sys.exit(3)
+        sys.exit(0)""")
+    st.create(_job("retry", [("Local", 1, [sys.executable, "-c", script])], restart="OnFailure"))
+    j = wait_for_phase(st, "default", "retry", {"Succeeded", "Failed"}, 60)
+    assert j.status.phase == "Succeeded"
+    (p,) = st.list("Pod")
+    assert p.status.containerStatuses[0].restartCount == 1
+    assert p.status.containerStatuses[0].lastTerminated.exitCode == 0
+    st.create(_job("never", [("Worker", 1, [sys.executable, "-c", "import sys; sys.exit(7)"])], restart="Never"))
+    j = wait_for_phase(st, "default", "never", {"Succeeded", "Failed"}, 60)
+    assert j.status.phase == "Failed"
+    fp = [p for p in st.list("Pod") if p.metadata.labels.get("tf_job_name") == "never"][0]
+    assert fp.status.phase == "Failed" and fp.status.containerStatuses[0].terminated.exitCode == 7
+
+
+def test_delete_tfjob_kills_replicas(node):
+    st, n, root = node
+    st.create(_job("sleeper", [("Worker", 2, [sys.executable, "-c", "import time; time.sleep(300)"])]))
+    deadline = time.time() + 30
+    while time.time() < deadline and len(n.supervisor.running()) < 2:
+        time.sleep(0.1)
+    pids = list(n.supervisor.running().values())
+    assert len(pids) == 2
+    st.delete(v1alpha1.TFJOB_KIND, "default", "sleeper")
+    deadline = time.time() + 20
+    while time.time() < deadline and any(os.path.exists(f"/proc/{p}") and
+                                         open(f"/proc/{p}/stat").read().split()[2] != "Z" for p in pids):
+        time.sleep(0.1)
+    left = st.list("Pod") + st.list("Service")
+    assert left == [], [(o.kind, o.metadata.name, o.metadata.resourceVersion, o.metadata.ownerReferences) for o in left]
+    for p in pids:
+        assert not os.path.exists(f"/proc/{p}") or open(f"/proc/{p}/stat").read().split()[2] == "Z"
+
+
+def test_gpu_binding_policy(tmp_path):
+    """Workers get one GPU each (HIP_VISIBLE_DEVICES), PS none; binding released on exit."""
+    st = ObjectStore()
+    n = Node(st, kubelet=True, root_dir=str(tmp_path), num_gpus=2, resync=30).start()
+    try:
+        cmd = [sys.executable, "-c", "import os; print('HIP=' + os.environ['HIP_VISIBLE_DEVICES'])"]
+        st.create(_job("g", [("PS", 1, cmd), ("Worker", 2, cmd)]))
+        wait_for_phase(st, "default", "g", {"Succeeded"}, 60)
+        pods = st.list("Pod")
+        w = sorted(p.status.gpus[0] for p in pods if p.metadata.labels["job_type"] == "Worker")
+        assert w == [0, 1]
+        assert [p.status.gpus for p in pods if p.metadata.labels["job_type"] == "PS"] == [[]]
+        for p in pods:
+            if p.metadata.labels["job_type"] == "Worker":
+                assert f"HIP={p.status.gpus[0]}" in _logs(str(tmp_path), p)
+    finally:
+        n.shutdown()
+
+
+@pytest.mark.slow
+def test_cli_standalone_controller_and_kfctl(tmp_path):
+    url_file = tmp_path / "url"
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1", KFA_NODE_GPUS="0", **ENV)
+    ctl = subprocess.Popen([sys.executable, os.path.join(ROOT, "bin", "kubeflow-controller"), "--standalone",
+                            "--url-file", str(url_file), "--root-dir", str(tmp_path / "pods"), "-v", "4"],
+                           env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    try:
+        deadline = time.time() + 60
+        while time.time() < deadline and not (url_file.exists() and url_file.read_text().strip()):
+            time.sleep(0.1)
+        url = url_file.read_text().strip()
+        kf = [sys.executable, os.path.join(ROOT, "bin", "kfctl"), "--master", url]
+        run = lambda *a: subprocess.run(kf + list(a), env=env, capture_output=True, text=True, timeout=120)
+        r = run("create", "-f", os.path.join(ROOT, "examples", "crd", "crd.yml"))
+        assert r.returncode == 0, r.stderr
+        r = run("create", "-f", os.path.join(ROOT, "examples", "tfjob", "local.yml"))
+        assert r.returncode == 0 and 'tfjob "local-training-job" created' in r.stdout, r.stderr
+        r = run("wait", "tfjob", "local-training-job", "--timeout", "120")
+        assert r.returncode == 0 and "Succeeded" in r.stdout, r.stdout + r.stderr
+        r = run("get", "tfjobs")
+        assert "local-training-job" in r.stdout and "Succeeded" in r.stdout
+        r = run("get", "pods", "-o", "wide")
+        assert "Succeeded" in r.stdout
+        r = run("describe", "tfjob", "local-training-job")
+        assert "SuccessfulCreate" in r.stdout and "Local: Succeeded=1" in r.stdout
+        r = run("get", "tfjob", "local-training-job", "-o", "json")
+        assert '"phase": "Succeeded"' in r.stdout
+        r = run("delete", "tfjob", "local-training-job")
+        assert r.returncode == 0
+    finally:
+        ctl.send_signal(signal.SIGTERM)
+        try:
+            ctl.wait(20)
+        except subprocess.TimeoutExpired:
+            ctl.kill()
