@@ -18,21 +18,29 @@ __device__ __forceinline__ void online_merge(float& m, float& s, float m2, float
 
 template <bool BF16>
 __global__ __launch_bounds__(256) void xent_kernel(const void* __restrict__ logits, const long* __restrict__ labels,
-                                                   float* __restrict__ row_loss, void* __restrict__ dlogits,
-                                                   int V, float gscale, float smoothing) {
+                                                   const float* __restrict__ bias, float* __restrict__ row_loss,
+                                                   void* __restrict__ dlogits, int V, float gscale, float smoothing) {
   const long row = blockIdx.x;
   const int t = threadIdx.x;
   const long lab = labels[row];
   const bf16_t* lb = reinterpret_cast<const bf16_t*>(logits) + row * V;
   const float* lf = reinterpret_cast<const float*>(logits) + row * V;
-  auto ld = [&](int i) -> float { return BF16 ? bf2f(lb[i]) : lf[i]; };
+  // optional per-column bias (e.g. the MLM decoder bias) is added on the fly
+  auto ld = [&](int i) -> float { return (BF16 ? bf2f(lb[i]) : lf[i]) + (bias ? bias[i] : 0.f); };
+  auto ldv = [&](int i, float f[8]) {
+    unpack8(*reinterpret_cast<const uint4*>(lb + i), f);
+    if (bias) {
+      const float4 b0 = *reinterpret_cast<const float4*>(bias + i), b1 = *reinterpret_cast<const float4*>(bias + i + 4);
+      f[0] += b0.x; f[1] += b0.y; f[2] += b0.z; f[3] += b0.w; f[4] += b1.x; f[5] += b1.y; f[6] += b1.z; f[7] += b1.w;
+    }
+  };
 
   float m = -INFINITY, s = 0.f, sum_z = 0.f;
   const bool vec = BF16 && (V % 8 == 0);
   if (vec) {
     for (int i = t * 8; i < V; i += 256 * 8) {
       float f[8];
-      unpack8(*reinterpret_cast<const uint4*>(lb + i), f);
+      ldv(i, f);
       float lm = f[0];
 #pragma unroll
       for (int j = 1; j < 8; j++) lm = fmaxf(lm, f[j]);
@@ -77,7 +85,7 @@ __global__ __launch_bounds__(256) void xent_kernel(const void* __restrict__ logi
   if (vec) {
     for (int i = t * 8; i < V; i += 256 * 8) {
       float f[8];
-      unpack8(*reinterpret_cast<const uint4*>(lb + i), f);
+      ldv(i, f);
 #pragma unroll
       for (int j = 0; j < 8; j++) {
         float p = __expf(f[j] - lse) - off;
@@ -126,15 +134,16 @@ __global__ __launch_bounds__(256) void argmax_kernel(const void* __restrict__ lo
 
 }  // namespace
 
-KFA_API int kfa_softmax_xent(const void* logits, int logits_bf16, const long* labels, float* row_loss,
-                             void* dlogits, long rows, int V, float gscale, float smoothing, hipStream_t s) {
+KFA_API int kfa_softmax_xent(const void* logits, int logits_bf16, const long* labels, const float* bias,
+                             float* row_loss, void* dlogits, long rows, int V, float gscale, float smoothing,
+                             hipStream_t s) {
   if (rows <= 0 || V <= 0) return -1;
   if (logits_bf16)
-    hipLaunchKernelGGL(xent_kernel<true>, dim3(rows), dim3(256), 0, s, logits, labels, row_loss, dlogits, V, gscale,
-                       smoothing);
+    hipLaunchKernelGGL(xent_kernel<true>, dim3(rows), dim3(256), 0, s, logits, labels, bias, row_loss, dlogits, V,
+                       gscale, smoothing);
   else
-    hipLaunchKernelGGL(xent_kernel<false>, dim3(rows), dim3(256), 0, s, logits, labels, row_loss, dlogits, V, gscale,
-                       smoothing);
+    hipLaunchKernelGGL(xent_kernel<false>, dim3(rows), dim3(256), 0, s, logits, labels, bias, row_loss, dlogits, V,
+                       gscale, smoothing);
   return kfa_status();
 }
 

@@ -1,0 +1,793 @@
+// Transformer building blocks for BERT / Wide&Deep (SURVEY §2.6 K1 epilogues,
+// K6 embedding, K10 LayerNorm, K11 attention softmax).
+//
+// Everything here is bandwidth-bound, so every kernel is one streaming pass
+// with 16-byte (8 x bf16) accesses, and the pieces an unfused graph would run
+// as separate elementwise kernels are folded in:
+//
+//  * LayerNorm fwd: y = LN(res + dropout(x + bias)) — the residual add, the
+//    bias of the producing GEMM and the hidden dropout ride along; the summed
+//    input is stored (bf16) for backward.
+//  * LayerNorm bwd: dx, the dropout-masked branch gradient, dgamma/dbeta and
+//    the producing GEMM's dbias in one pass (column sums via per-block partials
+//    + a deterministic finalize, no global atomics).
+//  * bias+activation fwd/bwd (GELU-erf / tanh / ReLU / identity) with fused
+//    dbias column sums.
+//  * QKV split (bias add + head split + 1/sqrt(d) scaling) and its inverse
+//    (head merge + dbias), context head merge/split.
+//  * masked, scaled softmax over attention scores with counter-hash dropout
+//    (mask recomputed in backward, never stored) and its backward.
+//  * multi-table embedding gather-sum and the sparse backward (fp32
+//    scatter-add into a self-cleaning scratch, then a fold into the bf16/fp32
+//    gradient that touches only the looked-up rows).
+//
+// Dropout RNG: keep(seed, i) = hash(seed, i) >= p * 2^32 — a stateless
+// counter hash (splitmix64 finaliser), so forward and backward regenerate the
+// same mask from (seed, element index).
+#include "common.h"
+
+namespace {
+
+constexpr int kRowsPerBlock = 4;  // one wave per row
+
+__device__ __forceinline__ uint32_t drop_hash(uint64_t seed, uint64_t i) {
+  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (i + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return (uint32_t)((z ^ (z >> 31)) >> 32);
+}
+
+__device__ __forceinline__ bool keep(uint64_t seed, uint64_t i, uint32_t thresh) {
+  return drop_hash(seed, i) >= thresh;
+}
+
+__device__ __forceinline__ void load8(const bf16_t* p, float f[8]) { unpack8(*reinterpret_cast<const uint4*>(p), f); }
+__device__ __forceinline__ void store8(bf16_t* p, const float f[8]) { *reinterpret_cast<uint4*>(p) = pack8(f); }
+__device__ __forceinline__ void load8f(const float* p, float f[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+
+// ----------------------------------------------------------------------------- LayerNorm
+template <int NV>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
+                                                     const float* __restrict__ bias, const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta, bf16_t* __restrict__ y,
+                                                     bf16_t* __restrict__ xsum, float* __restrict__ mean_out,
+                                                     float* __restrict__ rstd_out, long rows, int H, float eps,
+                                                     uint32_t thresh, float dscale, uint64_t seed) {
+  const long row = (long)blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const long base = row * (long)H;
+  float v[NV][8];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < NV; j++) {
+    const int c = (j * 64 + lane) * 8;
+    if (c < H) {
+      load8(x + base + c, v[j]);
+      if (bias) {
+        float b[8];
+        load8f(bias + c, b);
+#pragma unroll
+        for (int e = 0; e < 8; e++) v[j][e] += b[e];
+      }
+      if (thresh) {
+#pragma unroll
+        for (int e = 0; e < 8; e++) v[j][e] = keep(seed, base + c + e, thresh) ? v[j][e] * dscale : 0.f;
+      }
+      if (res) {
+        float r[8];
+        load8(res + base + c, r);
+#pragma unroll
+        for (int e = 0; e < 8; e++) v[j][e] += r[e];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; e++) s += v[j][e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; e++) v[j][e] = 0.f;
+    }
+  }
+  const float mean = wave_sum(s) / (float)H;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < NV; j++) {
+    const int c = (j * 64 + lane) * 8;
+    if (c < H) {
+#pragma unroll
+      for (int e = 0; e < 8; e++) { const float d = v[j][e] - mean; q += d * d; }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(q) / (float)H + eps);
+#pragma unroll
+  for (int j = 0; j < NV; j++) {
+    const int c = (j * 64 + lane) * 8;
+    if (c < H) {
+      if (xsum) store8(xsum + base + c, v[j]);
+      float g[8], b[8], o[8];
+      load8f(gamma + c, g);
+      load8f(beta + c, b);
+#pragma unroll
+      for (int e = 0; e < 8; e++) o[e] = (v[j][e] - mean) * rstd * g[e] + b[e];
+      store8(y + base + c, o);
+    }
+  }
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+// Backward. Each block walks a contiguous chunk of rows, one wave per row;
+// per-lane column accumulators are reduced across the 4 waves through LDS and
+// written as one partial row per block: part[blk][0:H]=dgamma, [H:2H]=dbeta,
+// [2H:3H]=dbias (sum of the branch gradient).
+template <int NV>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ xs,
+                                                     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
+                                                     const float* __restrict__ gamma, bf16_t* __restrict__ dx,
+                                                     bf16_t* __restrict__ dbranch, float* __restrict__ part, long rows,
+                                                     int H, long rows_per_block, uint32_t thresh, float dscale,
+                                                     uint64_t seed) {
+  extern __shared__ float red[];  // [4][H]
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long r0 = (long)blockIdx.x * rows_per_block;
+  const long r1 = min(rows, r0 + rows_per_block);
+  float ag[NV][8], ab[NV][8], ad[NV][8];
+#pragma unroll
+  for (int j = 0; j < NV; j++)
+#pragma unroll
+    for (int e = 0; e < 8; e++) ag[j][e] = ab[j][e] = ad[j][e] = 0.f;
+
+  for (long row = r0 + w; row < r1; row += kRowsPerBlock) {
+    const long base = row * (long)H;
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float xh[NV][8], g[NV][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < NV; j++) {
+      const int c = (j * 64 + lane) * 8;
+      if (c < H) {
+        float d[8], xv[8], gm[8];
+        load8(dy + base + c, d);
+        load8(xs + base + c, xv);
+        load8f(gamma + c, gm);
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+          xh[j][e] = (xv[e] - mean) * rstd;
+          g[j][e] = d[e] * gm[e];
+          ag[j][e] += d[e] * xh[j][e];
+          ab[j][e] += d[e];
+          s1 += g[j][e] * xh[j][e];
+          s2 += g[j][e];
+        }
+      }
+    }
+    const float c1 = wave_sum(s1) / (float)H, c2 = wave_sum(s2) / (float)H;
+#pragma unroll
+    for (int j = 0; j < NV; j++) {
+      const int c = (j * 64 + lane) * 8;
+      if (c < H) {
+        float o[8];
+#pragma unroll
+        for (int e = 0; e < 8; e++) o[e] = rstd * (g[j][e] - c2 - xh[j][e] * c1);
+        store8(dx + base + c, o);
+        if (thresh) {
+#pragma unroll
+          for (int e = 0; e < 8; e++) o[e] = keep(seed, base + c + e, thresh) ? o[e] * dscale : 0.f;
+          if (dbranch) store8(dbranch + base + c, o);
+        }
+#pragma unroll
+        for (int e = 0; e < 8; e++) ad[j][e] += o[e];
+      }
+    }
+  }
+  // block-reduce the three column accumulators
+  auto reduce_out = [&](float (&acc)[NV][8], int a) {
+#pragma unroll
+    for (int j = 0; j < NV; j++) {
+      const int c = (j * 64 + lane) * 8;
+      if (c < H)
+#pragma unroll
+        for (int e = 0; e < 8; e++) red[w * H + c + e] = acc[j][e];
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < H; c += 256)
+      part[(long)blockIdx.x * 3 * H + (long)a * H + c] = red[c] + red[H + c] + red[2 * H + c] + red[3 * H + c];
+    __syncthreads();
+  };
+  reduce_out(ag, 0);
+  reduce_out(ab, 1);
+  reduce_out(ad, 2);
+}
+
+// out[c] (+)= sum_b part[b * stride + c]   (deterministic column finalize)
+// block = 64 columns x 4 row-lanes; 8 independent loads in flight per lane.
+__global__ __launch_bounds__(256) void colsum_finalize_kernel(const float* __restrict__ part, int nblk, long stride,
+                                                              int N, float* __restrict__ out, int accumulate) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  float s = 0.f;
+  if (c < N) {
+    int b = rl;
+    for (; b + 28 < nblk; b += 32) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) v[u] = part[(long)(b + 4 * u) * stride + c];
+#pragma unroll
+      for (int u = 0; u < 8; u++) s += v[u];
+    }
+    for (; b < nblk; b += 4) s += part[(long)b * stride + c];
+  }
+  red[rl][cl] = s;
+  __syncthreads();
+  if (rl == 0 && c < N) {
+    const float t = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+    out[c] = accumulate ? out[c] + t : t;
+  }
+}
+
+// ----------------------------------------------------------------------------- bias + activation
+enum Act { kNone = 0, kGelu = 1, kTanh = 2, kRelu = 3 };
+
+__device__ __forceinline__ float act_f(float z, int act) {
+  switch (act) {
+    case kGelu: return 0.5f * z * (1.f + erff(z * 0.70710678118654752f));
+    case kTanh: return tanhf(z);
+    case kRelu: return fmaxf(z, 0.f);
+    default: return z;
+  }
+}
+
+__device__ __forceinline__ float act_grad(float z, int act) {
+  switch (act) {
+    case kGelu: {
+      const float cdf = 0.5f * (1.f + erff(z * 0.70710678118654752f));
+      const float pdf = 0.39894228040143268f * __expf(-0.5f * z * z);
+      return cdf + z * pdf;
+    }
+    case kTanh: { const float t = tanhf(z); return 1.f - t * t; }
+    case kRelu: return z > 0.f ? 1.f : 0.f;
+    default: return 1.f;
+  }
+}
+
+// y[r, c] = act(x[r, c] + b[c]); one thread per 8 columns, grid-stride rows.
+__global__ __launch_bounds__(256) void bias_act_fwd_kernel(const bf16_t* __restrict__ x, const float* __restrict__ b,
+                                                           bf16_t* __restrict__ y, long rows, int N, int act,
+                                                           uint32_t thresh, float dscale, uint64_t seed) {
+  const long nv = rows * (N / 8);
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < nv; i += (long)gridDim.x * 256) {
+    const long r = i / (N / 8);
+    const int c = (int)(i - r * (N / 8)) * 8;
+    float f[8];
+    load8(x + r * N + c, f);
+    if (b) {
+      float bb[8];
+      load8f(b + c, bb);
+#pragma unroll
+      for (int e = 0; e < 8; e++) f[e] += bb[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; e++) f[e] = act_f(f[e], act);
+    if (thresh)
+#pragma unroll
+      for (int e = 0; e < 8; e++) f[e] = keep(seed, r * N + c + e, thresh) ? f[e] * dscale : 0.f;
+    store8(y + r * N + c, f);
+  }
+}
+
+// dx = dy * act'(x + b), dbias partials.  Block = 64 column-lanes x 4 row-lanes
+// covering 512 columns; grid = (ceil(N/512), row chunks).
+__global__ __launch_bounds__(256) void bias_act_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                                                           const float* __restrict__ b, bf16_t* __restrict__ dx,
+                                                           float* __restrict__ part, long rows, int N, int act,
+                                                           long rows_per_block, uint32_t thresh, float dscale,
+                                                           uint64_t seed) {
+  __shared__ float red[4][512];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 512 + cl * 8;
+  const long r0 = (long)blockIdx.y * rows_per_block;
+  const long r1 = min(rows, r0 + rows_per_block);
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (c < N) {
+    float bb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (b) load8f(b + c, bb);
+    for (long r = r0 + rl; r < r1; r += 4) {
+      float d[8], z[8];
+      load8(dy + r * N + c, d);
+      if (thresh)
+#pragma unroll
+        for (int e = 0; e < 8; e++) d[e] = keep(seed, r * N + c + e, thresh) ? d[e] * dscale : 0.f;
+      if (act != kNone) {
+        load8(x + r * N + c, z);
+#pragma unroll
+        for (int e = 0; e < 8; e++) d[e] *= act_grad(z[e] + bb[e], act);
+      }
+      if (dx) store8(dx + r * N + c, d);
+#pragma unroll
+      for (int e = 0; e < 8; e++) acc[e] += d[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; e++) red[rl][cl * 8 + e] = acc[e];
+  __syncthreads();
+  for (int k = threadIdx.x; k < 512; k += 256) {
+    const int cc = blockIdx.x * 512 + k;
+    if (cc < N) part[(long)blockIdx.y * N + cc] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
+  }
+}
+
+// ----------------------------------------------------------------------------- attention layout
+// qkv [T, 3H] (+ bias) -> q, k, v  [B, h, S, d]; q scaled by `qscale`.
+__global__ __launch_bounds__(256) void qkv_split_kernel(const bf16_t* __restrict__ qkv, const float* __restrict__ bias,
+                                                        bf16_t* __restrict__ q, bf16_t* __restrict__ k,
+                                                        bf16_t* __restrict__ v, long T, int S, int heads, int d,
+                                                        float qscale) {
+  const int H = heads * d, W = 3 * H;
+  const long nv = T * (W / 8);
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < nv; i += (long)gridDim.x * 256) {
+    const long t = i / (W / 8);
+    const int c = (int)(i - t * (W / 8)) * 8;
+    const int which = c / H, cc = c - which * H, hh = cc / d, dd = cc - hh * d;
+    const long b = t / S, s = t - b * S;
+    float f[8];
+    load8(qkv + t * W + c, f);
+    if (bias) {
+      float bb[8];
+      load8f(bias + c, bb);
+#pragma unroll
+      for (int e = 0; e < 8; e++) f[e] += bb[e];
+    }
+    if (which == 0)
+#pragma unroll
+      for (int e = 0; e < 8; e++) f[e] *= qscale;
+    bf16_t* dst = which == 0 ? q : (which == 1 ? k : v);
+    store8(dst + ((b * heads + hh) * S + s) * d + dd, f);
+  }
+}
+
+// inverse: dq, dk, dv [B,h,S,d] -> dqkv [T, 3H] (dq scaled by qscale) + dbias partials
+__global__ __launch_bounds__(256) void qkv_merge_bwd_kernel(const bf16_t* __restrict__ dq, const bf16_t* __restrict__ dk,
+                                                            const bf16_t* __restrict__ dv, bf16_t* __restrict__ dqkv,
+                                                            float* __restrict__ part, long T, int S, int heads, int d,
+                                                            float qscale, long rows_per_block) {
+  __shared__ float red[4][512];
+  const int H = heads * d, W = 3 * H;
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 512 + cl * 8;
+  const long r0 = (long)blockIdx.y * rows_per_block;
+  const long r1 = min(T, r0 + rows_per_block);
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (c < W) {
+    const int which = c / H, cc = c - which * H, hh = cc / d, dd = cc - hh * d;
+    const bf16_t* src = which == 0 ? dq : (which == 1 ? dk : dv);
+    const float sc = which == 0 ? qscale : 1.f;
+    for (long t = r0 + rl; t < r1; t += 4) {
+      const long b = t / S, s = t - b * S;
+      float f[8];
+      load8(src + ((b * heads + hh) * S + s) * d + dd, f);
+#pragma unroll
+      for (int e = 0; e < 8; e++) { f[e] *= sc; acc[e] += f[e]; }
+      store8(dqkv + t * W + c, f);
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; e++) red[rl][cl * 8 + e] = acc[e];
+  __syncthreads();
+  if (part)
+    for (int k = threadIdx.x; k < 512; k += 256) {
+      const int cc = blockIdx.x * 512 + k;
+      if (cc < W) part[(long)blockIdx.y * W + cc] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
+    }
+}
+
+// [B,h,S,d] <-> [T, H]  (to_rows=1: heads -> rows)
+__global__ __launch_bounds__(256) void heads_permute_kernel(const bf16_t* __restrict__ src, bf16_t* __restrict__ dst,
+                                                            long T, int S, int heads, int d, int to_rows) {
+  const int H = heads * d;
+  const long nv = T * (H / 8);
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < nv; i += (long)gridDim.x * 256) {
+    const long t = i / (H / 8);
+    const int c = (int)(i - t * (H / 8)) * 8;
+    const int hh = c / d, dd = c - hh * d;
+    const long b = t / S, s = t - b * S;
+    const long hi = ((b * heads + hh) * S + s) * d + dd, ri = t * H + c;
+    *reinterpret_cast<uint4*>(dst + (to_rows ? ri : hi)) = *reinterpret_cast<const uint4*>(src + (to_rows ? hi : ri));
+  }
+}
+
+// ----------------------------------------------------------------------------- attention softmax
+// rows of S scores (bf16, q pre-scaled); key_bias [B, S] additive (nullable).
+// G = lanes per row (S/8 clamped to 64), 64/G rows per wave.
+template <int G, int NV>
+__global__ __launch_bounds__(256) void attn_softmax_fwd_kernel(bf16_t* __restrict__ sc, const float* __restrict__ key_bias,
+                                                               bf16_t* __restrict__ pdrop, long rows, int S, int heads,
+                                                               uint32_t thresh, float dscale, uint64_t seed) {
+  constexpr int RPW = 64 / G;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long row = ((long)blockIdx.x * 4 + w) * RPW + lane / G;
+  const int gl = lane % G;
+  const bool valid = row < rows;
+  const long b = valid ? row / ((long)heads * S) : 0;
+  float m = -INFINITY;
+  float f[NV][8];  // the row lives in registers: S == 8 * G * NV
+#pragma unroll
+  for (int j = 0; j < NV; j++) {
+    if (valid) {
+      const int c = (j * G + gl) * 8;
+      load8(sc + row * S + c, f[j]);
+      if (key_bias) {
+        float kb[8];
+        load8f(key_bias + b * S + c, kb);
+#pragma unroll
+        for (int e = 0; e < 8; e++) f[j][e] += kb[e];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; e++) m = fmaxf(m, f[j][e]);
+    }
+  }
+#pragma unroll
+  for (int o = G / 2; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < NV; j++)
+    if (valid)
+#pragma unroll
+      for (int e = 0; e < 8; e++) { f[j][e] = __expf(f[j][e] - m); s += f[j][e]; }
+#pragma unroll
+  for (int o = G / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  const float inv = 1.f / s;
+#pragma unroll
+  for (int j = 0; j < NV; j++) {
+    if (valid) {
+      const int c = (j * G + gl) * 8;
+#pragma unroll
+      for (int e = 0; e < 8; e++) f[j][e] *= inv;
+      store8(sc + row * S + c, f[j]);
+      if (pdrop) {
+#pragma unroll
+        for (int e = 0; e < 8; e++) f[j][e] = keep(seed, row * S + c + e, thresh) ? f[j][e] * dscale : 0.f;
+        store8(pdrop + row * S + c, f[j]);
+      }
+    }
+  }
+}
+
+// dS = P * (dP - sum(P * dP)),  dP = keep ? dPdrop * dscale : 0.  In place on dp.
+template <int G, int NV>
+__global__ __launch_bounds__(256) void attn_softmax_bwd_kernel(const bf16_t* __restrict__ p, bf16_t* __restrict__ dp,
+                                                               long rows, int S, uint32_t thresh, float dscale,
+                                                               uint64_t seed) {
+  constexpr int RPW = 64 / G;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long row = ((long)blockIdx.x * 4 + w) * RPW + lane / G;
+  const int gl = lane % G;
+  const bool valid = row < rows;
+  float pv[NV][8], dv[NV][8];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < NV; j++) {
+    if (valid) {
+      const int c = (j * G + gl) * 8;
+      load8(p + row * S + c, pv[j]);
+      load8(dp + row * S + c, dv[j]);
+#pragma unroll
+      for (int e = 0; e < 8; e++) {
+        if (thresh) dv[j][e] = keep(seed, row * S + c + e, thresh) ? dv[j][e] * dscale : 0.f;
+        s += pv[j][e] * dv[j][e];
+      }
+    }
+  }
+#pragma unroll
+  for (int o = G / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+#pragma unroll
+  for (int j = 0; j < NV; j++) {
+    if (valid) {
+      const int c = (j * G + gl) * 8;
+#pragma unroll
+      for (int e = 0; e < 8; e++) dv[j][e] = pv[j][e] * (dv[j][e] - s);
+      store8(dp + row * S + c, dv[j]);
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------- embeddings
+// out[r] = sum_k tab_k[ids_k[r]] (k < 3, nullable), tables bf16 or fp32 (D % 8 == 0)
+template <bool F32>
+__device__ __forceinline__ void load_row8(const void* tab, long row, int D, int c, float f[8]) {
+  if (F32) load8f(reinterpret_cast<const float*>(tab) + row * D + c, f);
+  else load8(reinterpret_cast<const bf16_t*>(tab) + row * D + c, f);
+}
+
+__global__ __launch_bounds__(256) void embed_fwd_kernel(const long* __restrict__ i0, const void* __restrict__ t0,
+                                                        const long* __restrict__ i1, const void* __restrict__ t1,
+                                                        const long* __restrict__ i2, const void* __restrict__ t2,
+                                                        int f32mask, bf16_t* __restrict__ out, long n, int D,
+                                                        long ostride) {
+  const long nv = n * (D / 8);
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < nv; i += (long)gridDim.x * 256) {
+    const long r = i / (D / 8);
+    const int c = (int)(i - r * (D / 8)) * 8;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, f[8];
+    const long* ids[3] = {i0, i1, i2};
+    const void* tabs[3] = {t0, t1, t2};
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      if (!tabs[k]) continue;
+      const long row = ids[k] ? ids[k][r] : r;
+      if (f32mask & (1 << k)) load_row8<true>(tabs[k], row, D, c, f);
+      else load_row8<false>(tabs[k], row, D, c, f);
+#pragma unroll
+      for (int e = 0; e < 8; e++) acc[e] += f[e];
+    }
+    store8(out + r * ostride + c, acc);
+  }
+}
+
+// scratch[ids[r]] += dout[r]  (fp32 atomics; scratch is kept all-zero between calls)
+__global__ __launch_bounds__(256) void embed_bwd_scatter_kernel(const long* __restrict__ ids,
+                                                                const bf16_t* __restrict__ dout, long dstride,
+                                                                float* __restrict__ scratch, long n, int D) {
+  const long nv = n * (D / 8);
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < nv; i += (long)gridDim.x * 256) {
+    const long r = i / (D / 8);
+    const int c = (int)(i - r * (D / 8)) * 8;
+    const long row = ids ? ids[r] : r;
+    float f[8];
+    load8(dout + r * dstride + c, f);
+#pragma unroll
+    for (int e = 0; e < 8; e++) atomicAdd(scratch + row * D + c + e, f[e]);
+  }
+}
+
+// grad[row] += exchange(scratch[row], 0) for every looked-up row; the atomic
+// exchange hands each element's sum to exactly one occurrence, the others see
+// 0 and skip the write, and the scratch is left zeroed for the next call.
+__global__ __launch_bounds__(256) void embed_bwd_fold_kernel(const long* __restrict__ ids, float* __restrict__ scratch,
+                                                             void* __restrict__ grad, int grad_f32, long n, int D,
+                                                             int accumulate) {
+  const long nv = n * (D / 8);
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < nv; i += (long)gridDim.x * 256) {
+    const long r = i / (D / 8);
+    const int c = (int)(i - r * (D / 8)) * 8;
+    const long row = ids ? ids[r] : r;
+    float v[8];
+    bool any = false;
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      v[e] = __hip_atomic_exchange(scratch + row * D + c + e, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      any |= v[e] != 0.f;
+    }
+    if (!any) continue;
+    if (grad_f32) {
+      float* g = reinterpret_cast<float*>(grad) + row * D + c;
+#pragma unroll
+      for (int e = 0; e < 8; e++)
+        if (v[e] != 0.f) g[e] = accumulate ? g[e] + v[e] : v[e];
+    } else {
+      bf16_t* g = reinterpret_cast<bf16_t*>(grad) + row * D + c;
+#pragma unroll
+      for (int e = 0; e < 8; e++)
+        if (v[e] != 0.f) g[e] = (bf16_t)f2bf(accumulate ? bf2f(g[e]) + v[e] : v[e]);
+    }
+  }
+}
+
+int grid_for(long nvec) {
+  long g = (nvec + 255) / 256;
+  return (int)(g < 1 ? 1 : (g > 8192 ? 8192 : g));
+}
+
+uint32_t drop_thresh(float p) {
+  if (p <= 0.f) return 0u;
+  const double t = (double)p * 4294967296.0;
+  return t >= 4294967295.0 ? 4294967295u : (uint32_t)t;
+}
+
+}  // namespace
+
+// ============================================================================= C ABI
+static long ln_bwd_blocks(long rows) { return rows < 2048 ? (rows + 3) / 4 : 512; }
+
+KFA_API long kfa_ln_part_floats(long rows, int H) {
+  long nblk = ln_bwd_blocks(rows);
+  return nblk * 3 * H;
+}
+
+namespace {
+template <int NV>
+void launch_ln_fwd(dim3 g, hipStream_t s, const void* x, const void* res, const float* bias, const float* gamma,
+                   const float* beta, void* y, void* xsum, float* mean, float* rstd, long rows, int H, float eps,
+                   uint32_t th, float ds, uint64_t seed) {
+  hipLaunchKernelGGL(ln_fwd_kernel<NV>, g, dim3(256), 0, s, (const bf16_t*)x, (const bf16_t*)res, bias, gamma, beta,
+                     (bf16_t*)y, (bf16_t*)xsum, mean, rstd, rows, H, eps, th, ds, seed);
+}
+template <int NV>
+void launch_ln_bwd(dim3 g, size_t lds, hipStream_t s, const void* dy, const void* xs, const float* mean,
+                   const float* rstd, const float* gamma, void* dx, void* dbranch, float* part, long rows, int H,
+                   long rpb, uint32_t th, float ds, uint64_t seed) {
+  hipLaunchKernelGGL(ln_bwd_kernel<NV>, g, dim3(256), lds, s, (const bf16_t*)dy, (const bf16_t*)xs, mean, rstd, gamma,
+                     (bf16_t*)dx, (bf16_t*)dbranch, part, rows, H, rpb, th, ds, seed);
+}
+template <int G, int NV>
+void launch_sm_fwd(hipStream_t s, void* scores, const float* key_bias, void* pdrop, long rows, int S, int heads,
+                   uint32_t th, float ds, uint64_t seed) {
+  const long rpb = 4 * (64 / G);
+  hipLaunchKernelGGL((attn_softmax_fwd_kernel<G, NV>), dim3((unsigned)((rows + rpb - 1) / rpb)), dim3(256), 0, s,
+                     (bf16_t*)scores, key_bias, th ? (bf16_t*)pdrop : nullptr, rows, S, heads, th, ds, seed);
+}
+template <int G, int NV>
+void launch_sm_bwd(hipStream_t s, const void* probs, void* dp, long rows, int S, uint32_t th, float ds,
+                   uint64_t seed) {
+  const long rpb = 4 * (64 / G);
+  hipLaunchKernelGGL((attn_softmax_bwd_kernel<G, NV>), dim3((unsigned)((rows + rpb - 1) / rpb)), dim3(256), 0, s,
+                     (const bf16_t*)probs, (bf16_t*)dp, rows, S, th, ds, seed);
+}
+}  // namespace
+
+KFA_API int kfa_ln_fwd(const void* x, const void* res, const float* bias, const float* gamma, const float* beta,
+                       void* y, void* xsum, float* mean, float* rstd, long rows, int H, float eps, float p,
+                       unsigned long long seed, hipStream_t s) {
+  if (rows <= 0 || H % 8 || H > 4096) return -1;
+  const uint32_t th = drop_thresh(p);
+  const float ds = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  dim3 g((unsigned)((rows + kRowsPerBlock - 1) / kRowsPerBlock));
+  if (H <= 512) launch_ln_fwd<1>(g, s, x, res, bias, gamma, beta, y, xsum, mean, rstd, rows, H, eps, th, ds, seed);
+  else if (H <= 1024) launch_ln_fwd<2>(g, s, x, res, bias, gamma, beta, y, xsum, mean, rstd, rows, H, eps, th, ds, seed);
+  else if (H <= 2048) launch_ln_fwd<4>(g, s, x, res, bias, gamma, beta, y, xsum, mean, rstd, rows, H, eps, th, ds, seed);
+  else launch_ln_fwd<8>(g, s, x, res, bias, gamma, beta, y, xsum, mean, rstd, rows, H, eps, th, ds, seed);
+  return kfa_status();
+}
+
+// dgamma/dbeta/dbias: fp32, (+)= when accumulate; any may be null.
+KFA_API int kfa_ln_bwd(const void* dy, const void* xs, const float* mean, const float* rstd, const float* gamma,
+                       void* dx, void* dbranch, float* part, float* dgamma, float* dbeta, float* dbias, long rows,
+                       int H, float p, unsigned long long seed, int accumulate, hipStream_t s) {
+  if (rows <= 0 || H % 8 || H > 4096) return -1;
+  const long nblk = ln_bwd_blocks(rows);
+  const long rpb = (rows + nblk - 1) / nblk;
+  const uint32_t th = drop_thresh(p);
+  const float ds = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const size_t lds = 4 * H * sizeof(float);
+  dim3 g((unsigned)nblk);
+  if (H <= 512) launch_ln_bwd<1>(g, lds, s, dy, xs, mean, rstd, gamma, dx, dbranch, part, rows, H, rpb, th, ds, seed);
+  else if (H <= 1024) launch_ln_bwd<2>(g, lds, s, dy, xs, mean, rstd, gamma, dx, dbranch, part, rows, H, rpb, th, ds, seed);
+  else if (H <= 2048) launch_ln_bwd<4>(g, lds, s, dy, xs, mean, rstd, gamma, dx, dbranch, part, rows, H, rpb, th, ds, seed);
+  else launch_ln_bwd<8>(g, lds, s, dy, xs, mean, rstd, gamma, dx, dbranch, part, rows, H, rpb, th, ds, seed);
+  float* outs[3] = {dgamma, dbeta, dbias};
+  for (int a = 0; a < 3; a++)
+    if (outs[a])
+      hipLaunchKernelGGL(colsum_finalize_kernel, dim3((H + 63) / 64), dim3(256), 0, s, part + (long)a * H,
+                         (int)nblk, 3L * H, H, outs[a], accumulate);
+  return kfa_status();
+}
+
+// y = dropout(act(x + b)); b nullable, p == 0 disables dropout
+KFA_API int kfa_bias_act_fwd(const void* x, const float* b, void* y, long rows, int N, int act, float p,
+                             unsigned long long seed, hipStream_t s) {
+  if (rows <= 0 || N % 8) return -1;
+  const uint32_t th = drop_thresh(p);
+  const float ds = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  hipLaunchKernelGGL(bias_act_fwd_kernel, dim3(grid_for(rows * (N / 8))), dim3(256), 0, s, (const bf16_t*)x, b,
+                     (bf16_t*)y, rows, N, act, th, ds, (uint64_t)seed);
+  return kfa_status();
+}
+
+// row chunks of the column-sum producers: ~16 rows per block-lane pass, capped
+static long colsum_chunks(long rows) { return rows < 1024 ? (rows + 15) / 16 : (rows < 8192 ? 64 : 256); }
+
+KFA_API long kfa_colsum_part_floats(long rows, int N) {
+  const long chunks = colsum_chunks(rows);
+  return chunks * (long)N;
+}
+
+// dx = dropout_mask(dy) * act'(x + b) (dx nullable: then only dbias is produced);
+// dbias (+)= column sums of dx.
+KFA_API int kfa_bias_act_bwd(const void* dy, const void* x, const float* b, void* dx, float* part, float* dbias,
+                             long rows, int N, int act, float p, unsigned long long seed, int accumulate,
+                             hipStream_t s) {
+  if (rows <= 0 || N % 8) return -1;
+  const long chunks = colsum_chunks(rows);
+  const long rpb = (rows + chunks - 1) / chunks;
+  const uint32_t th = drop_thresh(p);
+  const float ds = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  hipLaunchKernelGGL(bias_act_bwd_kernel, dim3((N + 511) / 512, (unsigned)chunks), dim3(256), 0, s,
+                     (const bf16_t*)dy, (const bf16_t*)x, b, (bf16_t*)dx, part, rows, N, act, rpb, th, ds,
+                     (uint64_t)seed);
+  if (dbias)
+    hipLaunchKernelGGL(colsum_finalize_kernel, dim3((N + 63) / 64), dim3(256), 0, s, part, (int)chunks, (long)N, N,
+                       dbias, accumulate);
+  return kfa_status();
+}
+
+KFA_API int kfa_qkv_split(const void* qkv, const float* bias, void* q, void* k, void* v, long T, int S, int heads,
+                          int d, float qscale, hipStream_t s) {
+  if (T <= 0 || T % S || d % 8) return -1;
+  hipLaunchKernelGGL(qkv_split_kernel, dim3(grid_for(T * 3 * heads * d / 8)), dim3(256), 0, s, (const bf16_t*)qkv,
+                     bias, (bf16_t*)q, (bf16_t*)k, (bf16_t*)v, T, S, heads, d, qscale);
+  return kfa_status();
+}
+
+KFA_API int kfa_qkv_merge_bwd(const void* dq, const void* dk, const void* dv, void* dqkv, float* part, float* dbias,
+                              long T, int S, int heads, int d, float qscale, int accumulate, hipStream_t s) {
+  if (T <= 0 || T % S || d % 8) return -1;
+  const int W = 3 * heads * d;
+  const long chunks = colsum_chunks(T);
+  const long rpb = (T + chunks - 1) / chunks;
+  hipLaunchKernelGGL(qkv_merge_bwd_kernel, dim3((W + 511) / 512, (unsigned)chunks), dim3(256), 0, s,
+                     (const bf16_t*)dq, (const bf16_t*)dk, (const bf16_t*)dv, (bf16_t*)dqkv, part, T, S, heads, d,
+                     qscale, rpb);
+  if (dbias)
+    hipLaunchKernelGGL(colsum_finalize_kernel, dim3((W + 63) / 64), dim3(256), 0, s, part, (int)chunks, (long)W, W,
+                       dbias, accumulate);
+  return kfa_status();
+}
+
+KFA_API int kfa_heads_permute(const void* src, void* dst, long T, int S, int heads, int d, int to_rows,
+                              hipStream_t s) {
+  if (T <= 0 || T % S || d % 8) return -1;
+  hipLaunchKernelGGL(heads_permute_kernel, dim3(grid_for(T * heads * d / 8)), dim3(256), 0, s, (const bf16_t*)src,
+                     (bf16_t*)dst, T, S, heads, d, to_rows);
+  return kfa_status();
+}
+
+static int sm_supported(int S) { return S == 64 || S == 128 || S == 256 || S == 512 || S == 1024 || S == 2048; }
+
+KFA_API int kfa_attn_softmax_fwd(void* scores, const float* key_bias, void* pdrop, long rows, int S, int heads,
+                                 float p, unsigned long long seed, hipStream_t s) {
+  if (rows <= 0 || !sm_supported(S)) return -1;
+  const uint32_t th = drop_thresh(p);
+  const float ds = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  switch (S) {
+    case 64: launch_sm_fwd<8, 1>(s, scores, key_bias, pdrop, rows, S, heads, th, ds, seed); break;
+    case 128: launch_sm_fwd<16, 1>(s, scores, key_bias, pdrop, rows, S, heads, th, ds, seed); break;
+    case 256: launch_sm_fwd<32, 1>(s, scores, key_bias, pdrop, rows, S, heads, th, ds, seed); break;
+    case 512: launch_sm_fwd<64, 1>(s, scores, key_bias, pdrop, rows, S, heads, th, ds, seed); break;
+    case 1024: launch_sm_fwd<64, 2>(s, scores, key_bias, pdrop, rows, S, heads, th, ds, seed); break;
+    default: launch_sm_fwd<64, 4>(s, scores, key_bias, pdrop, rows, S, heads, th, ds, seed); break;
+  }
+  return kfa_status();
+}
+
+KFA_API int kfa_attn_softmax_bwd(const void* probs, void* dp, long rows, int S, float p, unsigned long long seed,
+                                 hipStream_t s) {
+  if (rows <= 0 || !sm_supported(S)) return -1;
+  const uint32_t th = drop_thresh(p);
+  const float ds = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  switch (S) {
+    case 64: launch_sm_bwd<8, 1>(s, probs, dp, rows, S, th, ds, seed); break;
+    case 128: launch_sm_bwd<16, 1>(s, probs, dp, rows, S, th, ds, seed); break;
+    case 256: launch_sm_bwd<32, 1>(s, probs, dp, rows, S, th, ds, seed); break;
+    case 512: launch_sm_bwd<64, 1>(s, probs, dp, rows, S, th, ds, seed); break;
+    case 1024: launch_sm_bwd<64, 2>(s, probs, dp, rows, S, th, ds, seed); break;
+    default: launch_sm_bwd<64, 4>(s, probs, dp, rows, S, th, ds, seed); break;
+  }
+  return kfa_status();
+}
+
+KFA_API int kfa_embed_fwd(const long* i0, const void* t0, const long* i1, const void* t1, const long* i2,
+                          const void* t2, int f32mask, void* out, long n, int D, long ostride, hipStream_t s) {
+  if (n <= 0 || D % 8 || ostride % 8) return -1;
+  hipLaunchKernelGGL(embed_fwd_kernel, dim3(grid_for(n * (D / 8))), dim3(256), 0, s, i0, t0, i1, t1, i2, t2, f32mask,
+                     (bf16_t*)out, n, D, ostride);
+  return kfa_status();
+}
+
+// scratch: zero-initialised fp32 [rows_of_table, D], left zeroed on return.
+KFA_API int kfa_embed_bwd(const long* ids, const void* dout, long dstride, float* scratch, void* grad, int grad_f32,
+                          long n, int D, int accumulate, hipStream_t s) {
+  if (n <= 0 || D % 8 || dstride % 8) return -1;
+  const int g = grid_for(n * (D / 8));
+  hipLaunchKernelGGL(embed_bwd_scatter_kernel, dim3(g), dim3(256), 0, s, ids, (const bf16_t*)dout, dstride, scratch,
+                     n, D);
+  hipLaunchKernelGGL(embed_bwd_fold_kernel, dim3(g), dim3(256), 0, s, ids, scratch, grad, grad_f32, n, D, accumulate);
+  return kfa_status();
+}
+
+KFA_API int kfa_colsum(const void* x, float* part, float* out, long rows, int N, int accumulate, hipStream_t s) {
+  return kfa_bias_act_bwd(x, nullptr, nullptr, nullptr, part, out, rows, N, kNone, 0.f, 0ull, accumulate, s);
+}

@@ -166,15 +166,20 @@ class Controller:
         succeeded, _failed = get_status(worker_pods)
         active_ps = filter_active_pods(ps_pods)
 
-        if job_needs_sync and tfjob.metadata.deletionTimestamp is None:
-            self.manage_tfjob(active_worker, active_ps, worker_svcs, ps_svcs, succeeded, tfjob,
-                              succeeded_indices(worker_pods), succeeded_indices(ps_pods))
-
+        # Status first (reference order: controller.go:319-335 runs it after the
+        # planner): a job that just reached Succeeded/Failed — e.g. a worker failed
+        # under restartPolicy Never — must not get replacement replicas.
         if local:
             updater = LocalUpdater(tfjob, succeeded, worker_pods)
         else:
             updater = DistributedUpdater(tfjob, succeeded, worker_pods, ps_pods)
         status_changed = updater.should_update()
+        terminal = tfjob.status.phase in (v1alpha1.PHASE_SUCCEEDED, v1alpha1.PHASE_FAILED)
+
+        if job_needs_sync and tfjob.metadata.deletionTimestamp is None and not terminal:
+            self.manage_tfjob(active_worker, active_ps, worker_svcs, ps_svcs, succeeded, tfjob,
+                              succeeded_indices(worker_pods), succeeded_indices(ps_pods))
+
         spec_changed = to_json(tfjob.spec) != to_json(original.spec) or \
             to_json(tfjob.metadata) != to_json(original.metadata)
         if status_changed or spec_changed:

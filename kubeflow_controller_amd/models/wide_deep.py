@@ -1,0 +1,117 @@
+"""Wide & Deep recommender — BASELINE.json config "Wide&Deep recommender
+(embedding-heavy PS), 8 workers + 4 PS co-located on 8×MI355X"
+(SURVEY §2.4 parameter sharding, §2.6 K1/K6, §7.3 H6).
+
+* 26 categorical features, Criteo-like cardinalities (22.9 M rows in total),
+  one :class:`~kubeflow_controller_amd.parallel.embedding.ShardedEmbedding`
+  holding every table back to back (global row = table offset + id), rows
+  interleaved over the PS-owner ranks, owner-side sparse Adam.
+* Each row is ``embed_dim + 8`` wide: ``embed_dim`` deep features, then the
+  wide (linear) weight of that category value in column ``embed_dim`` (the
+  remaining 7 columns pad the row to a 16-byte multiple for the HIP gather).
+* Deep tower: [13 dense (padded to 16) ‖ 26×embed_dim] → 1024 → 512 → 256 → 1,
+  ReLU, GEMM + fused bias/ReLU epilogue kernels; wide part = Σ wide weights +
+  linear over the dense features.  Loss: sigmoid cross-entropy.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Optional, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops import transformer as T
+from ..parallel.embedding import ShardedEmbedding
+
+CRITEO_LIKE = (4_000_000,) * 4 + (1_000_000,) * 6 + (100_000,) * 8 + (10_000,) * 8
+
+
+@dataclass
+class WideDeepConfig:
+    num_dense: int = 13
+    cardinalities: Tuple[int, ...] = CRITEO_LIKE
+    embed_dim: int = 64
+    mlp: Tuple[int, ...] = (1024, 512, 256)
+    embed_lr: float = 1e-3
+    owners: Optional[int] = None       # PS-owner ranks for the tables (None = every rank)
+
+    @classmethod
+    def tiny(cls) -> "WideDeepConfig":
+        return cls(cardinalities=(1000,) * 4 + (100,) * 4, embed_dim=16, mlp=(64, 32))
+
+    @property
+    def row_width(self) -> int:
+        return self.embed_dim + 8
+
+    @property
+    def dense_pad(self) -> int:
+        return (self.num_dense + 7) // 8 * 8
+
+
+class WideDeep(nn.Module):
+    def __init__(self, cfg: WideDeepConfig, device=None):
+        super().__init__()
+        self.cfg = cfg
+        nf = len(cfg.cardinalities)
+        offs = [0]
+        for c in cfg.cardinalities[:-1]:
+            offs.append(offs[-1] + c)
+        self.register_buffer("offsets", torch.tensor(offs, dtype=torch.int64), persistent=False)
+        if device is None and torch.cuda.is_available():
+            device = torch.device("cuda", torch.cuda.current_device())
+        # the tables are created on their final device (22.9 M x 72 fp32 + Adam moments)
+        self.tables = ShardedEmbedding(sum(cfg.cardinalities), cfg.row_width, owners=cfg.owners,
+                                       lr=cfg.embed_lr, init_std=0.01, device=device)
+        dims = [cfg.dense_pad + nf * cfg.embed_dim, *cfg.mlp]
+        self.weights = nn.ParameterList()
+        self.biases = nn.ParameterList()
+        for a, b in zip(dims[:-1], dims[1:]):
+            w = nn.Parameter(torch.empty(b, a))
+            nn.init.kaiming_uniform_(w, nonlinearity="relu")
+            self.weights.append(w)
+            self.biases.append(nn.Parameter(torch.zeros(b)))
+        self.out_w = nn.Parameter(torch.empty(1, dims[-1]))
+        nn.init.normal_(self.out_w, 0.0, dims[-1] ** -0.5)
+        self.out_b = nn.Parameter(torch.zeros(1))
+        self.wide_dense = nn.Parameter(torch.zeros(1, cfg.dense_pad))
+
+    def forward(self, dense: torch.Tensor, ids: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+        cfg = self.cfg
+        B, nf = ids.shape
+        gids = (ids + self.offsets.view(1, nf)).reshape(-1)
+        rows = self.tables(gids).view(B, nf, cfg.row_width)               # bf16 [B, nf, E+8]
+        deep_emb = rows[:, :, :cfg.embed_dim].reshape(B, nf * cfg.embed_dim)
+        wide = rows[:, :, cfg.embed_dim].float().sum(1)
+        cdt = self.weights[0].dtype
+        dpad = F.pad(dense, (0, cfg.dense_pad - cfg.num_dense))
+        x = torch.cat([dpad.to(rows.dtype), deep_emb], 1)
+        if x.is_cuda:
+            x = x.to(cdt)
+            for w, b in zip(self.weights, self.biases):
+                x = T.dense(x, w, b, "relu")
+        else:
+            x = x.float()
+            for w, b in zip(self.weights, self.biases):
+                x = torch.relu(x @ w.float().t() + b.float())
+        deep = (x @ self.out_w.to(x.dtype).t()).float().squeeze(1) + self.out_b.float()
+        wide = wide + (dpad.float() @ self.wide_dense.float().t()).squeeze(1)
+        return F.binary_cross_entropy_with_logits(deep + wide, labels.float())
+
+
+def wide_deep_loss(model, *batch):
+    return model(*batch)
+
+
+def synthetic_batch(cfg: WideDeepConfig, batch: int, generator=None, device="cpu"):
+    """Log-normal dense features, power-law (Zipf-ish) categorical ids, 0/1 labels."""
+    g = generator
+    dense = torch.log1p(torch.rand(batch, cfg.num_dense, generator=g) * 100.0)
+    cols = []
+    for c in cfg.cardinalities:
+        u = torch.rand(batch, generator=g)
+        cols.append(torch.clamp((c ** u).long() - 1, 0, c - 1))      # heavy head, long tail
+    ids = torch.stack(cols, 1)
+    labels = torch.randint(0, 2, (batch,), generator=g)
+    return dense.to(device), ids.to(device), labels.to(device)

@@ -11,7 +11,8 @@ import torch
 
 from . import _lib
 
-_lib.register("kfa_softmax_xent", [_lib.P, _lib.I, _lib.P, _lib.P, _lib.P, _lib.L, _lib.I, _lib.F, _lib.F, _lib.P])
+_lib.register("kfa_softmax_xent", [_lib.P, _lib.I, _lib.P, _lib.P, _lib.P, _lib.P, _lib.L, _lib.I, _lib.F, _lib.F,
+                                    _lib.P])
 _lib.register("kfa_argmax", [_lib.P, _lib.I, _lib.P, _lib.L, _lib.I, _lib.P])
 
 
@@ -26,7 +27,7 @@ class _XentFn(torch.autograd.Function):
         row_loss = torch.empty(rows, dtype=torch.float32, device=z.device)
         dz = torch.empty_like(z) if logits.requires_grad else None
         valid = max(int(rows), 1)
-        _lib.call("kfa_softmax_xent", _lib.ptr(z), int(z.dtype == torch.bfloat16), _lib.ptr(lab), _lib.ptr(row_loss),
+        _lib.call("kfa_softmax_xent", _lib.ptr(z), int(z.dtype == torch.bfloat16), _lib.ptr(lab), None, _lib.ptr(row_loss),
                   _lib.ptr(dz), rows, V, 1.0 / valid, float(smoothing), _lib.stream())
         ctx.save_for_backward(dz)
         return row_loss.sum() / valid

@@ -1,0 +1,455 @@
+"""Transformer / recommender ops over the HIP kernels of ``csrc/kernels/transformer.hip``.
+
+SURVEY §2.6 K1 (GEMM epilogues), K6 (embedding), K10 (LayerNorm), K11
+(attention).  GEMMs are plain library GEMMs (``torch.mm``/``addmm``/``bmm`` →
+hipBLASLt); everything around them is a hand-written kernel that fuses the
+elementwise work (bias, activation, dropout, residual add, LayerNorm, head
+split/merge, column-sum bias gradients) into one streaming pass.
+
+The encoder layer is ONE autograd node (:class:`EncoderLayerFn`): backward is
+written out explicitly so that
+
+* weight gradients are accumulated straight into the flat gradient buffer
+  (``gW.addmm_(dY.T, X)`` = hipBLASLt with beta=1) and bias / LayerNorm
+  gradients are produced by the fused kernels into their flat views — the
+  direct-gradient protocol of ``parallel/flat.py`` (no AccumulateGrad adds);
+* the residual-gradient sums are folded into the dgrad GEMMs
+  (``addmm(dres, dY, W)``), so no separate add kernel runs;
+* dropout masks are regenerated from (seed, index) — never stored.
+
+Every op has a plain-PyTorch fp32 reference (``*_reference``) used by the CPU
+path and the numerics tests.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+from . import loss as _loss  # noqa: F401  (registers kfa_softmax_xent)
+from ..parallel.flat import direct_grad_view, notify_grad_ready
+
+P, L, I, Fl = _lib.P, _lib.L, _lib.I, _lib.F
+U64 = __import__("ctypes").c_ulonglong
+
+_lib.register("kfa_ln_part_floats", [L, I], L)
+_lib.register("kfa_colsum_part_floats", [L, I], L)
+_lib.register("kfa_ln_fwd", [P, P, P, P, P, P, P, P, P, L, I, Fl, Fl, U64, P])
+_lib.register("kfa_ln_bwd", [P, P, P, P, P, P, P, P, P, P, P, L, I, Fl, U64, I, P])
+_lib.register("kfa_bias_act_fwd", [P, P, P, L, I, I, Fl, U64, P])
+_lib.register("kfa_bias_act_bwd", [P, P, P, P, P, P, L, I, I, Fl, U64, I, P])
+_lib.register("kfa_qkv_split", [P, P, P, P, P, L, I, I, I, Fl, P])
+_lib.register("kfa_qkv_merge_bwd", [P, P, P, P, P, P, L, I, I, I, Fl, I, P])
+_lib.register("kfa_heads_permute", [P, P, L, I, I, I, I, P])
+_lib.register("kfa_attn_softmax_fwd", [P, P, P, L, I, I, Fl, U64, P])
+_lib.register("kfa_attn_softmax_bwd", [P, P, L, I, Fl, U64, P])
+_lib.register("kfa_embed_fwd", [P, P, P, P, P, P, I, P, L, I, L, P])
+_lib.register("kfa_embed_bwd", [P, P, L, P, P, I, L, I, I, P])
+_lib.register("kfa_colsum", [P, P, P, L, I, I, P])
+
+ACTS = {None: 0, "none": 0, "gelu": 1, "tanh": 2, "relu": 3}
+SMALL_TABLE_ROWS = 1024
+_MASK64 = (1 << 64) - 1
+
+
+def mix_seed(*parts: int) -> int:
+    """Deterministic 64-bit seed from integers (per layer / site / step)."""
+    h = 0x243F6A8885A308D3
+    for p in parts:
+        h ^= (int(p) + 0x9E3779B97F4A7C15 + (h << 6) + (h >> 2)) & _MASK64
+        h = (h * 0xBF58476D1CE4E5B9) & _MASK64
+    return h
+
+
+def _part(nfloats: int, device) -> torch.Tensor:
+    return _lib.workspace(nfloats * 4, device, "colsum_part").view(torch.float32)
+
+
+def _grad_target(p: torch.Tensor):
+    """(buffer, accumulate, direct): the flat fp32/bf16 grad view when the param
+    lives in a FlatGroup, else a fresh fp32 tensor returned through autograd."""
+    v = direct_grad_view(p)
+    if v is not None:
+        return v, 1, True
+    return torch.zeros(p.shape, dtype=torch.float32, device=p.device), 1, False
+
+
+def _finish(p, buf, direct):
+    if direct:
+        notify_grad_ready(p)
+        return None
+    return buf.to(p.dtype)
+
+
+# ----------------------------------------------------------------------------- raw launchers
+def ln_fwd(x, gamma, beta, res=None, bias=None, eps=1e-12, p=0.0, seed=0, save_sum=True):
+    rows, H = x.numel() // x.shape[-1], x.shape[-1]
+    y = torch.empty_like(x)
+    xs = torch.empty_like(x) if save_sum and (res is not None or bias is not None or p > 0) else None
+    mean = torch.empty(rows, dtype=torch.float32, device=x.device)
+    rstd = torch.empty_like(mean)
+    _lib.call("kfa_ln_fwd", _lib.ptr(x), _lib.ptr(res), _lib.ptr(bias), _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(y),
+              _lib.ptr(xs), _lib.ptr(mean), _lib.ptr(rstd), rows, H, eps, float(p), seed, _lib.stream())
+    return y, (xs if xs is not None else x), mean, rstd
+
+
+def ln_bwd(dy, xs, mean, rstd, gamma, dgamma, dbeta, dbias=None, p=0.0, seed=0, want_branch=False):
+    rows, H = dy.numel() // dy.shape[-1], dy.shape[-1]
+    dx = torch.empty_like(dy)
+    dbr = torch.empty_like(dy) if (want_branch and p > 0) else None
+    part = _part(_lib.lib().kfa_ln_part_floats(rows, H), dy.device)
+    _lib.call("kfa_ln_bwd", _lib.ptr(dy), _lib.ptr(xs), _lib.ptr(mean), _lib.ptr(rstd), _lib.ptr(gamma), _lib.ptr(dx),
+              _lib.ptr(dbr), _lib.ptr(part), _lib.ptr(dgamma), _lib.ptr(dbeta), _lib.ptr(dbias), rows, H, float(p), seed,
+              1, _lib.stream())
+    return dx, (dbr if dbr is not None else dx)
+
+
+def bias_act_fwd(x, bias, act, p=0.0, seed=0):
+    rows, N = x.numel() // x.shape[-1], x.shape[-1]
+    y = torch.empty_like(x)
+    _lib.call("kfa_bias_act_fwd", _lib.ptr(x), _lib.ptr(bias), _lib.ptr(y), rows, N, ACTS[act], float(p), seed,
+              _lib.stream())
+    return y
+
+
+def bias_act_bwd(dy, x, bias, act, dbias, p=0.0, seed=0, want_dx=True):
+    rows, N = dy.numel() // dy.shape[-1], dy.shape[-1]
+    dx = torch.empty_like(dy) if want_dx else None
+    part = _part(_lib.lib().kfa_colsum_part_floats(rows, N), dy.device)
+    _lib.call("kfa_bias_act_bwd", _lib.ptr(dy), _lib.ptr(x), _lib.ptr(bias), _lib.ptr(dx), _lib.ptr(part),
+              _lib.ptr(dbias), rows, N, ACTS[act], float(p), seed, 1, _lib.stream())
+    return dx
+
+
+def colsum_(x, out):
+    """out (+)= x.sum(0) over rows (fp32 out)."""
+    rows, N = x.numel() // x.shape[-1], x.shape[-1]
+    part = _part(_lib.lib().kfa_colsum_part_floats(rows, N), x.device)
+    _lib.call("kfa_colsum", _lib.ptr(x), _lib.ptr(part), _lib.ptr(out), rows, N, 1, _lib.stream())
+
+
+def _wgrad_(gw: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor) -> None:
+    """gW += dY^T · X (hipBLASLt, beta = 1) straight into the flat grad view."""
+    if gw.dtype == dy2.dtype:
+        gw.addmm_(dy2.t(), x2)
+    else:
+        gw.add_(torch.mm(dy2.t(), x2).to(gw.dtype))
+
+
+# ----------------------------------------------------------------------------- LayerNorm
+class LayerNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, eps):
+        x = x.contiguous()
+        y, xs, mean, rstd = ln_fwd(x, gamma, beta, eps=eps)
+        ctx.save_for_backward(xs, mean, rstd, gamma)
+        ctx.params = (gamma, beta)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xs, mean, rstd, gamma = ctx.saved_tensors
+        g, b = ctx.params
+        gg, _, dg = _grad_target(g)
+        gb, _, db = _grad_target(b)
+        dx, _ = ln_bwd(dy.contiguous(), xs, mean, rstd, gamma, gg, gb)
+        return dx, _finish(g, gg, dg), _finish(b, gb, db), None
+
+
+def layer_norm(x, gamma, beta, eps=1e-12):
+    if not x.is_cuda:
+        return F.layer_norm(x, (x.shape[-1],), gamma.to(x.dtype), beta.to(x.dtype), eps)
+    return LayerNormFn.apply(x, gamma, beta, eps)
+
+
+# ----------------------------------------------------------------------------- dense + bias + act
+class DenseFn(torch.autograd.Function):
+    """y = dropout(act(x · Wᵀ + b)) — GEMM then one fused epilogue pass."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, act, p, seed):
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1])
+        z = torch.mm(x2, weight.t())
+        y = bias_act_fwd(z, bias, act, p, seed) if (bias is not None or act not in (None, "none") or p > 0) else z
+        ctx.save_for_backward(x2, weight, z if act not in (None, "none") else None)
+        ctx.bias = bias
+        ctx.cfg = (act, p, seed, shp)
+        return y.view(*shp[:-1], weight.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, weight, z = ctx.saved_tensors
+        bias = ctx.bias
+        act, p, seed, shp = ctx.cfg
+        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        gb = db = None
+        if bias is not None:
+            gb, _, db = _grad_target(bias)
+        if act not in (None, "none") or p > 0 or bias is not None:
+            dz = bias_act_bwd(dy2, z, bias, act, gb, p, seed, want_dx=(act not in (None, "none") or p > 0))
+            dz = dy2 if dz is None else dz
+        else:
+            dz = dy2
+        dx = torch.mm(dz, weight).view(shp) if ctx.needs_input_grad[0] else None
+        gw, _, dw = _grad_target(weight)
+        _wgrad_(gw, dz, x2)
+        return dx, _finish(weight, gw, dw), (_finish(bias, gb, db) if bias is not None else None), None, None, None
+
+
+def dense(x, weight, bias=None, act=None, p=0.0, seed=0):
+    if not x.is_cuda:
+        return dense_reference(x, weight, bias, act)
+    return DenseFn.apply(x, weight, bias, act, float(p), int(seed))
+
+
+def _act_ref(z, act):
+    if act == "gelu":
+        return F.gelu(z)
+    if act == "tanh":
+        return torch.tanh(z)
+    if act == "relu":
+        return torch.relu(z)
+    return z
+
+
+def dense_reference(x, weight, bias=None, act=None):
+    z = x @ weight.to(x.dtype).t()
+    if bias is not None:
+        z = z + bias.to(z.dtype)
+    return _act_ref(z, act)
+
+
+# ----------------------------------------------------------------------------- embeddings
+class EmbeddingSumFn(torch.autograd.Function):
+    """out[r] = Σ_k table_k[ids_k[r]] (≤ 3 tables); sparse backward through a
+    self-cleaning fp32 scratch per table (touches only the looked-up rows)."""
+
+    @staticmethod
+    def forward(ctx, ids0, ids1, ids2, t0, t1, t2):
+        tabs = [t0, t1, t2]
+        ids = [ids0, ids1, ids2]
+        D = t0.shape[1]
+        n = ids0.numel()
+        out = torch.empty(n, D, dtype=torch.bfloat16, device=t0.device)
+        f32 = sum(1 << k for k, t in enumerate(tabs) if t is not None and t.dtype == torch.float32)
+        ids = [i.reshape(-1).contiguous() if i is not None else None for i in ids]
+        _lib.call("kfa_embed_fwd", _lib.ptr(ids[0]), _lib.ptr(t0), _lib.ptr(ids[1]), _lib.ptr(t1), _lib.ptr(ids[2]),
+                  _lib.ptr(t2), f32, _lib.ptr(out), n, D, D, _lib.stream())
+        ctx.save_for_backward(*[i if i is not None else torch.empty(0) for i in ids])
+        ctx.tabs = tabs
+        return out.view(*ids0.shape, D)
+
+    @staticmethod
+    def backward(ctx, dout):
+        ids = ctx.saved_tensors
+        dout = dout.reshape(-1, dout.shape[-1]).contiguous()
+        n, D = dout.shape
+        grads = []
+        for k, t in enumerate(ctx.tabs):
+            if t is None or not ctx.needs_input_grad[3 + k]:
+                grads.append(None)
+                continue
+            g, _, direct = _grad_target(t)
+            if t.shape[0] <= SMALL_TABLE_ROWS:
+                # few rows, many duplicates (position / segment tables): atomics would
+                # serialise on a handful of addresses; a one-hot GEMM (MFMA) reduces them
+                oh = torch.zeros(n, t.shape[0], dtype=dout.dtype, device=dout.device)
+                oh.scatter_(1, ids[k].view(-1, 1), 1.0)
+                _wgrad_(g, oh, dout)
+            else:
+                scratch = _lib.workspace(t.shape[0] * D * 4, t.device, f"embed_scratch{k}").view(torch.float32)
+                _lib.call("kfa_embed_bwd", _lib.ptr(ids[k]), _lib.ptr(dout), D, _lib.ptr(scratch), _lib.ptr(g),
+                          int(g.dtype == torch.float32), n, D, 1, _lib.stream())
+            grads.append(_finish(t, g, direct))
+        return (None, None, None, *grads)
+
+
+def embedding_sum(tables, ids):
+    """Σ_k tables[k][ids[k]] as bf16 ``[*ids[0].shape, D]``."""
+    tables = list(tables) + [None] * (3 - len(tables))
+    ids = list(ids) + [None] * (3 - len(ids))
+    if not tables[0].is_cuda:
+        out = 0
+        for t, i in zip(tables, ids):
+            if t is not None:
+                out = out + F.embedding(i, t.float())
+        return out
+    return EmbeddingSumFn.apply(ids[0], ids[1], ids[2], tables[0], tables[1], tables[2])
+
+
+# ----------------------------------------------------------------------------- encoder layer
+class EncoderLayerFn(torch.autograd.Function):
+    """Post-LN BERT encoder layer, forward + backward written out (see module doc).
+
+    Inputs: x [T, H] bf16 (T = B·S), key_bias [B, S] fp32 additive mask (or None),
+    then the 12 parameters.  cfg = (B, S, heads, p_hidden, p_attn, seed, eps)."""
+
+    @staticmethod
+    def forward(ctx, x, key_bias, cfg, wqkv, bqkv, wo, bo, g1, be1, w1, b1, w2, b2, g2, be2):
+        B, S, heads, ph, pa, seed, eps = cfg
+        T, H = x.shape
+        d = H // heads
+        qscale = 1.0 / math.sqrt(d)
+        st = _lib.stream()
+        dev = x.device
+        s_attn, s_h1, s_h2 = mix_seed(seed, 1), mix_seed(seed, 2), mix_seed(seed, 3)
+        # attention
+        qkv = torch.mm(x, wqkv.t())                                       # [T, 3H]
+        q = torch.empty(B * heads, S, d, dtype=x.dtype, device=dev)
+        k = torch.empty_like(q)
+        v = torch.empty_like(q)
+        _lib.call("kfa_qkv_split", _lib.ptr(qkv), _lib.ptr(bqkv), _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), T, S, heads,
+                  d, qscale, st)
+        del qkv
+        probs = torch.bmm(q, k.transpose(1, 2))                           # [BH, S, S]
+        pdrop = torch.empty_like(probs) if pa > 0 else None
+        _lib.call("kfa_attn_softmax_fwd", _lib.ptr(probs), _lib.ptr(key_bias), _lib.ptr(pdrop), B * heads * S, S,
+                  heads, float(pa), s_attn, st)
+        ctx_h = torch.bmm(pdrop if pdrop is not None else probs, v)        # [BH, S, d]
+        ctxr = torch.empty(T, H, dtype=x.dtype, device=dev)
+        _lib.call("kfa_heads_permute", _lib.ptr(ctx_h), _lib.ptr(ctxr), T, S, heads, d, 1, st)
+        del ctx_h
+        ao = torch.mm(ctxr, wo.t())
+        h1, h1s, m1, r1 = ln_fwd(ao, g1, be1, res=x, bias=bo, eps=eps, p=ph, seed=s_h1)
+        del ao
+        # feed-forward
+        f1 = torch.mm(h1, w1.t())                                          # [T, I]
+        f1a = bias_act_fwd(f1, b1, "gelu")
+        f2 = torch.mm(f1a, w2.t())
+        h2, h2s, m2, r2 = ln_fwd(f2, g2, be2, res=h1, bias=b2, eps=eps, p=ph, seed=s_h2)
+        ctx.save_for_backward(x, q, k, v, probs, pdrop, ctxr, h1, h1s, m1, r1, f1, f1a, h2s, m2, r2)
+        ctx.params = (wqkv, bqkv, wo, bo, g1, be1, w1, b1, w2, b2, g2, be2)
+        ctx.cfg = (B, S, heads, ph, pa, (s_attn, s_h1, s_h2), qscale)
+        return h2
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x, q, k, v, probs, pdrop, ctxr, h1, h1s, m1, r1, f1, f1a, h2s, m2, r2) = ctx.saved_tensors
+        wqkv, bqkv, wo, bo, g1, be1, w1, b1, w2, b2, g2, be2 = ctx.params
+        B, S, heads, ph, pa, (s_attn, s_h1, s_h2), qscale = ctx.cfg
+        T, H = x.shape
+        d = H // heads
+        st = _lib.stream()
+        dy = dy.contiguous()
+        tg = {id(p): _grad_target(p) for p in ctx.params}
+        G = lambda p: tg[id(p)][0]  # noqa: E731
+        # LN2 (+ FFN2 bias grad, hidden dropout): dres -> h1, dbranch -> f2
+        dh1_res, df2 = ln_bwd(dy, h2s, m2, r2, g2, G(g2), G(be2), G(b2), p=ph, seed=s_h2, want_branch=True)
+        _wgrad_(G(w2), df2, f1a)
+        df1a = torch.mm(df2, w2)
+        del df2
+        df1 = bias_act_bwd(df1a, f1, b1, "gelu", G(b1))
+        del df1a
+        _wgrad_(G(w1), df1, h1)
+        dh1 = torch.addmm(dh1_res, df1, w1)        # residual-gradient join inside the GEMM
+        del df1, dh1_res
+        # LN1 (+ out-proj bias grad)
+        dx_res, dao = ln_bwd(dh1, h1s, m1, r1, g1, G(g1), G(be1), G(bo), p=ph, seed=s_h1, want_branch=True)
+        del dh1
+        _wgrad_(G(wo), dao, ctxr)
+        dctxr = torch.mm(dao, wo)
+        del dao
+        dctx_h = torch.empty(B * heads, S, d, dtype=dy.dtype, device=dy.device)
+        _lib.call("kfa_heads_permute", _lib.ptr(dctxr), _lib.ptr(dctx_h), T, S, heads, d, 0, st)
+        del dctxr
+        pd = pdrop if pdrop is not None else probs
+        dv = torch.bmm(pd.transpose(1, 2), dctx_h)
+        dp = torch.bmm(dctx_h, v.transpose(1, 2))
+        del dctx_h
+        _lib.call("kfa_attn_softmax_bwd", _lib.ptr(probs), _lib.ptr(dp), B * heads * S, S, float(pa), s_attn, st)
+        dq = torch.bmm(dp, k)
+        dk = torch.bmm(dp.transpose(1, 2), q)
+        del dp
+        dqkv = torch.empty(T, 3 * H, dtype=dy.dtype, device=dy.device)
+        W3 = 3 * H
+        part = _part(_lib.lib().kfa_colsum_part_floats(T, W3), dy.device)
+        _lib.call("kfa_qkv_merge_bwd", _lib.ptr(dq), _lib.ptr(dk), _lib.ptr(dv), _lib.ptr(dqkv), _lib.ptr(part),
+                  _lib.ptr(G(bqkv)), T, S, heads, d, qscale, 1, st)
+        del dq, dk, dv
+        _wgrad_(G(wqkv), dqkv, x)
+        dx = torch.addmm(dx_res, dqkv, wqkv)
+        grads = [_finish(p, tg[id(p)][0], tg[id(p)][2]) for p in ctx.params]
+        return (dx, None, None, *grads)
+
+
+def encoder_layer_reference(x, key_bias, cfg, wqkv, bqkv, wo, bo, g1, be1, w1, b1, w2, b2, g2, be2):
+    """Plain PyTorch fp32 reference (no dropout)."""
+    B, S, heads, _, _, _, eps = cfg
+    T, H = x.shape
+    d = H // heads
+    f = lambda t: t.float()  # noqa: E731
+    x = f(x)
+    qkv = x @ f(wqkv).t() + f(bqkv)
+    q, k, v = qkv.view(B, S, 3, heads, d).permute(2, 0, 3, 1, 4)
+    sc = (q @ k.transpose(-1, -2)) / math.sqrt(d)
+    if key_bias is not None:
+        sc = sc + key_bias.view(B, 1, 1, S)
+    a = torch.softmax(sc, -1) @ v
+    a = a.permute(0, 2, 1, 3).reshape(T, H)
+    h1 = F.layer_norm(a @ f(wo).t() + f(bo) + x, (H,), f(g1), f(be1), eps)
+    ff = F.gelu(h1 @ f(w1).t() + f(b1)) @ f(w2).t() + f(b2)
+    return F.layer_norm(ff + h1, (H,), f(g2), f(be2), eps)
+
+
+# ----------------------------------------------------------------------------- dropout / decoder + loss
+class DropoutFn(torch.autograd.Function):
+    """Counter-hash dropout (mask regenerated in backward from the seed)."""
+
+    @staticmethod
+    def forward(ctx, x, p, seed):
+        x = x.contiguous()
+        ctx.cfg = (p, seed)
+        return bias_act_fwd(x, None, None, p, seed)
+
+    @staticmethod
+    def backward(ctx, dy):
+        p, seed = ctx.cfg
+        return bias_act_bwd(dy.contiguous(), None, None, None, None, p, seed), None, None
+
+
+def dense_dropout(x, p, seed):
+    if p <= 0:
+        return x
+    if not x.is_cuda:
+        return F.dropout(x, p)
+    return DropoutFn.apply(x, float(p), int(seed))
+
+
+class DecoderXentFn(torch.autograd.Function):
+    """mean softmax-xent of ``t · Wᵀ + b`` (tied MLM decoder): the bias is added
+    inside the loss kernel and dlogits is produced in the forward pass."""
+
+    @staticmethod
+    def forward(ctx, t, w, b, labels):
+        t = t.contiguous()
+        logits = torch.mm(t, w.t())
+        n, V = logits.shape
+        lab = labels.reshape(-1).to(torch.int64).contiguous()
+        row_loss = torch.empty(n, dtype=torch.float32, device=t.device)
+        dlog = torch.empty_like(logits)
+        _lib.call("kfa_softmax_xent", _lib.ptr(logits), 1, _lib.ptr(lab), _lib.ptr(b), _lib.ptr(row_loss),
+                  _lib.ptr(dlog), n, V, 1.0 / n, 0.0, _lib.stream())
+        del logits
+        ctx.save_for_backward(t, w, dlog)
+        ctx.params = (w, b)
+        return row_loss.sum() / n
+
+    @staticmethod
+    def backward(ctx, g):
+        t, w, dlog = ctx.saved_tensors
+        wp, bp = ctx.params
+        dlog.mul_(g.to(dlog.dtype))
+        dt = torch.mm(dlog, w)
+        gw, _, dw = _grad_target(wp)
+        _wgrad_(gw, dlog, t)
+        gb, _, db = _grad_target(bp)
+        colsum_(dlog, gb)
+        return dt, _finish(wp, gw, dw), _finish(bp, gb, db), None
+
+
+def decoder_xent(t, w, b, labels):
+    return DecoderXentFn.apply(t, w, b, labels)

@@ -87,7 +87,9 @@ class GradSync:
 
     def reset(self) -> None:
         for b in self.buckets:
-            b.pending = len(b.params)
+            # a tied parameter written by several direct-gradient kernels per step
+            # (e.g. BERT's word embedding: lookup + MLM decoder) declares _kfa_uses
+            b.pending = sum(getattr(self.groups[b.group].params[pi], "_kfa_uses", 1) for pi in b.params)
             b.work = None
 
     def _launch(self, b: _Bucket) -> None:

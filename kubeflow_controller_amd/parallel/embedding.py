@@ -1,0 +1,211 @@
+"""Row-sharded embedding tables with owner-side sparse optimizers — the
+"embedding-heavy PS" of BASELINE.json's Wide&Deep config (SURVEY §2.4
+"Parameter sharding across PS", §2.6 K6, §7.3 H6).
+
+Reference semantics: ``replica_device_setter`` places each variable on a PS
+task (``mnist_replica.py:137-141``); workers pull rows, push gradients, and
+the PS applies the optimizer (``:184, :256``).  MI355X design:
+
+* rows are interleaved over ``owners`` ranks (``owner = row % owners``) — with
+  PS replicas present the owners are the ranks co-located with the PS tasks
+  (SURVEY §7.3 H1 option a), otherwise every rank owns a slice;
+* **pull** = ``all_to_all`` of the requested ids to their owners, a HIP gather
+  of the fp32 master rows straight to bf16, and an ``all_to_all`` back;
+* **push** = ``all_to_all`` of the row gradients to the owners, a HIP
+  scatter-add into a self-cleaning fp32 scratch and a fused sparse Adam/SGD
+  that updates only the looked-up rows (``csrc/kernels/sparse.hip``) — applied
+  during backward, so no dense gradient or optimizer state is ever touched
+  for rows outside the batch;
+* with one rank (or CPU) the same code runs without collectives.
+
+Parameters marked ``_kfa_sparse`` are skipped by ``split_params`` (they are not
+part of the dense flat groups / all-reduce).
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from ..ops import _lib
+
+_P, _L, _I, _F = _lib.P, _lib.L, _lib.I, _lib.F
+_lib.register("kfa_scatter_add_rows", [_P, _P, _P, _L, _I, _P])
+_lib.register("kfa_sparse_adam", [_P, _P, _P, _P, _P, _L, _I, _F, _F, _F, _F, _F, _F, _F, _F, _P])
+_lib.register("kfa_sparse_sgd", [_P, _P, _P, _L, _I, _F, _F, _P])
+_lib.register("kfa_embed_fwd", [_P, _P, _P, _P, _P, _P, _I, _P, _L, _I, _L, _P])
+
+
+def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits: List[int], in_splits: List[int], pg) -> None:
+    dist.all_to_all_single(out, inp, out_splits, in_splits, group=pg)
+
+
+class _LookupFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, weight, emb: "ShardedEmbedding"):
+        ids = ids.reshape(-1)
+        n, D = ids.numel(), emb.dim
+        comm = emb.world > 1
+        if comm:
+            owner = ids % emb.owners
+            order = torch.argsort(owner, stable=True)
+            sorted_ids = ids.index_select(0, order)
+            send = torch.bincount(owner, minlength=emb.world)
+            recv = torch.empty_like(send)
+            dist.all_to_all_single(recv, send, group=emb.pg)
+            send_l, recv_l = send.tolist(), recv.tolist()
+            req = torch.empty(sum(recv_l), dtype=ids.dtype, device=ids.device)
+            _a2a(req, sorted_ids, recv_l, send_l, emb.pg)
+        else:
+            order, send_l, recv_l, req = None, None, None, ids
+        local = torch.div(req, emb.owners, rounding_mode="floor") if emb.owners > 1 else req
+        rows = emb.gather(local)
+        if comm:
+            out_sorted = torch.empty(n, D, dtype=rows.dtype, device=rows.device)
+            _a2a(out_sorted, rows, send_l, recv_l, emb.pg)
+            out = torch.empty_like(out_sorted)
+            out.index_copy_(0, order, out_sorted)
+        else:
+            out = rows
+        ctx.emb = emb
+        ctx.save_for_backward(local, order if order is not None else torch.empty(0, device=ids.device))
+        ctx.splits = (send_l, recv_l)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        local, order = ctx.saved_tensors
+        emb = ctx.emb
+        send_l, recv_l = ctx.splits
+        dout = dout.contiguous()
+        if emb.world > 1:
+            d_sorted = dout.index_select(0, order)
+            g = torch.empty(local.numel(), emb.dim, dtype=dout.dtype, device=dout.device)
+            _a2a(g, d_sorted, recv_l, send_l, emb.pg)
+        else:
+            g = dout
+        emb.apply_sparse(local, g)
+        return None, None, None
+
+
+class ShardedEmbedding(nn.Module):
+    def __init__(self, num_rows: int, dim: int, owners: Optional[int] = None, process_group=None,
+                 optimizer: str = "adam", lr: float = 1e-3, betas: Tuple[float, float] = (0.9, 0.999),
+                 eps: float = 1e-8, weight_decay: float = 0.0, init_std: float = 0.01, seed: int = 0,
+                 device=None):
+        super().__init__()
+        self.pg = process_group
+        init = dist.is_initialized()
+        self.world = dist.get_world_size(process_group) if init else 1
+        self.rank = dist.get_rank(process_group) if init else 0
+        self.owners = max(1, min(owners or self.world, self.world))
+        self.num_rows, self.dim = num_rows, dim
+        self.local_rows = len(range(self.rank, num_rows, self.owners)) if self.rank < self.owners else 0
+        self.optimizer, self.lr, self.betas, self.eps, self.wd = optimizer, lr, betas, eps, weight_decay
+        self.grad_scale = 1.0 / self.world  # data-parallel mean, like the dense groups
+        self.t = 0
+        dev = torch.device(device) if device is not None else torch.device("cpu")
+        self.weight = nn.Parameter(self._init(init_std, seed, dev))
+        self.weight._kfa_sparse = True
+        self.register_buffer("exp_avg", torch.zeros_like(self.weight) if optimizer == "adam" else None)
+        self.register_buffer("exp_avg_sq", torch.zeros_like(self.weight) if optimizer == "adam" else None)
+
+    def _init(self, std: float, seed: int, dev) -> torch.Tensor:
+        """World-size independent init: global row r gets the same values on any layout."""
+        w = torch.empty(self.local_rows, self.dim, dtype=torch.float32, device=dev)
+        if self.local_rows == 0:
+            return w
+        chunk = 1 << 20
+        g = torch.Generator(device=dev)
+        for c0 in range(0, self.num_rows, chunk):
+            c1 = min(self.num_rows, c0 + chunk)
+            g.manual_seed(seed * 1000003 + c0 // chunk)
+            blk = torch.randn(c1 - c0, self.dim, generator=g, device=dev) * std
+            first = c0 + ((self.rank - c0) % self.owners)       # first owned global row in the chunk
+            if first >= c1:
+                continue
+            rows = torch.arange(first, c1, self.owners, device=dev)
+            w[torch.div(rows, self.owners, rounding_mode="floor")] = blk[rows - c0]
+        return w
+
+    def extra_repr(self) -> str:
+        return (f"rows={self.num_rows}, dim={self.dim}, owners={self.owners}, local_rows={self.local_rows}, "
+                f"optimizer={self.optimizer}")
+
+    # ---------------------------------------------------------------- owner-side kernels
+    def gather(self, local: torch.Tensor) -> torch.Tensor:
+        n = local.numel()
+        if not self.weight.is_cuda:
+            return self.weight.detach().index_select(0, local)
+        out = torch.empty(n, self.dim, dtype=torch.bfloat16, device=local.device)
+        if n:
+            _lib.call("kfa_embed_fwd", _lib.ptr(local), _lib.ptr(self.weight), None, None, None, None, 1,
+                      _lib.ptr(out), n, self.dim, self.dim, _lib.stream())
+        return out
+
+    @torch.no_grad()
+    def apply_sparse(self, local: torch.Tensor, g: torch.Tensor) -> None:
+        self.t += 1
+        if local.numel() == 0:
+            return
+        b1, b2 = self.betas
+        if not self.weight.is_cuda:
+            self._apply_cpu(local, g.float(), b1, b2)
+            return
+        scratch = _lib.workspace(self.local_rows * self.dim * 4, self.weight.device,
+                                 f"sparse_scratch{id(self)}").view(torch.float32)
+        st = _lib.stream()
+        _lib.call("kfa_scatter_add_rows", _lib.ptr(local), _lib.ptr(g.to(torch.bfloat16)), _lib.ptr(scratch),
+                  local.numel(), self.dim, st)
+        if self.optimizer == "adam":
+            c1 = 1.0 / (1.0 - b1 ** self.t)
+            c2 = 1.0 / (1.0 - b2 ** self.t)
+            _lib.call("kfa_sparse_adam", _lib.ptr(local), _lib.ptr(scratch), _lib.ptr(self.weight),
+                      _lib.ptr(self.exp_avg), _lib.ptr(self.exp_avg_sq), local.numel(), self.dim, self.lr, b1, b2,
+                      self.eps, self.wd, c1, c2, self.grad_scale, st)
+        else:
+            _lib.call("kfa_sparse_sgd", _lib.ptr(local), _lib.ptr(scratch), _lib.ptr(self.weight), local.numel(),
+                      self.dim, self.lr, self.grad_scale, st)
+
+    def _apply_cpu(self, local, g, b1, b2) -> None:
+        """Plain-PyTorch reference of the same lazy row update."""
+        uniq, inv = torch.unique(local, return_inverse=True)
+        gs = torch.zeros(uniq.numel(), self.dim).index_add_(0, inv, g) * self.grad_scale
+        w = self.weight.data
+        if self.optimizer == "adam":
+            nz = gs != 0
+            m = self.exp_avg[uniq]
+            v = self.exp_avg_sq[uniq]
+            m = torch.where(nz, b1 * m + (1 - b1) * gs, m)
+            v = torch.where(nz, b2 * v + (1 - b2) * gs * gs, v)
+            c1 = 1.0 / (1.0 - b1 ** self.t)
+            c2 = 1.0 / (1.0 - b2 ** self.t)
+            rows = w[uniq]
+            upd = (m * c1) / ((v * c2).sqrt() + self.eps) + self.wd * rows
+            w[uniq] = torch.where(nz, rows - self.lr * upd, rows)
+            self.exp_avg[uniq] = m
+            self.exp_avg_sq[uniq] = v
+        else:
+            w.index_add_(0, uniq, -self.lr * gs)
+
+    def forward(self, ids: torch.Tensor) -> torch.Tensor:
+        out = _LookupFn.apply(ids, self.weight, self)
+        return out.view(*ids.shape, self.dim)
+
+    def full_table(self) -> torch.Tensor:
+        """Gather the whole table to every rank (tests / checkpoint export)."""
+        if self.world == 1:
+            return self.weight.detach().clone()
+        maxr = -(-self.num_rows // self.owners)  # equal-size pieces (gloo needs them)
+        mine = torch.zeros(maxr, self.dim, device=self.weight.device)
+        mine[:self.local_rows] = self.weight.detach()
+        parts = [torch.empty_like(mine) for _ in range(self.world)]
+        dist.all_gather(parts, mine, group=self.pg)
+        parts = [p[:len(range(r, self.num_rows, self.owners))] for r, p in enumerate(parts[:self.owners])]
+        full = torch.empty(self.num_rows, self.dim, device=self.weight.device)
+        for r in range(self.owners):
+            full[r::self.owners] = parts[r]
+        return full

@@ -108,8 +108,8 @@ def split_params(model: torch.nn.Module, compute_dtype=torch.bfloat16, pad_to: i
     (no decay — the usual large-batch recipe)."""
     big, small = [], []
     for p in model.parameters():
-        if not p.requires_grad:
-            continue
+        if not p.requires_grad or getattr(p, "_kfa_sparse", False):
+            continue  # frozen, or a row-sharded table updated by its owner (parallel/embedding.py)
         if p.dim() >= 2 and compute_dtype is not None and p.dtype != compute_dtype:
             p.data = p.data.to(compute_dtype)
         (big if p.dim() >= 2 else small).append(p)

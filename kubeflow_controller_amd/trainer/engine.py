@@ -54,7 +54,7 @@ class Engine:
     def __init__(self, model: torch.nn.Module, loss_fn: Callable, *, optimizer: str = "sgd", lr: float = 0.1,
                  momentum: float = 0.9, weight_decay: float = 5e-5, betas=(0.9, 0.999), eps: float = 1e-8,
                  compute_dtype=torch.bfloat16, bucket_mb: float = 16.0, dist_info: Optional[DistInfo] = None,
-                 channels_last: bool = True):
+                 channels_last: bool = True, ps: int = 0):
         from ..ops.optim import FusedAdam, FusedSGD
         from ..parallel.ddp import GradSync, broadcast_params
 
@@ -63,7 +63,8 @@ class Engine:
         if channels_last:
             self.model = self.model.to(memory_format=torch.channels_last)
         self.loss_fn = loss_fn
-        self.groups: List[FlatGroup] = split_params(self.model, compute_dtype)
+        # pad so every group splits evenly into per-rank reduce-scatter shards
+        self.groups: List[FlatGroup] = split_params(self.model, compute_dtype, pad_to=8 * max(1, self.info.world))
         if optimizer == "sgd":
             self.opt = FusedSGD(self.groups, lr=lr, momentum=momentum, weight_decay=weight_decay)
         elif optimizer in ("adam", "adamw"):
@@ -71,7 +72,15 @@ class Engine:
         else:
             raise ValueError(f"unknown optimizer {optimizer!r}")
         broadcast_params(self.groups)
-        self.sync = GradSync(self.groups, bucket_mb=bucket_mb)
+        # ps > 0: parameter-server layout — shards owned by the
+        # ranks, push = reduce-scatter, owner-side fused optimizer, pull = all-gather
+        self.sharded = ps > 0 and self.info.world > 1
+        if self.sharded:
+            from ..parallel.ps import ShardedGradSync
+            self.sync = ShardedGradSync(self.groups)
+            self.sync.configure(self.opt)
+        else:
+            self.sync = GradSync(self.groups, bucket_mb=bucket_mb)
         self.steps = 0
 
     def zero_grad(self) -> None:
@@ -82,8 +91,11 @@ class Engine:
         self.zero_grad()
         loss = self.loss_fn(self.model, *batch)
         loss.backward()
-        scale = self.sync.finish()
-        self.opt.step(grad_scale=scale)
+        if self.sharded:
+            self.opt.step(grad_scale=self.sync.push())
+            self.sync.pull()
+        else:
+            self.opt.step(grad_scale=self.sync.finish())
         self.steps += 1
         return loss
 

@@ -86,7 +86,9 @@ def build(args, device):
     if name in ("wide_deep", "wide_deep_tiny"):
         from ..models.wide_deep import WideDeep, WideDeepConfig, wide_deep_loss
         cfg = WideDeepConfig() if name == "wide_deep" else WideDeepConfig.tiny()
-        return WideDeep(cfg), None, wide_deep_loss
+        # tables live on the ranks co-located with the PS replicas
+        cfg.owners = getattr(args, "num_ps", 0) or None
+        return WideDeep(cfg, device=device), None, wide_deep_loss
     raise SystemExit(f"unknown --model {name}")
 
 
@@ -164,6 +166,7 @@ def run_worker(spec: ClusterSpec, args) -> int:
         dist.init_process_group("nccl" if use_gpu else "gloo", store=store, rank=rank, world_size=world,
                                 **({"device_id": device} if use_gpu else {}))
     torch.manual_seed(args.seed)  # identical init everywhere (+ broadcast below)
+    args.num_ps = 0 if spec.is_local else len(spec.ps)
     model, data, loss_fn = build(args, device)
     model = model.to(device)
     if model.__class__.__name__ == "ResNet":

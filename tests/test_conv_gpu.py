@@ -57,8 +57,18 @@ def _stack_grads(enabled, join, x, m):
         convmod.ENABLED = True
 
 
+def _fp32_reference_grads(x, m):
+    """Same network in fp32 on the CPU with plain PyTorch ops (conv2d/batch_norm/relu)."""
+    import copy
+    ref = copy.deepcopy(m).cpu().float()
+    xr = x.detach().float().cpu().contiguous().requires_grad_()
+    ref(xr).float().square().mean().backward()
+    return [xr.grad] + [p.grad for p in ref.parameters()]
+
+
 def test_resnet_block_grads_igemm_vs_vendor():
-    """Bottleneck stack incl. the fused residual-gradient joins (GradJoin) vs vendor convs."""
+    """Bottleneck stack incl. the fused residual-gradient joins (GradJoin): the HIP
+    conv path must be as close to an fp32 reference as the vendor bf16 convs are."""
     from kubeflow_controller_amd.models.resnet import ResNet
     d = torch.device("cuda")
     torch.manual_seed(0)
@@ -69,13 +79,19 @@ def test_resnet_block_grads_igemm_vs_vendor():
     for mod in m.modules():  # non-zero residual scale so every branch carries gradient
         if hasattr(mod, "bn3"):
             torch.nn.init.uniform_(mod.bn3.weight, 0.5, 1.5)
-    # large enough spatial extent that no BN normalises over a handful of values
     x = torch.randn(8, 3, 128, 128, device=d).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    ref = _fp32_reference_grads(x, m)
     fused = _stack_grads(True, True, x, m)
     unfused = _stack_grads(True, False, x, m)
     vendor = _stack_grads(False, False, x, m)
-    for a, b in zip(fused, unfused):  # the join changes only where the add happens
-        assert (a - b).abs().max().item() <= 0.05 * b.abs().max().item() + 1e-4
-    for a, b in zip(fused, vendor):
-        scale = max(1e-3, b.abs().max().item())
-        assert (a - b).abs().max().item() < 0.1 * scale, ((a - b).abs().max().item(), scale)
+    names = ["input"] + [n for n, _ in m.named_parameters()]
+    bad = []
+    for n, f, u, v, r in zip(names, fused, unfused, vendor, ref):
+        r = r.to(f.device).float()
+        if r.dim() == 4:
+            r = r.contiguous(memory_format=torch.channels_last)
+        scale = max(1e-4, r.abs().max().item())
+        e_f, e_u, e_v = ((t - r).abs().max().item() for t in (f, u, v))
+        if e_f > 2.0 * e_v + 0.02 * scale or e_u > 2.0 * e_v + 0.02 * scale:
+            bad.append((n, e_f, e_u, e_v, scale))
+    assert not bad, bad

@@ -109,3 +109,64 @@ def test_ps_assignment():
     greedy = ps_assignment(params, 2, "greedy")
     load = [sum(p.numel() for n, p in params if greedy[n] == k) for k in range(2)]
     assert max(load) == 100 and min(load) == 75
+
+
+def _wd_worker(rank, world, port, owners, out):
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    from kubeflow_controller_amd.models.wide_deep import WideDeep, WideDeepConfig, synthetic_batch, wide_deep_loss
+    from kubeflow_controller_amd.trainer.engine import DistInfo, Engine
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = WideDeepConfig.tiny()
+    cfg.owners = owners
+    torch.manual_seed(0)
+    m = WideDeep(cfg, device="cpu")
+    eng = Engine(m, wide_deep_loss, optimizer="adam", lr=1e-2, compute_dtype=None, channels_last=False,
+                 dist_info=DistInfo(rank=rank, world=world))
+    dense, ids, labels = synthetic_batch(cfg, 64, torch.Generator().manual_seed(5))
+    n = 64 // world
+    sl = slice(rank * n, (rank + 1) * n)
+    for _ in range(4):
+        eng.train_step(dense[sl], ids[sl], labels[sl])
+    table = m.tables.full_table()
+    if rank == 0:
+        sd = {k: v.clone() for k, v in m.state_dict().items() if not k.startswith("tables.")}
+        sd["table"] = table
+        torch.save(sd, out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("owners", [1, 2])
+def test_sharded_embedding_ps_matches_single_process(tmp_path, owners):
+    """Wide&Deep with row-sharded tables (all-to-all pull/push, owner-side sparse
+    Adam) on 2 ranks == one process on the whole batch."""
+    from kubeflow_controller_amd.models.wide_deep import WideDeep, WideDeepConfig, synthetic_batch, wide_deep_loss
+    from kubeflow_controller_amd.trainer.engine import Engine
+    out = str(tmp_path / "wd.pt")
+    mp.start_processes(_wd_worker, args=(2, _free_port(), owners, out), nprocs=2, join=True, start_method="spawn")
+    got = torch.load(out, weights_only=True)
+    cfg = WideDeepConfig.tiny()
+    torch.manual_seed(0)
+    m = WideDeep(cfg, device="cpu")
+    eng = Engine(m, wide_deep_loss, optimizer="adam", lr=1e-2, compute_dtype=None, channels_last=False)
+    dense, ids, labels = synthetic_batch(cfg, 64, torch.Generator().manual_seed(5))
+    for _ in range(4):
+        eng.train_step(dense, ids, labels)
+    torch.testing.assert_close(got["table"], m.tables.full_table(), atol=1e-5, rtol=1e-4)
+    for k, v in m.state_dict().items():
+        if not k.startswith("tables."):
+            torch.testing.assert_close(got[k], v, atol=1e-5, rtol=1e-4)
+
+
+def test_bert_tiny_cpu_trains():
+    from kubeflow_controller_amd.models.bert import BertConfig, BertForPreTraining, bert_loss, synthetic_mlm_batch
+    from kubeflow_controller_amd.trainer.engine import Engine
+    cfg = BertConfig.tiny()
+    torch.manual_seed(0)
+    m = BertForPreTraining(cfg)
+    eng = Engine(m, bert_loss, optimizer="adam", lr=2e-3, compute_dtype=None, channels_last=False)
+    batch = synthetic_mlm_batch(cfg, 4, 32, torch.Generator().manual_seed(0))
+    losses = [float(eng.train_step(*batch)) for _ in range(15)]
+    assert losses[-1] < losses[0] - 0.5, losses
