@@ -200,12 +200,37 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const bf16_t* __rest
           acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[ni], af[mi], acc[ni][mi], 0, 0, 0);
     }
   };
-  auto epilogue = [&](int tile) {
-    // lane holds D[n = n0 + wn*16TN + ni*16 + fq*4 + j][m = m0 + wm*16TM + mi*16 + fr]
+  // Epilogue through LDS: MFMA leaves each lane 4 consecutive channels of one
+  // pixel (8-B pieces, 32-B row segments per store instruction); staging the
+  // wave's tile in LDS (XOR-swizzled 16-B chunks, conflict-free both ways)
+  // lets every lane store 16 B and a wave cover 128-B row segments, so the
+  // HBM writes of the memory-bound layers (K = 64..256) coalesce.
+  constexpr int WT = 256 * TM * TN;   // wave tile elements (16TM rows x 16TN channels)
+  constexpr int RB = 32 * TN;         // staged row bytes
+  constexpr int CPR = 2 * TN;         // 16-B chunks per staged row
+  auto epilogue = [&](int tile, int buf) {
     const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
+    lds_barrier();  // every wave is done reading `buf`: reuse it as the staging area
+    char* stage;
+    {
+      const int e = wave * WT;
+      stage = reinterpret_cast<char*>(e < BM * BK ? As + buf * BM * BK + e : Bs + buf * BN * BK + (e - BM * BK));
+    }
 #pragma unroll
-    for (int mi = 0; mi < TM; mi++) {
-      const int m = m0 + wm * TM * 16 + mi * 16 + fr;
+    for (int mi = 0; mi < TM; mi++)
+#pragma unroll
+      for (int ni = 0; ni < TN; ni++) {
+        const int row = mi * 16 + fr, col = ni * 16 + fq * 4;
+        const uint2 o = make_uint2(pack2(acc[ni][mi][0], acc[ni][mi][1]), pack2(acc[ni][mi][2], acc[ni][mi][3]));
+        *reinterpret_cast<uint2*>(stage + row * RB + (((col >> 3) ^ (row & (CPR - 1))) << 4) + (col & 7) * 2) = o;
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const int c = lane % CPR;
+#pragma unroll
+    for (int it = 0; it < (16 * TM * CPR) / 64; it++) {
+      const int r = it * (64 / CPR) + lane / CPR;
+      const uint4 v = *reinterpret_cast<const uint4*>(stage + r * RB + ((c ^ (r & (CPR - 1))) << 4));
+      const int m = m0 + wm * TM * 16 + r;
       unsigned orow;  // byte offset of output row m (kOOB when m is a tail row)
       if (lin_d) {
         orow = (unsigned)m * (unsigned)g.ldd * 2u;
@@ -214,20 +239,19 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const bf16_t* __rest
         const int p = fdiv(rem, g.Q, rQ), q = rem - p * g.Q;
         orow = (unsigned)((nb * g.OH + p * g.os + g.oph) * g.OW + (q * g.os + g.opw)) * (unsigned)g.ldd * 2u;
       }
-      orow = m < g.M ? orow : kOOB;
+      const int n = n0 + wn * TN * 16 + c * 8;
+      const unsigned off = (m >= g.M || n >= g.N) ? kOOB : orow + (unsigned)n * 2u;
+      uint4 o = v;
+      if (E) {  // wave-uniform branch
+        const uint4 e = bload16(rE, off);
+        float f[8], h[8];
+        unpack8(v, f);
+        unpack8(e, h);
 #pragma unroll
-      for (int ni = 0; ni < TN; ni++) {
-        const int n = n0 + wn * TN * 16 + ni * 16 + fq * 4;
-        const unsigned off = (orow == kOOB || n >= g.N) ? kOOB : orow + (unsigned)n * 2u;
-        float v0 = acc[ni][mi][0], v1 = acc[ni][mi][1], v2 = acc[ni][mi][2], v3 = acc[ni][mi][3];
-        if (E) {  // wave-uniform branch
-          auto ev = __builtin_amdgcn_raw_buffer_load_b64(rE, off, 0, 0);
-          const uint2 e = *reinterpret_cast<uint2*>(&ev);
-          v0 += bf2f(e.x & 0xffff); v1 += bf2f(e.x >> 16); v2 += bf2f(e.y & 0xffff); v3 += bf2f(e.y >> 16);
-        }
-        uint2 o = make_uint2(pack2(v0, v1), pack2(v2, v3));
-        __builtin_amdgcn_raw_buffer_store_b64(*reinterpret_cast<decltype(__builtin_amdgcn_raw_buffer_load_b64(rD, 0, 0, 0))*>(&o), rD, off, 0, 0);
+        for (int j = 0; j < 8; j++) f[j] += h[j];
+        o = pack8(f);
       }
+      __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<decltype(__builtin_amdgcn_raw_buffer_load_b128(rD, 0, 0, 0))*>(&o), rD, off, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < TN; i++)
@@ -236,7 +260,10 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const bf16_t* __rest
   };
 
   if (nk == 0) {  // no taps reach these outputs (strided dgrad parity class): D = 0 (+ E)
-    for (int i = 0; i < my_tiles; i++) epilogue(tile_of(i));
+    for (int i = 0; i < my_tiles; i++) {
+      epilogue(tile_of(i), 0);
+      lds_barrier();
+    }
     return;
   }
   issue(0, 0);
@@ -252,7 +279,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const bf16_t* __rest
       asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
     }
     compute(buf);
-    if ((st + 1) % nk == 0) epilogue(tile_of(st / nk));
+    if ((st + 1) % nk == 0) epilogue(tile_of(st / nk), buf);
     lds_barrier();  // every wave is done reading `buf` before slice st+2 is DMA'd into it
   }
 }

@@ -9,8 +9,8 @@
 //    bias of the producing GEMM and the hidden dropout ride along; the summed
 //    input is stored (bf16) for backward.
 //  * LayerNorm bwd: dx, the dropout-masked branch gradient, dgamma/dbeta and
-//    the producing GEMM's dbias in one pass (column sums via per-block partials
-//    + a deterministic finalize, no global atomics).
+//    the producing GEMM's dbias in one pass (column sums reduced in LDS per
+//    block, then one fp32 atomic per column per block into the flat gradient).
 //  * bias+activation fwd/bwd (GELU-erf / tanh / ReLU / identity) with fused
 //    dbias column sums.
 //  * QKV split (bias add + head split + 1/sqrt(d) scaling) and its inverse
@@ -122,13 +122,15 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ 
 
 // Backward. Each block walks a contiguous chunk of rows, one wave per row;
 // per-lane column accumulators are reduced across the 4 waves through LDS and
-// written as one partial row per block: part[blk][0:H]=dgamma, [H:2H]=dbeta,
-// [2H:3H]=dbias (sum of the branch gradient).
+// each block adds its column sums to dgamma / dbeta / dbias (sum of the branch
+// gradient) with one fp32 atomic per column (no partial buffer, no finalize
+// launch).
 template <int NV>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ xs,
                                                      const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
                                                      const float* __restrict__ gamma, bf16_t* __restrict__ dx,
-                                                     bf16_t* __restrict__ dbranch, float* __restrict__ part, long rows,
+                                                     bf16_t* __restrict__ dbranch, float* __restrict__ o_gamma,
+                                                     float* __restrict__ o_beta, float* __restrict__ o_bias, long rows,
                                                      int H, long rows_per_block, uint32_t thresh, float dscale,
                                                      uint64_t seed) {
   extern __shared__ float red[];  // [4][H]
@@ -185,7 +187,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
     }
   }
   // block-reduce the three column accumulators
-  auto reduce_out = [&](float (&acc)[NV][8], int a) {
+  auto reduce_out = [&](float (&acc)[NV][8], float* out) {
+    if (!out) return;  // block-uniform
 #pragma unroll
     for (int j = 0; j < NV; j++) {
       const int c = (j * 64 + lane) * 8;
@@ -195,39 +198,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
     }
     __syncthreads();
     for (int c = threadIdx.x; c < H; c += 256)
-      part[(long)blockIdx.x * 3 * H + (long)a * H + c] = red[c] + red[H + c] + red[2 * H + c] + red[3 * H + c];
+      atomicAdd(out + c, red[c] + red[H + c] + red[2 * H + c] + red[3 * H + c]);
     __syncthreads();
   };
-  reduce_out(ag, 0);
-  reduce_out(ab, 1);
-  reduce_out(ad, 2);
-}
-
-// out[c] (+)= sum_b part[b * stride + c]   (deterministic column finalize)
-// block = 64 columns x 4 row-lanes; 8 independent loads in flight per lane.
-__global__ __launch_bounds__(256) void colsum_finalize_kernel(const float* __restrict__ part, int nblk, long stride,
-                                                              int N, float* __restrict__ out, int accumulate) {
-  __shared__ float red[4][64];
-  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
-  float s = 0.f;
-  if (c < N) {
-    int b = rl;
-    for (; b + 28 < nblk; b += 32) {
-      float v[8];
-#pragma unroll
-      for (int u = 0; u < 8; u++) v[u] = part[(long)(b + 4 * u) * stride + c];
-#pragma unroll
-      for (int u = 0; u < 8; u++) s += v[u];
-    }
-    for (; b < nblk; b += 4) s += part[(long)b * stride + c];
-  }
-  red[rl][cl] = s;
-  __syncthreads();
-  if (rl == 0 && c < N) {
-    const float t = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
-    out[c] = accumulate ? out[c] + t : t;
-  }
+  reduce_out(ag, o_gamma);
+  reduce_out(ab, o_beta);
+  reduce_out(ad, o_bias);
 }
 
 // ----------------------------------------------------------------------------- bias + activation
@@ -284,7 +260,7 @@ __global__ __launch_bounds__(256) void bias_act_fwd_kernel(const bf16_t* __restr
 // covering 512 columns; grid = (ceil(N/512), row chunks).
 __global__ __launch_bounds__(256) void bias_act_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                            const float* __restrict__ b, bf16_t* __restrict__ dx,
-                                                           float* __restrict__ part, long rows, int N, int act,
+                                                           float* __restrict__ dbias, long rows, int N, int act,
                                                            long rows_per_block, uint32_t thresh, float dscale,
                                                            uint64_t seed) {
   __shared__ float red[4][512];
@@ -315,10 +291,11 @@ __global__ __launch_bounds__(256) void bias_act_bwd_kernel(const bf16_t* __restr
 #pragma unroll
   for (int e = 0; e < 8; e++) red[rl][cl * 8 + e] = acc[e];
   __syncthreads();
-  for (int k = threadIdx.x; k < 512; k += 256) {
-    const int cc = blockIdx.x * 512 + k;
-    if (cc < N) part[(long)blockIdx.y * N + cc] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
-  }
+  if (dbias)
+    for (int k = threadIdx.x; k < 512; k += 256) {
+      const int cc = blockIdx.x * 512 + k;
+      if (cc < N) atomicAdd(dbias + cc, red[0][k] + red[1][k] + red[2][k] + red[3][k]);
+    }
 }
 
 // ----------------------------------------------------------------------------- attention layout
@@ -353,7 +330,7 @@ __global__ __launch_bounds__(256) void qkv_split_kernel(const bf16_t* __restrict
 // inverse: dq, dk, dv [B,h,S,d] -> dqkv [T, 3H] (dq scaled by qscale) + dbias partials
 __global__ __launch_bounds__(256) void qkv_merge_bwd_kernel(const bf16_t* __restrict__ dq, const bf16_t* __restrict__ dk,
                                                             const bf16_t* __restrict__ dv, bf16_t* __restrict__ dqkv,
-                                                            float* __restrict__ part, long T, int S, int heads, int d,
+                                                            float* __restrict__ dbias, long T, int S, int heads, int d,
                                                             float qscale, long rows_per_block) {
   __shared__ float red[4][512];
   const int H = heads * d, W = 3 * H;
@@ -378,10 +355,10 @@ __global__ __launch_bounds__(256) void qkv_merge_bwd_kernel(const bf16_t* __rest
 #pragma unroll
   for (int e = 0; e < 8; e++) red[rl][cl * 8 + e] = acc[e];
   __syncthreads();
-  if (part)
+  if (dbias)
     for (int k = threadIdx.x; k < 512; k += 256) {
       const int cc = blockIdx.x * 512 + k;
-      if (cc < W) part[(long)blockIdx.y * W + cc] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
+      if (cc < W) atomicAdd(dbias + cc, red[0][k] + red[1][k] + red[2][k] + red[3][k]);
     }
 }
 
@@ -593,9 +570,9 @@ uint32_t drop_thresh(float p) {
 // ============================================================================= C ABI
 static long ln_bwd_blocks(long rows) { return rows < 2048 ? (rows + 3) / 4 : 512; }
 
-KFA_API long kfa_ln_part_floats(long rows, int H) {
-  long nblk = ln_bwd_blocks(rows);
-  return nblk * 3 * H;
+KFA_API long kfa_ln_part_floats(long rows, int H) {  // no scratch needed any more (ABI stability)
+  (void)rows; (void)H;
+  return 0;
 }
 
 namespace {
@@ -608,10 +585,10 @@ void launch_ln_fwd(dim3 g, hipStream_t s, const void* x, const void* res, const 
 }
 template <int NV>
 void launch_ln_bwd(dim3 g, size_t lds, hipStream_t s, const void* dy, const void* xs, const float* mean,
-                   const float* rstd, const float* gamma, void* dx, void* dbranch, float* part, long rows, int H,
-                   long rpb, uint32_t th, float ds, uint64_t seed) {
+                   const float* rstd, const float* gamma, void* dx, void* dbranch, float* o0, float* o1, float* o2,
+                   long rows, int H, long rpb, uint32_t th, float ds, uint64_t seed) {
   hipLaunchKernelGGL(ln_bwd_kernel<NV>, g, dim3(256), lds, s, (const bf16_t*)dy, (const bf16_t*)xs, mean, rstd, gamma,
-                     (bf16_t*)dx, (bf16_t*)dbranch, part, rows, H, rpb, th, ds, seed);
+                     (bf16_t*)dx, (bf16_t*)dbranch, o0, o1, o2, rows, H, rpb, th, ds, seed);
 }
 template <int G, int NV>
 void launch_sm_fwd(hipStream_t s, void* scores, const float* key_bias, void* pdrop, long rows, int S, int heads,
@@ -643,30 +620,36 @@ KFA_API int kfa_ln_fwd(const void* x, const void* res, const float* bias, const 
   return kfa_status();
 }
 
-// dgamma/dbeta/dbias: fp32, (+)= when accumulate; any may be null.
+static void zero_if(float* p, int n, int accumulate, hipStream_t s) {
+  if (p && !accumulate) (void)hipMemsetAsync(p, 0, (size_t)n * sizeof(float), s);
+}
+
+// dgamma/dbeta/dbias: fp32, (+)= when accumulate (else overwritten); any may be
+// null.  `part` is unused (kept for ABI stability).
 KFA_API int kfa_ln_bwd(const void* dy, const void* xs, const float* mean, const float* rstd, const float* gamma,
                        void* dx, void* dbranch, float* part, float* dgamma, float* dbeta, float* dbias, long rows,
                        int H, float p, unsigned long long seed, int accumulate, hipStream_t s) {
+  (void)part;
   if (rows <= 0 || H % 8 || H > 4096) return -1;
   const long nblk = ln_bwd_blocks(rows);
   const long rpb = (rows + nblk - 1) / nblk;
   const uint32_t th = drop_thresh(p);
   const float ds = p > 0.f ? 1.f / (1.f - p) : 1.f;
   const size_t lds = 4 * H * sizeof(float);
+  zero_if(dgamma, H, accumulate, s);
+  zero_if(dbeta, H, accumulate, s);
+  zero_if(dbias, H, accumulate, s);
   dim3 g((unsigned)nblk);
-  if (H <= 512) launch_ln_bwd<1>(g, lds, s, dy, xs, mean, rstd, gamma, dx, dbranch, part, rows, H, rpb, th, ds, seed);
-  else if (H <= 1024) launch_ln_bwd<2>(g, lds, s, dy, xs, mean, rstd, gamma, dx, dbranch, part, rows, H, rpb, th, ds, seed);
-  else if (H <= 2048) launch_ln_bwd<4>(g, lds, s, dy, xs, mean, rstd, gamma, dx, dbranch, part, rows, H, rpb, th, ds, seed);
-  else launch_ln_bwd<8>(g, lds, s, dy, xs, mean, rstd, gamma, dx, dbranch, part, rows, H, rpb, th, ds, seed);
-  float* outs[3] = {dgamma, dbeta, dbias};
-  for (int a = 0; a < 3; a++)
-    if (outs[a])
-      hipLaunchKernelGGL(colsum_finalize_kernel, dim3((H + 63) / 64), dim3(256), 0, s, part + (long)a * H,
-                         (int)nblk, 3L * H, H, outs[a], accumulate);
+#define LNB(NV) launch_ln_bwd<NV>(g, lds, s, dy, xs, mean, rstd, gamma, dx, dbranch, dgamma, dbeta, dbias, rows, H, \
+                                  rpb, th, ds, seed)
+  if (H <= 512) LNB(1);
+  else if (H <= 1024) LNB(2);
+  else if (H <= 2048) LNB(4);
+  else LNB(8);
+#undef LNB
   return kfa_status();
 }
 
-// y = dropout(act(x + b)); b nullable, p == 0 disables dropout
 KFA_API int kfa_bias_act_fwd(const void* x, const float* b, void* y, long rows, int N, int act, float p,
                              unsigned long long seed, hipStream_t s) {
   if (rows <= 0 || N % 8) return -1;
@@ -680,27 +663,26 @@ KFA_API int kfa_bias_act_fwd(const void* x, const float* b, void* y, long rows, 
 // row chunks of the column-sum producers: ~16 rows per block-lane pass, capped
 static long colsum_chunks(long rows) { return rows < 1024 ? (rows + 15) / 16 : (rows < 8192 ? 64 : 256); }
 
-KFA_API long kfa_colsum_part_floats(long rows, int N) {
-  const long chunks = colsum_chunks(rows);
-  return chunks * (long)N;
+KFA_API long kfa_colsum_part_floats(long rows, int N) {  // no scratch needed any more (ABI stability)
+  (void)rows; (void)N;
+  return 0;
 }
 
 // dx = dropout_mask(dy) * act'(x + b) (dx nullable: then only dbias is produced);
-// dbias (+)= column sums of dx.
+// dbias (+)= column sums of dx (fp32 atomics, one per column per block).
 KFA_API int kfa_bias_act_bwd(const void* dy, const void* x, const float* b, void* dx, float* part, float* dbias,
                              long rows, int N, int act, float p, unsigned long long seed, int accumulate,
                              hipStream_t s) {
+  (void)part;
   if (rows <= 0 || N % 8) return -1;
   const long chunks = colsum_chunks(rows);
   const long rpb = (rows + chunks - 1) / chunks;
   const uint32_t th = drop_thresh(p);
   const float ds = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  zero_if(dbias, N, accumulate, s);
   hipLaunchKernelGGL(bias_act_bwd_kernel, dim3((N + 511) / 512, (unsigned)chunks), dim3(256), 0, s,
-                     (const bf16_t*)dy, (const bf16_t*)x, b, (bf16_t*)dx, part, rows, N, act, rpb, th, ds,
+                     (const bf16_t*)dy, (const bf16_t*)x, b, (bf16_t*)dx, dbias, rows, N, act, rpb, th, ds,
                      (uint64_t)seed);
-  if (dbias)
-    hipLaunchKernelGGL(colsum_finalize_kernel, dim3((N + 63) / 64), dim3(256), 0, s, part, (int)chunks, (long)N, N,
-                       dbias, accumulate);
   return kfa_status();
 }
 
@@ -714,16 +696,15 @@ KFA_API int kfa_qkv_split(const void* qkv, const float* bias, void* q, void* k, 
 
 KFA_API int kfa_qkv_merge_bwd(const void* dq, const void* dk, const void* dv, void* dqkv, float* part, float* dbias,
                               long T, int S, int heads, int d, float qscale, int accumulate, hipStream_t s) {
+  (void)part;
   if (T <= 0 || T % S || d % 8) return -1;
   const int W = 3 * heads * d;
   const long chunks = colsum_chunks(T);
   const long rpb = (T + chunks - 1) / chunks;
+  zero_if(dbias, W, accumulate, s);
   hipLaunchKernelGGL(qkv_merge_bwd_kernel, dim3((W + 511) / 512, (unsigned)chunks), dim3(256), 0, s,
-                     (const bf16_t*)dq, (const bf16_t*)dk, (const bf16_t*)dv, (bf16_t*)dqkv, part, T, S, heads, d,
+                     (const bf16_t*)dq, (const bf16_t*)dk, (const bf16_t*)dv, (bf16_t*)dqkv, dbias, T, S, heads, d,
                      qscale, rpb);
-  if (dbias)
-    hipLaunchKernelGGL(colsum_finalize_kernel, dim3((W + 63) / 64), dim3(256), 0, s, part, (int)chunks, (long)W, W,
-                       dbias, accumulate);
   return kfa_status();
 }
 

@@ -1,0 +1,348 @@
+// Weight gradient of NHWC convolution / dense layers on MFMA (bf16 in, fp32
+// accumulate) — SURVEY §2.6 K7 (conv wgrad) and K1 (dW = dYᵀ·X).
+//
+//   dW[co][n] = Σ_k dY[k][co] · X̂[k][n],   n = (r, s, ci),  k = (img, p, q)
+//   X̂[k][(r,s,ci)] = X[img][p*st - pad + r][q*st - pad + s][ci]   (0 outside)
+//
+// The reduction runs over output PIXELS, which are the slow (row) dimension of
+// both operands: dY and X are stored channel-contiguous, so a k-slice of either
+// operand arrives as [k][channel] rows.  MFMA wants each lane's 8 k-values of
+// one row/column, i.e. the transpose — CDNA4's ds_read_b64_tr_b16 (T10) does
+// it in the LDS read: tiles are DMA'd (global_load_lds, 16 B/lane) lane-linear
+// into [k][128]-element images with the conflict-free XOR swizzle
+//   off(row, chunk) = 256*row + 16*(chunk ^ (((row&3)<<2) | ((row>>2)&3)))
+// applied on the per-lane SOURCE address, and each MFMA operand is two
+// transposed 8-byte reads.
+//
+// Blocks: 256 threads, 128x128 (2x2 waves), 64x128 (Co <= 64) or 128x64 (N <= 64)
+// tiles, BK = 64 pixels,
+// double-buffered (<= 64 KiB LDS, 2 blocks/CU).  Split-K over pixels when the
+// weight has too few tiles to fill the chip: each block
+// writes an fp32 partial tile; a second kernel sums the partials and adds them
+// (converted) straight into the flat gradient buffer (bf16 or fp32).
+#include "common.h"
+
+namespace {
+
+constexpr int BKW = 64;
+
+struct WGeo {
+  int H, W, Ci, P, Q, Co, R, S, st, pad;
+  int N;        // R*S*Ci
+  int K;        // Nb*P*Q  (pixels)
+  int kchunk;   // pixels per split (multiple of BKW)
+};
+
+__device__ __forceinline__ int fdiv(int x, int d, float rcp) {
+  int q = (int)((float)x * rcp);
+  const int r = x - q * d;
+  q += (r >= d) - (r < 0);
+  return q;
+}
+
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+
+// [k][WIDTH] bf16 LDS images (WIDTH = 128 or 64 elements = 256 / 128-B rows),
+// 16-B chunks XOR-swizzled so both the lane-linear DMA fill and the
+// ds_read_b64_tr_b16 operand reads are conflict-free:
+//   256-B rows: chunk ^ (((row&3)<<2) | ((row>>2)&3))           (16 chunks)
+//   128-B rows: chunk ^ 2*(((row>>1)&1) | (((row>>3)&1)<<1))     (8 chunks; keeps 32-B pairs)
+template <int WIDTH>
+__device__ __forceinline__ int img_swz(int row) {
+  if constexpr (WIDTH == 128) return ((row & 3) << 2) | ((row >> 2) & 3);
+  else return 2 * (((row >> 1) & 1) | (((row >> 3) & 1) << 1));
+}
+template <int WIDTH>
+__device__ __forceinline__ int img_off(int row, int col) {  // byte offset of element (row, col)
+  return WIDTH * 2 * row + 16 * ((col >> 3) ^ img_swz<WIDTH>(row)) + 2 * (col & 7);
+}
+
+// MFMA operand (8 consecutive k of one column) via two transposed reads:
+// rows kb + 8g + q and kb + 8g + 4 + q, columns cb + 4p (T10 lane map).
+template <int WIDTH>
+__device__ __forceinline__ short8 tr_operand(const bf16_t* tile, int kb, int cb, int lane) {
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const int col = cb + 4 * p;
+  const int r0 = kb + 8 * g + q;
+  const char* base = reinterpret_cast<const char*>(tile);
+  const v4i16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(base + img_off<WIDTH>(r0, col)));
+  const v4i16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(base + img_off<WIDTH>(r0 + 4, col)));
+  return short8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+
+// WM x WN waves, each TM x TN MFMA 16x16 tiles: block tile BM = 16*WM*TM output
+// channels x BN = 16*WN*TN (r,s,ci) columns.  OUT_PART: fp32 split-K partials;
+// otherwise the epilogue accumulates straight into the (bf16/fp32) gradient.
+template <int WM, int WN, int TM, int TN>
+__global__ __launch_bounds__(256, 2) void wgrad_kernel(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X,
+                                                       float* __restrict__ part, void* __restrict__ grad,
+                                                       int grad_f32, int accumulate, const bf16_t* __restrict__ Z,
+                                                       WGeo g) {
+  constexpr int BM = 16 * WM * TM, BN = 16 * WN * TN;
+  constexpr int A_RPI = 1024 / (BM * 2), B_RPI = 1024 / (BN * 2);  // tile rows per 1-KiB wave instruction
+  constexpr int A_IPW = BKW / A_RPI / 4, B_IPW = BKW / B_RPI / 4;    // instructions per wave per k-step
+  constexpr int A_CPR = BM / 8, B_CPR = BN / 8;                      // 16-B chunks per row
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  bf16_t* As = smem;                    // [2][BKW][BM]
+  bf16_t* Bs = smem + 2 * BKW * BM;     // [2][BKW][BN]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  const int ntn = (g.N + BN - 1) / BN;
+  const int m0 = (blockIdx.x / ntn) * BM, n0 = (blockIdx.x % ntn) * BN;
+  const int split = blockIdx.y;
+  const int kb = split * g.kchunk;
+  const int ke = min(g.K, kb + g.kchunk);
+  if (kb >= ke) return;
+  const int nsteps = (ke - kb + BKW - 1) / BKW;
+
+  // staging plan: this lane fills row (j*RPI + lane / CPR), physical chunk lane % CPR
+  int a_m[A_IPW], a_row[A_IPW];
+  bool a_ok[A_IPW];
+#pragma unroll
+  for (int i = 0; i < A_IPW; i++) {
+    const int j = wave * A_IPW + i;
+    const int row = j * A_RPI + lane / A_CPR;
+    const int ch = (lane % A_CPR) ^ img_swz<BM>(row);
+    a_row[i] = row;
+    a_m[i] = m0 + ch * 8;
+    a_ok[i] = a_m[i] < g.Co;
+  }
+  int b_ci[B_IPW], b_r[B_IPW], b_s[B_IPW], b_row[B_IPW];
+  bool b_ok[B_IPW];
+#pragma unroll
+  for (int i = 0; i < B_IPW; i++) {
+    const int j = wave * B_IPW + i;
+    const int row = j * B_RPI + lane / B_CPR;
+    const int ch = (lane % B_CPR) ^ img_swz<BN>(row);
+    const int n = n0 + ch * 8;
+    b_row[i] = row;
+    b_ok[i] = n < g.N;
+    const int tap = b_ok[i] ? n / g.Ci : 0;
+    b_ci[i] = n - tap * g.Ci;
+    b_r[i] = tap / g.S;
+    b_s[i] = tap - b_r[i] * g.S;
+  }
+  const int PQ = g.P * g.Q;
+  const float rPQ = 1.f / (float)PQ, rQ = 1.f / (float)g.Q;
+  const bool lin_b = g.R == 1 && g.S == 1 && g.st == 1 && g.pad == 0;  // X row k is pixel k
+
+  auto issue = [&](int step, int buf) {
+    const int k0 = kb + step * BKW;
+#pragma unroll
+    for (int i = 0; i < A_IPW; i++) {
+      const int j = wave * A_IPW + i;
+      const int k = k0 + a_row[i];
+      const bf16_t* sa = (k < ke && a_ok[i]) ? dY + (long)k * g.Co + a_m[i] : Z;
+      __builtin_amdgcn_global_load_lds(sa, (__attribute__((address_space(3))) void*)(As + buf * BKW * BM + j * A_RPI * BM),
+                                       16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < B_IPW; i++) {
+      const int j = wave * B_IPW + i;
+      const int k = k0 + b_row[i];
+      const bf16_t* sb = Z;
+      if (k < ke && b_ok[i]) {
+        if (lin_b) {
+          sb = X + (long)k * g.Ci + b_ci[i];
+        } else {
+          const int img = fdiv(k, PQ, rPQ), rem = k - img * PQ;
+          const int p = fdiv(rem, g.Q, rQ), q = rem - p * g.Q;
+          const int h = p * g.st - g.pad + b_r[i], w = q * g.st - g.pad + b_s[i];
+          if ((unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W)
+            sb = X + (((long)img * g.H + h) * g.W + w) * g.Ci + b_ci[i];
+        }
+      }
+      __builtin_amdgcn_global_load_lds(sb, (__attribute__((address_space(3))) void*)(Bs + buf * BKW * BN + j * B_RPI * BN),
+                                       16, 0, 0);
+    }
+  };
+
+  floatx4 acc[TN][TM];
+#pragma unroll
+  for (int a = 0; a < TN; a++)
+#pragma unroll
+    for (int b = 0; b < TM; b++) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  issue(0, 0);
+  for (int st = 0; st < nsteps; st++) {
+    const int buf = st & 1;
+    if (st + 1 < nsteps) {
+      issue(st + 1, buf ^ 1);
+      if constexpr (A_IPW + B_IPW == 8) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+      else if constexpr (A_IPW + B_IPW == 6) asm volatile("s_waitcnt vmcnt(6)\n\ts_barrier" ::: "memory");
+      else if constexpr (A_IPW + B_IPW == 4) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    const bf16_t* At = As + buf * BKW * BM;
+    const bf16_t* Bt = Bs + buf * BKW * BN;
+#pragma unroll
+    for (int ks = 0; ks < 2; ks++) {
+      short8 af[TM], bf[TN];
+#pragma unroll
+      for (int i = 0; i < TM; i++) af[i] = tr_operand<BM>(At, ks * 32, wm * TM * 16 + i * 16, lane);
+#pragma unroll
+      for (int i = 0; i < TN; i++) bf[i] = tr_operand<BN>(Bt, ks * 32, wn * TN * 16 + i * 16, lane);
+#pragma unroll
+      for (int ni = 0; ni < TN; ni++)
+#pragma unroll
+        for (int mi = 0; mi < TM; mi++)
+          acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[ni], af[mi], acc[ni][mi], 0, 0, 0);
+    }
+    lds_barrier();
+  }
+  // lane holds D[n = .. + (lane>>4)*4 + i][m = .. + (lane&15)]: 4 consecutive n per store
+#pragma unroll
+  for (int ni = 0; ni < TN; ni++) {
+    const int n = n0 + wn * TN * 16 + ni * 16 + (lane >> 4) * 4;
+#pragma unroll
+    for (int mi = 0; mi < TM; mi++) {
+      const int m = m0 + wm * TM * 16 + mi * 16 + (lane & 15);
+      if (m >= g.Co || n >= g.N) continue;
+      floatx4 v = acc[ni][mi];
+      const long e = (long)m * g.N + n;
+      if (part) {
+        *reinterpret_cast<floatx4*>(part + (long)split * g.Co * g.N + e) = v;
+      } else if (grad_f32) {
+        floatx4* gp = reinterpret_cast<floatx4*>(reinterpret_cast<float*>(grad) + e);
+        *gp = accumulate ? *gp + v : v;
+      } else {
+        uint2* gp = reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(grad) + e);
+        if (accumulate) {
+          const uint2 o = *gp;
+          v[0] += bf2f(o.x & 0xffff); v[1] += bf2f(o.x >> 16); v[2] += bf2f(o.y & 0xffff); v[3] += bf2f(o.y >> 16);
+        }
+        *gp = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+      }
+    }
+  }
+}
+
+// grad[i] (+)= sum_s part[s][i].  Block = 64 element-lanes (4 elements each)
+// x 4 split-lanes; each thread keeps 8 independent loads in flight (the split
+// count reaches hundreds for the early, pixel-heavy layers), then an LDS
+// reduce over the split-lanes.
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int splits, long total,
+                                                           void* __restrict__ grad, int grad_f32, int accumulate) {
+  __shared__ floatx4 red[4][64];
+  const int el = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const long i = (long)blockIdx.x * 64 + el;  // float4 index
+  floatx4 s = floatx4{0.f, 0.f, 0.f, 0.f};
+  if (i < total / 4) {
+    int k = sl;
+    for (; k + 28 < splits; k += 32) {
+      floatx4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) v[u] = *reinterpret_cast<const floatx4*>(part + (long)(k + 4 * u) * total + i * 4);
+#pragma unroll
+      for (int u = 0; u < 8; u++) s += v[u];
+    }
+    for (; k < splits; k += 4) s += *reinterpret_cast<const floatx4*>(part + (long)k * total + i * 4);
+  }
+  red[sl][el] = s;
+  __syncthreads();
+  if (sl != 0 || i >= total / 4) return;
+  s = red[0][el] + red[1][el] + red[2][el] + red[3][el];
+  if (grad_f32) {
+    floatx4* g = reinterpret_cast<floatx4*>(grad) + i;
+    *g = accumulate ? *g + s : s;
+  } else {
+    uint2* g = reinterpret_cast<uint2*>(grad) + i;
+    if (accumulate) {
+      const uint2 o = *g;
+      s[0] += bf2f(o.x & 0xffff); s[1] += bf2f(o.x >> 16); s[2] += bf2f(o.y & 0xffff); s[3] += bf2f(o.y >> 16);
+    }
+    *g = make_uint2(pack2(s[0], s[1]), pack2(s[2], s[3]));
+  }
+}
+
+const bf16_t* zero_page() {
+  static bf16_t* z = nullptr;
+  if (!z) {
+    if (hipMalloc(&z, 256) != hipSuccess) return nullptr;
+    (void)hipMemset(z, 0, 256);
+    (void)hipDeviceSynchronize();
+  }
+  return z;
+}
+
+int num_cus() {
+  static int cached = 0;
+  if (!cached) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cached, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cached <= 0) cached = 256;
+  }
+  return cached;
+}
+
+struct WPlan {
+  int variant;   // 0: 128x128, 1: 64x128 (Co <= 64), 2: 128x64 (N <= 64), 3: 64x64 (both)
+  int BM, BN, tiles, splits, kchunk;
+};
+
+WPlan plan(long K, int Co, int N) {
+  WPlan p;
+  p.variant = Co <= 64 ? (N <= 64 ? 3 : 1) : (N <= 64 ? 2 : 0);
+  p.BM = (p.variant == 1 || p.variant == 3) ? 64 : 128;
+  p.BN = (p.variant == 2 || p.variant == 3) ? 64 : 128;
+  p.tiles = ((Co + p.BM - 1) / p.BM) * ((N + p.BN - 1) / p.BN);
+  // one wave of blocks (2 per CU), each >= 4 k-steps; big-weight layers run
+  // without split-K and accumulate in the epilogue (no partial round trip)
+  const long steps = (K + BKW - 1) / BKW;
+  long splits = (2L * num_cus()) / p.tiles;
+  splits = splits < 1 ? 1 : splits;
+  const long max_splits = steps / 4 > 0 ? steps / 4 : 1;
+  if (splits > max_splits) splits = max_splits;
+  const long per = (steps + splits - 1) / splits;
+  p.kchunk = (int)(per * BKW);
+  p.splits = (int)((steps + per - 1) / per);
+  return p;
+}
+
+}  // namespace
+
+KFA_API long kfa_wgrad_part_floats(int Nb, int P, int Q, int Co, int R, int S, int Ci) {
+  const WPlan p = plan((long)Nb * P * Q, Co, R * S * Ci);
+  return p.splits > 1 ? (long)p.splits * Co * R * S * Ci : 0;
+}
+
+// dW (+)= conv weight gradient, written into `grad` ([Co][R][S][Ci], bf16 or fp32).
+KFA_API int kfa_conv_wgrad(const bf16_t* dY, const bf16_t* X, void* grad, int grad_f32, int accumulate, float* part,
+                           int Nb, int H, int W, int Ci, int P, int Q, int Co, int R, int S, int st, int pad,
+                           hipStream_t s) {
+  if (Ci % 8 || Co % 8) return -1;
+  const long K = (long)Nb * P * Q;
+  if (K >= (1L << 24)) return -2;  // fp32-reciprocal pixel division is exact below 2^24
+  WGeo g{H, W, Ci, P, Q, Co, R, S, st, pad, R * S * Ci, (int)K, 0};
+  const WPlan p = plan(K, Co, g.N);
+  g.kchunk = p.kchunk;
+  const size_t lds = (size_t)2 * BKW * (p.BM + p.BN) * sizeof(bf16_t);
+  float* pp = p.splits > 1 ? part : nullptr;
+  if (p.splits > 1 && !part) return -3;
+  dim3 grid(p.tiles, p.splits);
+  if (p.variant == 0)
+    hipLaunchKernelGGL((wgrad_kernel<2, 2, 4, 4>), grid, dim3(256), lds, s, dY, X, pp, grad, grad_f32, accumulate,
+                       zero_page(), g);
+  else if (p.variant == 1)
+    hipLaunchKernelGGL((wgrad_kernel<1, 4, 4, 2>), grid, dim3(256), lds, s, dY, X, pp, grad, grad_f32, accumulate,
+                       zero_page(), g);
+  else if (p.variant == 2)
+    hipLaunchKernelGGL((wgrad_kernel<4, 1, 2, 4>), grid, dim3(256), lds, s, dY, X, pp, grad, grad_f32, accumulate,
+                       zero_page(), g);
+  else
+    hipLaunchKernelGGL((wgrad_kernel<2, 2, 2, 2>), grid, dim3(256), lds, s, dY, X, pp, grad, grad_f32, accumulate,
+                       zero_page(), g);
+  if (p.splits > 1) {
+    const long total = (long)Co * g.N;
+    const long blocks = (total / 4 + 63) / 64;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, part, p.splits, total, grad,
+                       grad_f32, accumulate);
+  }
+  return kfa_status();
+}

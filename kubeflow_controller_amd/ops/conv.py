@@ -9,7 +9,10 @@
   (``os = 2``); classes with no taps are zero-filled;
 * dgrad can take the residual branch's gradient as an epilogue addend
   (``D = A.B^T + E``) — used where a tensor feeds both a conv and a skip path;
-* wgrad: vendor path for now (``aten.convolution_backward``).
+* wgrad: ``csrc/kernels/wgrad.hip`` — split-K MFMA GEMM over output pixels
+  with ``ds_read_b64_tr_b16`` transposed operand reads; the partial sums are
+  reduced straight into the weight's flat gradient view (direct-gradient
+  protocol), so no dW tensor and no AccumulateGrad add exist.
 
 The weight lives as ``[Cout, Cin, kh, kw]`` in channels_last memory, i.e.
 physically ``[Cout][kh][kw][Cin]`` — exactly the K-contiguous B operand.
@@ -25,14 +28,18 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _lib
+from ..parallel.flat import direct_grad_view, notify_grad_ready
 
 P, I = _lib.P, _lib.I
 _lib.register("kfa_conv_igemm", [P, P, P, P] + [I] * 20 + [P])
 _lib.register("kfa_zero_bf16", [P, _lib.L, P])
 _lib.register("kfa_weight_transpose", [P, P] + [I] * 10 + [P])
+_lib.register("kfa_wgrad_part_floats", [I] * 7, _lib.L)
+_lib.register("kfa_conv_wgrad", [P, P, P, I, I, P] + [I] * 11 + [P])
 
-# Runtime switch (tests compare against the vendor path); env KFA_CONV_IGEMM=0 disables.
+# Runtime switches (tests compare against the vendor path); env KFA_CONV_IGEMM=0 / KFA_WGRAD=0 disable.
 ENABLED = os.environ.get("KFA_CONV_IGEMM", "1") != "0"
+WGRAD_ENABLED = os.environ.get("KFA_WGRAD", "1") != "0"
 
 
 def igemm_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
@@ -104,10 +111,44 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride: int, pad: int
     return dx
 
 
-def conv_wgrad(x: torch.Tensor, dy: torch.Tensor, w: torch.Tensor, stride: int, pad: int) -> torch.Tensor:
+def conv_wgrad_vendor(x: torch.Tensor, dy: torch.Tensor, w: torch.Tensor, stride: int, pad: int) -> torch.Tensor:
     _, gw, _ = torch.ops.aten.convolution_backward(dy, x, w, None, [stride, stride], [pad, pad], [1, 1],
                                                    False, [0, 0], 1, [False, True, False])
     return gw
+
+
+def wgrad_ok(x: torch.Tensor, dy: torch.Tensor, w: torch.Tensor) -> bool:
+    return (WGRAD_ENABLED and x.is_cuda and x.dtype == torch.bfloat16 and dy.dtype == torch.bfloat16
+            and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0
+            and dy.shape[0] * dy.shape[2] * dy.shape[3] < (1 << 24))
+
+
+def wgrad_into(x, dy, out, Nb, H, W, Ci, P_, Q_, Co, R, S, stride, pad, accumulate: bool) -> None:
+    """out (+)= dW  for NHWC x [Nb,H,W,Ci] / dy [Nb,P,Q,Co]; out is [Co][R][S][Ci] (bf16 or fp32)."""
+    nfl = _lib.lib().kfa_wgrad_part_floats(Nb, P_, Q_, Co, R, S, Ci)
+    part = _lib.workspace(nfl * 4, x.device, "wgrad_part").view(torch.float32)
+    _lib.call("kfa_conv_wgrad", _lib.ptr(dy), _lib.ptr(x), _lib.ptr(out), int(out.dtype == torch.float32),
+              int(accumulate), _lib.ptr(part), Nb, H, W, Ci, P_, Q_, Co, R, S, stride, pad, _lib.stream())
+
+
+def conv_wgrad(x: torch.Tensor, dy: torch.Tensor, w: torch.Tensor, stride: int, pad: int, wparam=None):
+    """Weight gradient.  Returns None when it was accumulated directly into the
+    parameter's flat gradient buffer (and the bucket notified), else dW."""
+    if not wgrad_ok(x, dy, w):
+        return conv_wgrad_vendor(x, dy, w, stride, pad)
+    x, dy = _cl(x), _cl(dy)
+    Nb, Ci, H, W = x.shape
+    Co, _, R, S = w.shape
+    P_, Q_ = dy.shape[2], dy.shape[3]
+    target = direct_grad_view(wparam) if wparam is not None else None
+    if target is not None and target.dtype in (torch.bfloat16, torch.float32) and \
+            target.is_contiguous(memory_format=torch.channels_last):
+        wgrad_into(x, dy, target, Nb, H, W, Ci, P_, Q_, Co, R, S, stride, pad, accumulate=True)
+        notify_grad_ready(wparam)
+        return None
+    dw = torch.empty_like(w, memory_format=torch.channels_last)
+    wgrad_into(x, dy, dw, Nb, H, W, Ci, P_, Q_, Co, R, S, stride, pad, accumulate=False)
+    return dw
 
 
 class GradJoin:
@@ -156,6 +197,7 @@ class _ConvFn(torch.autograd.Function):
     def forward(ctx, x, w, stride, pad, join):
         ctx.save_for_backward(x, w)
         ctx.stride, ctx.pad, ctx.join = stride, pad, join
+        ctx.wparam = w  # the Parameter itself (for the direct flat-gradient write)
         return conv_fwd(x, w, stride, pad)
 
     @staticmethod
@@ -177,7 +219,7 @@ class _ConvFn(torch.autograd.Function):
                 if addend is not None:
                     dx = dx + addend
         if ctx.needs_input_grad[1]:
-            dw = conv_wgrad(x, dy, w, ctx.stride, ctx.pad)
+            dw = conv_wgrad(x, dy, w, ctx.stride, ctx.pad, ctx.wparam)
         return dx, dw, None, None, None
 
 

@@ -95,3 +95,44 @@ def test_resnet_block_grads_igemm_vs_vendor():
         if e_f > 2.0 * e_v + 0.02 * scale or e_u > 2.0 * e_v + 0.02 * scale:
             bad.append((n, e_f, e_u, e_v, scale))
     assert not bad, bad
+
+
+@pytest.mark.parametrize("rows,out_f,in_f", [(8192, 2304, 768), (4096, 768, 3072), (1000, 64, 136)])
+def test_wgrad_dense_shapes(rows, out_f, in_f):
+    """dW = dYᵀ·X through the wgrad kernel as a 1x1 conv over `rows` pixels."""
+    from kubeflow_controller_amd.ops.conv import wgrad_into
+    torch.manual_seed(0)
+    d = torch.device("cuda")
+    x = torch.randn(rows, in_f, device=d).to(torch.bfloat16)
+    dy = torch.randn(rows, out_f, device=d).to(torch.bfloat16)
+    ref = dy.float().t() @ x.float()
+    out = torch.full((out_f, in_f), 0.5, device=d)  # fp32 target, accumulate
+    wgrad_into(x, dy, out, 1, 1, rows, in_f, 1, rows, out_f, 1, 1, 1, 0, accumulate=True)
+    err = (out - 0.5 - ref).abs().max().item()
+    assert err < 1e-2 * ref.abs().max().item(), err
+    outb = torch.zeros(out_f, in_f, device=d, dtype=torch.bfloat16)
+    wgrad_into(x, dy, outb, 1, 1, rows, in_f, 1, rows, out_f, 1, 1, 1, 0, accumulate=False)
+    err = (outb.float() - ref).abs().max().item()
+    assert err < 2e-2 * ref.abs().max().item(), err
+
+
+def test_wgrad_direct_into_flat_buffer():
+    from kubeflow_controller_amd.ops.conv import Conv2d
+    from kubeflow_controller_amd.parallel.flat import FlatGroup, set_ready_callback
+    d = torch.device("cuda")
+    torch.manual_seed(0)
+    conv = Conv2d(64, 128, 3, stride=2, padding=1).to(d)
+    conv.weight.data = conv.weight.data.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    g = FlatGroup([conv.weight])
+    seen = []
+    set_ready_callback(conv.weight, lambda p: seen.append(p))
+    x = torch.randn(4, 64, 28, 28, device=d).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y = conv(x)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xf = x.float().requires_grad_()
+    wf = conv.weight.detach().float().requires_grad_()
+    torch.nn.functional.conv2d(xf, wf, None, 2, 1).backward(dy.float())
+    assert len(seen) == 1 and conv.weight.grad.data_ptr() == g.grad.data_ptr()
+    err = (conv.weight.grad.float() - wf.grad).abs().max().item()
+    assert err < 3e-2 * wf.grad.abs().max().item(), err

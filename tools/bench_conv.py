@@ -2,7 +2,7 @@
 import sys
 import torch
 import torch.nn.functional as F
-from kubeflow_controller_amd.ops.conv import conv_fwd, conv_dgrad
+from kubeflow_controller_amd.ops.conv import conv_fwd, conv_dgrad, wgrad_into
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 torch.backends.cudnn.benchmark = True
@@ -30,7 +30,7 @@ def t(fn, it=20):
     return e0.elapsed_time(e1) / it
 
 
-tot = {"ours_f": 0, "torch_f": 0, "ours_d": 0, "torch_d": 0, "torch_w": 0}
+tot = {"ours_f": 0, "torch_f": 0, "ours_d": 0, "torch_d": 0, "ours_w": 0, "torch_w": 0}
 for (Cin, H, Cout, k, s, p, cnt) in SH:
     x = torch.randn(B, Cin, H, H, device=d, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
     w = (torch.randn(Cout, Cin, k, k, device=d) * 0.05).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
@@ -44,9 +44,13 @@ for (Cin, H, Cout, k, s, p, cnt) in SH:
                                                           [0, 0], 1, [True, False, False]))
     tw = t(lambda: torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [p, p], [1, 1], False,
                                                           [0, 0], 1, [False, True, False]))
-    for k_, v in (("ours_f", of), ("torch_f", tf), ("ours_d", od), ("torch_d", td), ("torch_w", tw)):
+    gw = torch.zeros_like(w)
+    P_, Q_ = y.shape[2], y.shape[3]
+    ow = t(lambda: wgrad_into(x, dy, gw, B, H, H, Cin, P_, Q_, Cout, k, k, s, p, True))
+    for k_, v in (("ours_f", of), ("torch_f", tf), ("ours_d", od), ("torch_d", td), ("ours_w", ow), ("torch_w", tw)):
         tot[k_] += v * cnt
     print(f"Cin{Cin:5d} H{H:3d} Cout{Cout:5d} k{k} s{s} x{cnt}: fwd ours {of:.3f}ms ({flops/of/1e9:.0f} TF) "
-          f"torch {tf:.3f}ms ({flops/tf/1e9:.0f} TF) | dgrad ours {od:.3f} torch {td:.3f} | wgrad torch {tw:.3f}",
+          f"torch {tf:.3f}ms ({flops/tf/1e9:.0f} TF) | dgrad ours {od:.3f} torch {td:.3f} | wgrad ours {ow:.3f} "
+          f"torch {tw:.3f}",
           flush=True)
 print("TOTAL (x count) ms:", {k: round(v, 2) for k, v in tot.items()})
