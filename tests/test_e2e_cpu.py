@@ -40,6 +40,15 @@ def _job(name, replicas_spec, restart="OnFailure", cmd=None):
                                      "metadata": {"name": name}, "spec": {"tfReplicaSpec": specs}})
 
 
+def _alive(pid):
+    """True while pid exists and is not a zombie (tolerates it vanishing mid-check)."""
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            return f.read().split()[2] != "Z"
+    except (FileNotFoundError, ProcessLookupError, IndexError):
+        return False
+
+
 def _logs(root, pod):
     d = os.path.join(root, f"default_{pod.metadata.name}")
     return "".join(open(os.path.join(d, f)).read() for f in os.listdir(d) if f.endswith(".log"))
@@ -124,13 +133,12 @@ def test_delete_tfjob_kills_replicas(node):
     assert len(pids) == 2
     st.delete(v1alpha1.TFJOB_KIND, "default", "sleeper")
     deadline = time.time() + 20
-    while time.time() < deadline and any(os.path.exists(f"/proc/{p}") and
-                                         open(f"/proc/{p}/stat").read().split()[2] != "Z" for p in pids):
+    while time.time() < deadline and any(_alive(p) for p in pids):
         time.sleep(0.1)
     left = st.list("Pod") + st.list("Service")
     assert left == [], [(o.kind, o.metadata.name, o.metadata.resourceVersion, o.metadata.ownerReferences) for o in left]
     for p in pids:
-        assert not os.path.exists(f"/proc/{p}") or open(f"/proc/{p}/stat").read().split()[2] == "Z"
+        assert not _alive(p)
 
 
 def test_gpu_binding_policy(tmp_path):
