@@ -1,0 +1,159 @@
+"""Asynchronous parameter server — the reference's DEFAULT update mode
+(``mnist_replica.py`` without ``--sync_replicas``: between-graph replication,
+variables round-robin on PS tasks via ``replica_device_setter`` :137-141, every
+worker's ``sess.run(train_step)`` pulls the variables, computes gradients
+against that (possibly stale) copy and pushes them to the PS, which applies
+Adam immediately :184,:256; the global step advances once per push).
+
+Transport (SURVEY §5.8 "Async PS = send/recv to the owner rank", H5): a
+process group over workers AND PS tasks (ranks ``0..W-1`` workers, ``W..W+P-1``
+PS tasks).  Each PS runs a single-threaded service loop that receives request
+headers from ANY worker (``recv(src=None)``), so workers progress
+independently — no collective, no lock-step:
+
+* ``PULL``  → PS sends its shard (all owned tensors, flattened fp32);
+* ``PUSH``  → PS receives the gradient for its shard, applies Adam to it in
+  place (owner-side apply, optimizer state lives only on the PS) and replies
+  with the new global step (PS 0 owns the global step counter);
+* ``DONE``  → a worker finished; the PS exits when every worker has.
+
+Headers and payloads use distinct tags, and every request from one worker is
+sequential, so a PS never interleaves two workers' payloads.  The payload is a
+host (CPU) tensor: on the gloo transport this is TF's gRPC PS in spirit.  The
+synchronous modes (``--sync_replicas``, or no PS) use RCCL reduce-scatter /
+all-gather on the GPUs instead (``parallel/ps.py``, ``parallel/ddp.py``).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+from .ps import ps_assignment
+
+PULL, PUSH, DONE = 1, 2, 3
+TAG_HDR, TAG_DATA, TAG_REPLY = 11, 12, 13
+
+
+def _layout(shapes: Sequence[Tuple[str, torch.Size]], assignment: Dict[str, int], ps: int):
+    """names owned by PS ``ps`` in declaration order, and the flat size."""
+    names = [n for n, _ in shapes if assignment[n] == ps]
+    sizes = {n: int(torch.Size(s).numel()) for n, s in shapes}
+    return names, sum(sizes[n] for n in names)
+
+
+class AsyncPSServer:
+    """Service loop of PS task ``ps_index`` (rank ``num_workers + ps_index``)."""
+
+    def __init__(self, init_params: Sequence[Tuple[str, torch.Tensor]], num_workers: int, num_ps: int, ps_index: int,
+                 lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, optimizer: str = "adam", group=None):
+        self.W, self.P, self.idx = num_workers, num_ps, ps_index
+        shapes = [(n, p.shape) for n, p in init_params]
+        self.assignment = ps_assignment(list(init_params), num_ps)
+        self.names, n = _layout(shapes, self.assignment, ps_index)
+        src = dict(init_params)
+        self.w = torch.cat([src[k].detach().float().reshape(-1).cpu() for k in self.names]) if self.names \
+            else torch.zeros(0)
+        self.m = torch.zeros_like(self.w)
+        self.v = torch.zeros_like(self.w)
+        self.lr, self.betas, self.eps, self.opt = lr, betas, eps, optimizer
+        self.t = 0
+        self.global_step = 0
+        self.group = group
+
+    def _apply(self, g: torch.Tensor) -> None:
+        self.t += 1
+        if self.opt == "sgd":
+            self.w.add_(g, alpha=-self.lr)
+            return
+        b1, b2 = self.betas
+        self.m.mul_(b1).add_(g, alpha=1 - b1)
+        self.v.mul_(b2).addcmul_(g, g, value=1 - b2)
+        step = self.lr * math.sqrt(1 - b2 ** self.t) / (1 - b1 ** self.t)  # TF AdamOptimizer form
+        self.w.addcdiv_(self.m, self.v.sqrt().add_(self.eps), value=-step)
+
+    def serve(self, log=None) -> int:
+        """Run until every worker sent DONE; returns the number of pushes applied."""
+        active = self.W
+        hdr = torch.zeros(2, dtype=torch.int64)
+        grad = torch.empty_like(self.w)
+        pushes = 0
+        while active > 0:
+            src = dist.recv(hdr, src=None, group=self.group, tag=TAG_HDR)
+            op = int(hdr[0])
+            if op == PULL:
+                dist.send(self.w, src, group=self.group, tag=TAG_DATA)
+            elif op == PUSH:
+                dist.recv(grad, src, group=self.group, tag=TAG_DATA)
+                self._apply(grad)
+                pushes += 1
+                self.global_step += 1
+                dist.send(torch.tensor([self.global_step], dtype=torch.int64), src, group=self.group,
+                          tag=TAG_REPLY)
+                if log and self.global_step % 50 == 0:
+                    log(f"PS {self.idx}: applied {self.global_step} updates")
+            elif op == DONE:
+                active -= 1
+            else:
+                raise RuntimeError(f"PS {self.idx}: bad request {op} from rank {src}")
+        return pushes
+
+
+class AsyncPSClient:
+    """Worker side: pull variables from / push gradients to every PS task."""
+
+    def __init__(self, params: Sequence[Tuple[str, torch.nn.Parameter]], num_workers: int, num_ps: int, group=None):
+        self.W, self.P, self.group = num_workers, num_ps, group
+        self.params = list(params)
+        self.assignment = ps_assignment(self.params, num_ps)
+        shapes = [(n, p.shape) for n, p in self.params]
+        by_name = dict(self.params)
+        self.plan: List[Tuple[int, List[torch.nn.Parameter], torch.Tensor]] = []
+        for k in range(num_ps):
+            names, n = _layout(shapes, self.assignment, k)
+            self.plan.append((num_workers + k, [by_name[x] for x in names], torch.zeros(n)))
+        self._hdr = torch.zeros(2, dtype=torch.int64)
+
+    def pull(self) -> None:
+        for rank, ps, buf in self.plan:
+            if not ps:
+                continue
+            self._hdr[0] = PULL
+            dist.send(self._hdr, rank, group=self.group, tag=TAG_HDR)
+            dist.recv(buf, rank, group=self.group, tag=TAG_DATA)
+            off = 0
+            with torch.no_grad():
+                for p in ps:
+                    n = p.numel()
+                    p.copy_(buf[off:off + n].view_as(p))
+                    off += n
+
+    def push(self) -> int:
+        """Send every PS its gradient shard; returns the global step reported by PS 0."""
+        step = -1
+        reply = torch.zeros(1, dtype=torch.int64)
+        for k, (rank, ps, buf) in enumerate(self.plan):
+            if not ps:
+                continue
+            off = 0
+            for p in ps:
+                n = p.numel()
+                if p.grad is None:
+                    buf[off:off + n].zero_()
+                else:
+                    buf[off:off + n].copy_(p.grad.reshape(-1))
+                off += n
+            self._hdr[0] = PUSH
+            dist.send(self._hdr, rank, group=self.group, tag=TAG_HDR)
+            dist.send(buf, rank, group=self.group, tag=TAG_DATA)
+            dist.recv(reply, rank, group=self.group, tag=TAG_REPLY)
+            if k == 0:
+                step = int(reply[0])
+        return step
+
+    def done(self) -> None:
+        self._hdr[0] = DONE
+        for rank, _, _ in self.plan:
+            dist.send(self._hdr, rank, group=self.group, tag=TAG_HDR)

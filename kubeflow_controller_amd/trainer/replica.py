@@ -17,13 +17,16 @@ Roles (``mnist_replica.py:107-122``):
   ``server.join()``s forever; here the job completes.
   Parameter shards are owned by worker ranks (``parallel/ps.py``).
 
-Update semantics: with PS replicas the step is push (reduce-scatter) ->
-owner-side fused optimizer -> pull (all-gather); without PS, bucketed
-all-reduce.  Both are synchronous.  ``--sync_replicas`` off (the reference's
-async default) keeps the reference's step ACCOUNTING — every worker's push
-advances the global step, so ``train_steps`` global steps take
-``ceil(train_steps / workers)`` local steps — but the update itself is
-synchronous (strictly stronger consistency than async PS).
+Update semantics (``--ps_mode``):
+* ``async`` — the reference's default (no ``--sync_replicas``): PS tasks hold
+  the variables and Adam state and serve pull/push requests from any worker
+  (``parallel/async_ps.py``); workers run at their own pace and stop once the
+  global step (advanced by every push) reaches ``train_steps``.
+* ``collective`` — push = RCCL reduce-scatter -> owner-side fused optimizer ->
+  pull = all-gather on the worker GPUs (PS processes coordinate only;
+  co-located PS); without PS, bucketed all-reduce.  Used for
+  ``--sync_replicas`` and for the large models (``auto``), where moving the
+  variables through host memory every step would dominate.
 """
 from __future__ import annotations
 
@@ -111,7 +114,107 @@ def synthetic_batch(args, model, device, rank: int):
     raise ValueError(args.model)
 
 
+def _async_mode(spec: ClusterSpec, args) -> bool:
+    if spec.is_local or not spec.ps:
+        return False
+    if args.ps_mode == "auto":
+        return not args.sync_replicas and args.model.startswith("mnist")
+    return args.ps_mode == "async"
+
+
 # ------------------------------------------------------------------ roles
+def run_ps_async(spec: ClusterSpec, args) -> int:
+    """PS task of the async mode: own the round-robin-placed variables, serve pulls/pushes."""
+    from ..parallel.async_ps import AsyncPSServer
+    W, P = spec.num_workers, len(spec.ps)
+    rank = W + spec.task_index
+    _log(f"PS {spec.task_index}: async parameter server, rank {rank} of {W} workers + {P} ps at "
+         f"{'%s:%d' % spec.rendezvous()}")
+    t0 = time.time()
+    store = None
+    while store is None:
+        try:
+            store = _store(spec, False, timeout=args.ps_connect_timeout)
+        except Exception as e:  # chief not up yet
+            if time.time() - t0 > args.ps_connect_timeout:
+                _log(f"PS {spec.task_index}: chief unreachable ({e}); exiting")
+                return 1
+            time.sleep(0.5)
+    dist.init_process_group("gloo", store=store, rank=rank, world_size=W + P)
+    torch.manual_seed(args.seed)  # same initial values as every worker's model
+    model, _, _ = build(args, torch.device("cpu"))
+    server = AsyncPSServer(list(model.named_parameters()), W, P, spec.task_index, lr=args.learning_rate,
+                           optimizer=args.optimizer)
+    _log(f"PS {spec.task_index}: serving {len(server.names)} variables ({server.w.numel()} values)")
+    pushes = server.serve(log=_log)
+    _log(f"PS {spec.task_index}: all {W} workers done after {pushes} updates; exiting")
+    dist.destroy_process_group()
+    return 0
+
+
+def run_worker_async(spec: ClusterSpec, args) -> int:
+    """Between-graph replicated async training against the PS tasks (``mnist_replica.py:251-264``)."""
+    from ..ops.loss import accuracy, cross_entropy
+    from ..parallel.async_ps import AsyncPSClient
+    W, P = spec.num_workers, len(spec.ps)
+    use_gpu = _use_gpu(args)
+    device = torch.device("cuda", 0) if use_gpu else torch.device("cpu")
+    if not use_gpu and not os.environ.get("OMP_NUM_THREADS"):
+        torch.set_num_threads(max(1, (os.cpu_count() or 1) // (W + P)))
+    if use_gpu:
+        torch.cuda.set_device(0)
+    store = _store(spec, spec.is_chief)
+    dist.init_process_group("gloo", store=store, rank=spec.task_index, world_size=W + P)
+    torch.manual_seed(args.seed)
+    args.num_ps = P
+    model, data, loss_fn = build(args, device)
+    model = model.to(device)
+    client = AsyncPSClient(list(model.named_parameters()), W, P)
+    _log(f"Worker {spec.task_index}: {W} workers, {P} ps, device {device}, model {args.model}, "
+         f"{sum(p.numel() for p in model.parameters())} params, async parameter server")
+    fixed = None if data is not None else synthetic_batch(args, model, device, spec.task_index)
+    t_begin = time.time()
+    _log(f"Training begins @ {t_begin:f}")
+    local_step, global_step, t_first, loss = 0, 0, None, None
+    while global_step < args.train_steps:
+        if data is not None:
+            xb, yb = data.next_batch(args.batch_size)
+            batch = (xb.to(device), yb.to(device))
+        else:
+            batch = fixed
+        client.pull()
+        model.zero_grad(set_to_none=False)
+        loss = loss_fn(model, *batch)
+        loss.backward()
+        global_step = client.push()
+        local_step += 1
+        if t_first is None:
+            t_first = time.time()
+        if args.log_every and local_step % args.log_every == 0:
+            _log(f"{time.time():f}: Worker {spec.task_index}: training step {local_step} done "
+                 f"(global step: {global_step})")
+    t_end = time.time()
+    _log(f"Training ends @ {t_end:f}")
+    _log(f"Training elapsed time: {t_end - t_begin:f} s")
+    if t_first is not None and local_step > 1:
+        sps = (local_step - 1) / max(t_end - t_first, 1e-9)
+        _log(f"Steady-state: {sps:.1f} steps/s/worker, {sps * args.batch_size:.1f} examples/s (this worker)")
+    client.pull()  # evaluate the PS's current variables, as the reference's session does
+    client.done()
+    if data is not None:
+        with torch.no_grad():
+            model.eval()
+            vx, vy = data.validation
+            ce = float(cross_entropy(model(vx.to(device)).float(), vy.to(device))) * vx.shape[0]
+            _log(f"After {global_step} training step(s), validation cross entropy = {ce:g}")
+            tx, ty = data.test
+            _log(f"Test accuracy: {float(accuracy(model(tx.to(device)).float(), ty.to(device))):.4f}")
+    elif loss is not None:
+        _log(f"Final loss: {float(loss):.5f}")
+    dist.destroy_process_group()
+    return 0
+
+
 def run_ps(spec: ClusterSpec, args) -> int:
     """PS coordinator: follow the global step until every worker is done."""
     _log(f"PS {spec.task_index}: joining job with {spec.num_workers} workers at "
@@ -279,6 +382,10 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--hidden_units", type=int, default=100)
     ap.add_argument("--seq_len", type=int, default=128)
     ap.add_argument("--sync_replicas", action="store_true")
+    ap.add_argument("--ps_mode", default="auto", choices=["auto", "async", "collective"],
+                    help="async: PS tasks own variables + Adam (reference default); collective: RCCL "
+                         "reduce-scatter/all-gather on the workers; auto: async for MNIST without "
+                         "--sync_replicas, collective otherwise")
     ap.add_argument("--replicas_to_aggregate", type=int, default=None, help="accepted; = #workers")
     ap.add_argument("--num_gpus", type=int, default=1, help="accepted (one GPU per replica)")
     ap.add_argument("--data_dir", default="", help="accepted (synthetic data; no network)")
@@ -295,6 +402,8 @@ def build_parser() -> argparse.ArgumentParser:
 def main(argv: Optional[list] = None) -> int:
     args = build_parser().parse_args(argv)
     spec = parse_cluster(args)
+    if _async_mode(spec, args):
+        return run_ps_async(spec, args) if spec.is_ps else run_worker_async(spec, args)
     if spec.is_ps:
         return run_ps(spec, args)
     return run_worker(spec, args)

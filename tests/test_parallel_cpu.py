@@ -170,3 +170,50 @@ def test_bert_tiny_cpu_trains():
     batch = synthetic_mlm_batch(cfg, 4, 32, torch.Generator().manual_seed(0))
     losses = [float(eng.train_step(*batch)) for _ in range(15)]
     assert losses[-1] < losses[0] - 0.5, losses
+
+
+def _async_ps_worker(rank, W, P, port, out):
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    from kubeflow_controller_amd.parallel.async_ps import AsyncPSClient, AsyncPSServer
+    torch.set_num_threads(1)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=W + P)
+    m = torch.nn.Sequential(torch.nn.Linear(300, 20), torch.nn.Linear(20, 4))
+    for p in m.parameters():
+        torch.nn.init.constant_(p, 0.5)
+    if rank >= W:
+        s = AsyncPSServer(list(m.named_parameters()), W, P, rank - W, lr=0.25, optimizer="sgd")
+        pushes = s.serve()
+        torch.save({"w": s.w, "names": s.names, "pushes": pushes, "step": s.global_step}, f"{out}.ps{rank - W}")
+    else:
+        c = AsyncPSClient(list(m.named_parameters()), W, P)
+        steps = []
+        for _ in range(7):
+            c.pull()
+            for p in m.parameters():
+                p.grad = torch.full_like(p, float(rank + 1))
+            steps.append(c.push())
+        c.pull()
+        c.done()
+        torch.save({"steps": steps, "final": {n: p.detach().clone() for n, p in m.named_parameters()}},
+                   f"{out}.w{rank}")
+    dist.destroy_process_group()
+
+
+def test_async_ps_applies_every_push_exactly_once(tmp_path):
+    """Async PS (reference default mode): any-source service loop, round-robin
+    placement over 2 PS tasks, every worker push applied once; global step from PS 0."""
+    W, P = 3, 2
+    out = str(tmp_path / "aps")
+    mp.start_processes(_async_ps_worker, args=(W, P, _free_port(), out), nprocs=W + P, join=True,
+                       start_method="spawn")
+    total = 0.25 * 7 * sum(range(1, W + 1))       # lr * steps * sum of the constant grads
+    names = ["0.weight", "0.bias", "1.weight", "1.bias"]
+    for k in range(P):
+        ps = torch.load(f"{out}.ps{k}", weights_only=True)
+        assert ps["names"] == names[k::P]                     # replica_device_setter round-robin
+        assert ps["pushes"] == 7 * W
+        torch.testing.assert_close(ps["w"], torch.full_like(ps["w"], 0.5 - total))
+    steps = sorted(s for w in range(W) for s in torch.load(f"{out}.w{w}", weights_only=True)["steps"])
+    assert steps == list(range(1, 7 * W + 1))                  # every push advanced the global step once
