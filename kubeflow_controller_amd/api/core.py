@@ -156,6 +156,35 @@ class Service(Model):
 
 
 @dataclass(eq=False)
+class LabelSelector(Model):
+    matchLabels: Dict[str, str] = jfield("matchLabels", factory=dict)
+
+
+@dataclass(eq=False)
+class ReplicaSetSpec(Model):
+    replicas: Optional[int] = jfield("replicas", None, ptr=True)
+    selector: LabelSelector = jfield("selector", factory=LabelSelector)
+    template: PodTemplateSpec = jfield("template", factory=PodTemplateSpec)
+
+
+@dataclass(eq=False)
+class ReplicaSetStatus(Model):
+    replicas: int = jfield("replicas", 0, omitempty=False)
+    readyReplicas: int = jfield("readyReplicas", 0)
+
+
+@dataclass(eq=False)
+class ReplicaSet(Model):
+    """``extensions/v1beta1`` ReplicaSet — only for the (unused) ReplicaSet control
+    the reference ships (``pkg/controller/control/replicaset.go``)."""
+    apiVersion: str = jfield("apiVersion", "extensions/v1beta1")
+    kind: str = jfield("kind", "ReplicaSet")
+    metadata: ObjectMeta = jfield("metadata", factory=ObjectMeta)
+    spec: ReplicaSetSpec = jfield("spec", factory=ReplicaSetSpec)
+    status: ReplicaSetStatus = jfield("status", factory=ReplicaSetStatus)
+
+
+@dataclass(eq=False)
 class ObjectReference(Model):
     kind: str = jfield("kind", "")
     namespace: str = jfield("namespace", "")

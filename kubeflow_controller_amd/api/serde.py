@@ -14,7 +14,7 @@ from typing import Any, Dict, Iterable, List, Optional
 import yaml
 
 from . import v1alpha1
-from .core import Event, Pod, Service
+from .core import Event, Pod, ReplicaSet, Service
 from .model import Model
 
 # kind -> class ; (apiVersion check is lenient for core kinds)
@@ -23,6 +23,7 @@ SCHEME = {
     "Pod": Pod,
     "Service": Service,
     "Event": Event,
+    "ReplicaSet": ReplicaSet,
 }
 
 # plural resource names used by the REST store / CLI
@@ -31,6 +32,7 @@ RESOURCES = {
     "pods": "Pod", "pod": "Pod", "po": "Pod",
     "services": "Service", "service": "Service", "svc": "Service",
     "events": "Event", "event": "Event", "ev": "Event",
+    "replicasets": "ReplicaSet", "replicaset": "ReplicaSet", "rs": "ReplicaSet",
 }
 
 _ENV_RE = re.compile(r"\$(\{([A-Za-z_][A-Za-z0-9_]*)\}|([A-Za-z_][A-Za-z0-9_]*))")

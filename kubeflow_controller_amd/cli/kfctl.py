@@ -250,6 +250,32 @@ def cmd_up(args) -> int:
     return controller_main(argv)
 
 
+def cmd_kill(args) -> int:
+    """Fault injection: signal a running replica's process group
+    (pid from the pod's container status), as a crashed container would be; the
+    kubelet then applies the pod's restartPolicy."""
+    import signal as _signal
+    st = _store(args)
+    pod = st.get("Pod", args.namespace, args.pod)
+    cs = pod.status.containerStatuses[0] if pod.status.containerStatuses else None
+    if not cs or not cs.pid or pod.status.phase != "Running":
+        raise ValueError(f"pod {args.pod} has no running replica process")
+    sig = getattr(_signal, args.signal if args.signal.startswith("SIG") else "SIG" + args.signal)
+    os.killpg(cs.pid, sig)
+    print(f"pod \"{args.pod}\" pid {cs.pid} sent {sig.name}")
+    return 0
+
+
+def cmd_metrics(args) -> int:
+    """Print the controller's Prometheus metrics (GET /metrics on the apiserver)."""
+    import urllib.request
+    if not args.master:
+        raise ValueError("kfctl metrics needs --master (the standalone apiserver URL)")
+    with urllib.request.urlopen(args.master.rstrip("/") + "/metrics", timeout=10) as r:
+        sys.stdout.write(r.read().decode())
+    return 0
+
+
 def build_parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser(prog="kfctl", description=__doc__,
                                  formatter_class=argparse.RawDescriptionHelpFormatter)
@@ -285,6 +311,11 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--for", dest="phase", default="Succeeded,Failed")
     p.add_argument("--timeout", type=float, default=600.0)
     p.set_defaults(fn=cmd_wait)
+    p = sub.add_parser("kill"); ns(p)
+    p.add_argument("pod"); p.add_argument("--signal", default="SIGKILL")
+    p.set_defaults(fn=cmd_kill)
+    p = sub.add_parser("metrics")
+    p.set_defaults(fn=cmd_metrics)
     p = sub.add_parser("apiserver")
     p.add_argument("--listen", default="127.0.0.1:8443"); p.add_argument("--data-dir", default="")
     p.add_argument("--url-file", default="")

@@ -73,6 +73,10 @@ class _CoreV1:
     def events(self, namespace: str = "") -> ResourceClient:
         return ResourceClient(self._store, "Event", namespace)
 
+    def replica_sets(self, namespace: str = "") -> ResourceClient:
+        """extensions/v1beta1 ReplicaSets (served here for the reference's ReplicaSet control)."""
+        return ResourceClient(self._store, "ReplicaSet", namespace)
+
     Pods = pods
     Services = services
     Events = events

@@ -22,6 +22,7 @@ import json
 import threading
 from typing import Dict, List, Optional
 
+from ..utils import metrics
 from ..api.core import CREATED_BY_ANNOTATION, Pod, PodTemplateSpec, Service
 from ..api.meta import ObjectMeta, OwnerReference
 from ..api.model import deep_copy
@@ -35,6 +36,8 @@ SUCCESSFUL_DELETE_POD_REASON = "SuccessfulDelete"
 FAILED_CREATE_SERVICE_REASON = "FailedCreate"
 SUCCESSFUL_CREATE_SERVICE_REASON = "SuccessfulCreate"
 FAILED_DELETE_SERVICE_REASON = "FailedDelete"
+FAILED_CREATE_REPLICASET_REASON = "FailedCreate"
+SUCCESSFUL_CREATE_REPLICASET_REASON = "SuccessfulCreate"
 SUCCESSFUL_DELETE_SERVICE_REASON = "SuccessfulDelete"
 
 
@@ -91,8 +94,10 @@ class RealPodControl:
             created = self.client.core_v1().pods(namespace).create(pod)
         except Exception as e:
             self.recorder.event(parent, WARNING, FAILED_CREATE_POD_REASON, f"Error creating: {e}")
+            metrics.CHILDREN_CREATED.labels("Pod", "failure").inc()
             raise
         self.recorder.event(parent, NORMAL, SUCCESSFUL_CREATE_POD_REASON, f"Created pod: {created.metadata.name}")
+        metrics.CHILDREN_CREATED.labels("Pod", "success").inc()
         return created
 
     def delete_pod(self, namespace: str, name: str, parent) -> None:
@@ -133,7 +138,9 @@ class RealServiceControl:
             created = self.client.core_v1().services(namespace).create(svc)
         except Exception as e:
             self.recorder.event(parent, WARNING, FAILED_CREATE_SERVICE_REASON, f"Error creating: {e}")
+            metrics.CHILDREN_CREATED.labels("Service", "failure").inc()
             raise
+        metrics.CHILDREN_CREATED.labels("Service", "success").inc()
         self.recorder.event(parent, NORMAL, SUCCESSFUL_CREATE_SERVICE_REASON,
                             f"Created service: {created.metadata.name}")
         return created
@@ -229,3 +236,40 @@ class FakeServiceControl:
     def delete_service(self, namespace, name, parent):
         if self.err:
             raise self.err
+
+
+class RealReplicaSetControl:
+    """ReplicaSet control (reference ``pkg/controller/control/replicaset.go:31-79``).
+
+    Dead code in the reference — never referenced by the controller — kept for
+    API parity: create (with an optional controller ref) and patch, with the
+    same SuccessfulCreate / FailedCreate events."""
+
+    def __init__(self, clientset, recorder):
+        self.client = clientset
+        self.recorder = recorder
+
+    def patch_replica_set(self, namespace: str, name: str, patch: Dict, expect_uid: Optional[str] = None):
+        return self.client.core_v1().replica_sets(namespace).patch(name, patch, expect_uid=expect_uid)
+
+    def create_replica_sets(self, namespace: str, rs, parent):
+        return self._create(namespace, rs, parent, None)
+
+    def create_replica_sets_with_controller_ref(self, namespace: str, rs, parent, controller_ref: OwnerReference):
+        validate_controller_ref(controller_ref)
+        return self._create(namespace, rs, parent, controller_ref)
+
+    def _create(self, namespace, rs, parent, controller_ref):
+        if not rs.spec.template.metadata.labels:
+            raise ValueError("unable to create ReplicaSet, no labels")
+        obj = deep_copy(rs)
+        if controller_ref is not None:
+            obj.metadata.ownerReferences.append(deep_copy(controller_ref))
+        try:
+            created = self.client.core_v1().replica_sets(namespace).create(obj)
+        except Exception as e:
+            self.recorder.event(parent, WARNING, FAILED_CREATE_REPLICASET_REASON, f"Error creating: {e}")
+            raise
+        self.recorder.event(parent, NORMAL, SUCCESSFUL_CREATE_REPLICASET_REASON,
+                            f"Created replicaset: {created.metadata.name}")
+        return created

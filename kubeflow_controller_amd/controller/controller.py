@@ -24,6 +24,7 @@ import threading
 import time
 from typing import List, Optional
 
+from ..utils import metrics
 from ..api import v1alpha1
 from ..api.core import filter_active_pods
 from ..api.meta import get_controller_of, key_of, split_key
@@ -117,17 +118,22 @@ class Controller:
             return False
         if key is None:  # timeout
             return True
+        t0 = time.perf_counter()
         try:
-            t0 = time.perf_counter()
             self.sync_handler(key)
             self.last_sync_seconds = time.perf_counter() - t0
             self.sync_count += 1
             self.workqueue.forget(key)
+            log.debug("Finished syncing %r (%.3f ms)", key, self.last_sync_seconds * 1e3)
         except Exception as e:  # noqa: BLE001 — runtime.HandleError + requeue
             log.warning("error syncing %r: %s", key, e)
+            metrics.SYNC_ERRORS.inc()
+            metrics.WORKQUEUE_RETRIES.inc()
             self.workqueue.add_rate_limited(key)
         finally:
+            metrics.SYNC_DURATION.observe(time.perf_counter() - t0)
             self.workqueue.done(key)
+            metrics.WORKQUEUE_DEPTH.set(len(self.workqueue))
         return True
 
     # ------------------------------------------------------------------ sync
@@ -184,6 +190,8 @@ class Controller:
             to_json(tfjob.metadata) != to_json(original.metadata)
         if status_changed or spec_changed:
             self.update_tfjob(tfjob)
+            if tfjob.status.phase != original.status.phase:
+                metrics.PHASE_TRANSITIONS.labels(tfjob.status.phase or "").inc()
         log.debug("Sync TFJob: %s", key)
 
     def manage_tfjob(self, active_worker, active_ps, worker_svcs, ps_svcs, succeeded: int,
@@ -245,6 +253,7 @@ class Controller:
     # ------------------------------------------------------------------ event handlers
     def enqueue_tfjob(self, obj) -> None:
         self.workqueue.add_rate_limited(key_of(obj))
+        metrics.WORKQUEUE_ADDS.inc()
 
     def _update_tfjob_event(self, old, new) -> None:
         if old.metadata.resourceVersion == new.metadata.resourceVersion:

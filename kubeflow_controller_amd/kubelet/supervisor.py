@@ -36,6 +36,7 @@ import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
+from ..utils import metrics
 from ..api import v1alpha1
 from ..api.core import (GPU_RESOURCE, POD_FAILED, POD_PENDING, POD_RUNNING, POD_SUCCEEDED, RESTART_ALWAYS,
                         RESTART_NEVER, RESTART_ON_FAILURE, ContainerStateTerminated, ContainerStatus, Pod,
@@ -270,6 +271,7 @@ class Supervisor:
             return
         p.started = time.monotonic()
         p.state = "running"
+        metrics.REPLICA_STARTS.labels(pod.metadata.labels.get("job_type", "")).inc()
         log.info("started pod %s pid=%d gpus=%s: %s", p.key, p.pid, p.gpus, " ".join(argv))
         self._set_status(pod, POD_RUNNING, pid=p.pid)
 
@@ -392,6 +394,8 @@ class Supervisor:
                         p.recycled = True
                     continue
                 code, sig = res
+                metrics.REPLICA_EXITS.labels(pod.metadata.labels.get("job_type", ""),
+                                             "success" if code == 0 else "failure").inc()
                 policy = pod.spec.restartPolicy or RESTART_ALWAYS
                 restart = (policy == RESTART_ALWAYS or (policy == RESTART_ON_FAILURE and code != 0)) and not (
                     finished or (code == 0 and self._job_finished(pod)))
@@ -435,6 +439,17 @@ class Supervisor:
     def running(self) -> Dict[str, int]:
         with self._lock:
             return {k: p.pid for k, p in self._procs.items() if p.state == "running"}
+
+    def inject_fault(self, namespace: str, name: str, sig: int = signal.SIGKILL) -> int:
+        """Fault injection: signal a running replica's process group,
+        as a node/container crash would.  The normal exit path then applies the
+        pod's restartPolicy.  Returns the pid signalled (0 if not running)."""
+        with self._lock:
+            p = self._procs.get(f"{namespace}/{name}")
+            if p is None or p.state != "running" or not p.pid:
+                return 0
+            self.rt.kill_group(p.pid, sig)
+            return p.pid
 
     def gpu_bindings(self) -> Dict[int, str]:
         with self._lock:

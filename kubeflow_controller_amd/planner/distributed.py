@@ -35,7 +35,7 @@ from ..api.meta import ObjectMeta
 from ..api.model import deep_copy
 from .local import job_labels
 from .types import Action, Event
-from .util import generate_name, generate_runtime_id
+from .util import generate_name, generate_runtime_id, with_job_dirs
 
 PORT_NAME = "kubeflow-port"
 WORKER_PORT = 2222
@@ -156,7 +156,7 @@ class DistributedJob:
         c0.args = self.generate_tf_cluster_spec(typ, index)
         c0.env = [e for e in c0.env if e.name != TF_CONFIG_ENV] + [
             EnvVar(name=TF_CONFIG_ENV, value=json.dumps(self.tf_config(typ, index)))]
-        return tmpl
+        return with_job_dirs(tmpl, self.tfjob)
 
     def _hosts(self, typ: str) -> List[str]:
         return [f"{self.service_names.get(self.get_service_name(typ, i), '')}:{WORKER_PORT}"

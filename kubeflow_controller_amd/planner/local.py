@@ -16,7 +16,7 @@ from typing import Dict, List
 from ..api import v1alpha1
 from ..api.core import Pod
 from .types import Action, Event
-from .util import generate_runtime_id
+from .util import generate_runtime_id, with_job_dirs
 
 EXPECTED_LOCAL_WORKER_NUMBER = 1
 log = logging.getLogger("kfa.planner")
@@ -61,4 +61,4 @@ class LocalJob:
         return job_labels(self.tfjob, self.tfjob.spec.specs[0].tfReplicaType)
 
     def get_template(self):
-        return self.tfjob.spec.specs[0].template
+        return with_job_dirs(self.tfjob.spec.specs[0].template, self.tfjob)

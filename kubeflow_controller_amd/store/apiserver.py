@@ -29,6 +29,7 @@ from .memory import ObjectStore
 
 _CORE_PLURALS = {"pods": "Pod", "services": "Service", "events": "Event"}
 _KF_PLURALS = {v1alpha1.TFJOB_PLURAL: v1alpha1.TFJOB_KIND}
+_EXT_PLURALS = {"replicasets": "ReplicaSet"}  # extensions/v1beta1
 
 _PATH_RE = re.compile(
     r"^/(?:api/v1|apis/(?P<group>[^/]+)/(?P<version>[^/]+))"
@@ -47,6 +48,8 @@ def _route(path: str) -> Tuple[str, Optional[str], Optional[str], Optional[str]]
         kind = _CORE_PLURALS.get(plural)
     elif group == v1alpha1.GROUP_NAME and m.group("version") == v1alpha1.GROUP_VERSION:
         kind = _KF_PLURALS.get(plural) or _CORE_PLURALS.get(plural)
+    elif group == "extensions" and m.group("version") == "v1beta1":
+        kind = _EXT_PLURALS.get(plural)
     else:
         kind = None
     if kind is None:
@@ -89,6 +92,15 @@ class _Handler(BaseHTTPRequestHandler):
             if u.path == "/version":
                 from ..version import version_info
                 self._send(200, version_info())
+                return
+            if u.path == "/metrics":  # Prometheus scrape (utils/metrics.py)
+                from ..utils import metrics
+                data = metrics.exposition()
+                self.send_response(200)
+                self.send_header("Content-Type", metrics.content_type())
+                self.send_header("Content-Length", str(len(data)))
+                self.end_headers()
+                self.wfile.write(data)
                 return
             kind, ns, name, sub = _route(u.path)
             getattr(self, "_" + verb)(kind, ns, name, sub, q)

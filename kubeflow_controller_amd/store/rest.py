@@ -18,12 +18,13 @@ from ..api.labels import Selector
 from ..api.model import Model
 from . import errors
 
-_PLURAL = {v1alpha1.TFJOB_KIND: v1alpha1.TFJOB_PLURAL, "Pod": "pods", "Service": "services", "Event": "events"}
+_PLURAL = {v1alpha1.TFJOB_KIND: v1alpha1.TFJOB_PLURAL, "Pod": "pods", "Service": "services", "Event": "events",
+           "ReplicaSet": "replicasets"}
 
 
 def _path(kind: str, ns: Optional[str], name: Optional[str] = None, sub: Optional[str] = None) -> str:
     base = (f"/apis/{v1alpha1.GROUP_NAME}/{v1alpha1.GROUP_VERSION}" if kind == v1alpha1.TFJOB_KIND
-            else "/api/v1")
+            else "/apis/extensions/v1beta1" if kind == "ReplicaSet" else "/api/v1")
     p = base + (f"/namespaces/{quote(ns)}" if ns else "") + "/" + _PLURAL[kind]
     if name:
         p += "/" + quote(name)

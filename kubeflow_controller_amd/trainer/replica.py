@@ -281,6 +281,10 @@ def run_worker(spec: ClusterSpec, args) -> int:
         opt = FusedAdam(groups, lr=args.learning_rate, weight_decay=args.weight_decay)
     else:
         opt = FusedSGD(groups, lr=args.learning_rate, momentum=args.momentum, weight_decay=args.weight_decay)
+    from . import checkpoint
+    resumed = checkpoint.restore(args.model_dir, rank, world, model, groups, opt) if args.model_dir else 0
+    if resumed:
+        _log(f"Worker {rank}: resumed from {args.model_dir} at global step {resumed}")
     broadcast_params(groups)
     sharded = num_ps > 0 and world > 1
     if sharded:
@@ -294,18 +298,25 @@ def run_worker(spec: ClusterSpec, args) -> int:
     else:
         sync = GradSync(groups, bucket_mb=args.bucket_mb)
 
-    steps_per_worker = args.train_steps if (args.sync_replicas or spec.is_local) else \
-        math.ceil(args.train_steps / world)
     inc = 1 if (args.sync_replicas or spec.is_local) else world
+    steps_per_worker = max(0, math.ceil((args.train_steps - resumed) / inc))
     fixed = None if data is not None else synthetic_batch(args, model, device, rank)
     _log(f"Worker {rank}: {'local' if spec.is_local else f'{world} workers, {num_ps} ps'}, device {device}, "
          f"model {args.model}, {sum(p.numel() for p in model.parameters())} params, "
          f"{'sharded push/pull' if sharded else 'all-reduce'}")
     t_begin = time.time()
     _log(f"Training begins @ {t_begin:f}")
-    global_step = 0
+    global_step = resumed
     t_first = None
     loss = None
+
+    def _save():
+        checkpoint.save(args.model_dir, global_step, rank, world, model, groups, opt, is_chief=False)
+        if store is not None:
+            dist.barrier()  # every rank's file is on disk before the manifest names the step
+        if spec.is_chief:
+            checkpoint.write_manifest(args.model_dir, global_step, world)
+
     for local_step in range(steps_per_worker):
         if data is not None:
             xb, yb = data.next_batch(args.batch_size)
@@ -328,6 +339,8 @@ def run_worker(spec: ClusterSpec, args) -> int:
             store.add(STEP_KEY, inc)
         if t_first is None:
             t_first = time.time()
+        if args.model_dir and args.checkpoint_every and (local_step + 1) % args.checkpoint_every == 0:
+            _save()
         if args.log_every and (local_step % args.log_every == 0 or local_step == steps_per_worker - 1):
             if spec.is_local:
                 _log(f"step: {local_step}")
@@ -354,12 +367,8 @@ def run_worker(spec: ClusterSpec, args) -> int:
             _log(f"Test accuracy: {acc:.4f}")
     elif loss is not None:
         _log(f"Final loss: {float(loss):.5f}")
-    if args.model_dir and spec.is_chief:
-        os.makedirs(args.model_dir, exist_ok=True)
-        torch.save({k: v.detach().cpu() for k, v in model.state_dict().items()},
-                   os.path.join(args.model_dir, f"model.step{global_step}.pt"))
-        with open(os.path.join(args.model_dir, "manifest.json"), "w") as f:
-            json.dump({"global_step": global_step, "model": args.model, "world": world, "ps": num_ps}, f)
+    if args.model_dir:
+        _save()
     if store is not None:
         store.add(DONE_KEY, 1)
         dist.barrier()
@@ -389,7 +398,9 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--replicas_to_aggregate", type=int, default=None, help="accepted; = #workers")
     ap.add_argument("--num_gpus", type=int, default=1, help="accepted (one GPU per replica)")
     ap.add_argument("--data_dir", default="", help="accepted (synthetic data; no network)")
-    ap.add_argument("--model_dir", default="")
+    ap.add_argument("--model_dir", default=os.environ.get("KFA_MODEL_DIR", ""),
+                    help="checkpoint / resume directory (TFJob spec.modelDir via $KFA_MODEL_DIR)")
+    ap.add_argument("--checkpoint_every", type=int, default=0, help="local steps between checkpoints")
     ap.add_argument("--device", default="auto", choices=["auto", "cpu", "gpu"])
     ap.add_argument("--bf16", type=int, default=1)
     ap.add_argument("--bucket_mb", type=float, default=16.0)

@@ -199,3 +199,30 @@ def test_rest_roundtrip_and_watch():
         assert "tfjobs.kubeflow.caicloud.io" in cl.crds()
     finally:
         srv.stop()
+
+
+def test_replicaset_control_and_rest_route():
+    """C15 (dead code in the reference): ReplicaSet create/patch with events, served over REST."""
+    from kubeflow_controller_amd.api.core import ReplicaSet
+    from kubeflow_controller_amd.client.clientset import Clientset
+    from kubeflow_controller_amd.client.events import FakeRecorder
+    from kubeflow_controller_amd.controller.control import RealReplicaSetControl
+    srv = APIServer(ObjectStore()).start()
+    try:
+        cl = RESTStore(srv.url)
+        job = cl.create(load("local.yml"))
+        rec = FakeRecorder()
+        ctl = RealReplicaSetControl(Clientset(cl), rec)
+        rs = ReplicaSet.from_json({"metadata": {"name": "rs1"}, "spec": {"replicas": 2, "template": {
+            "metadata": {"labels": {"a": "b"}}, "spec": {"containers": [{"name": "c"}]}}}})
+        ref = OwnerReference(apiVersion=job.apiVersion, kind=job.kind, name=job.metadata.name, uid=job.metadata.uid,
+                             controller=True, blockOwnerDeletion=True)
+        out = ctl.create_replica_sets_with_controller_ref("default", rs, job, ref)
+        assert out.metadata.uid and out.spec.replicas == 2
+        assert rec.events == ["Normal SuccessfulCreate Created replicaset: rs1"]
+        ctl.patch_replica_set("default", "rs1", {"spec": {"replicas": 3}})
+        assert cl.get("ReplicaSet", "default", "rs1").spec.replicas == 3
+        with pytest.raises(ValueError):
+            ctl.create_replica_sets("default", ReplicaSet(), job)
+    finally:
+        srv.stop()

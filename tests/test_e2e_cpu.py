@@ -188,6 +188,8 @@ def test_cli_standalone_controller_and_kfctl(tmp_path):
         assert "SuccessfulCreate" in r.stdout and "Local: Succeeded=1" in r.stdout
         r = run("get", "tfjob", "local-training-job", "-o", "json")
         assert '"phase": "Succeeded"' in r.stdout
+        r = run("metrics")
+        assert r.returncode == 0 and "kfa_sync_duration_seconds" in r.stdout, r.stderr
         r = run("delete", "tfjob", "local-training-job")
         assert r.returncode == 0
     finally:
@@ -196,3 +198,33 @@ def test_cli_standalone_controller_and_kfctl(tmp_path):
             ctl.wait(20)
         except subprocess.TimeoutExpired:
             ctl.kill()
+
+
+def test_fault_injection_restart_and_metrics(node):
+    """kill -9 of a running replica (SURVEY §5.3 fault injection): OnFailure restarts
+    it and the job still succeeds; the Prometheus metrics record the lifecycle."""
+    from kubeflow_controller_amd.utils import metrics
+    st, n, root = node
+    flag = str(root) + "_fi_flag"
+    script = textwrap.dedent(f"""
+        import os, sys, time
+        p = {flag!r}
+        if not os.path.exists(p):
+            open(p, "w").close(); time.sleep(60); sys.exit(5)
+        sys.exit(0)""")
+    st.create(_job("fi", [("Worker", 1, [sys.executable, "-c", script])], restart="OnFailure"))
+    deadline = time.time() + 30
+    while time.time() < deadline and not (n.supervisor.running() and os.path.exists(flag)):
+        time.sleep(0.05)
+    (key,) = n.supervisor.running()
+    assert n.supervisor.inject_fault(*key.split("/"), signal.SIGKILL) > 0
+    j = wait_for_phase(st, "default", "fi", {"Succeeded", "Failed"}, 60)
+    assert j.status.phase == "Succeeded"
+    (p,) = [p for p in st.list("Pod") if p.metadata.labels.get("tf_job_name") == "fi"]
+    cs = p.status.containerStatuses[0]
+    assert cs.restartCount == 1 and cs.terminated.exitCode == 0
+    text = metrics.exposition().decode()
+    if metrics.AVAILABLE:
+        assert 'kfa_children_created_total{kind="Pod",result="success"}' in text
+        assert "kfa_sync_duration_seconds_count" in text
+        assert 'kfa_replica_exits_total{result="failure",type="Worker"}' in text
