@@ -131,7 +131,7 @@ __global__ __launch_bounds__(256) void bn_finalize(const bf16_t* __restrict__ x,
   if (c >= C) return;
   double a, b;
   combine2(part, C, c, a, b);
-  const double K = (double)bf2f(x[c]);
+  const double K = x ? (double)bf2f(x[c]) : 0.0;  // x == nullptr: un-shifted sums (fused in the conv epilogue)
   const double m1 = a / (double)M;
   double var = b / (double)M - m1 * m1;
   if (var < 0.0) var = 0.0;
@@ -383,6 +383,31 @@ KFA_API int kfa_bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, cons
   hipLaunchKernelGGL(bn_stats_partial, dim3(g.gx), dim3(NT), 0, s, x, part, M, C, g.chunk, g.tpr, g.rpi);
   hipLaunchKernelGGL(bn_finalize, dim3(kfa_ceil_div(C, 64)), dim3(64), 0, s, x, part, g.gx, M, C, gamma, beta, rmean,
                      rvar, save_mean, save_invstd, scale, shift, eps, momentum);
+  if (relu && res)
+    hipLaunchKernelGGL((bn_apply<true, true>), dim3(g.gx), dim3(NT), 0, s, x, res, y, scale, shift, M, C, g.chunk, g.tpr, g.rpi);
+  else if (relu)
+    hipLaunchKernelGGL((bn_apply<true, false>), dim3(g.gx), dim3(NT), 0, s, x, res, y, scale, shift, M, C, g.chunk, g.tpr, g.rpi);
+  else if (res)
+    hipLaunchKernelGGL((bn_apply<false, true>), dim3(g.gx), dim3(NT), 0, s, x, res, y, scale, shift, M, C, g.chunk, g.tpr, g.rpi);
+  else
+    hipLaunchKernelGGL((bn_apply<false, false>), dim3(g.gx), dim3(NT), 0, s, x, res, y, scale, shift, M, C, g.chunk, g.tpr, g.rpi);
+  return kfa_status();
+}
+
+// Training forward whose statistics were already accumulated into `slots`
+// (un-shifted sum / sum of squares) by the producing convolution's epilogue
+// (kfa_conv_igemm with a stats pointer): finalize + apply only — the stats
+// pass over the conv output is gone.
+KFA_API int kfa_bn_fwd_train_prestats(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* gamma,
+                                      const float* beta, float* rmean, float* rvar, float* save_mean,
+                                      float* save_invstd, float* slots, float* coefws, long M, int C, float eps,
+                                      float momentum, int relu, hipStream_t s) {
+  if (!bn_shape_ok(M, C)) return -1;
+  Geom g = geom(M, C, max_row_blocks(C));
+  float* scale = coefws;
+  float* shift = scale + C;
+  hipLaunchKernelGGL(bn_finalize, dim3(kfa_ceil_div(C, 64)), dim3(64), 0, s, nullptr, slots, g.gx, M, C, gamma, beta,
+                     rmean, rvar, save_mean, save_invstd, scale, shift, eps, momentum);
   if (relu && res)
     hipLaunchKernelGGL((bn_apply<true, true>), dim3(g.gx), dim3(NT), 0, s, x, res, y, scale, shift, M, C, g.chunk, g.tpr, g.rpi);
   else if (relu)

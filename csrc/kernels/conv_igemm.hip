@@ -29,6 +29,7 @@
 namespace {
 
 constexpr int BK = 64;
+constexpr int kBnSlots = 64;  // must match batchnorm.hip kSlots (fused statistics land in its slots)
 
 struct Geo {
   int Nb, H, W, C;   // gathered tensor T
@@ -76,7 +77,8 @@ __device__ __forceinline__ int swz(int row, int chunk) { return row * BK + ((chu
 template <int WM, int WN, int TM, int TN>
 __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const bf16_t* __restrict__ T, const bf16_t* __restrict__ B,
                                                             bf16_t* __restrict__ D, const bf16_t* __restrict__ E,
-                                                            const bf16_t* __restrict__ Z, Geo g) {
+                                                            const bf16_t* __restrict__ Z, float* __restrict__ stats,
+                                                            Geo g) {
   constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
   constexpr int AR = BM / 32, BR = BN / 32;  // 16-B chunks per thread per k-tile
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
@@ -226,6 +228,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const bf16_t* __rest
       }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     const int c = lane % CPR;
+    float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // fused BN statistics
 #pragma unroll
     for (int it = 0; it < (16 * TM * CPR) / 64; it++) {
       const int r = it * (64 / CPR) + lane / CPR;
@@ -252,6 +255,37 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const bf16_t* __rest
         o = pack8(f);
       }
       __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<decltype(__builtin_amdgcn_raw_buffer_load_b128(rD, 0, 0, 0))*>(&o), rD, off, 0, 0);
+      if (stats && off != kOOB) {  // wave-uniform pointer test; per-lane row mask
+        float f[8];
+        unpack8(o, f);  // the bf16-rounded values the BatchNorm will normalise
+#pragma unroll
+        for (int j = 0; j < 8; j++) { s1[j] += f[j]; s2[j] += f[j] * f[j]; }
+      }
+    }
+    if (stats) {
+      // Butterfly-reduce over the lanes sharing channel chunk c = lane % CPR (xor
+      // 8, 16, 32): every lane ends with its chunk's wave totals.  Lane L then
+      // publishes channel (L % 8) * 8 + L / 8 — its own chunk, register L / 8
+      // (a select chain, no shuffles) — so ONE 64-lane atomic instruction per
+      // statistic covers the wave's 64 channels (CPR == 8: TN == 4).
+      static_assert(CPR == 8, "fused BN statistics assume 64-channel wave tiles");
+#pragma unroll
+      for (int o = CPR; o < 64; o <<= 1)
+#pragma unroll
+        for (int j = 0; j < 8; j++) { s1[j] += __shfl_xor(s1[j], o, 64); s2[j] += __shfl_xor(s2[j], o, 64); }
+      const int jj = lane >> 3;
+      float a = s1[0], b = s2[0];
+#pragma unroll
+      for (int j = 1; j < 8; j++) {
+        a = jj == j ? s1[j] : a;
+        b = jj == j ? s2[j] : b;
+      }
+      const int n = n0 + wn * TN * 16 + c * 8 + jj;
+      if (n < g.N) {
+        float* slot = stats + (long)(blockIdx.x % kBnSlots) * 2 * g.N;
+        __hip_atomic_fetch_add(slot + n, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(slot + g.N + n, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
 #pragma unroll
     for (int i = 0; i < TN; i++)
@@ -324,7 +358,7 @@ static const bf16_t* zero_page() {
 // variant: 0 = 128x128 tile, 1 = 128x64 tile (N <= 64)
 KFA_API int kfa_conv_igemm(const bf16_t* T, const bf16_t* B, bf16_t* D, const bf16_t* E, int Nb, int H, int W, int C,
                            int P, int Q, int R, int S, int sa, int ra, int oa, int ob, int N, int OH, int OW, int os,
-                           int oph, int opw, int ldd, int variant, hipStream_t st) {
+                           int oph, int opw, int ldd, int variant, float* stats, hipStream_t st) {
   if (C % BK != 0 || N % 8 != 0 || ldd % 8 != 0) return -1;
   Geo g{Nb, H, W, C, P, Q, R, S, sa, ra, oa, ob, Nb * P * Q, N, R * S * C, OH, OW, os, oph, opw, ldd, 0, 0, 0};
   if (g.K == 0) g.R = g.S = 1;  // keep index math defined; nk == 0 -> zero/addend-only epilogue
@@ -351,11 +385,11 @@ KFA_API int kfa_conv_igemm(const bf16_t* T, const bf16_t* B, bf16_t* D, const bf
     const long tiles = (long)kfa_ceil_div(g.M, 128) * kfa_ceil_div(N, 64);
     const int grid = (int)(tiles < 3L * cus ? tiles : 3L * cus);  // 160 VGPR, 48 KB LDS: 3 blocks / CU
     hipLaunchKernelGGL((conv_igemm_kernel<4, 1, 2, 4>), dim3(grid), dim3(256), 2 * (128 + 64) * BK * 2, st, T, B, D,
-                       E, zero_page(), g);
+                       E, zero_page(), stats, g);
   } else {  // 128 x 128 tile: 2x2 waves of 64x64
     const int grid = pgrid((long)kfa_ceil_div(g.M, 128) * kfa_ceil_div(N, 128));
     hipLaunchKernelGGL((conv_igemm_kernel<2, 2, 4, 4>), dim3(grid), dim3(256), 2 * (128 + 128) * BK * 2, st, T, B, D,
-                       E, zero_page(), g);
+                       E, zero_page(), stats, g);
   }
   return kfa_status();
 }

@@ -38,16 +38,19 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         # x feeds two branches; its gradient sum is fused into a dgrad epilogue
-        # (ops.conv.GradJoin) instead of a separate add kernel.
+        # (ops.conv.GradJoin) instead of a separate add kernel.  In training every
+        # conv accumulates its BatchNorm's statistics in its epilogue (st=True):
+        # the BN then only finalizes + applies (no stats pass over the output).
         join = GradJoin()
+        st = self.training
         if self.downsample is None:
-            y = self.bn1(self.conv1(x, join=join))
-            y = self.bn2(self.conv2(y))
-            return self.bn3(self.conv3(y), residual=join.branch(x))
-        idn = self.downsample["bn"](self.downsample["conv"](x, join=join))
-        y = self.bn1(self.conv1(join.branch(x)))
-        y = self.bn2(self.conv2(y))
-        return self.bn3(self.conv3(y), residual=idn)
+            y = self.bn1(self.conv1(x, join=join, bn_stats=st))
+            y = self.bn2(self.conv2(y, bn_stats=st))
+            return self.bn3(self.conv3(y, bn_stats=st), residual=join.branch(x))
+        idn = self.downsample["bn"](self.downsample["conv"](x, join=join, bn_stats=st))
+        y = self.bn1(self.conv1(join.branch(x), bn_stats=st))
+        y = self.bn2(self.conv2(y, bn_stats=st))
+        return self.bn3(self.conv3(y, bn_stats=st), residual=idn)
 
 
 class ResNet(nn.Module):

@@ -34,6 +34,15 @@ def _mc(t: torch.Tensor):
     return t.numel() // C, C
 
 
+_lib.register("kfa_bn_fwd_train_prestats", [_lib.P] * 11 + [_lib.L, _lib.I, _lib.F, _lib.F, _lib.I, _lib.P])
+
+
+def bn_slot_workspace(C: int, device) -> torch.Tensor:
+    """The zero-initialised, self-cleaning statistics slots shared by every BN
+    (and by convolutions that accumulate a BN's statistics in their epilogue)."""
+    return _lib.workspace(_lib.lib().kfa_bn_slot_floats(C) * 4, device, "bn_slots")
+
+
 def _workspaces(C: int, device):
     L = _lib.lib()
     slots = _lib.workspace(L.kfa_bn_slot_floats(C) * 4, device, "bn_slots")  # zero-init, self-cleaning
@@ -43,7 +52,8 @@ def _workspaces(C: int, device):
 
 class _BNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, residual, training, momentum, eps, relu):
+    def forward(ctx, x, weight, bias, running_mean, running_var, residual, training, momentum, eps, relu,
+                prestats=False):
         x = _as_rows(x)
         M, C = _mc(x)
         if x.dtype != torch.bfloat16:
@@ -57,7 +67,8 @@ class _BNActFn(torch.autograd.Function):
         if training:
             mean = torch.empty(C, dtype=torch.float32, device=x.device)
             invstd = torch.empty_like(mean)
-            _lib.call("kfa_bn_fwd_train", _lib.ptr(x), _lib.ptr(res), _lib.ptr(y), _lib.ptr(weight), _lib.ptr(bias),
+            _lib.call("kfa_bn_fwd_train_prestats" if prestats else "kfa_bn_fwd_train", _lib.ptr(x), _lib.ptr(res),
+                      _lib.ptr(y), _lib.ptr(weight), _lib.ptr(bias),
                       _lib.ptr(running_mean), _lib.ptr(running_var), _lib.ptr(mean), _lib.ptr(invstd),
                       _lib.ptr(slots), _lib.ptr(coef), M, C, eps, momentum, int(relu), s)
         else:
@@ -98,15 +109,21 @@ class _BNActFn(torch.autograd.Function):
         if direct:
             notify_grad_ready(ctx.params[0])
             notify_grad_ready(ctx.params[1])
-            return dx, None, None, None, None, dres, None, None, None, None
+            return dx, None, None, None, None, dres, None, None, None, None, None
         if dgamma is not None and weight is not None and weight.dtype != torch.float32:
             dgamma, dbeta = dgamma.to(weight.dtype), dbeta.to(weight.dtype)
-        return dx, dgamma, dbeta, None, None, dres, None, None, None, None
+        return dx, dgamma, dbeta, None, None, dres, None, None, None, None, None
 
 
 def bn_act(x, weight, bias, running_mean, running_var, residual=None, training=True, momentum=0.1, eps=1e-5,
-           relu=True):
-    return _BNActFn.apply(x, weight, bias, running_mean, running_var, residual, training, momentum, eps, relu)
+           relu=True, prestats=False):
+    """``prestats``: the statistics of ``x`` already sit in the BN slot workspace
+    (accumulated by the producing convolution's epilogue)."""
+    if prestats and not training:  # never leave the self-cleaning slots dirty
+        bn_slot_workspace(x.shape[1], x.device).zero_()
+        prestats = False
+    return _BNActFn.apply(x, weight, bias, running_mean, running_var, residual, training, momentum, eps, relu,
+                          prestats)
 
 
 def bn_act_reference(x, weight, bias, running_mean, running_var, residual=None, training=True, momentum=0.1,
@@ -139,7 +156,7 @@ class BatchNorm2dAct(nn.Module):
     def forward(self, x, residual=None):
         if x.is_cuda:
             return bn_act(x, self.weight, self.bias, self.running_mean, self.running_var, residual,
-                          self.training, self.momentum, self.eps, self.relu)
+                          self.training, self.momentum, self.eps, self.relu, getattr(x, "_kfa_prestats", False))
         # CPU path (plumbing tests / CPU-only MNIST-style jobs): plain PyTorch.
         y = torch.nn.functional.batch_norm(x, self.running_mean, self.running_var, self.weight.to(x.dtype),
                                            self.bias.to(x.dtype), self.training, self.momentum, self.eps)

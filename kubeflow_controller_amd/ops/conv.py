@@ -31,7 +31,7 @@ from . import _lib
 from ..parallel.flat import direct_grad_view, notify_grad_ready
 
 P, I = _lib.P, _lib.I
-_lib.register("kfa_conv_igemm", [P, P, P, P] + [I] * 20 + [P])
+_lib.register("kfa_conv_igemm", [P, P, P, P] + [I] * 20 + [P, P])
 _lib.register("kfa_zero_bf16", [P, _lib.L, P])
 _lib.register("kfa_weight_transpose", [P, P] + [I] * 10 + [P])
 _lib.register("kfa_wgrad_part_floats", [I] * 7, _lib.L)
@@ -55,7 +55,10 @@ def _cl(t: torch.Tensor) -> torch.Tensor:
     return t if t.is_contiguous(memory_format=torch.channels_last) else t.contiguous(memory_format=torch.channels_last)
 
 
-def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int) -> torch.Tensor:
+def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, stats=None) -> torch.Tensor:
+    """Forward conv; with ``stats`` (the BatchNorm slot workspace of Cout) the
+    epilogue also accumulates the per-channel sum / sum of squares of the output
+    for the BatchNorm that consumes it (``kfa_bn_fwd_train_prestats``)."""
     x, w = _cl(x), _cl(w)
     Nb, C, H, W = x.shape
     Co, _, R, S = w.shape
@@ -63,7 +66,7 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int) -> torch.T
     Qo = (W + 2 * pad - S) // stride + 1
     y = torch.empty((Nb, Co, Po, Qo), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
     _lib.call("kfa_conv_igemm", _lib.ptr(x), _lib.ptr(w), _lib.ptr(y), None, Nb, H, W, C, Po, Qo, R, S, stride, 1,
-              -pad, -pad, Co, Po, Qo, 1, 0, 0, Co, _variant(Nb * Po * Qo, Co), _lib.stream())
+              -pad, -pad, Co, Po, Qo, 1, 0, 0, Co, _variant(Nb * Po * Qo, Co), _lib.ptr(stats), _lib.stream())
     return y
 
 
@@ -87,7 +90,7 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride: int, pad: int
     if stride == 1:
         wt = _transposed_weight(w, 0, 1, R, 0, 1, S)
         _lib.call("kfa_conv_igemm", _lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), _lib.ptr(E), Nb, Po, Qo, Co, H, W, R, S,
-                  1, -1, pad, pad, Ci, H, W, 1, 0, 0, Ci, _variant(Nb * H * W, Ci), st)
+                  1, -1, pad, pad, Ci, H, W, 1, 0, 0, Ci, _variant(Nb * H * W, Ci), None, st)
         return dx
     # stride s: output parity classes.  For class (ph, pw) the rows h = s*i + ph
     # receive taps r with (ph + pad - r) % s == 0, from dY row i + (ph + pad - r)/s.
@@ -107,7 +110,8 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride: int, pad: int
             oa_h = (ph + pad - r0) // stride
             oa_w = (pw + pad - s0) // stride
             _lib.call("kfa_conv_igemm", _lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), _lib.ptr(E), Nb, Po, Qo, Co, Hc, Wc,
-                      Rs, Ss, 1, -1, oa_h, oa_w, Ci, H, W, stride, ph, pw, Ci, _variant(Nb * Hc * Wc, Ci), st)
+                      Rs, Ss, 1, -1, oa_h, oa_w, Ci, H, W, stride, ph, pw, Ci, _variant(Nb * Hc * Wc, Ci), None,
+                      st)
     return dx
 
 
@@ -194,11 +198,11 @@ class _Branch(torch.autograd.Function):
 
 class _ConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, stride, pad, join):
+    def forward(ctx, x, w, stride, pad, join, stats):
         ctx.save_for_backward(x, w)
         ctx.stride, ctx.pad, ctx.join = stride, pad, join
         ctx.wparam = w  # the Parameter itself (for the direct flat-gradient write)
-        return conv_fwd(x, w, stride, pad)
+        return conv_fwd(x, w, stride, pad, stats)
 
     @staticmethod
     def backward(ctx, dy):
@@ -220,14 +224,24 @@ class _ConvFn(torch.autograd.Function):
                     dx = dx + addend
         if ctx.needs_input_grad[1]:
             dw = conv_wgrad(x, dy, w, ctx.stride, ctx.pad, ctx.wparam)
-        return dx, dw, None, None, None
+        return dx, dw, None, None, None, None
 
 
-def conv2d(x, w, stride: int = 1, pad: int = 0, join: "GradJoin | None" = None):
+def conv2d(x, w, stride: int = 1, pad: int = 0, join: "GradJoin | None" = None, bn_stats: bool = False):
+    """``bn_stats``: the caller guarantees a training-mode ``BatchNorm2dAct``
+    consumes the output next; the epilogue then accumulates its statistics and
+    the output is tagged ``_kfa_prestats`` (the BN skips its stats pass)."""
     if igemm_ok(x, w):
         if join is not None:
             join.fused = True
-        return _ConvFn.apply(x, w, stride, pad, join)
+        stats = None
+        if bn_stats:
+            from .batchnorm import bn_slot_workspace
+            stats = bn_slot_workspace(w.shape[0], x.device)
+        y = _ConvFn.apply(x, w, stride, pad, join, stats)
+        if stats is not None:
+            y._kfa_prestats = True
+        return y
     return F.conv2d(x, w, None, stride, pad)  # unfused: join.branch() is a no-op alias
 
 
@@ -245,9 +259,9 @@ class Conv2d(nn.Module):
         self.weight = nn.Parameter(w.contiguous(memory_format=torch.channels_last))
         self.bias = nn.Parameter(torch.zeros(out_channels)) if bias else None
 
-    def forward(self, x, join: "GradJoin | None" = None):
+    def forward(self, x, join: "GradJoin | None" = None, bn_stats: bool = False):
         w = self.weight if self.weight.dtype == x.dtype else self.weight.to(x.dtype)
-        y = conv2d(x, w, self.stride, self.padding, join)
+        y = conv2d(x, w, self.stride, self.padding, join, bn_stats and self.bias is None)
         if self.bias is not None:
             y = y + self.bias.to(y.dtype).view(1, -1, 1, 1)
         return y

@@ -136,3 +136,29 @@ def test_wgrad_direct_into_flat_buffer():
     assert len(seen) == 1 and conv.weight.grad.data_ptr() == g.grad.data_ptr()
     err = (conv.weight.grad.float() - wf.grad).abs().max().item()
     assert err < 3e-2 * wf.grad.abs().max().item(), err
+
+
+@pytest.mark.parametrize("Cin,Cout,k,stride", [(64, 256, 1, 1), (128, 128, 3, 2), (64, 64, 3, 1)])
+def test_bn_stats_fused_into_conv_epilogue(Cin, Cout, k, stride):
+    """conv(bn_stats=True) accumulates the BN statistics in its epilogue; the BN
+    then skips its stats pass — same outputs / running stats as the unfused pair,
+    and the self-cleaning slot workspace is left zeroed."""
+    from kubeflow_controller_amd.ops.batchnorm import BatchNorm2dAct, bn_slot_workspace
+    from kubeflow_controller_amd.ops.conv import Conv2d
+    d = torch.device("cuda")
+    torch.manual_seed(0)
+    conv = Conv2d(Cin, Cout, k, stride=stride, padding=k // 2).to(d)
+    conv.weight.data = conv.weight.data.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    bn_a, bn_b = BatchNorm2dAct(Cout).to(d), BatchNorm2dAct(Cout).to(d)
+    x = (torch.randn(6, Cin, 30, 30, device=d) + 0.5).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y1 = conv(x, bn_stats=True)
+    assert getattr(y1, "_kfa_prestats", False)
+    out_a = bn_a(y1)
+    y2 = conv(x)
+    out_b = bn_b(y2)
+    assert torch.equal(y1, y2)
+    assert (out_a.float() - out_b.float()).abs().max().item() < 3e-2
+    torch.testing.assert_close(bn_a.running_mean, bn_b.running_mean, atol=1e-3, rtol=1e-3)
+    torch.testing.assert_close(bn_a.running_var, bn_b.running_var, atol=1e-3, rtol=1e-3)
+    torch.cuda.synchronize()
+    assert bn_slot_workspace(Cout, d).abs().max().item() == 0
