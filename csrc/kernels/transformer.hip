@@ -143,9 +143,26 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
 #pragma unroll
     for (int e = 0; e < 8; e++) ag[j][e] = ab[j][e] = ad[j][e] = 0.f;
 
+  // software pipeline: the next row's dy / x are in flight while this row reduces
+  uint4 nd[NV], nx[NV];
+  auto fetch = [&](long row) {
+#pragma unroll
+    for (int j = 0; j < NV; j++) {
+      const int c = (j * 64 + lane) * 8;
+      if (c < H && row < r1) {
+        nd[j] = *reinterpret_cast<const uint4*>(dy + row * (long)H + c);
+        nx[j] = *reinterpret_cast<const uint4*>(xs + row * (long)H + c);
+      }
+    }
+  };
+  fetch(r0 + w);
   for (long row = r0 + w; row < r1; row += kRowsPerBlock) {
     const long base = row * (long)H;
     const float mean = mean_in[row], rstd = rstd_in[row];
+    uint4 cd[NV], cx[NV];
+#pragma unroll
+    for (int j = 0; j < NV; j++) { cd[j] = nd[j]; cx[j] = nx[j]; }
+    fetch(row + kRowsPerBlock);
     float xh[NV][8], g[NV][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -153,8 +170,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
       const int c = (j * 64 + lane) * 8;
       if (c < H) {
         float d[8], xv[8], gm[8];
-        load8(dy + base + c, d);
-        load8(xs + base + c, xv);
+        unpack8(cd[j], d);
+        unpack8(cx[j], xv);
         load8f(gamma + c, gm);
 #pragma unroll
         for (int e = 0; e < 8; e++) {

@@ -132,7 +132,22 @@ def colsum_(x, out):
 
 
 def _wgrad_(gw: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor) -> None:
-    """gW += dY^T · X (hipBLASLt, beta = 1) straight into the flat grad view."""
+    """gW += dYᵀ·X straight into the flat grad view.
+
+    The hand-written split-K MFMA wgrad kernel (``csrc/kernels/wgrad.hip``, the
+    conv weight-gradient kernel run as a 1x1 conv over the token rows) beats
+    hipBLASLt's transposed-A GEMM on these shapes (e.g. 16384x768x768: 374 vs
+    215 TFLOP/s, ``tools/probe_wgrad_layouts.py``); hipBLASLt (``addmm_``,
+    beta = 1) covers the shapes it does not take (dims not multiples of 8)."""
+    from . import conv as _conv
+    rows, out_f = dy2.shape
+    in_f = x2.shape[1]
+    if (_conv.WGRAD_ENABLED and gw.is_cuda and dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16
+            and out_f % 8 == 0 and in_f % 8 == 0 and rows < (1 << 24) and gw.is_contiguous()
+            and gw.dtype in (torch.bfloat16, torch.float32)):
+        _conv.wgrad_into(x2.contiguous(), dy2.contiguous(), gw, 1, 1, rows, in_f, 1, rows, out_f, 1, 1, 1, 0,
+                         accumulate=True)
+        return
     if gw.dtype == dy2.dtype:
         gw.addmm_(dy2.t(), x2)
     else:
