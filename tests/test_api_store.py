@@ -226,3 +226,14 @@ def test_replicaset_control_and_rest_route():
             ctl.create_replica_sets("default", ReplicaSet(), job)
     finally:
         srv.stop()
+
+
+def test_all_example_tfjobs_parse_and_validate():
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "examples", "tfjob", "*.yml")))
+    assert len(files) >= 6
+    for f in files:
+        (job,) = serde.load_file(f, env=ENV)
+        set_defaults(job)
+        validate(job)
+        assert job.to_json()["spec"]["tfReplicaSpec"]

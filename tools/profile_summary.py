@@ -1,0 +1,63 @@
+"""Turn a rocprofv3 ``--kernel-trace`` CSV into a committed markdown summary.
+
+    python tools/profile_summary.py gpurun_out/prof/r50_kernel_trace.csv STEPS STEP_MS "title" > profiles/x.md
+
+Only the last ``STEPS`` steps' worth of kernels (by wall window) are counted, so
+warm-up / autotuning launches do not pollute the per-step numbers.  Kernels
+are grouped into own HIP kernels (``kfa``'s anonymous-namespace kernels) vs
+vendor libraries (hipBLASLt ``Cijk_*``, MIOpen / CK) vs PyTorch elementwise.
+"""
+import collections
+import csv
+import sys
+
+OWN_MARKERS = ("(anonymous namespace)::",)
+
+
+def origin(name: str) -> str:
+    if any(m in name for m in OWN_MARKERS):
+        return "own HIP (csrc/kernels)"
+    if name.startswith("Cijk_") or name.startswith("Custom_Cijk"):
+        return "hipBLASLt"
+    if "igemm_" in name or "ck::" in name or "SubTensor" in name or "MIOpen" in name:
+        return "MIOpen / CK"
+    if "at::native" in name:
+        return "PyTorch ATen"
+    if "rocclr" in name:
+        return "runtime copy / fill"
+    return "other"
+
+
+def short(name: str) -> str:
+    n = name.replace("(anonymous namespace)::", "").replace("void ", "")
+    return n.split("(")[0][:90]
+
+
+def main(path, steps, step_ms, title):
+    rows = list(csv.DictReader(open(path)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    end = int(rows[-1]["End_Timestamp"])
+    win = [r for r in rows if int(r["Start_Timestamp"]) > end - steps * step_ms * 1e6]
+    per = collections.defaultdict(lambda: [0, 0])
+    for r in win:
+        d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        per[r["Kernel_Name"]][0] += d
+        per[r["Kernel_Name"]][1] += 1
+    tot = sum(v[0] for v in per.values())
+    by_origin = collections.defaultdict(float)
+    for k, (d, _) in per.items():
+        by_origin[origin(k)] += d
+    print(f"# {title}\n")
+    print(f"Source: `{path}` (rocprofv3 --kernel-trace --stats), last {steps} steps "
+          f"(window {steps * step_ms:.1f} ms).\n")
+    print(f"Kernel-busy time per step: **{tot / steps / 1e6:.2f} ms** ({len(win) / steps:.0f} launches/step)\n")
+    print("| origin | ms/step | share |\n|---|---|---|")
+    for k, v in sorted(by_origin.items(), key=lambda kv: -kv[1]):
+        print(f"| {k} | {v / steps / 1e6:.2f} | {100 * v / tot:.1f}% |")
+    print("\n| kernel | origin | ms/step | calls/step |\n|---|---|---|---|")
+    for k, (d, c) in sorted(per.items(), key=lambda kv: -kv[1][0])[:30]:
+        print(f"| `{short(k)}` | {origin(k)} | {d / steps / 1e6:.3f} | {c / steps:.1f} |")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], int(sys.argv[2]), float(sys.argv[3]), sys.argv[4] if len(sys.argv) > 4 else "profile")
