@@ -440,6 +440,30 @@ KFA_API int kfa_bn_fwd_eval(const bf16_t* x, const bf16_t* res, bf16_t* y, const
 }
 
 // y is the forward OUTPUT (ReLU mask source); required when relu != 0.
+// Backward whose partial sums (sum(dz), sum(dz*(x-mean))) were accumulated into
+// `slots` by the dgrad epilogue that produced dy (kfa_conv_igemm with bn_x):
+// finalize + apply only.
+KFA_API int kfa_bn_bwd_prestats(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const float* gamma,
+                                const float* save_mean, const float* save_invstd, bf16_t* dx, bf16_t* dres,
+                                float* dgamma, float* dbeta, float* slots, float* coefws, long M, int C, int relu,
+                                int accumulate, hipStream_t s) {
+  if (!bn_shape_ok(M, C)) return -1;
+  if (relu && !y) return -2;
+  Geom g = geom(M, C, max_row_blocks(C));
+  float* coef = coefws;
+  hipLaunchKernelGGL(bn_bwd_finalize, dim3(kfa_ceil_div(C, 64)), dim3(64), 0, s, slots, g.gx, M, C, gamma, save_mean,
+                     save_invstd, dgamma, dbeta, coef, accumulate);
+  if (relu && dres)
+    hipLaunchKernelGGL((bn_bwd_apply<true, true>), dim3(g.gx), dim3(NT), 0, s, dy, x, y, coef, dx, dres, M, C, g.chunk, g.tpr, g.rpi);
+  else if (relu)
+    hipLaunchKernelGGL((bn_bwd_apply<true, false>), dim3(g.gx), dim3(NT), 0, s, dy, x, y, coef, dx, dres, M, C, g.chunk, g.tpr, g.rpi);
+  else if (dres)
+    hipLaunchKernelGGL((bn_bwd_apply<false, true>), dim3(g.gx), dim3(NT), 0, s, dy, x, y, coef, dx, dres, M, C, g.chunk, g.tpr, g.rpi);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply<false, false>), dim3(g.gx), dim3(NT), 0, s, dy, x, y, coef, dx, dres, M, C, g.chunk, g.tpr, g.rpi);
+  return kfa_status();
+}
+
 KFA_API int kfa_bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const float* gamma, const float* save_mean,
                        const float* save_invstd, bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta, float* slots,
                        float* coefws, long M, int C, int relu, int accumulate, hipStream_t s) {

@@ -31,6 +31,18 @@ namespace {
 constexpr int BK = 64;
 constexpr int kBnSlots = 64;  // must match batchnorm.hip kSlots (fused statistics land in its slots)
 
+// Backward BatchNorm statistics fused into a dgrad epilogue: the dgrad output is
+// dL/dy of a BatchNorm(+ReLU) whose input x / output y / batch mean are given;
+// the epilogue accumulates sum(dz) and sum(dz * (x - mean)), dz = dy * (y > 0),
+// into the BN slots (what bn_bwd_partial computes), so the BN backward skips
+// that pass.  x == nullptr: forward statistics (sum, sum of squares) instead.
+struct BnBwd {
+  const bf16_t* x;
+  const bf16_t* y;
+  const float* mean;
+  int relu;
+};
+
 struct Geo {
   int Nb, H, W, C;   // gathered tensor T
   int P, Q;          // GEMM row space (m = nb*P*Q + p*Q + q)
@@ -78,7 +90,7 @@ template <int WM, int WN, int TM, int TN>
 __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const bf16_t* __restrict__ T, const bf16_t* __restrict__ B,
                                                             bf16_t* __restrict__ D, const bf16_t* __restrict__ E,
                                                             const bf16_t* __restrict__ Z, float* __restrict__ stats,
-                                                            Geo g) {
+                                                            BnBwd bnb, Geo g) {
   constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
   constexpr int AR = BM / 32, BR = BN / 32;  // 16-B chunks per thread per k-tile
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
@@ -113,6 +125,8 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const bf16_t* __rest
   unsigned b_off[BR];
   const __amdgpu_buffer_rsrc_t rT = rsrc(T, g.t_bytes), rB = rsrc(B, g.b_bytes), rD = rsrc(D, g.d_bytes);
   const __amdgpu_buffer_rsrc_t rE = rsrc(E ? E : D, E ? g.d_bytes : 0u);
+  const __amdgpu_buffer_rsrc_t rBX = rsrc(bnb.x ? bnb.x : D, bnb.x ? g.d_bytes : 0u);
+  const __amdgpu_buffer_rsrc_t rBY = rsrc(bnb.y ? bnb.y : D, bnb.y ? g.d_bytes : 0u);
   auto setup = [&](int tile) {
     const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
 #pragma unroll
@@ -211,7 +225,43 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const bf16_t* __rest
   constexpr int RB = 32 * TN;         // staged row bytes
   constexpr int CPR = 2 * TN;         // 16-B chunks per staged row
   auto epilogue = [&](int tile, int buf) {
+    constexpr int IT = (16 * TM * CPR) / 64;  // 16-B row pieces per lane
     const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
+    const int c = lane % CPR;
+    const int n = n0 + wn * TN * 16 + c * 8;
+    // output offsets first, so the epilogue's global loads (residual-grad addend,
+    // BN input / output for the fused backward statistics) are all in flight
+    // while the tile is staged through LDS
+    unsigned offs[IT];
+#pragma unroll
+    for (int it = 0; it < IT; it++) {
+      const int m = m0 + wm * TM * 16 + it * (64 / CPR) + lane / CPR;
+      unsigned orow;  // byte offset of output row m
+      if (lin_d) {
+        orow = (unsigned)m * (unsigned)g.ldd * 2u;
+      } else {
+        const int nb = fdiv(m, PQ, rPQ), rem = m - nb * PQ;
+        const int p = fdiv(rem, g.Q, rQ), q = rem - p * g.Q;
+        orow = (unsigned)((nb * g.OH + p * g.os + g.oph) * g.OW + (q * g.os + g.opw)) * (unsigned)g.ldd * 2u;
+      }
+      offs[it] = (m >= g.M || n >= g.N) ? kOOB : orow + (unsigned)n * 2u;
+    }
+    const bool bstat = stats && bnb.x;
+    uint4 ev[IT], bx[IT], by[IT];
+    if (E)
+#pragma unroll
+      for (int it = 0; it < IT; it++) ev[it] = bload16(rE, offs[it]);
+    if (bstat)
+#pragma unroll
+      for (int it = 0; it < IT; it++) {
+        bx[it] = bload16(rBX, offs[it]);
+        if (bnb.relu) by[it] = bload16(rBY, offs[it]);
+      }
+    float mu[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (bstat)
+#pragma unroll
+      for (int j = 0; j < 8; j++) mu[j] = n + j < g.N ? bnb.mean[n + j] : 0.f;
+
     lds_barrier();  // every wave is done reading `buf`: reuse it as the staging area
     char* stage;
     {
@@ -227,29 +277,17 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const bf16_t* __rest
         *reinterpret_cast<uint2*>(stage + row * RB + (((col >> 3) ^ (row & (CPR - 1))) << 4) + (col & 7) * 2) = o;
       }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    const int c = lane % CPR;
     float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // fused BN statistics
 #pragma unroll
-    for (int it = 0; it < (16 * TM * CPR) / 64; it++) {
+    for (int it = 0; it < IT; it++) {
       const int r = it * (64 / CPR) + lane / CPR;
       const uint4 v = *reinterpret_cast<const uint4*>(stage + r * RB + ((c ^ (r & (CPR - 1))) << 4));
-      const int m = m0 + wm * TM * 16 + r;
-      unsigned orow;  // byte offset of output row m (kOOB when m is a tail row)
-      if (lin_d) {
-        orow = (unsigned)m * (unsigned)g.ldd * 2u;
-      } else {
-        const int nb = fdiv(m, PQ, rPQ), rem = m - nb * PQ;
-        const int p = fdiv(rem, g.Q, rQ), q = rem - p * g.Q;
-        orow = (unsigned)((nb * g.OH + p * g.os + g.oph) * g.OW + (q * g.os + g.opw)) * (unsigned)g.ldd * 2u;
-      }
-      const int n = n0 + wn * TN * 16 + c * 8;
-      const unsigned off = (m >= g.M || n >= g.N) ? kOOB : orow + (unsigned)n * 2u;
+      const unsigned off = offs[it];
       uint4 o = v;
       if (E) {  // wave-uniform branch
-        const uint4 e = bload16(rE, off);
         float f[8], h[8];
         unpack8(v, f);
-        unpack8(e, h);
+        unpack8(ev[it], h);
 #pragma unroll
         for (int j = 0; j < 8; j++) f[j] += h[j];
         o = pack8(f);
@@ -257,9 +295,22 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const bf16_t* __rest
       __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<decltype(__builtin_amdgcn_raw_buffer_load_b128(rD, 0, 0, 0))*>(&o), rD, off, 0, 0);
       if (stats && off != kOOB) {  // wave-uniform pointer test; per-lane row mask
         float f[8];
-        unpack8(o, f);  // the bf16-rounded values the BatchNorm will normalise
+        unpack8(o, f);  // the bf16-rounded values the BatchNorm will see
+        if (bstat) {    // backward statistics of the BN this dgrad feeds
+          float xf[8];
+          unpack8(bx[it], xf);
+          if (bnb.relu) {
+            float yf[8];
+            unpack8(by[it], yf);
 #pragma unroll
-        for (int j = 0; j < 8; j++) { s1[j] += f[j]; s2[j] += f[j] * f[j]; }
+            for (int j = 0; j < 8; j++) f[j] = yf[j] > 0.f ? f[j] : 0.f;
+          }
+#pragma unroll
+          for (int j = 0; j < 8; j++) { s1[j] += f[j]; s2[j] += f[j] * (xf[j] - mu[j]); }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; j++) { s1[j] += f[j]; s2[j] += f[j] * f[j]; }
+        }
       }
     }
     if (stats) {
@@ -280,11 +331,11 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const bf16_t* __rest
         a = jj == j ? s1[j] : a;
         b = jj == j ? s2[j] : b;
       }
-      const int n = n0 + wn * TN * 16 + c * 8 + jj;
-      if (n < g.N) {
+      const int nc = n + jj;
+      if (nc < g.N) {
         float* slot = stats + (long)(blockIdx.x % kBnSlots) * 2 * g.N;
-        __hip_atomic_fetch_add(slot + n, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add(slot + g.N + n, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(slot + nc, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(slot + g.N + nc, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
 #pragma unroll
@@ -358,7 +409,9 @@ static const bf16_t* zero_page() {
 // variant: 0 = 128x128 tile, 1 = 128x64 tile (N <= 64)
 KFA_API int kfa_conv_igemm(const bf16_t* T, const bf16_t* B, bf16_t* D, const bf16_t* E, int Nb, int H, int W, int C,
                            int P, int Q, int R, int S, int sa, int ra, int oa, int ob, int N, int OH, int OW, int os,
-                           int oph, int opw, int ldd, int variant, float* stats, hipStream_t st) {
+                           int oph, int opw, int ldd, int variant, float* stats, const bf16_t* bn_x,
+                           const bf16_t* bn_y, const float* bn_mean, int bn_relu, hipStream_t st) {
+  const BnBwd bnb{bn_x, bn_y, bn_mean, bn_relu};
   if (C % BK != 0 || N % 8 != 0 || ldd % 8 != 0) return -1;
   Geo g{Nb, H, W, C, P, Q, R, S, sa, ra, oa, ob, Nb * P * Q, N, R * S * C, OH, OW, os, oph, opw, ldd, 0, 0, 0};
   if (g.K == 0) g.R = g.S = 1;  // keep index math defined; nk == 0 -> zero/addend-only epilogue
@@ -385,11 +438,11 @@ KFA_API int kfa_conv_igemm(const bf16_t* T, const bf16_t* B, bf16_t* D, const bf
     const long tiles = (long)kfa_ceil_div(g.M, 128) * kfa_ceil_div(N, 64);
     const int grid = (int)(tiles < 3L * cus ? tiles : 3L * cus);  // 160 VGPR, 48 KB LDS: 3 blocks / CU
     hipLaunchKernelGGL((conv_igemm_kernel<4, 1, 2, 4>), dim3(grid), dim3(256), 2 * (128 + 64) * BK * 2, st, T, B, D,
-                       E, zero_page(), stats, g);
+                       E, zero_page(), stats, bnb, g);
   } else {  // 128 x 128 tile: 2x2 waves of 64x64
     const int grid = pgrid((long)kfa_ceil_div(g.M, 128) * kfa_ceil_div(N, 128));
     hipLaunchKernelGGL((conv_igemm_kernel<2, 2, 4, 4>), dim3(grid), dim3(256), 2 * (128 + 128) * BK * 2, st, T, B, D,
-                       E, zero_page(), stats, g);
+                       E, zero_page(), stats, bnb, g);
   }
   return kfa_status();
 }

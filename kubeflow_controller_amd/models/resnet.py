@@ -41,15 +41,17 @@ class Bottleneck(nn.Module):
         # (ops.conv.GradJoin) instead of a separate add kernel.  In training every
         # conv accumulates its BatchNorm's statistics in its epilogue (st=True):
         # the BN then only finalizes + applies (no stats pass over the output).
+        # bn1 / bn2 outputs feed exactly one conv (conv2 / conv3): their backward
+        # statistics are accumulated in that conv's dgrad epilogue (bwd_link).
         join = GradJoin()
         st = self.training
         if self.downsample is None:
-            y = self.bn1(self.conv1(x, join=join, bn_stats=st))
-            y = self.bn2(self.conv2(y, bn_stats=st))
+            y = self.bn1(self.conv1(x, join=join, bn_stats=st), bwd_link=st)
+            y = self.bn2(self.conv2(y, bn_stats=st), bwd_link=st)
             return self.bn3(self.conv3(y, bn_stats=st), residual=join.branch(x))
         idn = self.downsample["bn"](self.downsample["conv"](x, join=join, bn_stats=st))
-        y = self.bn1(self.conv1(join.branch(x), bn_stats=st))
-        y = self.bn2(self.conv2(y, bn_stats=st))
+        y = self.bn1(self.conv1(join.branch(x), bn_stats=st), bwd_link=st)
+        y = self.bn2(self.conv2(y, bn_stats=st), bwd_link=st)
         return self.bn3(self.conv3(y, bn_stats=st), residual=idn)
 
 

@@ -35,6 +35,22 @@ def _mc(t: torch.Tensor):
 
 
 _lib.register("kfa_bn_fwd_train_prestats", [_lib.P] * 11 + [_lib.L, _lib.I, _lib.F, _lib.F, _lib.I, _lib.P])
+_lib.register("kfa_bn_bwd_prestats", [_lib.P] * 12 + [_lib.L, _lib.I, _lib.I, _lib.I, _lib.P])
+
+
+class BnBwdLink:
+    """Hand-off from a BatchNorm to the ONE convolution consuming its output: the
+    conv's dgrad epilogue accumulates this BN's backward statistics (sum dz,
+    sum dz*(x-mean)) into the BN slots and sets ``prestats``; the BN backward
+    then skips its statistics pass.  Only valid when that conv is the sole
+    consumer of the BN output (the model decides: ResNet bn1/bn2)."""
+
+    __slots__ = ("x", "y", "mean", "relu", "prestats")
+
+    def __init__(self):
+        self.x = self.y = self.mean = None
+        self.relu = False
+        self.prestats = False
 
 
 def bn_slot_workspace(C: int, device) -> torch.Tensor:
@@ -53,7 +69,7 @@ def _workspaces(C: int, device):
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, residual, training, momentum, eps, relu,
-                prestats=False):
+                prestats=False, link=None):
         x = _as_rows(x)
         M, C = _mc(x)
         if x.dtype != torch.bfloat16:
@@ -78,6 +94,9 @@ class _BNActFn(torch.autograd.Function):
             mean = running_mean.clone()
             invstd = torch.rsqrt(var + eps)
         ctx.save_for_backward(x, y if relu else None, weight, mean, invstd)
+        ctx.link = link if training else None
+        if ctx.link is not None:
+            link.x, link.y, link.mean, link.relu, link.prestats = x, (y if relu else None), mean, bool(relu), False
         ctx.relu = relu
         ctx.has_res = residual is not None
         ctx.params = (weight, bias)
@@ -102,28 +121,39 @@ class _BNActFn(torch.autograd.Function):
                 dgamma = torch.empty(C, dtype=torch.float32, device=x.device)
                 dbeta = torch.empty(C, dtype=torch.float32, device=x.device)
         slots, coef = _workspaces(C, x.device)
-        _lib.call("kfa_bn_bwd", _lib.ptr(dy), _lib.ptr(x), _lib.ptr(y), _lib.ptr(weight), _lib.ptr(mean),
+        lk = ctx.link
+        pre = lk is not None and lk.prestats
+        if lk is not None:
+            lk.prestats = False
+            lk.x = lk.y = lk.mean = None
+        _lib.call("kfa_bn_bwd_prestats" if pre else "kfa_bn_bwd", _lib.ptr(dy), _lib.ptr(x), _lib.ptr(y), _lib.ptr(weight), _lib.ptr(mean),
                   _lib.ptr(invstd), _lib.ptr(dx), _lib.ptr(dres), _lib.ptr(dgamma), _lib.ptr(dbeta), _lib.ptr(slots),
                   _lib.ptr(coef),
                   M, C, int(ctx.relu), int(direct), _lib.stream())
         if direct:
             notify_grad_ready(ctx.params[0])
             notify_grad_ready(ctx.params[1])
-            return dx, None, None, None, None, dres, None, None, None, None, None
+            return dx, None, None, None, None, dres, None, None, None, None, None, None
         if dgamma is not None and weight is not None and weight.dtype != torch.float32:
             dgamma, dbeta = dgamma.to(weight.dtype), dbeta.to(weight.dtype)
-        return dx, dgamma, dbeta, None, None, dres, None, None, None, None, None
+        return dx, dgamma, dbeta, None, None, dres, None, None, None, None, None, None
 
 
 def bn_act(x, weight, bias, running_mean, running_var, residual=None, training=True, momentum=0.1, eps=1e-5,
-           relu=True, prestats=False):
+           relu=True, prestats=False, bwd_link=False):
     """``prestats``: the statistics of ``x`` already sit in the BN slot workspace
-    (accumulated by the producing convolution's epilogue)."""
+    (accumulated by the producing convolution's epilogue).  ``bwd_link``: the
+    output feeds exactly one igemm convolution, whose dgrad epilogue may compute
+    this BN's backward statistics (``BnBwdLink``)."""
     if prestats and not training:  # never leave the self-cleaning slots dirty
         bn_slot_workspace(x.shape[1], x.device).zero_()
         prestats = False
-    return _BNActFn.apply(x, weight, bias, running_mean, running_var, residual, training, momentum, eps, relu,
-                          prestats)
+    link = BnBwdLink() if (bwd_link and training) else None
+    y = _BNActFn.apply(x, weight, bias, running_mean, running_var, residual, training, momentum, eps, relu,
+                       prestats, link)
+    if link is not None:
+        y._kfa_bn_link = link
+    return y
 
 
 def bn_act_reference(x, weight, bias, running_mean, running_var, residual=None, training=True, momentum=0.1,
@@ -153,10 +183,11 @@ class BatchNorm2dAct(nn.Module):
         self.register_buffer("running_mean", torch.zeros(num_features))
         self.register_buffer("running_var", torch.ones(num_features))
 
-    def forward(self, x, residual=None):
+    def forward(self, x, residual=None, bwd_link: bool = False):
         if x.is_cuda:
             return bn_act(x, self.weight, self.bias, self.running_mean, self.running_var, residual,
-                          self.training, self.momentum, self.eps, self.relu, getattr(x, "_kfa_prestats", False))
+                          self.training, self.momentum, self.eps, self.relu, getattr(x, "_kfa_prestats", False),
+                          bwd_link)
         # CPU path (plumbing tests / CPU-only MNIST-style jobs): plain PyTorch.
         y = torch.nn.functional.batch_norm(x, self.running_mean, self.running_var, self.weight.to(x.dtype),
                                            self.bias.to(x.dtype), self.training, self.momentum, self.eps)

@@ -31,7 +31,7 @@ from . import _lib
 from ..parallel.flat import direct_grad_view, notify_grad_ready
 
 P, I = _lib.P, _lib.I
-_lib.register("kfa_conv_igemm", [P, P, P, P] + [I] * 20 + [P, P])
+_lib.register("kfa_conv_igemm", [P, P, P, P] + [I] * 20 + [P, P, P, P, I, P])
 _lib.register("kfa_zero_bf16", [P, _lib.L, P])
 _lib.register("kfa_weight_transpose", [P, P] + [I] * 10 + [P])
 _lib.register("kfa_wgrad_part_floats", [I] * 7, _lib.L)
@@ -66,7 +66,8 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, stats=None
     Qo = (W + 2 * pad - S) // stride + 1
     y = torch.empty((Nb, Co, Po, Qo), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
     _lib.call("kfa_conv_igemm", _lib.ptr(x), _lib.ptr(w), _lib.ptr(y), None, Nb, H, W, C, Po, Qo, R, S, stride, 1,
-              -pad, -pad, Co, Po, Qo, 1, 0, 0, Co, _variant(Nb * Po * Qo, Co), _lib.ptr(stats), _lib.stream())
+              -pad, -pad, Co, Po, Qo, 1, 0, 0, Co, _variant(Nb * Po * Qo, Co), _lib.ptr(stats), None, None, None, 0,
+              _lib.stream())
     return y
 
 
@@ -79,7 +80,10 @@ def _transposed_weight(w: torch.Tensor, r0: int, dr: int, Rs: int, s0: int, ds: 
     return wt
 
 
-def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride: int, pad: int, addend=None) -> torch.Tensor:
+def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride: int, pad: int, addend=None,
+               bn=None) -> torch.Tensor:
+    """``bn``: a ``batchnorm.BnBwdLink`` of the BatchNorm whose output is this conv's
+    input — the epilogue then also accumulates that BN's backward statistics."""
     dy, w = _cl(dy), _cl(w)
     Nb, Co, Po, Qo = dy.shape
     _, Ci, R, S = w.shape
@@ -87,10 +91,16 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride: int, pad: int
     dx = torch.empty((Nb, Ci, H, W), dtype=dy.dtype, device=dy.device, memory_format=torch.channels_last)
     E = None if addend is None else _cl(addend)
     st = _lib.stream()
+    bn_args = (None, None, None, None, 0)
+    if bn is not None:
+        from .batchnorm import bn_slot_workspace
+        bn_args = (_lib.ptr(bn_slot_workspace(Ci, dy.device)), _lib.ptr(bn.x), _lib.ptr(bn.y), _lib.ptr(bn.mean),
+                   int(bn.relu))
+        bn.prestats = True
     if stride == 1:
         wt = _transposed_weight(w, 0, 1, R, 0, 1, S)
         _lib.call("kfa_conv_igemm", _lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), _lib.ptr(E), Nb, Po, Qo, Co, H, W, R, S,
-                  1, -1, pad, pad, Ci, H, W, 1, 0, 0, Ci, _variant(Nb * H * W, Ci), None, st)
+                  1, -1, pad, pad, Ci, H, W, 1, 0, 0, Ci, _variant(Nb * H * W, Ci), *bn_args, st)
         return dx
     # stride s: output parity classes.  For class (ph, pw) the rows h = s*i + ph
     # receive taps r with (ph + pad - r) % s == 0, from dY row i + (ph + pad - r)/s.
@@ -110,7 +120,7 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride: int, pad: int
             oa_h = (ph + pad - r0) // stride
             oa_w = (pw + pad - s0) // stride
             _lib.call("kfa_conv_igemm", _lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), _lib.ptr(E), Nb, Po, Qo, Co, Hc, Wc,
-                      Rs, Ss, 1, -1, oa_h, oa_w, Ci, H, W, stride, ph, pw, Ci, _variant(Nb * Hc * Wc, Ci), None,
+                      Rs, Ss, 1, -1, oa_h, oa_w, Ci, H, W, stride, ph, pw, Ci, _variant(Nb * Hc * Wc, Ci), *bn_args,
                       st)
     return dx
 
@@ -202,6 +212,7 @@ class _ConvFn(torch.autograd.Function):
         ctx.save_for_backward(x, w)
         ctx.stride, ctx.pad, ctx.join = stride, pad, join
         ctx.wparam = w  # the Parameter itself (for the direct flat-gradient write)
+        ctx.bn_link = getattr(x, "_kfa_bn_link", None)  # x = output of a BatchNorm (see conv_dgrad)
         return conv_fwd(x, w, stride, pad, stats)
 
     @staticmethod
@@ -217,7 +228,7 @@ class _ConvFn(torch.autograd.Function):
                 else:
                     j.state = "consumer-first"
             if w.shape[0] % 64 == 0 and w.shape[1] % 8 == 0:
-                dx = conv_dgrad(dy, w, x.shape, ctx.stride, ctx.pad, addend)
+                dx = conv_dgrad(dy, w, x.shape, ctx.stride, ctx.pad, addend, ctx.bn_link)
             else:
                 dx = torch.nn.grad.conv2d_input(x.shape, w, dy, ctx.stride, ctx.pad)
                 if addend is not None:

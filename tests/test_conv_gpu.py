@@ -162,3 +162,35 @@ def test_bn_stats_fused_into_conv_epilogue(Cin, Cout, k, stride):
     torch.testing.assert_close(bn_a.running_var, bn_b.running_var, atol=1e-3, rtol=1e-3)
     torch.cuda.synchronize()
     assert bn_slot_workspace(Cout, d).abs().max().item() == 0
+
+
+@pytest.mark.parametrize("C,Cout,k,stride", [(64, 64, 3, 1), (128, 128, 3, 2), (64, 256, 1, 1)])
+def test_bn_bwd_stats_fused_into_dgrad_epilogue(C, Cout, k, stride):
+    """BN(+ReLU) -> conv: the conv's dgrad epilogue accumulates the BN's backward
+    statistics (BnBwdLink); gradients match the unfused pair and the slots end clean."""
+    from kubeflow_controller_amd.ops.batchnorm import BatchNorm2dAct, bn_slot_workspace
+    from kubeflow_controller_amd.ops.conv import Conv2d
+    d = torch.device("cuda")
+    torch.manual_seed(0)
+    bn = BatchNorm2dAct(C).to(d)
+    torch.nn.init.uniform_(bn.weight, 0.5, 1.5)
+    torch.nn.init.uniform_(bn.bias, -0.2, 0.2)
+    conv = Conv2d(C, Cout, k, stride=stride, padding=k // 2).to(d)
+    conv.weight.data = conv.weight.data.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x = torch.randn(4, C, 28, 28, device=d).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dy = None
+    grads = []
+    for link in (True, False):
+        xr = x.clone().requires_grad_()
+        for p in list(bn.parameters()) + list(conv.parameters()):
+            p.grad = None
+        y = conv(bn(xr, bwd_link=link))
+        if dy is None:
+            dy = torch.randn_like(y)
+        y.backward(dy)
+        grads.append([xr.grad.float(), bn.weight.grad.clone(), bn.bias.grad.clone(), conv.weight.grad.float()])
+    for a, b in zip(*grads):
+        scale = max(1e-3, b.abs().max().item())
+        assert (a - b).abs().max().item() < 2e-2 * scale, ((a - b).abs().max().item(), scale)
+    torch.cuda.synchronize()
+    assert bn_slot_workspace(C, d).abs().max().item() == 0
