@@ -1,0 +1,329 @@
+// Dense GEMM with fused epilogues on MFMA (bf16 in, fp32 accumulate) — SURVEY
+// §2.6 K1 "GEMM + bias (+ReLU/GELU) epilogue": the BERT encoder projections
+// (forward and dgrad), the MLM transform / pooler and the Wide&Deep MLP.
+//
+//   C[m][n] = epilogue( Σ_k A[m][k] · B[n][k] )    A [M][lda], B [N][ldb]: K-contiguous
+//
+//   forward  y  = act(x·Wᵀ + b) : A = x,  B = W   ([out][in], as stored)
+//   dgrad    dx = dy·W          : A = dy, B = Wᵀ  (transposed once per backward)
+//
+// Epilogue, fused into the tile write-out:
+//   v = acc + bias[n]                (fp32, before any rounding)
+//   v += E[m][n]                     (residual-gradient join)
+//   Z[m][n] = v                      (pre-activation, kept for the backward)
+//   v = act(v);  v *= act'(Zin[m][n]) (forward activation / backward of one)
+//   C[m][n] = v;  dbias[n] += Σ_m v  (fp32 column sums: one atomic per column per wave tile)
+//
+// CDNA4 tiling (cdna_hip_programming.md §5): 512 threads = 8 waves, block tile
+// 256 x BN (BN = 256: 2x4 waves of 128x64; BN = 128: 4x2 waves of 64x64),
+// v_mfma_f32_16x16x32_bf16, K advances 32 per LDS slot.  Operands move
+// HBM/L2 -> LDS by LDS-DMA (global_load_lds, 16 B per lane) into a 4-slot
+// ring: k-step t+3 is issued while t is multiplied, ONE raw s_barrier per
+// k-step, and the counted vmcnt in front of it keeps the two younger k-steps
+// in flight (never vmcnt(0) in the main loop — "Pipelining across barriers").
+// Slot rows are 64 B; 16-B chunk c of row r is stored at c ^ ((r >> 2) & 2),
+// applied on the per-lane SOURCE address (rule 21): with MI355X's ds_read_b128
+// lane groups ({0-3,12-15,20-27}, ...) every 16x16x32 operand read is
+// conflict-free.  Blocks sharing an XCD take consecutive tiles of one A
+// row-panel (T1, bijective remap).  Each wave stages its tile through LDS so
+// the write-out is 16 B per lane, 8 rows x 128 B per wave instruction.
+#include "common.h"
+
+namespace {
+
+constexpr int GK = 32;     // k per ring slot (one MFMA k-step)
+constexpr int NSLOT = 4;   // ring depth: prefetch distance NSLOT - 1
+constexpr unsigned kOOB = 0x80000000u;
+
+enum Act { kNone = 0, kGelu = 1, kTanh = 2, kRelu = 3 };
+
+__device__ __forceinline__ float act_fwd(float z, int act) {
+  switch (act) {
+    case kGelu: return 0.5f * z * (1.f + erff(z * 0.70710678118654752f));
+    case kTanh: return tanhf(z);
+    case kRelu: return fmaxf(z, 0.f);
+    default: return z;
+  }
+}
+
+__device__ __forceinline__ float act_bwd(float z, int act) {
+  switch (act) {
+    case kGelu: {
+      const float cdf = 0.5f * (1.f + erff(z * 0.70710678118654752f));
+      return cdf + z * 0.39894228040143268f * __expf(-0.5f * z * z);
+    }
+    case kTanh: {
+      const float t = tanhf(z);
+      return 1.f - t * t;
+    }
+    case kRelu: return z > 0.f ? 1.f : 0.f;
+    default: return 1.f;
+  }
+}
+
+struct GemmArgs {
+  const bf16_t* A;
+  const bf16_t* B;
+  bf16_t* C;
+  const bf16_t* E;     // addend [M][ldc] or null
+  const float* bias;   // [N] or null
+  bf16_t* Z;           // pre-activation out [M][ldc] or null
+  const bf16_t* Zin;   // activation-derivative input [M][ldc] or null
+  float* dbias;        // column sums [N] (atomic) or null
+  int M, N, K, lda, ldb, ldc, act, dact;
+  unsigned c_bytes;    // extent of C / E / Z / Zin
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ uint4 bload(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+  return *reinterpret_cast<uint4*>(&v);
+}
+__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, unsigned off, uint4 v) {
+  using V = decltype(__builtin_amdgcn_raw_buffer_load_b128(r, 0, 0, 0));
+  __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<V*>(&v), r, off, 0, 0);
+}
+
+// 16 B per lane HBM/L2 -> LDS.  A plain device function: the builtin named
+// directly inside the templated kernel's lambda stops clang's host pass from
+// emitting the kernel's launch stub.
+__device__ __forceinline__ void lds_dma16(const bf16_t* src, bf16_t* dst) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else static_assert(N < 0, "vm_wait: add the literal");
+}
+
+// k-step t+1 landed for this wave; `ahead` younger k-steps (0..2) may stay in flight
+template <int GL>
+__device__ __forceinline__ void ring_wait(int ahead) {
+  if (ahead >= 2) vm_wait<2 * GL>();
+  else if (ahead == 1) vm_wait<GL>();
+  else vm_wait<0>();
+}
+
+template <int BN>
+__global__ __launch_bounds__(512) void gemm_nt_kernel(GemmArgs g, const bf16_t* __restrict__ zp) {
+  constexpr int BM = 256;
+  constexpr int WN = BN / 64, WM = 8 / WN;           // waves along N / M
+  constexpr int TM = BM / WM / 16, TN = 4;           // wave tile: 16*TM rows x 64 columns
+  constexpr int A_SLOT = BM * GK, B_SLOT = BN * GK;  // elements per ring slot
+  constexpr int GA = BM / 128, GB = BN / 128;        // LDS-DMA instructions per wave per k-step (16 rows each)
+  constexpr int GL = GA + GB;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[NSLOT * (A_SLOT + B_SLOT)];
+  bf16_t* As = smem;
+  bf16_t* Bs = smem + NSLOT * A_SLOT;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  // T1: blocks that share an XCD (blockIdx % 8) take consecutive tiles (bijective remap)
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q8 = nwg >> 3, r8 = nwg & 7, x8 = bid & 7;
+  const int wg = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + (bid >> 3);
+  const int ntn = (g.N + BN - 1) / BN;
+  const int m0 = (wg / ntn) * BM, n0 = (wg % ntn) * BN;
+
+  // LDS-DMA plan: instruction i of wave w fills rows (w*G + i)*16 + lane/4, physical
+  // chunk lane&3, from logical chunk (lane&3) ^ swz(row), swz(row) = (row >> 2) & 2
+  const int lrow = lane >> 2, lch = (lane & 3) ^ ((lane >> 4) & 2);
+  const bf16_t* a_src[GA];
+  const bf16_t* b_src[GB];
+#pragma unroll
+  for (int i = 0; i < GA; i++) {
+    const int m = m0 + (wave * GA + i) * 16 + lrow;
+    a_src[i] = m < g.M ? g.A + (long)m * g.lda + lch * 8 : nullptr;
+  }
+#pragma unroll
+  for (int i = 0; i < GB; i++) {
+    const int n = n0 + (wave * GB + i) * 16 + lrow;
+    b_src[i] = n < g.N ? g.B + (long)n * g.ldb + lch * 8 : nullptr;
+  }
+  auto issue = [&](int kt) {
+    const int slot = kt & (NSLOT - 1), k0 = kt * GK;
+    const bool kin = k0 + lch * 8 < g.K;  // K tail (K % 8 == 0): chunks past K read the zero page
+#pragma unroll
+    for (int i = 0; i < GA; i++)
+      lds_dma16((a_src[i] && kin) ? a_src[i] + k0 : zp, As + slot * A_SLOT + (wave * GA + i) * 16 * GK);
+#pragma unroll
+    for (int i = 0; i < GB; i++)
+      lds_dma16((b_src[i] && kin) ? b_src[i] + k0 : zp, Bs + slot * B_SLOT + (wave * GB + i) * 16 * GK);
+  };
+
+  // this lane's 16-B operand piece of a 16-row tile: row fr, logical chunk fq
+  const int fr = lane & 15, fq = lane >> 4;
+  const int loff = fr * GK + ((fq ^ ((fr >> 2) & 2)) << 3);
+  floatx4 acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; i++)
+#pragma unroll
+    for (int j = 0; j < TM; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (g.K + GK - 1) / GK;
+  issue(0);
+  if (nk > 1) issue(1);
+  if (nk > 2) issue(2);
+  ring_wait<GL>(nk > 2 ? 2 : nk - 1);
+  asm volatile("s_barrier" ::: "memory");
+  for (int t = 0; t < nk; t++) {
+    if (t + 3 < nk) issue(t + 3);  // slot (t+3)&3 = (t-1)&3: every wave passed the barrier after reading it
+    const bf16_t* At = As + (t & (NSLOT - 1)) * A_SLOT + wm * TM * 16 * GK + loff;
+    const bf16_t* Bt = Bs + (t & (NSLOT - 1)) * B_SLOT + wn * TN * 16 * GK + loff;
+    short8 af[TM], bq[TN];
+#pragma unroll
+    for (int i = 0; i < TN; i++) bq[i] = *reinterpret_cast<const short8*>(Bt + i * 16 * GK);
+#pragma unroll
+    for (int i = 0; i < TM; i++) af[i] = *reinterpret_cast<const short8*>(At + i * 16 * GK);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ni = 0; ni < TN; ni++)
+#pragma unroll
+      for (int mi = 0; mi < TM; mi++)
+        acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[ni], af[mi], acc[ni][mi], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    ring_wait<GL>((t + 3 < nk ? t + 3 : nk - 1) - (t + 1));
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+
+  // ---- epilogue: acc[ni][mi][r] = C(m = m0 + wm*16TM + 16mi + fr, n = n0 + wn*64 + 16ni + 4fq + r)
+  constexpr int ROWS = 16 * TM, RB = 32 * TN, IT = ROWS / 8;  // staged rows, bytes per row, row groups per lane
+  char* stage = reinterpret_cast<char*>(smem) + wave * ROWS * RB;  // ring is idle: every wave passed the last barrier
+  const int nw = n0 + wn * 64;
+  if (g.bias) {
+#pragma unroll
+    for (int ni = 0; ni < TN; ni++) {
+      const int n = nw + ni * 16 + fq * 4;
+      const float4 bb = n < g.N ? *reinterpret_cast<const float4*>(g.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int mi = 0; mi < TM; mi++) {
+        acc[ni][mi][0] += bb.x;
+        acc[ni][mi][1] += bb.y;
+        acc[ni][mi][2] += bb.z;
+        acc[ni][mi][3] += bb.w;
+      }
+    }
+  }
+#pragma unroll
+  for (int mi = 0; mi < TM; mi++)
+#pragma unroll
+    for (int ni = 0; ni < TN; ni++) {
+      const int row = mi * 16 + fr, col = ni * 16 + fq * 4;
+      *reinterpret_cast<uint2*>(stage + row * RB + (((col >> 3) ^ (row & 7)) << 4) + (col & 7) * 2) =
+          make_uint2(pack2(acc[ni][mi][0], acc[ni][mi][1]), pack2(acc[ni][mi][2], acc[ni][mi][3]));
+    }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave reads back only its own stage
+
+  const int c = lane & 7;
+  const int n = nw + c * 8;
+  const bool nok = n < g.N;
+  const __amdgpu_buffer_rsrc_t rC = rsrc(g.C, g.c_bytes);
+  const __amdgpu_buffer_rsrc_t rE = rsrc(g.E ? g.E : g.C, g.E ? g.c_bytes : 0u);
+  const __amdgpu_buffer_rsrc_t rZ = rsrc(g.Z ? g.Z : g.C, g.Z ? g.c_bytes : 0u);
+  const __amdgpu_buffer_rsrc_t rZi = rsrc(g.Zin ? g.Zin : g.C, g.Zin ? g.c_bytes : 0u);
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int it = 0; it < IT; it++) {
+    const int r = it * 8 + (lane >> 3);
+    const int m = m0 + wm * ROWS + r;
+    const unsigned off = (m < g.M && nok) ? ((unsigned)m * (unsigned)g.ldc + (unsigned)n) * 2u : kOOB;
+    float f[8];
+    unpack8(*reinterpret_cast<const uint4*>(stage + r * RB + ((c ^ (r & 7)) << 4)), f);
+    if (g.E) {
+      float h[8];
+      unpack8(bload(rE, off), h);
+#pragma unroll
+      for (int j = 0; j < 8; j++) f[j] += h[j];
+    }
+    if (g.Z) bstore(rZ, off, pack8(f));
+    if (g.act) {
+#pragma unroll
+      for (int j = 0; j < 8; j++) f[j] = act_fwd(f[j], g.act);
+    }
+    if (g.Zin) {
+      float z[8];
+      unpack8(bload(rZi, off), z);
+#pragma unroll
+      for (int j = 0; j < 8; j++) f[j] *= act_bwd(z[j], g.dact);
+    }
+    const uint4 o = pack8(f);
+    bstore(rC, off, o);
+    if (g.dbias && off != kOOB) {
+      float q[8];
+      unpack8(o, q);  // the bf16-rounded values the next layer sees
+#pragma unroll
+      for (int j = 0; j < 8; j++) cs[j] += q[j];
+    }
+  }
+  if (g.dbias) {
+#pragma unroll
+    for (int o = 8; o < 64; o <<= 1)
+#pragma unroll
+      for (int j = 0; j < 8; j++) cs[j] += __shfl_xor(cs[j], o, 64);
+    if (lane < 8 && nok)
+#pragma unroll
+      for (int j = 0; j < 8; j++) atomicAdd(g.dbias + n + j, cs[j]);
+  }
+}
+
+}  // namespace
+
+static const bf16_t* gemm_zero_page() {
+  static bf16_t* z = nullptr;
+  if (!z) {
+    if (hipMalloc(&z, 256) != hipSuccess) return nullptr;
+    (void)hipMemset(z, 0, 256);
+    (void)hipDeviceSynchronize();
+  }
+  return z;
+}
+
+static int gemm_cus() {
+  static int c = 0;
+  if (!c) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+    if (c <= 0) c = 256;
+  }
+  return c;
+}
+
+// Tile width for an M x N output: whole waves of tiles over the CUs, a 256x128
+// tile costing ~0.55 of a 256x256 one (lower arithmetic intensity).
+KFA_API int kfa_gemm_pick_bn(int M, int N) {
+  const long tm = (M + 255) / 256;
+  const long cus = gemm_cus();
+  const long w256 = (tm * ((N + 255) / 256) + cus - 1) / cus;
+  const long w128 = (tm * ((N + 127) / 128) + cus - 1) / cus;
+  return (N <= 128 || 0.55 * (double)w128 < (double)w256) ? 128 : 256;
+}
+
+// C = epilogue(A · Bᵀ); see the file comment.  bn: 0 = auto, 128 or 256.
+KFA_API int kfa_gemm_nt(const bf16_t* A, const bf16_t* B, bf16_t* C, const bf16_t* E, const float* bias, bf16_t* Z,
+                        const bf16_t* Zin, float* dbias, int M, int N, int K, int lda, int ldb, int ldc, int act,
+                        int dact, int bn, hipStream_t st) {
+  if (M <= 0 || N <= 0) return 0;
+  if (K <= 0 || K % 8 || N % 8 || lda % 8 || ldb % 8 || ldc % 8 || lda < K || ldb < K || ldc < N) return -1;
+  if (act < 0 || act > 3 || dact < 0 || dact > 3) return -1;
+  const long cb = (long)M * ldc * 2;
+  if (cb >= (long)kOOB) return -2;  // 32-bit buffer offsets in the epilogue
+  if (bn == 0) bn = kfa_gemm_pick_bn(M, N);
+  const long tiles = (long)((M + 255) / 256) * ((N + bn - 1) / bn);
+  if (tiles >= (1L << 31)) return -2;
+  const GemmArgs g{A, B, C, E, bias, Z, Zin, dbias, M, N, K, lda, ldb, ldc, act, dact, (unsigned)cb};
+  if (bn == 256)
+    hipLaunchKernelGGL((gemm_nt_kernel<256>), dim3((unsigned)tiles), dim3(512), 0, st, g, gemm_zero_page());
+  else if (bn == 128)
+    hipLaunchKernelGGL((gemm_nt_kernel<128>), dim3((unsigned)tiles), dim3(512), 0, st, g, gemm_zero_page());
+  else
+    return -1;
+  return kfa_status();
+}

@@ -102,6 +102,19 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found (ROCm toolchain required to build the HIP kernels)")
 
 
+def _check_stubs(so: str) -> None:
+    """Fail the build if a kernel's host launch stub is missing from the .so
+    (clang's host pass silently drops the stub of a templated kernel whose body
+    it cannot instantiate; the library then only fails at dlopen on the GPU box)."""
+    nm = shutil.which("nm")
+    if not nm:
+        return
+    out = subprocess.run([nm, "-u", so], capture_output=True, text=True).stdout
+    bad = [l.split()[-1] for l in out.splitlines() if "__device_stub__" in l]
+    if bad:
+        raise RuntimeError(f"HIP kernel build: undefined launch stubs in {so}: {bad}")
+
+
 def build_kernels(force: bool = False, jobs: int = 8) -> str:
     """Compile every ``csrc/kernels/*.hip`` for gfx950 and link one .so."""
     srcs = kernel_sources()
@@ -133,6 +146,7 @@ def build_kernels(force: bool = False, jobs: int = 8) -> str:
             raise RuntimeError("HIP kernel build failed:\n" + "\n".join(errs))
         tmp = tgt + f".tmp{os.getpid()}"
         _run([cc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp], quiet=True)
+        _check_stubs(tmp)
         os.replace(tmp, tgt)
         _write_stamp(tgt, srcs)
     return tgt

@@ -1,0 +1,125 @@
+"""Dense GEMM + fused epilogues on the hand-written MFMA kernel
+(``csrc/kernels/gemm.hip``) — SURVEY §2.6 K1 "GEMM + bias (+ReLU/GELU) epilogue".
+
+``gemm_nt(a, b)`` computes ``epilogue(a @ b.T)`` for bf16 ``a [M, K]`` and
+``b [N, K]`` (both K-contiguous): the forward of a dense layer (``b`` = the
+weight as stored, ``[out, in]``) and its dgrad (``b`` = :func:`transpose` of
+the weight).  Epilogue options, all fused into the tile write-out:
+
+* ``bias`` (fp32, added to the fp32 accumulator before any rounding);
+* ``addend`` (bf16 ``[M, N]``, e.g. a residual-gradient join);
+* ``want_z`` (also return the pre-activation, for the backward);
+* ``act`` (``gelu`` / ``tanh`` / ``relu``);
+* ``zin`` + ``dact`` (multiply by ``act'(zin)``: the backward of the NEXT
+  layer's activation, fused into this dgrad);
+* ``dbias`` (fp32 ``[N]``: column sums of the output accumulated into a
+  bias-gradient vector, e.g. a flat-buffer gradient view).
+
+``gemm_reference`` is the plain PyTorch fp32 definition the tests compare to.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+from . import conv as _conv  # noqa: F401  (registers kfa_weight_transpose)
+
+P, I = _lib.P, _lib.I
+_lib.register("kfa_gemm_nt", [P] * 8 + [I] * 9 + [P])
+_lib.register("kfa_gemm_pick_bn", [I, I])
+
+ACTS = {None: 0, "none": 0, "gelu": 1, "tanh": 2, "relu": 3}
+# Dense layers route their projections through this kernel only with KFA_GEMM=1.
+# Measured on MI355X (tools/bench_gemm.py, profiles/r1_gemm_attention.md):
+# hipBLASLt runs the plain BERT / Wide&Deep projections at 800-1250 TFLOP/s vs
+# 550-830 here, and the fused epilogue does not make up the difference, so the
+# default keeps plain GEMMs on the library (the one place it is allowed).
+ROUTE_LAYERS = os.environ.get("KFA_GEMM", "0") == "1"
+
+
+def gemm_ok(a: torch.Tensor, b: torch.Tensor) -> bool:
+    """Operands the kernel takes: bf16 CUDA matrices, K-contiguous, K / N / row
+    strides multiples of 8 (16-B LDS-DMA pieces), 16-B aligned."""
+    return (a.is_cuda and b.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16
+            and a.dim() == 2 and b.dim() == 2 and a.shape[1] == b.shape[1] and a.shape[1] % 8 == 0
+            and b.shape[0] % 8 == 0 and a.shape[0] > 0 and a.stride(1) == 1 and b.stride(1) == 1
+            and a.stride(0) % 8 == 0 and b.stride(0) % 8 == 0 and a.data_ptr() % 16 == 0
+            and b.data_ptr() % 16 == 0 and a.shape[0] * b.shape[0] * 2 < (1 << 31))
+
+
+def _check_mn(t, M, N, what):
+    if t is not None and (t.dtype != torch.bfloat16 or tuple(t.shape) != (M, N) or not t.is_contiguous()
+                          or t.data_ptr() % 16):
+        raise ValueError(f"gemm_nt: {what} must be a contiguous bf16 [{M}, {N}] tensor")
+
+
+def _check_vec(t, N, what):
+    if t is not None and (t.dtype != torch.float32 or t.numel() != N or not t.is_contiguous()
+                          or t.data_ptr() % 16):
+        raise ValueError(f"gemm_nt: {what} must be a contiguous, 16-B aligned fp32 [{N}] vector")
+
+
+def gemm_nt(a, b, *, bias=None, act=None, addend=None, want_z=False, zin=None, dact=None, dbias=None, out=None,
+            bn: int = 0):
+    """``(C, Z)`` with ``C = epilogue(a @ b.T)`` (see module doc); ``Z`` is None unless ``want_z``."""
+    if not gemm_ok(a, b):
+        raise ValueError(f"gemm_nt: unsupported operands {tuple(a.shape)}/{a.dtype} x {tuple(b.shape)}/{b.dtype}")
+    M, K = a.shape
+    N = b.shape[0]
+    c = out if out is not None else torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
+    _check_mn(c, M, N, "out")
+    _check_mn(addend, M, N, "addend")
+    _check_mn(zin, M, N, "zin")
+    _check_vec(bias, N, "bias")
+    if dbias is not None and (dbias.dtype != torch.float32 or dbias.numel() != N or not dbias.is_contiguous()):
+        raise ValueError(f"gemm_nt: dbias must be a contiguous fp32 [{N}] vector")
+    if (zin is None) != (dact in (None, "none")):
+        raise ValueError("gemm_nt: zin and dact go together")
+    z = torch.empty_like(c) if want_z else None
+    _lib.call("kfa_gemm_nt", _lib.ptr(a), _lib.ptr(b), _lib.ptr(c), _lib.ptr(addend), _lib.ptr(bias), _lib.ptr(z),
+              _lib.ptr(zin), _lib.ptr(dbias), M, N, K, a.stride(0), b.stride(0), N, ACTS[act], ACTS[dact], int(bn),
+              _lib.stream())
+    return c, z
+
+
+def transpose(w: torch.Tensor) -> torch.Tensor:
+    """Contiguous ``w.T`` of a bf16 ``[R, C]`` matrix on the LDS-tiled HIP transpose
+    (the dgrad B operand: ``dx = dy · W`` is ``gemm_nt(dy, transpose(W))``)."""
+    R, C = w.shape
+    w = w.contiguous()
+    wt = torch.empty(C, R, dtype=w.dtype, device=w.device)
+    _lib.call("kfa_weight_transpose", _lib.ptr(w), _lib.ptr(wt), R, 1, 1, C, 0, 1, 1, 0, 1, 1, _lib.stream())
+    return wt
+
+
+def _act(z, act):
+    if act == "gelu":
+        return F.gelu(z)
+    if act == "tanh":
+        return torch.tanh(z)
+    if act == "relu":
+        return torch.relu(z)
+    return z
+
+
+def _act_grad(z, act):
+    zz = z.detach().float().requires_grad_()
+    _act(zz, act).sum().backward()
+    return zz.grad
+
+
+def gemm_reference(a, b, bias=None, act=None, addend=None, zin=None, dact=None):
+    """Plain PyTorch fp32 ``(C, Z)`` of :func:`gemm_nt`."""
+    v = a.float() @ b.float().t()
+    if bias is not None:
+        v = v + bias.float()
+    if addend is not None:
+        v = v + addend.float()
+    z = v
+    v = _act(v, act)
+    if zin is not None:
+        v = v * _act_grad(zin, dact)
+    return v, z

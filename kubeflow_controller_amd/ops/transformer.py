@@ -23,12 +23,14 @@ path and the numerics tests.
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
 import torch.nn.functional as F
 
 from . import _lib
+from . import gemm as _gemm
 from . import loss as _loss  # noqa: F401  (registers kfa_softmax_xent)
 from ..parallel.flat import direct_grad_view, notify_grad_ready
 
@@ -49,6 +51,11 @@ _lib.register("kfa_attn_softmax_bwd", [P, P, L, I, Fl, U64, P])
 _lib.register("kfa_embed_fwd", [P, P, P, P, P, P, I, P, L, I, L, P])
 _lib.register("kfa_embed_bwd", [P, P, L, P, P, I, L, I, I, P])
 _lib.register("kfa_colsum", [P, P, P, L, I, I, P])
+_lib.register("kfa_attn_fwd", [P, P, P, P, P, I, I, I, I, Fl, Fl, U64, P])
+_lib.register("kfa_attn_bwd", [P, P, P, P, P, P, P, P, I, I, I, I, Fl, Fl, U64, P])
+
+# env KFA_FUSED_ATTN=0 falls back to the split kernels + batched library GEMMs
+FUSED_ATTN = os.environ.get("KFA_FUSED_ATTN", "1") != "0"
 
 ACTS = {None: 0, "none": 0, "gelu": 1, "tanh": 2, "relu": 3}
 SMALL_TABLE_ROWS = 1024
@@ -182,34 +189,53 @@ def layer_norm(x, gamma, beta, eps=1e-12):
 
 # ----------------------------------------------------------------------------- dense + bias + act
 class DenseFn(torch.autograd.Function):
-    """y = dropout(act(x · Wᵀ + b)) — GEMM then one fused epilogue pass."""
+    """y = dropout(act(x · Wᵀ + b)).
+
+    Without dropout the whole layer is ONE launch of the MFMA GEMM with the
+    bias / activation epilogue (``ops/gemm.py``), which also keeps the
+    pre-activation for the backward; the dgrad runs on the same kernel against
+    the transposed weight.  With dropout: library GEMM + one fused epilogue pass."""
 
     @staticmethod
     def forward(ctx, x, weight, bias, act, p, seed):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
-        z = torch.mm(x2, weight.t())
-        y = bias_act_fwd(z, bias, act, p, seed) if (bias is not None or act not in (None, "none") or p > 0) else z
-        ctx.save_for_backward(x2, weight, z if act not in (None, "none") else None)
+        has_act = act not in (None, "none")
+        fused = p == 0 and _gemm.ROUTE_LAYERS and _gemm.gemm_ok(x2, weight) and (
+            bias is None or (bias.dtype == torch.float32 and bias.is_contiguous() and bias.data_ptr() % 16 == 0))
+        if fused:
+            y, z = _gemm.gemm_nt(x2, weight, bias=bias, act=act, want_z=has_act)  # z includes the bias
+        else:
+            z = torch.mm(x2, weight.t())
+            y = bias_act_fwd(z, bias, act, p, seed) if (bias is not None or has_act or p > 0) else z
+        ctx.save_for_backward(x2, weight, z if has_act else None)
         ctx.bias = bias
-        ctx.cfg = (act, p, seed, shp)
+        ctx.cfg = (act, p, seed, shp, fused)
         return y.view(*shp[:-1], weight.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
         x2, weight, z = ctx.saved_tensors
         bias = ctx.bias
-        act, p, seed, shp = ctx.cfg
+        act, p, seed, shp, fused = ctx.cfg
+        has_act = act not in (None, "none")
         dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
         gb = db = None
         if bias is not None:
             gb, _, db = _grad_target(bias)
-        if act not in (None, "none") or p > 0 or bias is not None:
-            dz = bias_act_bwd(dy2, z, bias, act, gb, p, seed, want_dx=(act not in (None, "none") or p > 0))
+        if has_act or p > 0 or bias is not None:
+            # fused forward: z already holds the bias, so act' is evaluated at z itself
+            dz = bias_act_bwd(dy2, z, None if fused else bias, act, gb, p, seed, want_dx=(has_act or p > 0))
             dz = dy2 if dz is None else dz
         else:
             dz = dy2
-        dx = torch.mm(dz, weight).view(shp) if ctx.needs_input_grad[0] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            wt = _gemm.transpose(weight) if (fused and weight.shape[1] % 8 == 0) else None
+            if wt is not None and _gemm.gemm_ok(dz, wt):
+                dx = _gemm.gemm_nt(dz, wt)[0].view(shp)
+            else:
+                dx = torch.mm(dz, weight).view(shp)
         gw, _, dw = _grad_target(weight)
         _wgrad_(gw, dz, x2)
         return dx, _finish(weight, gw, dw), (_finish(bias, gb, db) if bias is not None else None), None, None, None
@@ -296,12 +322,75 @@ def embedding_sum(tables, ids):
     return EmbeddingSumFn.apply(ids[0], ids[1], ids[2], tables[0], tables[1], tables[2])
 
 
+# ----------------------------------------------------------------------------- fused attention
+def fused_attention_ok(S: int, d: int) -> bool:
+    """``csrc/kernels/attention.hip`` covers sequence 128 x head dim 64 (BERT-base/large phase 1)."""
+    return FUSED_ATTN and S == 128 and d == 64
+
+
+def _attn_biases(bqkv, key_bias, W3, T_, dev):
+    """The kernels always read both biases (no branches around their prologue
+    loads): absent ones become zeros."""
+    if bqkv is None:
+        bqkv = torch.zeros(W3, dtype=torch.float32, device=dev)
+    elif bqkv.dtype != torch.float32 or bqkv.numel() != W3 or not bqkv.is_contiguous():
+        raise ValueError("attention: bqkv must be a contiguous fp32 [3H] vector")
+    if key_bias is None:
+        key_bias = torch.zeros(T_, dtype=torch.float32, device=dev)
+    return bqkv, key_bias
+
+
+def attn_fwd(qkv, bqkv, key_bias, B, S, heads, p=0.0, seed=0):
+    """(ctx [B*S, H], lse [B*heads, S]) of softmax((q+b)(k+b)ᵀ/√d + key_bias)·(v+b), dropout p."""
+    T_, W3 = qkv.shape
+    H = W3 // 3
+    d = H // heads
+    if not (fused_attention_ok(S, d) and T_ == B * S and qkv.is_contiguous() and qkv.dtype == torch.bfloat16):
+        raise ValueError(f"attn_fwd: unsupported shape qkv {tuple(qkv.shape)}, B={B} S={S} heads={heads}")
+    if key_bias is not None and (key_bias.dtype != torch.float32 or key_bias.numel() != B * S
+                                 or not key_bias.is_contiguous()):
+        raise ValueError("attn_fwd: key_bias must be a contiguous fp32 [B, S] tensor")
+    bqkv, key_bias = _attn_biases(bqkv, key_bias, W3, B * S, qkv.device)
+    out = torch.empty(T_, H, dtype=qkv.dtype, device=qkv.device)
+    lse = torch.empty(B * heads, S, dtype=torch.float32, device=qkv.device)
+    _lib.call("kfa_attn_fwd", _lib.ptr(qkv), _lib.ptr(bqkv), _lib.ptr(key_bias), _lib.ptr(out), _lib.ptr(lse), B, S,
+              heads, d, 1.0 / math.sqrt(d), float(p), int(seed) & _MASK64, _lib.stream())
+    return out, lse
+
+
+def attn_bwd(qkv, bqkv, key_bias, out, lse, dout, dbqkv, B, S, heads, p=0.0, seed=0):
+    """dqkv [B*S, 3H] of :func:`attn_fwd` (``out``, ``lse``: its outputs); the bias
+    gradient is added into ``dbqkv`` (fp32, nullable)."""
+    T_, W3 = qkv.shape
+    H = W3 // 3
+    d = H // heads
+    dout = dout.contiguous()
+    if tuple(dout.shape) != (T_, H) or dout.dtype != qkv.dtype:
+        raise ValueError("attn_bwd: dout must be bf16 [B*S, H]")
+    if tuple(out.shape) != (T_, H) or out.dtype != qkv.dtype or not out.is_contiguous():
+        raise ValueError("attn_bwd: out must be the contiguous bf16 [B*S, H] forward output")
+    bqkv, key_bias = _attn_biases(bqkv, key_bias, W3, B * S, qkv.device)
+    dqkv = torch.empty_like(qkv)
+    _lib.call("kfa_attn_bwd", _lib.ptr(qkv), _lib.ptr(bqkv), _lib.ptr(key_bias), _lib.ptr(out), _lib.ptr(lse),
+              _lib.ptr(dout), _lib.ptr(dqkv), _lib.ptr(dbqkv), B, S, heads, d, 1.0 / math.sqrt(d), float(p),
+              int(seed) & _MASK64, _lib.stream())
+    return dqkv
+
+
 # ----------------------------------------------------------------------------- encoder layer
 class EncoderLayerFn(torch.autograd.Function):
     """Post-LN BERT encoder layer, forward + backward written out (see module doc).
 
     Inputs: x [T, H] bf16 (T = B·S), key_bias [B, S] fp32 additive mask (or None),
-    then the 12 parameters.  cfg = (B, S, heads, p_hidden, p_attn, seed, eps)."""
+    then the 12 parameters.  cfg = (B, S, heads, p_hidden, p_attn, seed, eps).
+
+    MI355X path: the four projections (forward and dgrad) run on the MFMA GEMM of
+    ``ops/gemm.py`` — FFN-up with its bias + GELU epilogue (keeping the
+    pre-activation), its dgrad with the GELU backward + bias-gradient column sums
+    fused in, the residual-gradient joins as GEMM addends — and attention is ONE
+    fused kernel each way (``csrc/kernels/attention.hip``, S = 128, d = 64) that
+    reads the QKV projection and writes the context / the QKV gradient directly.
+    Other shapes fall back to library GEMMs + the split attention kernels."""
 
     @staticmethod
     def forward(ctx, x, key_bias, cfg, wqkv, bqkv, wo, bo, g1, be1, w1, b1, w2, b2, g2, be2):
@@ -312,40 +401,53 @@ class EncoderLayerFn(torch.autograd.Function):
         st = _lib.stream()
         dev = x.device
         s_attn, s_h1, s_h2 = mix_seed(seed, 1), mix_seed(seed, 2), mix_seed(seed, 3)
+        use_g = _gemm.ROUTE_LAYERS and _gemm.gemm_ok(x, wqkv) and _gemm.gemm_ok(x, w1) and w2.shape[0] % 8 == 0 and w2.shape[1] % 8 == 0
+        mm = (lambda a, w: _gemm.gemm_nt(a, w)[0]) if use_g else (lambda a, w: torch.mm(a, w.t()))  # noqa: E731
+        fused = fused_attention_ok(S, d)
         # attention
-        qkv = torch.mm(x, wqkv.t())                                       # [T, 3H]
-        q = torch.empty(B * heads, S, d, dtype=x.dtype, device=dev)
-        k = torch.empty_like(q)
-        v = torch.empty_like(q)
-        _lib.call("kfa_qkv_split", _lib.ptr(qkv), _lib.ptr(bqkv), _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), T, S, heads,
-                  d, qscale, st)
-        del qkv
-        probs = torch.bmm(q, k.transpose(1, 2))                           # [BH, S, S]
-        pdrop = torch.empty_like(probs) if pa > 0 else None
-        _lib.call("kfa_attn_softmax_fwd", _lib.ptr(probs), _lib.ptr(key_bias), _lib.ptr(pdrop), B * heads * S, S,
-                  heads, float(pa), s_attn, st)
-        ctx_h = torch.bmm(pdrop if pdrop is not None else probs, v)        # [BH, S, d]
-        ctxr = torch.empty(T, H, dtype=x.dtype, device=dev)
-        _lib.call("kfa_heads_permute", _lib.ptr(ctx_h), _lib.ptr(ctxr), T, S, heads, d, 1, st)
-        del ctx_h
-        ao = torch.mm(ctxr, wo.t())
+        qkv = mm(x, wqkv)                                                 # [T, 3H]
+        if fused:
+            ctxr, lse = attn_fwd(qkv, bqkv, key_bias, B, S, heads, pa, s_attn)
+            att = (qkv, lse)
+        else:
+            q = torch.empty(B * heads, S, d, dtype=x.dtype, device=dev)
+            k = torch.empty_like(q)
+            v = torch.empty_like(q)
+            _lib.call("kfa_qkv_split", _lib.ptr(qkv), _lib.ptr(bqkv), _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), T, S,
+                      heads, d, qscale, st)
+            del qkv
+            probs = torch.bmm(q, k.transpose(1, 2))                       # [BH, S, S]
+            pdrop = torch.empty_like(probs) if pa > 0 else None
+            _lib.call("kfa_attn_softmax_fwd", _lib.ptr(probs), _lib.ptr(key_bias), _lib.ptr(pdrop), B * heads * S,
+                      S, heads, float(pa), s_attn, st)
+            ctx_h = torch.bmm(pdrop if pdrop is not None else probs, v)    # [BH, S, d]
+            ctxr = torch.empty(T, H, dtype=x.dtype, device=dev)
+            _lib.call("kfa_heads_permute", _lib.ptr(ctx_h), _lib.ptr(ctxr), T, S, heads, d, 1, st)
+            del ctx_h
+            att = (q, k, v, probs, pdrop)
+        ao = mm(ctxr, wo)
         h1, h1s, m1, r1 = ln_fwd(ao, g1, be1, res=x, bias=bo, eps=eps, p=ph, seed=s_h1)
         del ao
-        # feed-forward
-        f1 = torch.mm(h1, w1.t())                                          # [T, I]
-        f1a = bias_act_fwd(f1, b1, "gelu")
-        f2 = torch.mm(f1a, w2.t())
+        # feed-forward; f1 = pre-activation (GEMM path: bias included)
+        if use_g:
+            f1a, f1 = _gemm.gemm_nt(h1, w1, bias=b1, act="gelu", want_z=True)
+        else:
+            f1 = torch.mm(h1, w1.t())                                      # [T, I]
+            f1a = bias_act_fwd(f1, b1, "gelu")
+        f2 = mm(f1a, w2)
         h2, h2s, m2, r2 = ln_fwd(f2, g2, be2, res=h1, bias=b2, eps=eps, p=ph, seed=s_h2)
-        ctx.save_for_backward(x, q, k, v, probs, pdrop, ctxr, h1, h1s, m1, r1, f1, f1a, h2s, m2, r2)
+        ctx.save_for_backward(x, ctxr, h1, h1s, m1, r1, f1, f1a, h2s, m2, r2, *att)
         ctx.params = (wqkv, bqkv, wo, bo, g1, be1, w1, b1, w2, b2, g2, be2)
-        ctx.cfg = (B, S, heads, ph, pa, (s_attn, s_h1, s_h2), qscale)
+        ctx.cfg = (B, S, heads, ph, pa, (s_attn, s_h1, s_h2), qscale, use_g, fused)
+        ctx.key_bias = key_bias
         return h2
 
     @staticmethod
     def backward(ctx, dy):
-        (x, q, k, v, probs, pdrop, ctxr, h1, h1s, m1, r1, f1, f1a, h2s, m2, r2) = ctx.saved_tensors
+        (x, ctxr, h1, h1s, m1, r1, f1, f1a, h2s, m2, r2, *att) = ctx.saved_tensors
         wqkv, bqkv, wo, bo, g1, be1, w1, b1, w2, b2, g2, be2 = ctx.params
-        B, S, heads, ph, pa, (s_attn, s_h1, s_h2), qscale = ctx.cfg
+        B, S, heads, ph, pa, (s_attn, s_h1, s_h2), qscale, use_g, fused = ctx.cfg
+        key_bias = ctx.key_bias
         T, H = x.shape
         d = H // heads
         st = _lib.stream()
@@ -355,38 +457,51 @@ class EncoderLayerFn(torch.autograd.Function):
         # LN2 (+ FFN2 bias grad, hidden dropout): dres -> h1, dbranch -> f2
         dh1_res, df2 = ln_bwd(dy, h2s, m2, r2, g2, G(g2), G(be2), G(b2), p=ph, seed=s_h2, want_branch=True)
         _wgrad_(G(w2), df2, f1a)
-        df1a = torch.mm(df2, w2)
+        if use_g:   # df1 = (df2 · W2) * gelu'(z1), db1 += colsum(df1): one GEMM launch
+            df1 = _gemm.gemm_nt(df2, _gemm.transpose(w2), zin=f1, dact="gelu", dbias=G(b1))[0]
+        else:
+            df1 = bias_act_bwd(torch.mm(df2, w2), f1, b1, "gelu", G(b1))
         del df2
-        df1 = bias_act_bwd(df1a, f1, b1, "gelu", G(b1))
-        del df1a
         _wgrad_(G(w1), df1, h1)
-        dh1 = torch.addmm(dh1_res, df1, w1)        # residual-gradient join inside the GEMM
+        if use_g:   # residual-gradient join as the GEMM addend
+            dh1 = _gemm.gemm_nt(df1, _gemm.transpose(w1), addend=dh1_res)[0]
+        else:
+            dh1 = torch.addmm(dh1_res, df1, w1)
         del df1, dh1_res
         # LN1 (+ out-proj bias grad)
         dx_res, dao = ln_bwd(dh1, h1s, m1, r1, g1, G(g1), G(be1), G(bo), p=ph, seed=s_h1, want_branch=True)
         del dh1
         _wgrad_(G(wo), dao, ctxr)
-        dctxr = torch.mm(dao, wo)
+        dctxr = _gemm.gemm_nt(dao, _gemm.transpose(wo))[0] if use_g else torch.mm(dao, wo)
         del dao
-        dctx_h = torch.empty(B * heads, S, d, dtype=dy.dtype, device=dy.device)
-        _lib.call("kfa_heads_permute", _lib.ptr(dctxr), _lib.ptr(dctx_h), T, S, heads, d, 0, st)
-        del dctxr
-        pd = pdrop if pdrop is not None else probs
-        dv = torch.bmm(pd.transpose(1, 2), dctx_h)
-        dp = torch.bmm(dctx_h, v.transpose(1, 2))
-        del dctx_h
-        _lib.call("kfa_attn_softmax_bwd", _lib.ptr(probs), _lib.ptr(dp), B * heads * S, S, float(pa), s_attn, st)
-        dq = torch.bmm(dp, k)
-        dk = torch.bmm(dp.transpose(1, 2), q)
-        del dp
-        dqkv = torch.empty(T, 3 * H, dtype=dy.dtype, device=dy.device)
-        W3 = 3 * H
-        part = _part(_lib.lib().kfa_colsum_part_floats(T, W3), dy.device)
-        _lib.call("kfa_qkv_merge_bwd", _lib.ptr(dq), _lib.ptr(dk), _lib.ptr(dv), _lib.ptr(dqkv), _lib.ptr(part),
-                  _lib.ptr(G(bqkv)), T, S, heads, d, qscale, 1, st)
-        del dq, dk, dv
+        if fused:
+            qkv, lse = att
+            dqkv = attn_bwd(qkv, bqkv, key_bias, ctxr, lse, dctxr, G(bqkv), B, S, heads, pa, s_attn)
+            del dctxr
+        else:
+            q, k, v, probs, pdrop = att
+            dctx_h = torch.empty(B * heads, S, d, dtype=dy.dtype, device=dy.device)
+            _lib.call("kfa_heads_permute", _lib.ptr(dctxr), _lib.ptr(dctx_h), T, S, heads, d, 0, st)
+            del dctxr
+            pd = pdrop if pdrop is not None else probs
+            dv = torch.bmm(pd.transpose(1, 2), dctx_h)
+            dp = torch.bmm(dctx_h, v.transpose(1, 2))
+            del dctx_h
+            _lib.call("kfa_attn_softmax_bwd", _lib.ptr(probs), _lib.ptr(dp), B * heads * S, S, float(pa), s_attn, st)
+            dq = torch.bmm(dp, k)
+            dk = torch.bmm(dp.transpose(1, 2), q)
+            del dp
+            dqkv = torch.empty(T, 3 * H, dtype=dy.dtype, device=dy.device)
+            W3 = 3 * H
+            part = _part(_lib.lib().kfa_colsum_part_floats(T, W3), dy.device)
+            _lib.call("kfa_qkv_merge_bwd", _lib.ptr(dq), _lib.ptr(dk), _lib.ptr(dv), _lib.ptr(dqkv), _lib.ptr(part),
+                      _lib.ptr(G(bqkv)), T, S, heads, d, qscale, 1, st)
+            del dq, dk, dv
         _wgrad_(G(wqkv), dqkv, x)
-        dx = torch.addmm(dx_res, dqkv, wqkv)
+        if use_g:
+            dx = _gemm.gemm_nt(dqkv, _gemm.transpose(wqkv), addend=dx_res)[0]
+        else:
+            dx = torch.addmm(dx_res, dqkv, wqkv)
         grads = [_finish(p, tg[id(p)][0], tg[id(p)][2]) for p in ctx.params]
         return (dx, None, None, *grads)
 

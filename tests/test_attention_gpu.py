@@ -1,0 +1,83 @@
+"""Fused attention (csrc/kernels/attention.hip) vs a plain PyTorch fp32 reference.
+
+The dropout case rebuilds the kernels' counter-hash keep mask in numpy (uint64
+splitmix finaliser, same constants) so forward AND backward are checked
+element-wise against the reference with the identical mask."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+D = torch.device("cuda")
+
+
+def _close(a, b, tol, what=""):
+    a, b = a.float(), b.float()
+    err = (a - b).abs().max().item()
+    scale = max(1.0, b.abs().max().item())
+    assert err <= tol * scale, f"{what}: err {err} scale {scale}"
+
+
+def _keep_mask(seed, B, heads, S, p):
+    i = np.arange(B * heads * S * S, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + np.uint64(0x9E3779B97F4A7C15) * (i + np.uint64(1))
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        h = ((z ^ (z >> np.uint64(31))) >> np.uint64(32)).astype(np.uint32)
+    thresh = min(int(p * 4294967296.0), 4294967295)
+    return torch.from_numpy((h >= thresh).reshape(B, heads, S, S).astype(np.float32))
+
+
+def _reference(qkv, bqkv, kb, B, S, heads, d, mask, p):
+    x = qkv + bqkv
+    q, k, v = x.view(B, S, 3, heads, d).permute(2, 0, 3, 1, 4)
+    sc = q @ k.transpose(-1, -2) / math.sqrt(d)
+    if kb is not None:
+        sc = sc + kb.view(B, 1, 1, S)
+    pr = torch.softmax(sc, -1)
+    if mask is not None:
+        pr = pr * mask / (1.0 - p)
+    return (pr @ v).permute(0, 2, 1, 3).reshape(B * S, heads * d)
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_fused_attention_fwd_bwd(p):
+    from kubeflow_controller_amd.ops import transformer as T
+    torch.manual_seed(0)
+    B, S, heads, d = 3, 128, 4, 64
+    H = heads * d
+    qkv = torch.randn(B * S, 3 * H, device=D).to(torch.bfloat16)
+    bqkv = torch.randn(3 * H, device=D) * 0.1
+    m = torch.ones(B, S, device=D)
+    m[1, 90:] = 0
+    kb = ((1 - m) * -10000.0).contiguous()
+    seed = 987654321
+    out, lse = T.attn_fwd(qkv, bqkv, kb, B, S, heads, p, seed)
+    mask = _keep_mask(seed, B, heads, S, p).to(D) if p > 0 else None
+    xr = qkv.float().requires_grad_()
+    br = bqkv.clone().requires_grad_()
+    ref = _reference(xr, br, kb, B, S, heads, d, mask, p)
+    _close(out, ref, 2e-2, "ctx")
+    dout = torch.randn(B * S, H, device=D)
+    ref.backward(dout)
+    db = torch.zeros(3 * H, device=D)
+    dqkv = T.attn_bwd(qkv, bqkv, kb, out, lse, dout.to(torch.bfloat16), db, B, S, heads, p, seed)
+    _close(dqkv, xr.grad, 3e-2, "dqkv")
+    _close(db, br.grad, 3e-2, "dbqkv")
+
+
+def test_fused_attention_lse_matches():
+    from kubeflow_controller_amd.ops import transformer as T
+    torch.manual_seed(1)
+    B, S, heads, d = 2, 128, 2, 64
+    H = heads * d
+    qkv = torch.randn(B * S, 3 * H, device=D).to(torch.bfloat16)
+    bqkv = torch.zeros(3 * H, device=D)
+    _, lse = T.attn_fwd(qkv, bqkv, None, B, S, heads)
+    q, k, _ = qkv.float().view(B, S, 3, heads, d).permute(2, 0, 3, 1, 4)
+    ref = torch.logsumexp((q @ k.transpose(-1, -2)) / math.sqrt(d), -1)   # [B, heads, S]
+    _close(lse.view(B, heads, S), ref, 2e-2, "lse")

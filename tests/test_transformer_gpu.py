@@ -111,8 +111,12 @@ def _layer_params(H, I, dev):
     return out
 
 
-def test_encoder_layer_vs_reference():
+@pytest.mark.parametrize("route_gemm,fused_attn", [(False, True), (True, True), (False, False)])
+def test_encoder_layer_vs_reference(monkeypatch, route_gemm, fused_attn):
+    from kubeflow_controller_amd.ops import gemm as G
     from kubeflow_controller_amd.ops import transformer as T
+    monkeypatch.setattr(G, "ROUTE_LAYERS", route_gemm)
+    monkeypatch.setattr(T, "FUSED_ATTN", fused_attn)
     B, S, heads, H, I = 4, 128, 4, 256, 1024
     params = _layer_params(H, I, D)
     x = _bf(torch.randn(B * S, H)).requires_grad_()

@@ -1,12 +1,20 @@
-"""GEMM microbenchmark on MI355X: hipBLASLt (torch.mm) vs the hand-written MFMA
-kernels (conv_igemm as a 1x1 conv for Y = X·Wᵀ; wgrad for dW = dYᵀ·X) on the
-BERT-base / Wide&Deep / ResNet shapes.  Prints TFLOP/s per shape."""
-import sys
+"""GEMM / attention microbenchmark on MI355X.
+
+Dense: hipBLASLt (``torch.mm``) vs the hand-written MFMA GEMM
+(``ops/gemm.py``, both tile widths) for Y = X·Wᵀ, and hipBLASLt vs the
+hand-written wgrad kernel for dW = dYᵀ·X, on the BERT-base / Wide&Deep shapes.
+Attention (BERT-base, S = 128, d = 64): the fused kernel each way vs the split
+path (QKV split, batched library GEMMs, softmax kernel).  Prints ms and TFLOP/s.
+"""
+import math
 import os
+import sys
+
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from kubeflow_controller_amd.ops import _lib  # noqa: E402
+from kubeflow_controller_amd.ops import gemm as G  # noqa: E402
+from kubeflow_controller_amd.ops import transformer as T  # noqa: E402
 from kubeflow_controller_amd.ops.conv import wgrad_into  # noqa: E402
 
 
@@ -23,40 +31,59 @@ def timeit(fn, iters=20):
     return s.elapsed_time(e) / iters
 
 
-def main():
+def dense():
     d = torch.device("cuda")
-    shapes = [(8192, 2304, 768), (8192, 768, 768), (8192, 3072, 768), (8192, 768, 3072),
-              (16384, 3072, 768), (16384, 768, 3072), (8192, 1024, 1680), (802816, 256, 64), (200704, 512, 128)]
-    print(f"{'M':>7} {'N':>5} {'K':>5} | {'mm ms':>7} {'TF/s':>6} | {'igemm':>7} {'TF/s':>6} | "
-          f"{'wg mm':>7} {'TF/s':>6} | {'wg kfa':>7} {'TF/s':>6}")
+    shapes = [(32768, 2304, 768), (32768, 768, 768), (32768, 3072, 768), (32768, 768, 3072),
+              (8192, 2304, 768), (8192, 768, 3072), (65536, 1024, 1680), (65536, 512, 1024)]
+    print(f"{'M':>6} {'N':>5} {'K':>5} | {'mm ms':>7} {'TF/s':>5} | {'g128':>7} {'TF/s':>5} | {'g256':>7} {'TF/s':>5}"
+          f" | {'gelu+z':>7} | {'wg mm':>7} {'TF/s':>5} | {'wg kfa':>7} {'TF/s':>5}")
     for M, N, K in shapes:
         x = torch.randn(M, K, device=d).to(torch.bfloat16)
         w = torch.randn(N, K, device=d).to(torch.bfloat16)
+        b = torch.randn(N, device=d)
         dy = torch.randn(M, N, device=d).to(torch.bfloat16)
-        y = torch.empty(M, N, device=d, dtype=torch.bfloat16)
         fl = 2.0 * M * N * K
         t_mm = timeit(lambda: torch.mm(x, w.t()))
-        variant = 1 if N <= 64 else 0
-
-        def ig():
-            _lib.call("kfa_conv_igemm", _lib.ptr(x), _lib.ptr(w), _lib.ptr(y), None, 1, 1, M, K, 1, M, 1, 1, 1, 1,
-                      0, 0, N, 1, M, 1, 0, 0, N, variant, _lib.stream())
-        t_ig = timeit(ig) if K % 64 == 0 else float("nan")
+        t_128 = timeit(lambda: G.gemm_nt(x, w, bn=128))
+        t_256 = timeit(lambda: G.gemm_nt(x, w, bn=256))
+        t_ep = timeit(lambda: G.gemm_nt(x, w, bias=b, act="gelu", want_z=True))
         gw = torch.zeros(N, K, device=d, dtype=torch.bfloat16)
         t_wm = timeit(lambda: gw.addmm_(dy.t(), x))
         t_wk = timeit(lambda: wgrad_into(x, dy, gw, 1, 1, M, K, 1, M, N, 1, 1, 1, 0, True))
-        print(f"{M:7d} {N:5d} {K:5d} | {t_mm:7.3f} {fl / t_mm / 1e9:6.0f} | {t_ig:7.3f} {fl / t_ig / 1e9:6.0f} | "
-              f"{t_wm:7.3f} {fl / t_wm / 1e9:6.0f} | {t_wk:7.3f} {fl / t_wk / 1e9:6.0f}", flush=True)
-    # numerics spot check of the igemm-as-GEMM path
-    M, N, K = 4096, 768, 768
-    x = torch.randn(M, K, device=d).to(torch.bfloat16)
-    w = torch.randn(N, K, device=d).to(torch.bfloat16)
-    y = torch.empty(M, N, device=d, dtype=torch.bfloat16)
-    _lib.call("kfa_conv_igemm", _lib.ptr(x), _lib.ptr(w), _lib.ptr(y), None, 1, 1, M, K, 1, M, 1, 1, 1, 1,
-              0, 0, N, 1, M, 1, 0, 0, N, 0, _lib.stream())
-    ref = x.float() @ w.float().t()
-    print("igemm-as-GEMM max rel err", ((y.float() - ref).abs().max() / ref.abs().max()).item())
+        tf = lambda t: fl / t / 1e9  # noqa: E731
+        print(f"{M:6d} {N:5d} {K:5d} | {t_mm:7.3f} {tf(t_mm):5.0f} | {t_128:7.3f} {tf(t_128):5.0f} | "
+              f"{t_256:7.3f} {tf(t_256):5.0f} | {t_ep:7.3f} | {t_wm:7.3f} {tf(t_wm):5.0f} | {t_wk:7.3f} {tf(t_wk):5.0f}",
+              flush=True)
+
+
+def attention():
+    d = torch.device("cuda")
+    B, S, heads, hd = 256, 128, 12, 64
+    H = heads * hd
+    qkv = torch.randn(B * S, 3 * H, device=d).to(torch.bfloat16)
+    bqkv = torch.randn(3 * H, device=d) * 0.1
+    kb = torch.zeros(B, S, device=d)
+    dout = torch.randn(B * S, H, device=d).to(torch.bfloat16)
+    fl = 4.0 * B * heads * S * S * hd
+    for p in (0.0, 0.1):
+        t_f = timeit(lambda: T.attn_fwd(qkv, bqkv, kb, B, S, heads, p, 1))
+        out, lse = T.attn_fwd(qkv, bqkv, kb, B, S, heads, p, 1)
+        db = torch.zeros(3 * H, device=d)
+        t_b = timeit(lambda: T.attn_bwd(qkv, bqkv, kb, out, lse, dout, db, B, S, heads, p, 1))
+
+        def split_fwd():
+            x = (qkv.float() + bqkv).to(torch.bfloat16).view(B, S, 3, heads, hd).permute(2, 0, 3, 1, 4)
+            q, k, v = x[0], x[1], x[2]
+            sc = torch.matmul(q, k.transpose(-1, -2)) * (1.0 / math.sqrt(hd)) + kb.view(B, 1, 1, S).to(q.dtype)
+            pr = torch.softmax(sc.float(), -1).to(q.dtype)
+            if p > 0:
+                pr = torch.nn.functional.dropout(pr, p)
+            return torch.matmul(pr, v)
+        t_s = timeit(split_fwd)
+        print(f"attention B={B} S={S} heads={heads} p={p}: fused fwd {t_f:.3f} ms ({fl / t_f / 1e9:.0f} TF/s), "
+              f"fused bwd {t_b:.3f} ms ({2.5 * fl / t_b / 1e9:.0f} TF/s), torch split fwd {t_s:.3f} ms", flush=True)
 
 
 if __name__ == "__main__":
-    main()
+    dense()
+    attention()
