@@ -1,8 +1,11 @@
 """Per-layer timing: hand-written implicit GEMM vs PyTorch/MIOpen, ResNet-50 shapes (bs 256)."""
+import os
 import sys
+
 import torch
 import torch.nn.functional as F
-from kubeflow_controller_amd.ops.conv import conv_fwd, conv_dgrad, wgrad_into
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from kubeflow_controller_amd.ops.conv import conv_fwd, conv_dgrad, wgrad_into  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 torch.backends.cudnn.benchmark = True
@@ -37,6 +40,9 @@ for (Cin, H, Cout, k, s, p, cnt) in SH:
     y = F.conv2d(x, w, None, s, p)
     dy = torch.randn_like(y)
     flops = 2 * y.numel() * Cin * k * k
+    # floor = max(HBM bytes at 5 TB/s, FLOPs at 2 PF/s) for x + y (+ w) moved once
+    byts = 2 * (x.numel() + y.numel() + w.numel())
+    floor = max(byts / 5e9, flops / 2e12)
     of = t(lambda: conv_fwd(x, w, s, p))
     tf = t(lambda: F.conv2d(x, w, None, s, p))
     od = t(lambda: conv_dgrad(dy, w, x.shape, s, p))
@@ -49,7 +55,8 @@ for (Cin, H, Cout, k, s, p, cnt) in SH:
     ow = t(lambda: wgrad_into(x, dy, gw, B, H, H, Cin, P_, Q_, Cout, k, k, s, p, True))
     for k_, v in (("ours_f", of), ("torch_f", tf), ("ours_d", od), ("torch_d", td), ("ours_w", ow), ("torch_w", tw)):
         tot[k_] += v * cnt
-    print(f"Cin{Cin:5d} H{H:3d} Cout{Cout:5d} k{k} s{s} x{cnt}: fwd ours {of:.3f}ms ({flops/of/1e9:.0f} TF) "
+    tot["floor"] = tot.get("floor", 0) + 3 * floor * cnt
+    print(f"Cin{Cin:5d} H{H:3d} Cout{Cout:5d} k{k} s{s} x{cnt}: floor {floor:.3f} | fwd ours {of:.3f}ms ({flops/of/1e9:.0f} TF) "
           f"torch {tf:.3f}ms ({flops/tf/1e9:.0f} TF) | dgrad ours {od:.3f} torch {td:.3f} | wgrad ours {ow:.3f} "
           f"torch {tw:.3f}",
           flush=True)
