@@ -43,14 +43,18 @@ class BnBwdLink:
     conv's dgrad epilogue accumulates this BN's backward statistics (sum dz,
     sum dz*(x-mean)) into the BN slots and sets ``prestats``; the BN backward
     then skips its statistics pass.  Only valid when that conv is the sole
-    consumer of the BN output (the model decides: ResNet bn1/bn2)."""
+    consumer of the BN output's gradient: the model decides (ResNet bn1/bn2, and
+    bn3 whose other consumer, the residual, hands its gradient to that conv's
+    epilogue through a ``GradJoin``).  ``convs`` counts the convolutions that
+    took the output as input; with more than one, none of them uses the link."""
 
-    __slots__ = ("x", "y", "mean", "relu", "prestats")
+    __slots__ = ("x", "y", "mean", "relu", "prestats", "convs")
 
     def __init__(self):
         self.x = self.y = self.mean = None
         self.relu = False
         self.prestats = False
+        self.convs = 0
 
 
 def bn_slot_workspace(C: int, device) -> torch.Tensor:

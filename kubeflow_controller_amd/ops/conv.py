@@ -213,6 +213,8 @@ class _ConvFn(torch.autograd.Function):
         ctx.stride, ctx.pad, ctx.join = stride, pad, join
         ctx.wparam = w  # the Parameter itself (for the direct flat-gradient write)
         ctx.bn_link = getattr(x, "_kfa_bn_link", None)  # x = output of a BatchNorm (see conv_dgrad)
+        if ctx.bn_link is not None:
+            ctx.bn_link.convs += 1
         return conv_fwd(x, w, stride, pad, stats)
 
     @staticmethod
@@ -221,14 +223,18 @@ class _ConvFn(torch.autograd.Function):
         dx = dw = None
         if ctx.needs_input_grad[0]:
             addend = None
+            bn_link = ctx.bn_link if (ctx.bn_link is not None and ctx.bn_link.convs == 1) else None
             j = ctx.join
             if j is not None:
                 if j.state == "deposited":
                     addend, j.grad, j.state = j.grad, None, "empty"
                 else:
                     j.state = "consumer-first"
+                    # this epilogue sees only part of x's gradient: the BN whose output x
+                    # is must compute its backward statistics itself
+                    bn_link = None
             if w.shape[0] % 64 == 0 and w.shape[1] % 8 == 0:
-                dx = conv_dgrad(dy, w, x.shape, ctx.stride, ctx.pad, addend, ctx.bn_link)
+                dx = conv_dgrad(dy, w, x.shape, ctx.stride, ctx.pad, addend, bn_link)
             else:
                 dx = torch.nn.grad.conv2d_input(x.shape, w, dy, ctx.stride, ctx.pad)
                 if addend is not None:
