@@ -84,6 +84,26 @@ def attention():
               f"fused bwd {t_b:.3f} ms ({2.5 * fl / t_b / 1e9:.0f} TF/s), torch split fwd {t_s:.3f} ms", flush=True)
 
 
+def wgrad_layouts():
+    """hipBLASLt on the weight-gradient contraction over tokens, every operand layout."""
+    d = torch.device("cuda")
+    for M, N, K in [(32768, 2304, 768), (32768, 768, 768), (32768, 3072, 768), (32768, 768, 3072)]:
+        x = torch.randn(M, K, device=d).to(torch.bfloat16)
+        dy = torch.randn(M, N, device=d).to(torch.bfloat16)
+        xt, dyt = x.t().contiguous(), dy.t().contiguous()
+        fl = 2.0 * M * N * K
+        r = {
+            "dy.t()@x": timeit(lambda: torch.mm(dy.t(), x)),
+            "x.t()@dy": timeit(lambda: torch.mm(x.t(), dy)),
+            "dyT@xT.t()": timeit(lambda: torch.mm(dyt, xt.t())),
+            "dyT@x": timeit(lambda: torch.mm(dyt, x)),
+            "transpose dy": timeit(lambda: dy.t().contiguous()),
+        }
+        print(f"wgrad {M}x{N}x{K}: " + ", ".join(f"{k} {v:.3f} ms ({fl / v / 1e9:.0f} TF/s)" for k, v in r.items()),
+              flush=True)
+
+
 if __name__ == "__main__":
     dense()
     attention()
+    wgrad_layouts()
