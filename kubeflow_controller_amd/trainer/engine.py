@@ -31,7 +31,11 @@ class DistInfo:
 
 
 def init_distributed(backend: Optional[str] = None, prefer_gpu: bool = True) -> DistInfo:
-    """Initialise from torchrun-style env (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR/PORT)."""
+    """Initialise from torchrun-style env (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR/PORT).
+
+    ``KFA_DIST_BACKEND=gloo`` forces gloo even on GPUs: a rehearsal of the
+    multi-rank path with several ranks sharing one GPU (RCCL refuses two ranks
+    on one device in a communicator)."""
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -42,7 +46,7 @@ def init_distributed(backend: Optional[str] = None, prefer_gpu: bool = True) -> 
     else:
         dev = torch.device("cpu")
     if world > 1 and not dist.is_initialized():
-        be = backend or ("nccl" if use_gpu else "gloo")
+        be = backend or os.environ.get("KFA_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
         kw = {"device_id": dev} if (be == "nccl" and use_gpu) else {}
         dist.init_process_group(be, rank=rank, world_size=world, **kw)
     return DistInfo(rank, world, local, dev)
