@@ -101,7 +101,7 @@ class Engine:
         else:
             self.opt.step(grad_scale=self.sync.finish())
         self.steps += 1
-        return loss
+        return loss.detach()
 
     def num_params(self) -> int:
         return sum(p.numel() for g in self.groups for p in g.params)
