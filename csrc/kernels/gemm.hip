@@ -129,8 +129,14 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(GemmArgs g, const bf16_t* 
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int q8 = nwg >> 3, r8 = nwg & 7, x8 = bid & 7;
   const int wg = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + (bid >> 3);
-  const int ntn = (g.N + BN - 1) / BN;
-  const int m0 = (wg / ntn) * BM, n0 = (wg % ntn) * BN;
+  // Grouped raster: consecutive tiles walk GM row-panels column-major, so the
+  // ~32 tiles an XCD runs at once form a GM x (32/GM) block whose A and B
+  // panels fit its 4 MB L2 together (row-major order would stream all of B
+  // past every A panel).
+  const int ntn = (g.N + BN - 1) / BN, ntm = (g.M + BM - 1) / BM;
+  constexpr int GM = 4;
+  const int grp = wg / (GM * ntn), gm0 = grp * GM, gmn = min(GM, ntm - gm0), rem = wg - grp * GM * ntn;
+  const int m0 = (gm0 + rem % gmn) * BM, n0 = (rem / gmn) * BN;
 
   // LDS-DMA plan: instruction i of wave w fills rows (w*G + i)*16 + lane/4, physical
   // chunk lane&3, from logical chunk (lane&3) ^ swz(row), swz(row) = (row >> 2) & 2

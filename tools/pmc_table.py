@@ -9,19 +9,20 @@ import sys
 
 
 def main(paths):
-    vals = collections.defaultdict(lambda: collections.defaultdict(list))
+    # counter -> {dispatch: summed value}; a counter's mean is over the dispatches of ITS pass
+    vals = collections.defaultdict(lambda: collections.defaultdict(lambda: collections.defaultdict(float)))
     ns = collections.defaultdict(dict)
     for path in paths:
         for r in csv.DictReader(open(path)):
             k = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0][:60]
-            vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
-            ns[k][(path, r["Dispatch_Id"])] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            d = (path, r["Dispatch_Id"])
+            vals[k][r["Counter_Name"]][d] += float(r["Counter_Value"])
+            ns[k][d] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
     for k, cs in vals.items():
         t = sum(ns[k].values()) / max(len(ns[k]), 1)
         print(f"## {k}  (mean dispatch {t / 1e3:.1f} us over {len(ns[k])} dispatches)")
-        for c, v in sorted(cs.items()):
-            per = sum(v) / max(len(ns[k]), 1)
-            print(f"  {c:36s} {per:16.4g}")
+        for c, per_d in sorted(cs.items()):
+            print(f"  {c:36s} {sum(per_d.values()) / len(per_d):16.4g}")
 
 
 if __name__ == "__main__":
