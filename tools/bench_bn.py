@@ -47,8 +47,8 @@ def main():
             dy = torch.randn_like(out)
             t_b = timeit(lambda: torch.autograd.grad(out, [xr], dy, retain_graph=True))
             nbytes_b = 2 * M * C * (2 * 3 + 1 + (1 if has_res else 0))  # stats pass (dy, x, y) + apply pass + dx (+ dres)
-            print(f"M {M:7d} C {C:4d} res {int(has_res)}: fwd {t_f:.3f} ms ({nbytes_f / t_f / 1e9:.0f} GB/s incl. stats "
-                  f"pass)  bwd {t_b:.3f} ms ({nbytes_b / t_b / 1e9:.0f} GB/s incl. stats pass)", flush=True)
+            print(f"M {M:7d} C {C:4d} res {int(has_res)}: fwd {t_f:.3f} ms ({nbytes_f / t_f / 1e6:.0f} GB/s incl. stats "
+                  f"pass)  bwd {t_b:.3f} ms ({nbytes_b / t_b / 1e6:.0f} GB/s incl. stats pass)", flush=True)
             del y, out
 
 
