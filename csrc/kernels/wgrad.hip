@@ -77,17 +77,22 @@ __device__ __forceinline__ short8 tr_operand(const bf16_t* tile, int kb, int cb,
 // channels x BN = 16*WN*TN (r,s,ci) columns.  OUT_PART: fp32 split-K partials;
 // otherwise the epilogue accumulates straight into the (bf16/fp32) gradient.
 template <int WM, int WN, int TM, int TN>
-__global__ __launch_bounds__(256, 2) void wgrad_kernel(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X,
-                                                       float* __restrict__ part, void* __restrict__ grad,
-                                                       int grad_f32, int accumulate, const bf16_t* __restrict__ Z,
-                                                       WGeo g) {
+__global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_kernel(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X,
+                                                                float* __restrict__ part, void* __restrict__ grad,
+                                                                int grad_f32, int accumulate, const bf16_t* __restrict__ Z,
+                                                                WGeo g) {
+  constexpr int NW = WM * WN;
   constexpr int BM = 16 * WM * TM, BN = 16 * WN * TN;
-  constexpr int A_RPI = 1024 / (BM * 2), B_RPI = 1024 / (BN * 2);  // tile rows per 1-KiB wave instruction
-  constexpr int A_IPW = BKW / A_RPI / 4, B_IPW = BKW / B_RPI / 4;    // instructions per wave per k-step
-  constexpr int A_CPR = BM / 8, B_CPR = BN / 8;                      // 16-B chunks per row
+  // a 256-wide tile is held as two 128-wide sub-images (the swizzles are for 64 / 128)
+  constexpr int WA = BM > 128 ? 128 : BM, WB = BN > 128 ? 128 : BN;  // sub-image widths
+  constexpr int A_RPI = 1024 / (WA * 2), B_RPI = 1024 / (WB * 2);    // sub-image rows per 1-KiB wave instruction
+  constexpr int A_IPS = BKW / A_RPI, B_IPS = BKW / B_RPI;            // instructions per sub-image per k-step
+  constexpr int A_IPW = (BM / WA) * A_IPS / NW, B_IPW = (BN / WB) * B_IPS / NW;  // instructions per wave per k-step
+  constexpr int A_CPR = WA / 8, B_CPR = WB / 8;                      // 16-B chunks per sub-image row
+  static_assert(A_IPW * NW == (BM / WA) * A_IPS && B_IPW * NW == (BN / WB) * B_IPS, "wgrad staging split");
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
-  bf16_t* As = smem;                    // [2][BKW][BM]
-  bf16_t* Bs = smem + 2 * BKW * BM;     // [2][BKW][BN]
+  bf16_t* As = smem;                    // [2][BM / WA][BKW][WA]
+  bf16_t* Bs = smem + 2 * BKW * BM;     // [2][BN / WB][BKW][WB]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM;
   const int ntn = (g.N + BN - 1) / BN;
@@ -98,28 +103,31 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const bf16_t* __restrict_
   if (kb >= ke) return;
   const int nsteps = (ke - kb + BKW - 1) / BKW;
 
-  // staging plan: this lane fills row (j*RPI + lane / CPR), physical chunk lane % CPR
-  int a_m[A_IPW], a_row[A_IPW];
+  // staging plan: instruction j fills sub-image j / IPS, rows (j % IPS)*RPI + lane / CPR,
+  // physical chunk lane % CPR (logical chunk ^ swizzle applied on the source address)
+  int a_m[A_IPW], a_row[A_IPW], a_lds[A_IPW];
   bool a_ok[A_IPW];
 #pragma unroll
   for (int i = 0; i < A_IPW; i++) {
-    const int j = wave * A_IPW + i;
-    const int row = j * A_RPI + lane / A_CPR;
-    const int ch = (lane % A_CPR) ^ img_swz<BM>(row);
+    const int j = wave * A_IPW + i, si = j / A_IPS, jj = j % A_IPS;
+    const int row = jj * A_RPI + lane / A_CPR;
+    const int ch = (lane % A_CPR) ^ img_swz<WA>(row);
     a_row[i] = row;
-    a_m[i] = m0 + ch * 8;
+    a_m[i] = m0 + si * WA + ch * 8;
     a_ok[i] = a_m[i] < g.Co;
+    a_lds[i] = si * BKW * WA + jj * A_RPI * WA;
   }
-  int b_ci[B_IPW], b_r[B_IPW], b_s[B_IPW], b_row[B_IPW];
+  int b_ci[B_IPW], b_r[B_IPW], b_s[B_IPW], b_row[B_IPW], b_lds[B_IPW];
   bool b_ok[B_IPW];
 #pragma unroll
   for (int i = 0; i < B_IPW; i++) {
-    const int j = wave * B_IPW + i;
-    const int row = j * B_RPI + lane / B_CPR;
-    const int ch = (lane % B_CPR) ^ img_swz<BN>(row);
-    const int n = n0 + ch * 8;
+    const int j = wave * B_IPW + i, si = j / B_IPS, jj = j % B_IPS;
+    const int row = jj * B_RPI + lane / B_CPR;
+    const int ch = (lane % B_CPR) ^ img_swz<WB>(row);
+    const int n = n0 + si * WB + ch * 8;
     b_row[i] = row;
     b_ok[i] = n < g.N;
+    b_lds[i] = si * BKW * WB + jj * B_RPI * WB;
     const int tap = b_ok[i] ? n / g.Ci : 0;
     b_ci[i] = n - tap * g.Ci;
     b_r[i] = tap / g.S;
@@ -133,15 +141,13 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const bf16_t* __restrict_
     const int k0 = kb + step * BKW;
 #pragma unroll
     for (int i = 0; i < A_IPW; i++) {
-      const int j = wave * A_IPW + i;
       const int k = k0 + a_row[i];
       const bf16_t* sa = (k < ke && a_ok[i]) ? dY + (long)k * g.Co + a_m[i] : Z;
-      __builtin_amdgcn_global_load_lds(sa, (__attribute__((address_space(3))) void*)(As + buf * BKW * BM + j * A_RPI * BM),
+      __builtin_amdgcn_global_load_lds(sa, (__attribute__((address_space(3))) void*)(As + buf * BKW * BM + a_lds[i]),
                                        16, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < B_IPW; i++) {
-      const int j = wave * B_IPW + i;
       const int k = k0 + b_row[i];
       const bf16_t* sb = Z;
       if (k < ke && b_ok[i]) {
@@ -155,7 +161,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const bf16_t* __restrict_
             sb = X + (((long)img * g.H + h) * g.W + w) * g.Ci + b_ci[i];
         }
       }
-      __builtin_amdgcn_global_load_lds(sb, (__attribute__((address_space(3))) void*)(Bs + buf * BKW * BN + j * B_RPI * BN),
+      __builtin_amdgcn_global_load_lds(sb, (__attribute__((address_space(3))) void*)(Bs + buf * BKW * BN + b_lds[i]),
                                        16, 0, 0);
     }
   };
@@ -184,9 +190,15 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const bf16_t* __restrict_
     for (int ks = 0; ks < 2; ks++) {
       short8 af[TM], bf[TN];
 #pragma unroll
-      for (int i = 0; i < TM; i++) af[i] = tr_operand<BM>(At, ks * 32, wm * TM * 16 + i * 16, lane);
+      for (int i = 0; i < TM; i++) {
+        const int c = wm * TM * 16 + i * 16;  // within one sub-image (TM * 16 <= 128, aligned)
+        af[i] = tr_operand<WA>(At + (c / WA) * BKW * WA, ks * 32, c % WA, lane);
+      }
 #pragma unroll
-      for (int i = 0; i < TN; i++) bf[i] = tr_operand<BN>(Bt, ks * 32, wn * TN * 16 + i * 16, lane);
+      for (int i = 0; i < TN; i++) {
+        const int c = wn * TN * 16 + i * 16;
+        bf[i] = tr_operand<WB>(Bt + (c / WB) * BKW * WB, ks * 32, c % WB, lane);
+      }
 #pragma unroll
       for (int ni = 0; ni < TN; ni++)
 #pragma unroll
@@ -282,20 +294,25 @@ int num_cus() {
 }
 
 struct WPlan {
-  int variant;   // 0: 128x128, 1: 64x128 (Co <= 64), 2: 128x64 (N <= 64), 3: 64x64 (both)
-  int BM, BN, tiles, splits, kchunk;
+  int variant;   // 0: 128x128, 1: 64x128 (Co <= 64), 2: 128x64 (N <= 64), 3: 64x64 (both), 4: 256x256 (8 waves)
+  int BM, BN, tiles, splits, kchunk, threads, blocks_per_cu;
 };
 
 WPlan plan(long K, int Co, int N) {
   WPlan p;
-  p.variant = Co <= 64 ? (N <= 64 ? 3 : 1) : (N <= 64 ? 2 : 0);
-  p.BM = (p.variant == 1 || p.variant == 3) ? 64 : 128;
-  p.BN = (p.variant == 2 || p.variant == 3) ? 64 : 128;
+  // 256x256 (8 waves of 128x64, one block per CU): half the operand bytes per
+  // MFMA of the 128x128 tile — for the long reductions of big weights
+  if (Co % 256 == 0 && N % 256 == 0 && K >= 8192) p.variant = 4;
+  else p.variant = Co <= 64 ? (N <= 64 ? 3 : 1) : (N <= 64 ? 2 : 0);
+  p.BM = p.variant == 4 ? 256 : ((p.variant == 1 || p.variant == 3) ? 64 : 128);
+  p.BN = p.variant == 4 ? 256 : ((p.variant == 2 || p.variant == 3) ? 64 : 128);
+  p.threads = p.variant == 4 ? 512 : 256;
+  p.blocks_per_cu = p.variant == 4 ? 1 : 2;
   p.tiles = ((Co + p.BM - 1) / p.BM) * ((N + p.BN - 1) / p.BN);
-  // one wave of blocks (2 per CU), each >= 4 k-steps; big-weight layers run
+  // one wave of blocks, each >= 4 k-steps; big-weight layers run
   // without split-K and accumulate in the epilogue (no partial round trip)
   const long steps = (K + BKW - 1) / BKW;
-  long splits = (2L * num_cus()) / p.tiles;
+  long splits = ((long)p.blocks_per_cu * num_cus()) / p.tiles;
   splits = splits < 1 ? 1 : splits;
   const long max_splits = steps / 4 > 0 ? steps / 4 : 1;
   if (splits > max_splits) splits = max_splits;
@@ -335,9 +352,19 @@ KFA_API int kfa_conv_wgrad(const bf16_t* dY, const bf16_t* X, void* grad, int gr
   else if (p.variant == 2)
     hipLaunchKernelGGL((wgrad_kernel<4, 1, 2, 4>), grid, dim3(256), lds, s, dY, X, pp, grad, grad_f32, accumulate,
                        zero_page(), g);
-  else
+  else if (p.variant == 3)
     hipLaunchKernelGGL((wgrad_kernel<2, 2, 2, 2>), grid, dim3(256), lds, s, dY, X, pp, grad, grad_f32, accumulate,
                        zero_page(), g);
+  else {
+    static bool attr = false;  // 128 KiB of dynamic LDS
+    if (!attr) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_kernel<2, 4, 8, 4>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      attr = true;
+    }
+    hipLaunchKernelGGL((wgrad_kernel<2, 4, 8, 4>), grid, dim3(512), lds, s, dY, X, pp, grad, grad_f32, accumulate,
+                       zero_page(), g);
+  }
   if (p.splits > 1) {
     const long total = (long)Co * g.N;
     const long blocks = (total / 4 + 63) / 64;
