@@ -86,13 +86,18 @@ __device__ __forceinline__ void lds_barrier() {
 __device__ __forceinline__ int swz(int row, int chunk) { return row * BK + ((chunk ^ ((row >> 1) & 7)) << 3); }
 
 // WM x WN waves, each owning TM x TN MFMA 16x16 tiles (wave tile 16TM x 16TN)
+// (8 waves: 256 x 256 tiles of 128 x 64 per wave, one block per CU — half the
+// operand bytes per MFMA of the 4-wave 128 x 128 tile; the epilogue then stages
+// the wave tile in NHALF passes so it fits the one ring buffer it may use.)
 template <int WM, int WN, int TM, int TN>
-__global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const bf16_t* __restrict__ T, const bf16_t* __restrict__ B,
-                                                            bf16_t* __restrict__ D, const bf16_t* __restrict__ E,
-                                                            const bf16_t* __restrict__ Z, float* __restrict__ stats,
-                                                            BnBwd bnb, Geo g) {
+__global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_t* __restrict__ T,
+                                                                     const bf16_t* __restrict__ B,
+                                                                     bf16_t* __restrict__ D, const bf16_t* __restrict__ E,
+                                                                     const bf16_t* __restrict__ Z,
+                                                                     float* __restrict__ stats, BnBwd bnb, Geo g) {
+  constexpr int NW = WM * WN, RPP = 8 * NW;  // waves; tile rows per staging pass (8 per wave)
   constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
-  constexpr int AR = BM / 32, BR = BN / 32;  // 16-B chunks per thread per k-tile
+  constexpr int AR = BM / RPP, BR = BN / RPP;  // 16-B chunks per thread per k-tile
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
   bf16_t* As = smem;                  // [2][BM][BK]
   bf16_t* Bs = smem + 2 * BM * BK;    // [2][BN][BK]
@@ -115,7 +120,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const bf16_t* __rest
   auto tile_of = [&](int i) { return t_lo + slot + i * nslot; };
 
   const int kc = tid & 7;
-  const int rbase = tid >> 3;  // 0..31
+  const int rbase = tid >> 3;  // 0..RPP-1
   const int PQ = g.P * g.Q;
   const float rPQ = 1.f / (float)PQ, rQ = 1.f / (float)g.Q;
   // pointwise fast paths: A row m is T[m] (1x1 / stride 1 / no pad) and/or D row m is D[m]
@@ -131,7 +136,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const bf16_t* __rest
     const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
 #pragma unroll
     for (int i = 0; i < AR; i++) {
-      const int m = m0 + rbase + 32 * i;
+      const int m = m0 + rbase + RPP * i;
       if (m < g.M && lin_a) {
         a_hb[i] = 0;
         a_wb[i] = 0;
@@ -150,7 +155,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const bf16_t* __rest
     }
 #pragma unroll
     for (int i = 0; i < BR; i++) {
-      const int n = n0 + rbase + 32 * i;
+      const int n = n0 + rbase + RPP * i;
       b_off[i] = n < g.N ? (unsigned)(n * g.K + kc * 8) * 2u : kOOB;
     }
   };
@@ -172,20 +177,20 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const bf16_t* __rest
     const int dh = r * g.ra, dw = s * g.ra;
 #pragma unroll
     for (int i = 0; i < AR; i++) {
-      const int row = i * 32 + wave * 8 + l8;
+      const int row = i * RPP + wave * 8 + l8;
       const int c = pos ^ ((row >> 1) & 7);
       const int ih = a_hb[i] + dh, iw = a_wb[i] + dw;
       const bool ok = (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
       const bf16_t* src = ok ? T + (unsigned)(a_base[i] + (ih * g.W + iw) * g.C + c0 + c * 8) : Z;
-      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(As + buf * BM * BK + (i * 32 + wave * 8) * BK),
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(As + buf * BM * BK + (i * RPP + wave * 8) * BK),
                                        16, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < BR; i++) {
-      const int row = i * 32 + wave * 8 + l8;
+      const int row = i * RPP + wave * 8 + l8;
       const int c = pos ^ ((row >> 1) & 7);
       const bf16_t* src = b_off[i] == kOOB ? Z : B + b_off[i] / 2 + k0 + (c - pos) * 8;
-      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(Bs + buf * BN * BK + (i * 32 + wave * 8) * BK),
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(Bs + buf * BN * BK + (i * RPP + wave * 8) * BK),
                                        16, 0, 0);
     }
   };
@@ -221,95 +226,105 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const bf16_t* __rest
   // wave's tile in LDS (XOR-swizzled 16-B chunks, conflict-free both ways)
   // lets every lane store 16 B and a wave cover 128-B row segments, so the
   // HBM writes of the memory-bound layers (K = 64..256) coalesce.
-  constexpr int WT = 256 * TM * TN;   // wave tile elements (16TM rows x 16TN channels)
+  // staging passes over the wave's rows: 1 for the 4-wave tiles; 4 for the 8-wave
+  // 128-row wave tiles (keeps the epilogue's in-flight loads at 48 VGPRs)
+  constexpr int NHALF = NW == 4 ? 1 : TM / 2;
+  constexpr int TMH = TM / NHALF;     // MFMA row tiles per pass
+  constexpr int WT = 256 * TMH * TN;  // staged elements per wave per pass (16TMH rows x 16TN channels)
   constexpr int RB = 32 * TN;         // staged row bytes
   constexpr int CPR = 2 * TN;         // 16-B chunks per staged row
+  static_assert(NW * WT <= (BM + BN) * BK, "conv epilogue stage must fit one ring buffer");
   auto epilogue = [&](int tile, int buf) {
-    constexpr int IT = (16 * TM * CPR) / 64;  // 16-B row pieces per lane
+    constexpr int IT = (16 * TMH * CPR) / 64;  // 16-B row pieces per lane per pass
     const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
     const int c = lane % CPR;
     const int n = n0 + wn * TN * 16 + c * 8;
-    // output offsets first, so the epilogue's global loads (residual-grad addend,
-    // BN input / output for the fused backward statistics) are all in flight
-    // while the tile is staged through LDS
-    unsigned offs[IT];
-#pragma unroll
-    for (int it = 0; it < IT; it++) {
-      const int m = m0 + wm * TM * 16 + it * (64 / CPR) + lane / CPR;
-      unsigned orow;  // byte offset of output row m
-      if (lin_d) {
-        orow = (unsigned)m * (unsigned)g.ldd * 2u;
-      } else {
-        const int nb = fdiv(m, PQ, rPQ), rem = m - nb * PQ;
-        const int p = fdiv(rem, g.Q, rQ), q = rem - p * g.Q;
-        orow = (unsigned)((nb * g.OH + p * g.os + g.oph) * g.OW + (q * g.os + g.opw)) * (unsigned)g.ldd * 2u;
-      }
-      offs[it] = (m >= g.M || n >= g.N) ? kOOB : orow + (unsigned)n * 2u;
-    }
-    const bool bstat = stats && bnb.x;
-    uint4 ev[IT], bx[IT], by[IT];
-    if (E)
-#pragma unroll
-      for (int it = 0; it < IT; it++) ev[it] = bload16(rE, offs[it]);
-    if (bstat)
-#pragma unroll
-      for (int it = 0; it < IT; it++) {
-        bx[it] = bload16(rBX, offs[it]);
-        if (bnb.relu) by[it] = bload16(rBY, offs[it]);
-      }
     float mu[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const bool bstat = stats && bnb.x;
     if (bstat)
 #pragma unroll
       for (int j = 0; j < 8; j++) mu[j] = n + j < g.N ? bnb.mean[n + j] : 0.f;
-
-    lds_barrier();  // every wave is done reading `buf`: reuse it as the staging area
+    float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // fused BN statistics
     char* stage;
     {
       const int e = wave * WT;
       stage = reinterpret_cast<char*>(e < BM * BK ? As + buf * BM * BK + e : Bs + buf * BN * BK + (e - BM * BK));
     }
 #pragma unroll
-    for (int mi = 0; mi < TM; mi++)
+    for (int hh = 0; hh < NHALF; hh++) {
+      // output offsets first, so the epilogue's global loads (residual-grad addend,
+      // BN input / output for the fused backward statistics) are all in flight
+      // while the tile is staged through LDS
+      unsigned offs[IT];
 #pragma unroll
-      for (int ni = 0; ni < TN; ni++) {
-        const int row = mi * 16 + fr, col = ni * 16 + fq * 4;
-        const uint2 o = make_uint2(pack2(acc[ni][mi][0], acc[ni][mi][1]), pack2(acc[ni][mi][2], acc[ni][mi][3]));
-        *reinterpret_cast<uint2*>(stage + row * RB + (((col >> 3) ^ (row & (CPR - 1))) << 4) + (col & 7) * 2) = o;
-      }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // fused BN statistics
-#pragma unroll
-    for (int it = 0; it < IT; it++) {
-      const int r = it * (64 / CPR) + lane / CPR;
-      const uint4 v = *reinterpret_cast<const uint4*>(stage + r * RB + ((c ^ (r & (CPR - 1))) << 4));
-      const unsigned off = offs[it];
-      uint4 o = v;
-      if (E) {  // wave-uniform branch
-        float f[8], h[8];
-        unpack8(v, f);
-        unpack8(ev[it], h);
-#pragma unroll
-        for (int j = 0; j < 8; j++) f[j] += h[j];
-        o = pack8(f);
-      }
-      __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<decltype(__builtin_amdgcn_raw_buffer_load_b128(rD, 0, 0, 0))*>(&o), rD, off, 0, 0);
-      if (stats && off != kOOB) {  // wave-uniform pointer test; per-lane row mask
-        float f[8];
-        unpack8(o, f);  // the bf16-rounded values the BatchNorm will see
-        if (bstat) {    // backward statistics of the BN this dgrad feeds
-          float xf[8];
-          unpack8(bx[it], xf);
-          if (bnb.relu) {
-            float yf[8];
-            unpack8(by[it], yf);
-#pragma unroll
-            for (int j = 0; j < 8; j++) f[j] = yf[j] > 0.f ? f[j] : 0.f;
-          }
-#pragma unroll
-          for (int j = 0; j < 8; j++) { s1[j] += f[j]; s2[j] += f[j] * (xf[j] - mu[j]); }
+      for (int it = 0; it < IT; it++) {
+        const int m = m0 + wm * TM * 16 + hh * TMH * 16 + it * (64 / CPR) + lane / CPR;
+        unsigned orow;  // byte offset of output row m
+        if (lin_d) {
+          orow = (unsigned)m * (unsigned)g.ldd * 2u;
         } else {
+          const int nb = fdiv(m, PQ, rPQ), rem = m - nb * PQ;
+          const int p = fdiv(rem, g.Q, rQ), q = rem - p * g.Q;
+          orow = (unsigned)((nb * g.OH + p * g.os + g.oph) * g.OW + (q * g.os + g.opw)) * (unsigned)g.ldd * 2u;
+        }
+        offs[it] = (m >= g.M || n >= g.N) ? kOOB : orow + (unsigned)n * 2u;
+      }
+      uint4 ev[IT], bx[IT], by[IT];
+      if (E)
 #pragma unroll
-          for (int j = 0; j < 8; j++) { s1[j] += f[j]; s2[j] += f[j] * f[j]; }
+        for (int it = 0; it < IT; it++) ev[it] = bload16(rE, offs[it]);
+      if (bstat)
+#pragma unroll
+        for (int it = 0; it < IT; it++) {
+          bx[it] = bload16(rBX, offs[it]);
+          if (bnb.relu) by[it] = bload16(rBY, offs[it]);
+        }
+
+      if (hh == 0) lds_barrier();  // every wave is done reading `buf`: reuse it as the staging area
+      else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave read back its previous pass
+#pragma unroll
+      for (int mj = 0; mj < TMH; mj++)
+#pragma unroll
+        for (int ni = 0; ni < TN; ni++) {
+          const int mi = hh * TMH + mj;
+          const int row = mj * 16 + fr, col = ni * 16 + fq * 4;
+          const uint2 o = make_uint2(pack2(acc[ni][mi][0], acc[ni][mi][1]), pack2(acc[ni][mi][2], acc[ni][mi][3]));
+          *reinterpret_cast<uint2*>(stage + row * RB + (((col >> 3) ^ (row & (CPR - 1))) << 4) + (col & 7) * 2) = o;
+        }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int it = 0; it < IT; it++) {
+        const int r = it * (64 / CPR) + lane / CPR;
+        const uint4 v = *reinterpret_cast<const uint4*>(stage + r * RB + ((c ^ (r & (CPR - 1))) << 4));
+        const unsigned off = offs[it];
+        uint4 o = v;
+        if (E) {  // wave-uniform branch
+          float f[8], h[8];
+          unpack8(v, f);
+          unpack8(ev[it], h);
+#pragma unroll
+          for (int j = 0; j < 8; j++) f[j] += h[j];
+          o = pack8(f);
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<decltype(__builtin_amdgcn_raw_buffer_load_b128(rD, 0, 0, 0))*>(&o), rD, off, 0, 0);
+        if (stats && off != kOOB) {  // wave-uniform pointer test; per-lane row mask
+          float f[8];
+          unpack8(o, f);  // the bf16-rounded values the BatchNorm will see
+          if (bstat) {    // backward statistics of the BN this dgrad feeds
+            float xf[8];
+            unpack8(bx[it], xf);
+            if (bnb.relu) {
+              float yf[8];
+              unpack8(by[it], yf);
+#pragma unroll
+              for (int j = 0; j < 8; j++) f[j] = yf[j] > 0.f ? f[j] : 0.f;
+            }
+#pragma unroll
+            for (int j = 0; j < 8; j++) { s1[j] += f[j]; s2[j] += f[j] * (xf[j] - mu[j]); }
+          } else {
+#pragma unroll
+            for (int j = 0; j < 8; j++) { s1[j] += f[j]; s2[j] += f[j] * f[j]; }
+          }
         }
       }
     }
@@ -406,7 +421,7 @@ static const bf16_t* zero_page() {
   return z;
 }
 
-// variant: 0 = 128x128 tile, 1 = 128x64 tile (N <= 64)
+// variant: 0 = 128x128 tile, 1 = 128x64 tile (N <= 64), 2 = 256x256 tile (8 waves)
 KFA_API int kfa_conv_igemm(const bf16_t* T, const bf16_t* B, bf16_t* D, const bf16_t* E, int Nb, int H, int W, int C,
                            int P, int Q, int R, int S, int sa, int ra, int oa, int ob, int N, int OH, int OW, int os,
                            int oph, int opw, int ldd, int variant, float* stats, const bf16_t* bn_x,
@@ -439,6 +454,18 @@ KFA_API int kfa_conv_igemm(const bf16_t* T, const bf16_t* B, bf16_t* D, const bf
     const int grid = (int)(tiles < 3L * cus ? tiles : 3L * cus);  // 160 VGPR, 48 KB LDS: 3 blocks / CU
     hipLaunchKernelGGL((conv_igemm_kernel<4, 1, 2, 4>), dim3(grid), dim3(256), 2 * (128 + 64) * BK * 2, st, T, B, D,
                        E, zero_page(), stats, bnb, g);
+  } else if (variant == 2) {  // 256 x 256 tile: 2x4 waves of 128x64, one block per CU (128 KiB LDS)
+    const long tiles = (long)kfa_ceil_div(g.M, 256) * kfa_ceil_div(N, 256);
+    const int grid = (int)(tiles < cus ? tiles : cus);
+    const int lds = 2 * (256 + 256) * BK * 2;
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_igemm_kernel<2, 4, 8, 4>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      attr = true;
+    }
+    hipLaunchKernelGGL((conv_igemm_kernel<2, 4, 8, 4>), dim3(grid), dim3(512), lds, st, T, B, D, E, zero_page(), stats,
+                       bnb, g);
   } else {  // 128 x 128 tile: 2x2 waves of 64x64
     const int grid = pgrid((long)kfa_ceil_div(g.M, 128) * kfa_ceil_div(N, 128));
     hipLaunchKernelGGL((conv_igemm_kernel<2, 2, 4, 4>), dim3(grid), dim3(256), 2 * (128 + 128) * BK * 2, st, T, B, D,

@@ -47,8 +47,21 @@ def igemm_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
             and x.dim() == 4 and x.shape[1] % 64 == 0 and w.shape[0] % 8 == 0 and w.shape[2] == w.shape[3])
 
 
-def _variant(M: int, N: int) -> int:
-    return 1 if N <= 64 else 0
+# 256x256 8-wave tiles for wide layers: opt-in (KFA_CONV_BIG=1).  On the ResNet-50 shapes they
+# lose to the 4-wave 128x128 tiles (tools/bench_conv.py: fwd 4.76 -> 6.20 ms, dgrad 5.40 ->
+# 7.09 ms per step): the late stages have too few 256x256 tiles to fill 256 CUs and convs
+# have no split-K.  KFA_CONV_BIG_MINK: minimum reduction length K = R*S*C.
+BIG = os.environ.get("KFA_CONV_BIG", "0") == "1"
+BIG_MIN_K = int(os.environ.get("KFA_CONV_BIG_MINK", "256"))
+
+
+def _variant(M: int, N: int, K: int = 0) -> int:
+    """Tile shape of one implicit-GEMM launch: M output pixels x N channels, reduction K."""
+    if N <= 64:
+        return 1
+    if BIG and N % 256 == 0 and K >= BIG_MIN_K:
+        return 2
+    return 0
 
 
 def _cl(t: torch.Tensor) -> torch.Tensor:
@@ -66,8 +79,8 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, stats=None
     Qo = (W + 2 * pad - S) // stride + 1
     y = torch.empty((Nb, Co, Po, Qo), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
     _lib.call("kfa_conv_igemm", _lib.ptr(x), _lib.ptr(w), _lib.ptr(y), None, Nb, H, W, C, Po, Qo, R, S, stride, 1,
-              -pad, -pad, Co, Po, Qo, 1, 0, 0, Co, _variant(Nb * Po * Qo, Co), _lib.ptr(stats), None, None, None, 0,
-              _lib.stream())
+              -pad, -pad, Co, Po, Qo, 1, 0, 0, Co, _variant(Nb * Po * Qo, Co, R * S * C), _lib.ptr(stats), None, None,
+              None, 0, _lib.stream())
     return y
 
 
@@ -100,7 +113,7 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride: int, pad: int
     if stride == 1:
         wt = _transposed_weight(w, 0, 1, R, 0, 1, S)
         _lib.call("kfa_conv_igemm", _lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), _lib.ptr(E), Nb, Po, Qo, Co, H, W, R, S,
-                  1, -1, pad, pad, Ci, H, W, 1, 0, 0, Ci, _variant(Nb * H * W, Ci), *bn_args, st)
+                  1, -1, pad, pad, Ci, H, W, 1, 0, 0, Ci, _variant(Nb * H * W, Ci, R * S * Co), *bn_args, st)
         return dx
     # stride s: output parity classes.  For class (ph, pw) the rows h = s*i + ph
     # receive taps r with (ph + pad - r) % s == 0, from dY row i + (ph + pad - r)/s.
@@ -120,8 +133,8 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride: int, pad: int
             oa_h = (ph + pad - r0) // stride
             oa_w = (pw + pad - s0) // stride
             _lib.call("kfa_conv_igemm", _lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), _lib.ptr(E), Nb, Po, Qo, Co, Hc, Wc,
-                      Rs, Ss, 1, -1, oa_h, oa_w, Ci, H, W, stride, ph, pw, Ci, _variant(Nb * Hc * Wc, Ci), *bn_args,
-                      st)
+                      Rs, Ss, 1, -1, oa_h, oa_w, Ci, H, W, stride, ph, pw, Ci, _variant(Nb * Hc * Wc, Ci, Rs * Ss * Co),
+                      *bn_args, st)
     return dx
 
 

@@ -14,12 +14,20 @@ SHAPES = [
     (3, 64, 9, 9, 192, 3, 2, 1),
     (1, 512, 7, 7, 2048, 1, 1, 0),
     (5, 64, 8, 8, 64, 3, 1, 1),
+    # 256x256 8-wave tiles (Cout / Cin multiples of 256, K >= 256), incl. M tails
+    (3, 256, 9, 11, 256, 3, 1, 1),
+    (2, 256, 16, 16, 512, 3, 2, 1),
 ]
 
 
+@pytest.mark.parametrize("big", [False, True])
 @pytest.mark.parametrize("N,Cin,H,W,Cout,k,stride,pad", SHAPES)
-def test_conv_igemm_fwd_dgrad(N, Cin, H, W, Cout, k, stride, pad):
+def test_conv_igemm_fwd_dgrad(N, Cin, H, W, Cout, k, stride, pad, big, monkeypatch):
+    from kubeflow_controller_amd.ops import conv as convmod
     from kubeflow_controller_amd.ops.conv import conv2d
+    if big and not (Cout % 256 == 0 or Cin % 256 == 0):
+        pytest.skip("256x256 tiles only for 256-multiple channel counts")
+    monkeypatch.setattr(convmod, "BIG", big)
     torch.manual_seed(0)
     d = torch.device("cuda")
     x = torch.randn(N, Cin, H, W, device=d).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
@@ -138,13 +146,15 @@ def test_wgrad_direct_into_flat_buffer():
     assert err < 3e-2 * wf.grad.abs().max().item(), err
 
 
-@pytest.mark.parametrize("Cin,Cout,k,stride", [(64, 256, 1, 1), (128, 128, 3, 2), (64, 64, 3, 1)])
-def test_bn_stats_fused_into_conv_epilogue(Cin, Cout, k, stride):
+@pytest.mark.parametrize("Cin,Cout,k,stride", [(64, 256, 1, 1), (128, 128, 3, 2), (64, 64, 3, 1), (256, 256, 3, 1)])
+def test_bn_stats_fused_into_conv_epilogue(Cin, Cout, k, stride, monkeypatch):
     """conv(bn_stats=True) accumulates the BN statistics in its epilogue; the BN
     then skips its stats pass — same outputs / running stats as the unfused pair,
     and the self-cleaning slot workspace is left zeroed."""
+    from kubeflow_controller_amd.ops import conv as convmod
     from kubeflow_controller_amd.ops.batchnorm import BatchNorm2dAct, bn_slot_workspace
     from kubeflow_controller_amd.ops.conv import Conv2d
+    monkeypatch.setattr(convmod, "BIG", Cout % 256 == 0)  # the 256x256 tiles' epilogue too
     d = torch.device("cuda")
     torch.manual_seed(0)
     conv = Conv2d(Cin, Cout, k, stride=stride, padding=k // 2).to(d)
@@ -164,12 +174,14 @@ def test_bn_stats_fused_into_conv_epilogue(Cin, Cout, k, stride):
     assert bn_slot_workspace(Cout, d).abs().max().item() == 0
 
 
-@pytest.mark.parametrize("C,Cout,k,stride", [(64, 64, 3, 1), (128, 128, 3, 2), (64, 256, 1, 1)])
-def test_bn_bwd_stats_fused_into_dgrad_epilogue(C, Cout, k, stride):
+@pytest.mark.parametrize("C,Cout,k,stride", [(64, 64, 3, 1), (128, 128, 3, 2), (64, 256, 1, 1), (256, 256, 3, 1)])
+def test_bn_bwd_stats_fused_into_dgrad_epilogue(C, Cout, k, stride, monkeypatch):
     """BN(+ReLU) -> conv: the conv's dgrad epilogue accumulates the BN's backward
     statistics (BnBwdLink); gradients match the unfused pair and the slots end clean."""
+    from kubeflow_controller_amd.ops import conv as convmod
     from kubeflow_controller_amd.ops.batchnorm import BatchNorm2dAct, bn_slot_workspace
     from kubeflow_controller_amd.ops.conv import Conv2d
+    monkeypatch.setattr(convmod, "BIG", C % 256 == 0)
     d = torch.device("cuda")
     torch.manual_seed(0)
     bn = BatchNorm2dAct(C).to(d)
