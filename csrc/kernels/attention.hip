@@ -27,9 +27,9 @@
 // BERT-base layer at 256 x 128 tokens).
 //
 // LDS images: [rows][64] bf16 (128-B rows) keep 16-B chunk c of row r at
-// c ^ ((r >> 1) & 7); [rows][128] (256-B rows) at c ^ (r & 15).  Both make the
-// 16x16x32 row-fragment reads (ds_read_b128) conflict-free; the transposed
-// reads are at most 2-way.
+// c ^ m(r) (see off64: conflict-free for row AND transposed reads); [rows][128]
+// (256-B rows) at c ^ (r & 15) (row reads conflict-free, transposed reads at
+// most 2-way).
 #include "common.h"
 
 namespace {
@@ -48,8 +48,15 @@ __device__ __forceinline__ uint32_t drop_hash(uint64_t seed, uint64_t i) {
   return (uint32_t)((z ^ (z >> 31)) >> 32);
 }
 
+// [rows][64] images: chunk c of row r at c ^ m(r), m(r) = 2·((r>>1)&1) + 4·(((r>>2)^(r>>3))&1) + ((r>>3)&1).
+// Conflict-free for the 16x16x32 row reads (ds_read_b128, 16-row groups) AND for
+// both transposed-read row sets (8 consecutive rows; rows R..R+3 with R+8..R+11):
+// within a parity the 4 rows' masks differ in bits 1-2, so the two logical
+// chunks of a transposed read land in 8 distinct 16-B slots.  (The plain
+// c ^ ((r>>1)&7) swizzle is 2-way on the transposed reads.)
 __device__ __forceinline__ int off64(int row, int col) {
-  return row * 128 + ((((col >> 3) ^ (row >> 1)) & 7) << 4) + (col & 7) * 2;
+  const int m = (((row >> 1) & 1) << 1) | ((((row >> 2) ^ (row >> 3)) & 1) << 2) | ((row >> 3) & 1);
+  return row * 128 + ((((col >> 3) ^ m) & 7) << 4) + (col & 7) * 2;
 }
 __device__ __forceinline__ int off128(int row, int col) {
   return row * 256 + ((((col >> 3) ^ row) & 15) << 4) + (col & 7) * 2;
@@ -444,14 +451,20 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(const bf16_t* __restri
             pack4(ds[qt][kt][0], ds[qt][kt][1], ds[qt][kt][2], ds[qt][kt][3]);
     // dVᵀ[d][key] += Σ_q dOᵀ[d][q]·Pd[q][key];  dKᵀ[d][key] += Σ_q Qᵀ[d][q]·dS[q][key]
     const int ra = 32 * j + 4 * fq, rb = ra + 16;
+    short8 gtr[4], qtr[4];  // dO / Q columns, shared by both key tiles
+#pragma unroll
+    for (int dt = 0; dt < 4; dt++) {
+      gtr[dt] = rd_tr2<64>(Gi, ra, rb, dt * 16, lane);
+      qtr[dt] = rd_tr2<64>(Qi, ra, rb, dt * 16, lane);
+    }
 #pragma unroll
     for (int kt = 0; kt < 2; kt++) {
       const short8 bp = pack_pair(pd[0][kt], pd[1][kt]);
       const short8 bs = pack_pair(ds[0][kt], ds[1][kt]);
 #pragma unroll
       for (int dt = 0; dt < 4; dt++) {
-        dvT[dt][kt] = mma(rd_tr2<64>(Gi, ra, rb, dt * 16, lane), bp, dvT[dt][kt]);
-        dkT[dt][kt] = mma(rd_tr2<64>(Qi, ra, rb, dt * 16, lane), bs, dkT[dt][kt]);
+        dvT[dt][kt] = mma(gtr[dt], bp, dvT[dt][kt]);
+        dkT[dt][kt] = mma(qtr[dt], bs, dkT[dt][kt]);
       }
     }
   }
