@@ -523,50 +523,41 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const long* __restrict__
 }
 
 // scratch[ids[r]] += dout[r]  (fp32 atomics; scratch is kept all-zero between calls)
+// One element per lane: the 64 lanes of a wave touch 64 consecutive floats of one
+// scratch row (one 256-B atomic wave-instruction).  (8 elements per lane made
+// every atomic instruction span 2 KiB in 32-B steps: ~9x slower.)
 __global__ __launch_bounds__(256) void embed_bwd_scatter_kernel(const long* __restrict__ ids,
                                                                 const bf16_t* __restrict__ dout, long dstride,
                                                                 float* __restrict__ scratch, long n, int D) {
-  const long nv = n * (D / 8);
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < nv; i += (long)gridDim.x * 256) {
-    const long r = i / (D / 8);
-    const int c = (int)(i - r * (D / 8)) * 8;
+  const long ne = n * D;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < ne; i += (long)gridDim.x * 256) {
+    const long r = i / D;
+    const int c = (int)(i - r * D);
     const long row = ids ? ids[r] : r;
-    float f[8];
-    load8(dout + r * dstride + c, f);
-#pragma unroll
-    for (int e = 0; e < 8; e++) atomicAdd(scratch + row * D + c + e, f[e]);
+    atomicAdd(scratch + row * D + c, bf2f(dout[r * dstride + c]));
   }
 }
 
 // grad[row] += exchange(scratch[row], 0) for every looked-up row; the atomic
 // exchange hands each element's sum to exactly one occurrence, the others see
 // 0 and skip the write, and the scratch is left zeroed for the next call.
+// One element per lane (contiguous 256-B wave accesses), as the scatter.
 __global__ __launch_bounds__(256) void embed_bwd_fold_kernel(const long* __restrict__ ids, float* __restrict__ scratch,
                                                              void* __restrict__ grad, int grad_f32, long n, int D,
                                                              int accumulate) {
-  const long nv = n * (D / 8);
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < nv; i += (long)gridDim.x * 256) {
-    const long r = i / (D / 8);
-    const int c = (int)(i - r * (D / 8)) * 8;
+  const long ne = n * D;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < ne; i += (long)gridDim.x * 256) {
+    const long r = i / D;
+    const int c = (int)(i - r * D);
     const long row = ids ? ids[r] : r;
-    float v[8];
-    bool any = false;
-#pragma unroll
-    for (int e = 0; e < 8; e++) {
-      v[e] = __hip_atomic_exchange(scratch + row * D + c + e, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      any |= v[e] != 0.f;
-    }
-    if (!any) continue;
+    const float v = __hip_atomic_exchange(scratch + row * D + c, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (v == 0.f) continue;
     if (grad_f32) {
       float* g = reinterpret_cast<float*>(grad) + row * D + c;
-#pragma unroll
-      for (int e = 0; e < 8; e++)
-        if (v[e] != 0.f) g[e] = accumulate ? g[e] + v[e] : v[e];
+      *g = accumulate ? *g + v : v;
     } else {
       bf16_t* g = reinterpret_cast<bf16_t*>(grad) + row * D + c;
-#pragma unroll
-      for (int e = 0; e < 8; e++)
-        if (v[e] != 0.f) g[e] = (bf16_t)f2bf(accumulate ? bf2f(g[e]) + v[e] : v[e]);
+      *g = (bf16_t)f2bf(accumulate ? bf2f(*g) + v : v);
     }
   }
 }
@@ -779,10 +770,10 @@ KFA_API int kfa_embed_fwd(const long* i0, const void* t0, const long* i1, const 
 KFA_API int kfa_embed_bwd(const long* ids, const void* dout, long dstride, float* scratch, void* grad, int grad_f32,
                           long n, int D, int accumulate, hipStream_t s) {
   if (n <= 0 || D % 8 || dstride % 8) return -1;
-  const int g = grid_for(n * (D / 8));
-  hipLaunchKernelGGL(embed_bwd_scatter_kernel, dim3(g), dim3(256), 0, s, ids, (const bf16_t*)dout, dstride, scratch,
+  const int ge = grid_for(n * D);
+  hipLaunchKernelGGL(embed_bwd_scatter_kernel, dim3(ge), dim3(256), 0, s, ids, (const bf16_t*)dout, dstride, scratch,
                      n, D);
-  hipLaunchKernelGGL(embed_bwd_fold_kernel, dim3(g), dim3(256), 0, s, ids, scratch, grad, grad_f32, n, D, accumulate);
+  hipLaunchKernelGGL(embed_bwd_fold_kernel, dim3(ge), dim3(256), 0, s, ids, scratch, grad, grad_f32, n, D, accumulate);
   return kfa_status();
 }
 
