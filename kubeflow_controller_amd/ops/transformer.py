@@ -466,7 +466,7 @@ class EncoderLayerFn(torch.autograd.Function):
         if use_g:   # residual-gradient join as the GEMM addend
             dh1 = _gemm.gemm_nt(df1, _gemm.transpose(w1), addend=dh1_res)[0]
         else:
-            dh1 = torch.addmm(dh1_res, df1, w1)
+            dh1 = dh1_res.addmm_(df1, w1)  # in place: addmm(C, ..) would first copy C (a D2D memcpy)
         del df1, dh1_res
         # LN1 (+ out-proj bias grad)
         dx_res, dao = ln_bwd(dh1, h1s, m1, r1, g1, G(g1), G(be1), G(bo), p=ph, seed=s_h1, want_branch=True)
@@ -501,7 +501,7 @@ class EncoderLayerFn(torch.autograd.Function):
         if use_g:
             dx = _gemm.gemm_nt(dqkv, _gemm.transpose(wqkv), addend=dx_res)[0]
         else:
-            dx = torch.addmm(dx_res, dqkv, wqkv)
+            dx = dx_res.addmm_(dqkv, wqkv)
         grads = [_finish(p, tg[id(p)][0], tg[id(p)][2]) for p in ctx.params]
         return (dx, None, None, *grads)
 
