@@ -153,7 +153,8 @@ def wgrad_ok(x: torch.Tensor, dy: torch.Tensor, w: torch.Tensor) -> bool:
 def wgrad_into(x, dy, out, Nb, H, W, Ci, P_, Q_, Co, R, S, stride, pad, accumulate: bool) -> None:
     """out (+)= dW  for NHWC x [Nb,H,W,Ci] / dy [Nb,P,Q,Co]; out is [Co][R][S][Ci] (bf16 or fp32)."""
     nfl = _lib.lib().kfa_wgrad_part_floats(Nb, P_, Q_, Co, R, S, Ci)
-    part = _lib.workspace(nfl * 4, x.device, "wgrad_part").view(torch.float32)
+    # one split-K partial workspace per stream (BERT's encoder wgrads run on the side stream, ops/streams.py)
+    part = _lib.workspace(nfl * 4, x.device, f"wgrad_part{_lib.stream() or 0}").view(torch.float32)
     _lib.call("kfa_conv_wgrad", _lib.ptr(dy), _lib.ptr(x), _lib.ptr(out), int(out.dtype == torch.float32),
               int(accumulate), _lib.ptr(part), Nb, H, W, Ci, P_, Q_, Co, R, S, stride, pad, _lib.stream())
 

@@ -31,6 +31,7 @@ import torch.nn.functional as F
 
 from . import _lib
 from . import gemm as _gemm
+from . import streams as _streams
 from . import loss as _loss  # noqa: F401  (registers kfa_softmax_xent)
 from ..parallel.flat import direct_grad_view, notify_grad_ready
 
@@ -161,37 +162,13 @@ def _wgrad_(gw: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor) -> None:
         gw.add_(torch.mm(dy2.t(), x2).to(gw.dtype))
 
 
-# Weight gradients of the encoder layer run on a side stream, concurrently with
-# the data-gradient chain (dgrad GEMMs, LayerNorm / GELU / attention backward)
-# on the main stream: the wgrad launches are 1-block-per-CU 256x256 tiles and
-# fill the CUs that the main stream's tails and memory-bound kernels leave idle.
-# env KFA_SIDE_STREAM=0 keeps everything on one stream.
-SIDE_STREAM = os.environ.get("KFA_SIDE_STREAM", "1") != "0"
-_side = {}
-
-
-def _side_stream(dev: torch.device) -> torch.cuda.Stream:
-    s = _side.get(dev.index)
-    if s is None:
-        s = _side[dev.index] = torch.cuda.Stream(dev)
-    return s
-
-
-def _wgrad_side_(gw: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor) -> Optional[torch.cuda.Stream]:
-    """:func:`_wgrad_` on the side stream (ordered after everything already queued on
-    the current stream); returns the side stream, which the caller must join
-    (``current_stream().wait_stream(side)``) before the gradient is consumed."""
-    if not (SIDE_STREAM and gw.is_cuda):
+def _wgrad_side_(gw: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor) -> None:
+    """:func:`_wgrad_` on the weight-gradient side stream (``ops/streams.py``):
+    concurrent with the layer's data-gradient chain on the main stream."""
+    if _streams.enabled(gw):
+        _streams.run_on_side(lambda: _wgrad_(gw, dy2, x2), gw.device, (gw, dy2, x2))
+    else:
         _wgrad_(gw, dy2, x2)
-        return None
-    main = torch.cuda.current_stream(gw.device)
-    side = _side_stream(gw.device)
-    side.wait_stream(main)
-    with torch.cuda.stream(side):
-        _wgrad_(gw, dy2, x2)
-    for t in (gw, dy2, x2):  # the allocator must not hand their memory to the main stream before side is done
-        t.record_stream(side)
-    return side
 
 
 # ----------------------------------------------------------------------------- LayerNorm
@@ -489,7 +466,7 @@ class EncoderLayerFn(torch.autograd.Function):
         G = lambda p: tg[id(p)][0]  # noqa: E731
         # LN2 (+ FFN2 bias grad, hidden dropout): dres -> h1, dbranch -> f2
         dh1_res, df2 = ln_bwd(dy, h2s, m2, r2, g2, G(g2), G(be2), G(b2), p=ph, seed=s_h2, want_branch=True)
-        side = _wgrad_side_(G(w2), df2, f1a)
+        _wgrad_side_(G(w2), df2, f1a)
         if use_g:   # df1 = (df2 · W2) * gelu'(z1), db1 += colsum(df1): one GEMM launch
             df1 = _gemm.gemm_nt(df2, _gemm.transpose(w2), zin=f1, dact="gelu", dbias=G(b1))[0]
         else:
@@ -538,8 +515,6 @@ class EncoderLayerFn(torch.autograd.Function):
             dx = _gemm.gemm_nt(dqkv, _gemm.transpose(wqkv), addend=dx_res)[0]
         else:
             dx = dx_res.addmm_(dqkv, wqkv)
-        if side is not None:  # weight gradients complete before the buckets see them
-            torch.cuda.current_stream(dx.device).wait_stream(side)
         grads = [_finish(p, tg[id(p)][0], tg[id(p)][2]) for p in ctx.params]
         return (dx, None, None, *grads)
 

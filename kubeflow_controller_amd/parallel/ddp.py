@@ -94,6 +94,9 @@ class GradSync:
 
     def _launch(self, b: _Bucket) -> None:
         view = self.groups[b.group].grad[b.start:b.end]
+        if view.is_cuda:  # weight-gradient kernels on the side stream wrote into this bucket
+            from ..ops import streams
+            streams.join(view.device)
         b.work = dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
 
     def finish(self) -> float:
