@@ -1,13 +1,15 @@
 """In-tree build of the native parts.
 
-* ``_native_runtime`` — C++ control-plane runtime (``csrc/runtime/runtime.cpp``),
-  compiled with g++ against pybind11.
+* ``_native_runtime`` — C++ control-plane runtime (core in
+  ``csrc/runtime/runtime_core.h``, bindings in ``runtime.cpp``), compiled with
+  g++ against pybind11.
 * ``ops/_hip_kernels.so`` — the hand-written CDNA4 kernels (``csrc/kernels/*.hip``)
   compiled by ``hipcc --offload-arch=gfx950`` into ONE shared object with a C
   ABI; Python binds it with ``ctypes`` (``ops/_lib.py``), so no torch headers
   are compiled and rebuilds take seconds.
-* ``parallel/_comm.so`` — C++ bucket planner / flat-buffer packing helpers
-  (``csrc/comm/*.cpp``).
+* ``build/sanitize/runtime_selftest_{asan,tsan}`` — the runtime core's native
+  self-test (``csrc/runtime/selftest.cpp``) under ASan+UBSan and TSan
+  (``--sanitize``; host code only).
 
 Everything lands inside the package directory so it travels with the repo
 snapshot to the GPU box (``gpurun``) and is visible as an in-tree ``.so``.
@@ -71,9 +73,10 @@ def runtime_target() -> str:
 def build_runtime(force: bool = False) -> str:
     import pybind11
     src = os.path.join(CSRC, "runtime", "runtime.cpp")
+    srcs = [src, os.path.join(CSRC, "runtime", "runtime_core.h")]
     tgt = runtime_target()
     with _lock:
-        if not force and _up_to_date(tgt, [src]):
+        if not force and _up_to_date(tgt, srcs):
             return tgt
         cxx = os.environ.get("CXX", "g++")
         tmp = tgt + f".tmp{os.getpid()}"
@@ -82,7 +85,7 @@ def build_runtime(force: bool = False) -> str:
                src, "-o", tmp, "-lpthread"]
         _run(cmd, quiet=True)
         os.replace(tmp, tgt)
-        _write_stamp(tgt, [src])
+        _write_stamp(tgt, srcs)
     return tgt
 
 
@@ -152,34 +155,75 @@ def build_kernels(force: bool = False, jobs: int = 8) -> str:
     return tgt
 
 
-def comm_target() -> str:
-    return os.path.join(PKG, "parallel", "_comm" + _ext_suffix())
+SANITIZERS = {
+    "asan": ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"],
+    "tsan": ["-fsanitize=thread"],
+}
 
 
-def build_comm(force: bool = False) -> str:
-    import pybind11
-    srcs = sorted(glob.glob(os.path.join(CSRC, "comm", "*.cpp")))
-    if not srcs:
-        return ""
-    tgt = comm_target()
+def sanitize_cxx() -> str:
+    """ROCm's clang++ when present: gcc-11's TSan does not intercept
+    ``pthread_cond_clockwait`` (what ``condition_variable::wait_for`` uses), so
+    it reports a false "double lock" on every timed wait; clang's runtime does."""
+    for c in (os.environ.get("KFA_SANITIZE_CXX"), "/opt/rocm/lib/llvm/bin/clang++", shutil.which("clang++")):
+        if c and os.path.exists(c):
+            return c
+    return os.environ.get("CXX", "g++")
+
+
+def sanitize_target(kind: str, canary: bool = False) -> str:
+    return os.path.join(ROOT, "build", "sanitize", f"runtime_selftest_{kind}" + ("_canary" if canary else ""))
+
+
+def build_sanitized(kind: str, force: bool = False, canary: bool = False) -> str:
+    """Compile the runtime core's self-test under one sanitizer (host code only).
+
+    ``canary=True`` also compiles in a deliberate defect (a data race under
+    TSan, a heap overflow under ASan) so a test can prove the tool is live."""
+    srcs = [os.path.join(CSRC, "runtime", "selftest.cpp"), os.path.join(CSRC, "runtime", "runtime_core.h")]
+    tgt = sanitize_target(kind, canary)
     with _lock:
         if not force and _up_to_date(tgt, srcs):
             return tgt
+        os.makedirs(os.path.dirname(tgt), exist_ok=True)
         tmp = tgt + f".tmp{os.getpid()}"
-        cmd = [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-shared", "-fPIC",
-               f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}", *srcs, "-o", tmp]
+        cmd = [sanitize_cxx(), "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-Wall",
+               "-Wno-unused-function", *SANITIZERS[kind], *(["-DKFA_SELFTEST_INJECT"] if canary else []),
+               srcs[0], "-o", tmp, "-lpthread"]
         _run(cmd, quiet=True)
         os.replace(tmp, tgt)
         _write_stamp(tgt, srcs)
     return tgt
 
 
+def run_sanitized(kind: str, timeout: float = 300.0, canary: bool = False) -> subprocess.CompletedProcess:
+    """Build and run one sanitizer self-test; a sanitizer report makes it exit
+    23 (ASan / UBSan build) or 25 (TSan build)."""
+    exe = build_sanitized(kind, canary=canary)
+    env = dict(os.environ)
+    env.pop("LD_PRELOAD", None)  # a preloaded runtime ahead of libasan/libtsan aborts the run
+    if kind == "asan":  # UBSan shares the common flags (exitcode) of the ASan runtime
+        env["ASAN_OPTIONS"] = "detect_leaks=1:abort_on_error=0:halt_on_error=1:exitcode=23"
+        env["UBSAN_OPTIONS"] = "print_stacktrace=1:halt_on_error=1"
+    else:
+        env["TSAN_OPTIONS"] = "halt_on_error=1:exitcode=25:second_deadlock_stack=1"
+    return subprocess.run([exe], capture_output=True, text=True, timeout=timeout, env=env)
+
+
 def build_all(force: bool = False) -> None:
     build_runtime(force)
-    build_comm(force)
     build_kernels(force)
 
 
 if __name__ == "__main__":
+    if "--sanitize" in sys.argv:
+        rc = 0
+        for kind in SANITIZERS:
+            r = run_sanitized(kind)
+            sys.stdout.write(f"[{kind}] " + r.stdout)
+            if r.returncode != 0:
+                sys.stderr.write(r.stderr[-8000:])
+                rc = r.returncode
+        sys.exit(rc)
     build_all(force="--force" in sys.argv)
-    print("built:", runtime_target(), comm_target(), kernels_target())
+    print("built:", runtime_target(), kernels_target())
