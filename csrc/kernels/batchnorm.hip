@@ -108,29 +108,57 @@ __global__ __launch_bounds__(NT) void bn_stats_partial(const bf16_t* __restrict_
 // kSlots slot rows ([kSlots][2][C], slot = block % kSlots, so each address
 // sees gx/kSlots adds); finalize sums the slots in fp64 and ZEROES them again,
 // leaving the workspace clean for the next BN layer on the stream.
-__device__ __forceinline__ void combine2(float* __restrict__ part, int C, int c, double& a, double& b) {
+// Finalize blocks are 64 channels x kGroups slot groups (1024 threads): each
+// thread read-and-zeroes kSlots / kGroups slot pairs, all in flight at once,
+// and the groups are summed through LDS in a fixed order (deterministic).  One
+// 64-thread block per 64 channels walking all 64 slots serially was latency
+// bound (128 dependent-batch device-scope atomics: ~6.6 us per finalize).
+constexpr int kGroups = 16;
+static_assert(kSlots % kGroups == 0, "slot groups");
+
+__device__ __forceinline__ bool combine2(float* __restrict__ part, int C, int c, double& a, double& b) {
+  __shared__ double ra[kGroups][64], rb[kGroups][64];
+  const int lx = threadIdx.x, ly = threadIdx.y;
+  float va[kSlots / kGroups], vb[kSlots / kGroups];
+#pragma unroll
+  for (int i = 0; i < kSlots / kGroups; i++) {
+    va[i] = vb[i] = 0.f;
+    if (c < C) {
+      float* pa = part + ((long)(ly + kGroups * i) * 2) * C + c;
+      // read-and-zero at the coherence point: the adds came from other XCDs'
+      // workgroups, so plain loads could hit a stale line of THIS XCD's L2
+      va[i] = __hip_atomic_exchange(pa, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      vb[i] = __hip_atomic_exchange(pa + C, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  double sa = 0.0, sb = 0.0;
+#pragma unroll
+  for (int i = 0; i < kSlots / kGroups; i++) {
+    sa += (double)va[i];
+    sb += (double)vb[i];
+  }
+  ra[ly][lx] = sa;
+  rb[ly][lx] = sb;
+  __syncthreads();
+  if (ly != 0 || c >= C) return false;
   a = 0.0;
   b = 0.0;
-#pragma unroll 8
-  for (int i = 0; i < kSlots; i++) {
-    float* pa = part + ((long)i * 2) * C + c;
-    float* pb = pa + C;
-    // read-and-zero at the coherence point: the adds came from other XCDs'
-    // workgroups, so plain loads could hit a stale line of THIS XCD's L2
-    a += (double)__hip_atomic_exchange(pa, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    b += (double)__hip_atomic_exchange(pb, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+  for (int j = 0; j < kGroups; j++) {
+    a += ra[j][lx];
+    b += rb[j][lx];
   }
+  return true;
 }
 
-__global__ __launch_bounds__(256) void bn_finalize(const bf16_t* __restrict__ x, float* __restrict__ part, int gx, long M, int C,
+__global__ __launch_bounds__(64 * kGroups) void bn_finalize(const bf16_t* __restrict__ x, float* __restrict__ part, int gx, long M, int C,
                             const float* __restrict__ gamma, const float* __restrict__ beta,
                             float* __restrict__ rmean, float* __restrict__ rvar, float* __restrict__ save_mean,
                             float* __restrict__ save_invstd, float* __restrict__ scale, float* __restrict__ shift,
                             float eps, float momentum) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+  const int c = blockIdx.x * 64 + threadIdx.x;
   double a, b;
-  combine2(part, C, c, a, b);
+  if (!combine2(part, C, c, a, b)) return;
   const double K = x ? (double)bf2f(x[c]) : 0.0;  // x == nullptr: un-shifted sums (fused in the conv epilogue)
   const double m1 = a / (double)M;
   double var = b / (double)M - m1 * m1;
@@ -300,14 +328,13 @@ __global__ __launch_bounds__(NT) void bn_bwd_partial(const bf16_t* __restrict__ 
 }
 
 // coef layout: [3][C] = a, b, k   ;  dx = a*dz + b*x + k
-__global__ __launch_bounds__(256) void bn_bwd_finalize(float* __restrict__ part, int gx, long M, int C, const float* __restrict__ gamma,
+__global__ __launch_bounds__(64 * kGroups) void bn_bwd_finalize(float* __restrict__ part, int gx, long M, int C, const float* __restrict__ gamma,
                                 const float* __restrict__ mean, const float* __restrict__ invstd,
                                 float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ coef,
                                 int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+  const int c = blockIdx.x * 64 + threadIdx.x;
   double sdy, sdx;
-  combine2(part, C, c, sdy, sdx);
+  if (!combine2(part, C, c, sdy, sdx)) return;
   const float inv = invstd[c];
   const float g = gamma ? gamma[c] : 1.f;
   const float dg = (float)sdx * inv;  // sum(dz * xhat)
@@ -381,7 +408,7 @@ KFA_API int kfa_bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, cons
   float* scale = coefws;
   float* shift = scale + C;
   hipLaunchKernelGGL(bn_stats_partial, dim3(g.gx), dim3(NT), 0, s, x, part, M, C, g.chunk, g.tpr, g.rpi);
-  hipLaunchKernelGGL(bn_finalize, dim3(kfa_ceil_div(C, 64)), dim3(64), 0, s, x, part, g.gx, M, C, gamma, beta, rmean,
+  hipLaunchKernelGGL(bn_finalize, dim3(kfa_ceil_div(C, 64)), dim3(64, kGroups), 0, s, x, part, g.gx, M, C, gamma, beta, rmean,
                      rvar, save_mean, save_invstd, scale, shift, eps, momentum);
   if (relu && res)
     hipLaunchKernelGGL((bn_apply<true, true>), dim3(g.gx), dim3(NT), 0, s, x, res, y, scale, shift, M, C, g.chunk, g.tpr, g.rpi);
@@ -391,6 +418,16 @@ KFA_API int kfa_bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, cons
     hipLaunchKernelGGL((bn_apply<false, true>), dim3(g.gx), dim3(NT), 0, s, x, res, y, scale, shift, M, C, g.chunk, g.tpr, g.rpi);
   else
     hipLaunchKernelGGL((bn_apply<false, false>), dim3(g.gx), dim3(NT), 0, s, x, res, y, scale, shift, M, C, g.chunk, g.tpr, g.rpi);
+  return kfa_status();
+}
+
+// Statistics pass alone (shifted sums into `slots`); used by the conv forward
+// tuner (ops/conv.py) to price "vendor conv + separate BN statistics pass"
+// against the fused-statistics implicit GEMM.  The caller cleans `slots`.
+KFA_API int kfa_bn_stats_partial(const bf16_t* x, float* slots, long M, int C, hipStream_t s) {
+  if (!bn_shape_ok(M, C)) return -1;
+  Geom g = geom(M, C, max_row_blocks(C));
+  hipLaunchKernelGGL(bn_stats_partial, dim3(g.gx), dim3(NT), 0, s, x, slots, M, C, g.chunk, g.tpr, g.rpi);
   return kfa_status();
 }
 
@@ -406,7 +443,7 @@ KFA_API int kfa_bn_fwd_train_prestats(const bf16_t* x, const bf16_t* res, bf16_t
   Geom g = geom(M, C, max_row_blocks(C));
   float* scale = coefws;
   float* shift = scale + C;
-  hipLaunchKernelGGL(bn_finalize, dim3(kfa_ceil_div(C, 64)), dim3(64), 0, s, nullptr, slots, g.gx, M, C, gamma, beta,
+  hipLaunchKernelGGL(bn_finalize, dim3(kfa_ceil_div(C, 64)), dim3(64, kGroups), 0, s, nullptr, slots, g.gx, M, C, gamma, beta,
                      rmean, rvar, save_mean, save_invstd, scale, shift, eps, momentum);
   if (relu && res)
     hipLaunchKernelGGL((bn_apply<true, true>), dim3(g.gx), dim3(NT), 0, s, x, res, y, scale, shift, M, C, g.chunk, g.tpr, g.rpi);
@@ -451,7 +488,7 @@ KFA_API int kfa_bn_bwd_prestats(const bf16_t* dy, const bf16_t* x, const bf16_t*
   if (relu && !y) return -2;
   Geom g = geom(M, C, max_row_blocks(C));
   float* coef = coefws;
-  hipLaunchKernelGGL(bn_bwd_finalize, dim3(kfa_ceil_div(C, 64)), dim3(64), 0, s, slots, g.gx, M, C, gamma, save_mean,
+  hipLaunchKernelGGL(bn_bwd_finalize, dim3(kfa_ceil_div(C, 64)), dim3(64, kGroups), 0, s, slots, g.gx, M, C, gamma, save_mean,
                      save_invstd, dgamma, dbeta, coef, accumulate);
   if (relu && dres)
     hipLaunchKernelGGL((bn_bwd_apply<true, true>), dim3(g.gx), dim3(NT), 0, s, dy, x, y, coef, dx, dres, M, C, g.chunk, g.tpr, g.rpi);
@@ -476,7 +513,7 @@ KFA_API int kfa_bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const
     hipLaunchKernelGGL(bn_bwd_partial<true>, dim3(g.gx), dim3(NT), 0, s, dy, x, y, save_mean, part, M, C, g.chunk, g.tpr, g.rpi);
   else
     hipLaunchKernelGGL(bn_bwd_partial<false>, dim3(g.gx), dim3(NT), 0, s, dy, x, y, save_mean, part, M, C, g.chunk, g.tpr, g.rpi);
-  hipLaunchKernelGGL(bn_bwd_finalize, dim3(kfa_ceil_div(C, 64)), dim3(64), 0, s, part, g.gx, M, C, gamma, save_mean,
+  hipLaunchKernelGGL(bn_bwd_finalize, dim3(kfa_ceil_div(C, 64)), dim3(64, kGroups), 0, s, part, g.gx, M, C, gamma, save_mean,
                      save_invstd, dgamma, dbeta, coef, accumulate);
   if (relu && dres)
     hipLaunchKernelGGL((bn_bwd_apply<true, true>), dim3(g.gx), dim3(NT), 0, s, dy, x, y, coef, dx, dres, M, C, g.chunk, g.tpr, g.rpi);

@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import math
 import os
+import sys
 
 import torch
 import torch.nn as nn
@@ -36,6 +37,7 @@ _lib.register("kfa_zero_bf16", [P, _lib.L, P])
 _lib.register("kfa_weight_transpose", [P, P] + [I] * 10 + [P])
 _lib.register("kfa_wgrad_part_floats", [I] * 7, _lib.L)
 _lib.register("kfa_conv_wgrad", [P, P, P, I, I, P] + [I] * 11 + [P])
+_lib.register("kfa_bn_stats_partial", [P, P, _lib.L, I, P])
 
 # Runtime switches (tests compare against the vendor path); env KFA_CONV_IGEMM=0 / KFA_WGRAD=0 disable.
 ENABLED = os.environ.get("KFA_CONV_IGEMM", "1") != "0"
@@ -53,6 +55,58 @@ def igemm_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
 # have no split-K.  KFA_CONV_BIG_MINK: minimum reduction length K = R*S*C.
 BIG = os.environ.get("KFA_CONV_BIG", "0") == "1"
 BIG_MIN_K = int(os.environ.get("KFA_CONV_BIG_MINK", "256"))
+
+
+# Forward tuner (like cudnn.benchmark, per layer shape): the implicit GEMM with the
+# BatchNorm statistics fused in its epilogue vs the vendor (MIOpen) forward plus
+# the separate statistics pass the BN then runs.  Measured once per shape on first
+# use, outside any graph capture; env KFA_CONV_TUNE=0 keeps every layer on the
+# implicit GEMM.  tools/bench_conv.py shows where MIOpen's forward wins: the
+# compute-heavy 3x3 / K >= 1024 layers of the late stages (e.g. 256->256 3x3 at
+# 14x14: 0.075 vs 0.110 ms), never the memory-bound expand 1x1s.
+TUNE = os.environ.get("KFA_CONV_TUNE", "1") != "0"
+TUNE_LOG = os.environ.get("KFA_CONV_TUNE_LOG", "0") == "1"
+_fwd_plan: dict = {}  # shape key -> True: vendor forward + BN stats pass
+
+
+def _time_ms(fn, reps: int = 5) -> float:
+    for _ in range(2):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+def _use_vendor_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, stats) -> bool:
+    if not (TUNE and x.is_cuda):
+        return False
+    key = (tuple(x.shape), tuple(w.shape), stride, pad, stats is not None)
+    hit = _fwd_plan.get(key)
+    if hit is not None:
+        return hit
+    if torch.cuda.is_current_stream_capturing():
+        return False
+    with torch.no_grad():
+        x, w = _cl(x), _cl(w)
+        scratch = torch.zeros(_lib.lib().kfa_bn_slot_floats(w.shape[0]), dtype=torch.float32, device=x.device) \
+            if stats is not None else None
+        t_ours = _time_ms(lambda: conv_fwd(x, w, stride, pad, scratch))
+        y = F.conv2d(x, w, None, stride, pad)
+        t_vendor = _time_ms(lambda: F.conv2d(x, w, None, stride, pad))
+        if stats is not None:
+            M, C = y.numel() // y.shape[1], y.shape[1]
+            t_vendor += _time_ms(lambda: _lib.call("kfa_bn_stats_partial", _lib.ptr(y), _lib.ptr(scratch), M, C,
+                                                   _lib.stream()))
+    hit = _fwd_plan[key] = t_vendor < 0.95 * t_ours
+    if TUNE_LOG:
+        print(f"[kfa conv tune] x{tuple(x.shape)} w{tuple(w.shape)} s{stride} stats={stats is not None}: "
+              f"igemm {t_ours:.3f} ms, vendor{'+stats' if stats is not None else ''} {t_vendor:.3f} ms -> "
+              f"{'vendor' if hit else 'igemm'}", file=sys.stderr, flush=True)
+    return hit
 
 
 def _variant(M: int, N: int, K: int = 0) -> int:
@@ -222,13 +276,15 @@ class _Branch(torch.autograd.Function):
 
 class _ConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, stride, pad, join, stats):
+    def forward(ctx, x, w, stride, pad, join, stats, vendor=False):
         ctx.save_for_backward(x, w)
         ctx.stride, ctx.pad, ctx.join = stride, pad, join
         ctx.wparam = w  # the Parameter itself (for the direct flat-gradient write)
         ctx.bn_link = getattr(x, "_kfa_bn_link", None)  # x = output of a BatchNorm (see conv_dgrad)
         if ctx.bn_link is not None:
             ctx.bn_link.convs += 1
+        if vendor:
+            return _cl(F.conv2d(_cl(x), _cl(w), None, stride, pad))
         return conv_fwd(x, w, stride, pad, stats)
 
     @staticmethod
@@ -255,7 +311,7 @@ class _ConvFn(torch.autograd.Function):
                     dx = dx + addend
         if ctx.needs_input_grad[1]:
             dw = conv_wgrad(x, dy, w, ctx.stride, ctx.pad, ctx.wparam)
-        return dx, dw, None, None, None, None
+        return dx, dw, None, None, None, None, None
 
 
 def conv2d(x, w, stride: int = 1, pad: int = 0, join: "GradJoin | None" = None, bn_stats: bool = False):
@@ -269,7 +325,10 @@ def conv2d(x, w, stride: int = 1, pad: int = 0, join: "GradJoin | None" = None, 
         if bn_stats:
             from .batchnorm import bn_slot_workspace
             stats = bn_slot_workspace(w.shape[0], x.device)
-        y = _ConvFn.apply(x, w, stride, pad, join, stats)
+        vendor = _use_vendor_fwd(x, w, stride, pad, stats)
+        if vendor:
+            stats = None  # the BN runs its own statistics pass
+        y = _ConvFn.apply(x, w, stride, pad, join, stats, vendor)
         if stats is not None:
             y._kfa_prestats = True
         return y

@@ -4,6 +4,14 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
+
+@pytest.fixture(autouse=True)
+def _no_forward_tuner(monkeypatch):
+    """These tests check the implicit GEMM itself: keep the forward tuner from
+    routing a shape to the vendor forward (test_conv_forward_tuner covers it)."""
+    from kubeflow_controller_amd.ops import conv as convmod
+    monkeypatch.setattr(convmod, "TUNE", False)
+
 SHAPES = [
     # N, Cin, H, W, Cout, k, stride, pad
     (2, 64, 14, 14, 64, 1, 1, 0),
@@ -206,3 +214,42 @@ def test_bn_bwd_stats_fused_into_dgrad_epilogue(C, Cout, k, stride, monkeypatch)
         assert (a - b).abs().max().item() < 2e-2 * scale, ((a - b).abs().max().item(), scale)
     torch.cuda.synchronize()
     assert bn_slot_workspace(C, d).abs().max().item() == 0
+
+
+def test_conv_forward_tuner(monkeypatch):
+    """The per-shape forward tuner: timing both forwards records a decision; a
+    vendor-forward layer leaves the BN statistics to the BN (no prestats tag, slots
+    clean) and matches the fused path's outputs and gradients (the backward stays on
+    the implicit-GEMM dgrad / wgrad)."""
+    from kubeflow_controller_amd.ops import conv as convmod
+    from kubeflow_controller_amd.ops.batchnorm import BatchNorm2dAct, bn_slot_workspace
+    from kubeflow_controller_amd.ops.conv import Conv2d
+    d = torch.device("cuda")
+    torch.manual_seed(0)
+    conv = Conv2d(128, 128, 3, stride=1, padding=1).to(d)
+    conv.weight.data = conv.weight.data.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x = torch.randn(4, 128, 20, 20, device=d).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    monkeypatch.setattr(convmod, "TUNE", True)
+    monkeypatch.setattr(convmod, "_fwd_plan", {})
+    key = (tuple(x.shape), tuple(conv.weight.shape), 1, 1, True)
+    choice = convmod._use_vendor_fwd(x, conv.weight, 1, 1, bn_slot_workspace(128, d))
+    assert convmod._fwd_plan[key] is choice
+    torch.cuda.synchronize()
+    assert bn_slot_workspace(128, d).abs().max().item() == 0  # tuning used its own scratch slots
+    outs, grads = [], []
+    for vendor in (True, False):
+        convmod._fwd_plan[key] = vendor
+        bn = BatchNorm2dAct(128).to(d)
+        xr = x.clone().requires_grad_()
+        conv.weight.grad = None
+        y = conv(xr, bn_stats=True)
+        assert getattr(y, "_kfa_prestats", False) is (not vendor)
+        out = bn(y)
+        out.float().square().sum().backward()
+        outs.append(out.float())
+        grads.append((xr.grad.float(), conv.weight.grad.float(), bn.running_mean.clone()))
+    torch.cuda.synchronize()
+    assert bn_slot_workspace(128, d).abs().max().item() == 0
+    assert (outs[0] - outs[1]).abs().max().item() < 5e-2
+    for a, b in zip(grads[0], grads[1]):
+        assert (a - b).abs().max().item() < 5e-2 * max(1.0, b.abs().max().item())
