@@ -213,6 +213,35 @@ def wgrad_into(x, dy, out, Nb, H, W, Ci, P_, Q_, Co, R, S, stride, pad, accumula
               int(accumulate), _lib.ptr(part), Nb, H, W, Ci, P_, Q_, Co, R, S, stride, pad, _lib.stream())
 
 
+_wgrad_plan: dict = {}  # shape key -> True: vendor weight gradient
+
+
+def _use_vendor_wgrad(x: torch.Tensor, dy: torch.Tensor, w: torch.Tensor, stride: int, pad: int) -> bool:
+    """Weight-gradient side of the per-shape tuner: split-K MFMA wgrad vs the vendor's
+    (plus the add into the fp32 flat gradient it then needs).  On ResNet-50 the vendor
+    wins the 64-channel 3x3 at 56x56 (0.17 vs 0.23 ms)."""
+    if not (TUNE and x.is_cuda):
+        return False
+    key = (tuple(x.shape), tuple(w.shape), stride, pad)
+    hit = _wgrad_plan.get(key)
+    if hit is not None:
+        return hit
+    if torch.cuda.is_current_stream_capturing():
+        return False
+    Nb, Ci, H, W = x.shape
+    Co, _, R, S = w.shape
+    with torch.no_grad():
+        acc = torch.zeros(w.shape, dtype=torch.float32, device=x.device).contiguous(memory_format=torch.channels_last)
+        t_ours = _time_ms(lambda: wgrad_into(x, dy, acc, Nb, H, W, Ci, dy.shape[2], dy.shape[3], Co, R, S, stride, pad,
+                                             True))
+        t_vendor = _time_ms(lambda: acc.add_(conv_wgrad_vendor(x, dy, w, stride, pad)))
+    hit = _wgrad_plan[key] = t_vendor < 0.95 * t_ours
+    if TUNE_LOG:
+        print(f"[kfa conv tune] wgrad x{tuple(x.shape)} w{tuple(w.shape)} s{stride}: ours {t_ours:.3f} ms, "
+              f"vendor {t_vendor:.3f} ms -> {'vendor' if hit else 'ours'}", file=sys.stderr, flush=True)
+    return hit
+
+
 def conv_wgrad(x: torch.Tensor, dy: torch.Tensor, w: torch.Tensor, stride: int, pad: int, wparam=None):
     """Weight gradient.  Returns None when it was accumulated directly into the
     parameter's flat gradient buffer (and the bucket notified), else dW."""
@@ -223,8 +252,16 @@ def conv_wgrad(x: torch.Tensor, dy: torch.Tensor, w: torch.Tensor, stride: int, 
     Co, _, R, S = w.shape
     P_, Q_ = dy.shape[2], dy.shape[3]
     target = direct_grad_view(wparam) if wparam is not None else None
-    if target is not None and target.dtype in (torch.bfloat16, torch.float32) and \
-            target.is_contiguous(memory_format=torch.channels_last):
+    direct = target is not None and target.dtype in (torch.bfloat16, torch.float32) and \
+        target.is_contiguous(memory_format=torch.channels_last)
+    if _use_vendor_wgrad(x, dy, w, stride, pad):
+        gw = conv_wgrad_vendor(x, dy, w, stride, pad)
+        if not direct:
+            return gw
+        target.add_(gw)
+        notify_grad_ready(wparam)
+        return None
+    if direct:
         wgrad_into(x, dy, target, Nb, H, W, Ci, P_, Q_, Co, R, S, stride, pad, accumulate=True)
         notify_grad_ready(wparam)
         return None

@@ -132,8 +132,15 @@ def test_wgrad_dense_shapes(rows, out_f, in_f):
     assert err < 2e-2 * ref.abs().max().item(), err
 
 
-def test_wgrad_direct_into_flat_buffer():
+@pytest.mark.parametrize("vendor", [False, True])
+def test_wgrad_direct_into_flat_buffer(vendor, monkeypatch):
+    """Direct-gradient protocol on both wgrad routes the tuner can pick: the HIP
+    split-K wgrad accumulates into the flat view; the vendor's dW is added into it."""
+    from kubeflow_controller_amd.ops import conv as convmod
     from kubeflow_controller_amd.ops.conv import Conv2d
+    if vendor:
+        monkeypatch.setattr(convmod, "TUNE", True)
+        monkeypatch.setattr(convmod, "_use_vendor_wgrad", lambda *a: True)
     from kubeflow_controller_amd.parallel.flat import FlatGroup, set_ready_callback
     d = torch.device("cuda")
     torch.manual_seed(0)
