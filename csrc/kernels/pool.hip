@@ -7,18 +7,22 @@
 
 namespace {
 
+// Index math in 32 bits (the launchers require < 2^31 16-B vectors): 64-bit
+// div/mod by runtime divisors were the bulk of the instruction stream, leaving
+// the stem pool at ~2 TB/s.  One vector per thread, no grid-stride loop.
+template <typename IT>
 __global__ __launch_bounds__(256) void maxpool_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
                                                    uint8_t* __restrict__ idx, int N, int H, int W, int C, int Ho,
                                                    int Wo, int k, int s, int p) {
-  const int cv = C / 8;
-  const long total = (long)N * Ho * Wo * cv;
-  for (long v = (long)blockIdx.x * blockDim.x + threadIdx.x; v < total; v += (long)gridDim.x * blockDim.x) {
+  const IT cv = C / 8;
+  const IT total = (IT)N * Ho * Wo * cv;
+  for (IT v = (IT)blockIdx.x * blockDim.x + threadIdx.x; v < total; v += (IT)gridDim.x * blockDim.x) {
     const int cg = (int)(v % cv);
-    long t = v / cv;
-    const int ow = (int)(t % Wo);
-    t /= Wo;
-    const int oh = (int)(t % Ho);
-    const int n = (int)(t / Ho);
+    IT t = v / cv;
+    const int ow = (int)(t % (IT)Wo);
+    t /= (IT)Wo;
+    const int oh = (int)(t % (IT)Ho);
+    const int n = (int)(t / (IT)Ho);
     float best[8];
     int bi[8];
 #pragma unroll
@@ -48,18 +52,19 @@ __global__ __launch_bounds__(256) void maxpool_fwd(const bf16_t* __restrict__ x,
   }
 }
 
+template <typename IT>
 __global__ __launch_bounds__(256) void maxpool_bwd(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ idx,
                                                    bf16_t* __restrict__ dx, int N, int H, int W, int C, int Ho,
                                                    int Wo, int k, int s, int p) {
-  const int cv = C / 8;
-  const long total = (long)N * H * W * cv;
-  for (long v = (long)blockIdx.x * blockDim.x + threadIdx.x; v < total; v += (long)gridDim.x * blockDim.x) {
+  const IT cv = C / 8;
+  const IT total = (IT)N * H * W * cv;
+  for (IT v = (IT)blockIdx.x * blockDim.x + threadIdx.x; v < total; v += (IT)gridDim.x * blockDim.x) {
     const int cg = (int)(v % cv);
-    long t = v / cv;
-    const int iw = (int)(t % W);
-    t /= W;
-    const int ih = (int)(t % H);
-    const int n = (int)(t / H);
+    IT t = v / cv;
+    const int iw = (int)(t % (IT)W);
+    t /= (IT)W;
+    const int ih = (int)(t % (IT)H);
+    const int n = (int)(t / (IT)H);
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     // windows oh with oh*s - p <= ih <= oh*s - p + k - 1
     const int oh0 = max(0, (ih + p - k + s) / s), oh1 = min(Ho - 1, (ih + p) / s);
@@ -85,9 +90,107 @@ __global__ __launch_bounds__(256) void maxpool_bwd(const bf16_t* __restrict__ dy
   }
 }
 
+// 3x3 / stride 2 (the ResNet stem): every window load issued before any is
+// used — the generic loops' bounds `continue`s serialised the 9 (fwd) / 4 (bwd)
+// loads of a thread, leaving the pool latency-bound at 2-3 TB/s.  Out-of-range
+// taps load a clamped (valid) address and are masked afterwards.
+__global__ __launch_bounds__(256) void maxpool3s2_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                      uint8_t* __restrict__ idx, int N, int H, int W, int C, int Ho,
+                                                      int Wo, int p) {
+  const unsigned cv = C / 8;
+  const unsigned total = (unsigned)N * Ho * Wo * cv;
+  const unsigned v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= total) return;
+  const int cg = (int)(v % cv);
+  unsigned t = v / cv;
+  const int ow = (int)(t % (unsigned)Wo);
+  t /= (unsigned)Wo;
+  const int oh = (int)(t % (unsigned)Ho);
+  const int n = (int)(t / (unsigned)Ho);
+  const bf16_t* xb = x + (long)n * H * W * C + cg * 8;
+  uint4 in[9];
+  bool ok[9];
+#pragma unroll
+  for (int kh = 0; kh < 3; kh++)
+#pragma unroll
+    for (int kw = 0; kw < 3; kw++) {
+      const int ih = oh * 2 - p + kh, iw = ow * 2 - p + kw;
+      ok[kh * 3 + kw] = ih >= 0 && ih < H && iw >= 0 && iw < W;
+      const int ch = min(max(ih, 0), H - 1), cw = min(max(iw, 0), W - 1);
+      in[kh * 3 + kw] = *reinterpret_cast<const uint4*>(xb + ((long)ch * W + cw) * C);
+    }
+  float best[8];
+  int bi[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) { best[j] = -INFINITY; bi[j] = 0; }
+#pragma unroll
+  for (int pos = 0; pos < 9; pos++) {
+    if (!ok[pos]) continue;
+    float f[8];
+    unpack8(in[pos], f);
+#pragma unroll
+    for (int j = 0; j < 8; j++)
+      if (f[j] > best[j] || (f[j] != f[j] && best[j] == best[j])) { best[j] = f[j]; bi[j] = pos; }
+  }
+  const long o = (long)v * 8;  // output NHWC offset == vector index * 8
+  *reinterpret_cast<uint4*>(y + o) = pack8(best);
+  if (idx) {
+    uint2 packed;
+    packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24);
+    packed.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24);
+    *reinterpret_cast<uint2*>(idx + o) = packed;
+  }
+}
+
+__global__ __launch_bounds__(256) void maxpool3s2_bwd(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ idx,
+                                                      bf16_t* __restrict__ dx, int N, int H, int W, int C, int Ho,
+                                                      int Wo, int p) {
+  const unsigned cv = C / 8;
+  const unsigned total = (unsigned)N * H * W * cv;
+  const unsigned v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= total) return;
+  const int cg = (int)(v % cv);
+  unsigned t = v / cv;
+  const int iw = (int)(t % (unsigned)W);
+  t /= (unsigned)W;
+  const int ih = (int)(t % (unsigned)H);
+  const int n = (int)(t / (unsigned)H);
+  // covering windows: oh in {oh1 - 1, oh1} with oh1 = (ih + p) / 2 (k = 3, s = 2)
+  const int oh1 = (ih + p) >> 1, ow1 = (iw + p) >> 1;
+  uint4 g[4];
+  uint2 pk[4];
+  bool ok[4];
+  int pos[4];
+#pragma unroll
+  for (int a = 0; a < 2; a++)
+#pragma unroll
+    for (int b = 0; b < 2; b++) {
+      const int oh = oh1 - a, ow = ow1 - b;
+      const int kh = ih - (oh * 2 - p), kw = iw - (ow * 2 - p);
+      const int w = a * 2 + b;
+      ok[w] = oh >= 0 && oh < Ho && ow >= 0 && ow < Wo && kh < 3 && kw < 3;
+      pos[w] = kh * 3 + kw;
+      const long o = (((long)n * Ho + min(max(oh, 0), Ho - 1)) * Wo + min(max(ow, 0), Wo - 1)) * C + cg * 8;
+      g[w] = *reinterpret_cast<const uint4*>(dy + o);
+      pk[w] = *reinterpret_cast<const uint2*>(idx + o);
+    }
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    if (!ok[w]) continue;
+    float f[8];
+    unpack8(g[w], f);
+    const uint32_t q[2] = {pk[w].x, pk[w].y};
+#pragma unroll
+    for (int j = 0; j < 8; j++)
+      if ((int)((q[j >> 2] >> ((j & 3) * 8)) & 0xff) == pos[w]) acc[j] += f[j];
+  }
+  *reinterpret_cast<uint4*>(dx + (long)v * 8) = pack8(acc);
+}
+
 int grid_for(long work) {
   long b = (work + 255) / 256;
-  return (int)(b < 4096 ? (b < 1 ? 1 : b) : 4096);
+  return (int)(b < (1L << 20) ? (b < 1 ? 1 : b) : (1L << 20));
 }
 
 }  // namespace
@@ -95,15 +198,31 @@ int grid_for(long work) {
 KFA_API int kfa_maxpool_fwd(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H, int W, int C, int Ho, int Wo,
                             int k, int s, int p, hipStream_t st) {
   if (C % 8 || k > 15) return -1;
-  hipLaunchKernelGGL(maxpool_fwd, dim3(grid_for((long)N * Ho * Wo * (C / 8))), dim3(256), 0, st, x, y, idx, N, H, W,
-                     C, Ho, Wo, k, s, p);
+  const long work = (long)N * Ho * Wo * (C / 8);
+  if (k == 3 && s == 2 && p <= 1 && work < (1L << 31) && (long)N * H * W * C < (1L << 40))
+    hipLaunchKernelGGL(maxpool3s2_fwd, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, st, x, y, idx, N, H, W, C,
+                       Ho, Wo, p);
+  else if (work < (1L << 31))
+    hipLaunchKernelGGL(maxpool_fwd<unsigned>, dim3(grid_for(work)), dim3(256), 0, st, x, y, idx, N, H, W, C, Ho, Wo, k,
+                       s, p);
+  else
+    hipLaunchKernelGGL(maxpool_fwd<long>, dim3(grid_for(work)), dim3(256), 0, st, x, y, idx, N, H, W, C, Ho, Wo, k, s,
+                       p);
   return kfa_status();
 }
 
 KFA_API int kfa_maxpool_bwd(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, int H, int W, int C, int Ho,
                             int Wo, int k, int s, int p, hipStream_t st) {
   if (C % 8 || k > 15) return -1;
-  hipLaunchKernelGGL(maxpool_bwd, dim3(grid_for((long)N * H * W * (C / 8))), dim3(256), 0, st, dy, idx, dx, N, H, W,
-                     C, Ho, Wo, k, s, p);
+  const long work = (long)N * H * W * (C / 8);
+  if (k == 3 && s == 2 && p <= 1 && work < (1L << 31))
+    hipLaunchKernelGGL(maxpool3s2_bwd, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, st, dy, idx, dx, N, H, W, C,
+                       Ho, Wo, p);
+  else if (work < (1L << 31))
+    hipLaunchKernelGGL(maxpool_bwd<unsigned>, dim3(grid_for(work)), dim3(256), 0, st, dy, idx, dx, N, H, W, C, Ho, Wo,
+                       k, s, p);
+  else
+    hipLaunchKernelGGL(maxpool_bwd<long>, dim3(grid_for(work)), dim3(256), 0, st, dy, idx, dx, N, H, W, C, Ho, Wo, k,
+                       s, p);
   return kfa_status();
 }

@@ -152,16 +152,18 @@ def test_resnet_tiny_step_runs_native():
     assert losses[-1] < losses[0]
 
 
+@pytest.mark.parametrize("k,s,p", [(3, 2, 1), (3, 2, 0), (2, 2, 0), (3, 1, 1)])
 @pytest.mark.parametrize("N,C,H,W", [(2, 64, 112, 112), (3, 16, 9, 7)])
-def test_maxpool_fwd_bwd(N, C, H, W):
+def test_maxpool_fwd_bwd(N, C, H, W, k, s, p):
+    """3x3/s2 takes the batched-load fast path; other windows the generic kernels."""
     from kubeflow_controller_amd.ops.pool import max_pool2d
     d = _dev()
     torch.manual_seed(4)
     x = torch.randn(N, C, H, W, device=d).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     xr = x.detach().clone().requires_grad_()
-    y = max_pool2d(xr, 3, 2, 1)
+    y = max_pool2d(xr, k, s, p)
     xf = x.float().detach().requires_grad_()
-    yf = torch.nn.functional.max_pool2d(xf, 3, 2, 1)
+    yf = torch.nn.functional.max_pool2d(xf, k, s, p)
     torch.testing.assert_close(y.float(), yf)
     dy = torch.randn_like(y)
     y.backward(dy)
