@@ -249,23 +249,41 @@ __global__ __launch_bounds__(NT) void bn_apply(const bf16_t* __restrict__ x, con
 }
 
 // ------------------------------------------------------------------ backward
-template <bool RELU>
-__device__ __forceinline__ void masked_dy(const uint4 dv, const uint4 yv, float dz[8]) {
+// ReLU mask of the backward.  MASK 0: none; 1: from the forward output y
+// (y > 0); 2: recomputed from the forward input x and the layer's saved
+// scale / shift (relu(fma(x, sc, sh)) > 0 exactly as bn_apply evaluated it), so
+// the bn1 / bn2 backward of a bottleneck never reads y — 2 of its 8 bytes per
+// element (ResNet: 33 BN backward passes per step).
+template <int MASK>
+__device__ __forceinline__ void masked_dy(const uint4 dv, const uint4 yv, const float xf[8], const float sc[8],
+                                          const float sf[8], float dz[8]) {
   unpack8(dv, dz);
-  if (RELU) {
+  if (MASK == 1) {
     float yy[8];
     unpack8(yv, yy);
 #pragma unroll
     for (int j = 0; j < 8; j++) dz[j] = yy[j] > 0.f ? dz[j] : 0.f;
+  } else if (MASK == 2) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) dz[j] = fmaf(xf[j], sc[j], sf[j]) > 0.f ? dz[j] : 0.f;
+  }
+}
+
+template <int MASK>
+__device__ __forceinline__ void load_ss(const float* __restrict__ ss, int C, int c0, float sc[8], float sf[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    sc[j] = MASK == 2 ? ss[c0 + j] : 0.f;
+    sf[j] = MASK == 2 ? ss[C + c0 + j] : 0.f;
   }
 }
 
 // block sums -> slot accumulators [kSlots][2][C]: sum(dz), sum(dz*(x-mean))
-template <bool RELU>
+template <int MASK>
 __global__ __launch_bounds__(NT) void bn_bwd_partial(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
-                                                     const bf16_t* __restrict__ y, const float* __restrict__ mean,
-                                                     float* __restrict__ part, long M, int C, long chunk, int tpr,
-                                                     int rpi) {
+                                                     const bf16_t* __restrict__ y, const float* __restrict__ ss,
+                                                     const float* __restrict__ mean, float* __restrict__ part, long M,
+                                                     int C, long chunk, int tpr, int rpi) {
   __shared__ float sh[2][NT * 8];
   const int t = threadIdx.x;
   const int cg = t % tpr, r0 = t / tpr;
@@ -277,33 +295,34 @@ __global__ __launch_bounds__(NT) void bn_bwd_partial(const bf16_t* __restrict__ 
     const int c0 = (g0 + cg) * 8;
     float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (active && g0 + cg < cv) {
-      float mu[8];
+      float mu[8], sc[8], sf[8];
 #pragma unroll
       for (int j = 0; j < 8; j++) mu[j] = mean[c0 + j];
+      load_ss<MASK>(ss, C, c0, sc, sf);
       long r = rb + r0;
       for (; r + rpi < re; r += 2L * rpi) {
         const long o0 = r * C + c0, o1 = (r + rpi) * C + c0;
         uint4 d0 = ld16(dy + o0), d1 = ld16(dy + o1);
         uint4 x0 = ld16(x + o0), x1 = ld16(x + o1);
         uint4 y0 = make_uint4(0, 0, 0, 0), y1 = y0;
-        if (RELU) { y0 = ld16(y + o0); y1 = ld16(y + o1); }
+        if (MASK == 1) { y0 = ld16(y + o0); y1 = ld16(y + o1); }
         float dz[8], xf[8];
-        masked_dy<RELU>(d0, y0, dz);
         unpack8(x0, xf);
+        masked_dy<MASK>(d0, y0, xf, sc, sf, dz);
 #pragma unroll
         for (int j = 0; j < 8; j++) { s1[j] += dz[j]; s2[j] += dz[j] * (xf[j] - mu[j]); }
-        masked_dy<RELU>(d1, y1, dz);
         unpack8(x1, xf);
+        masked_dy<MASK>(d1, y1, xf, sc, sf, dz);
 #pragma unroll
         for (int j = 0; j < 8; j++) { s1[j] += dz[j]; s2[j] += dz[j] * (xf[j] - mu[j]); }
       }
       for (; r < re; r += rpi) {
         const long o = r * C + c0;
         uint4 yv = make_uint4(0, 0, 0, 0);
-        if (RELU) yv = ld16(y + o);
+        if (MASK == 1) yv = ld16(y + o);
         float dz[8], xf[8];
-        masked_dy<RELU>(ld16(dy + o), yv, dz);
         unpack8(ld16(x + o), xf);
+        masked_dy<MASK>(ld16(dy + o), yv, xf, sc, sf, dz);
 #pragma unroll
         for (int j = 0; j < 8; j++) { s1[j] += dz[j]; s2[j] += dz[j] * (xf[j] - mu[j]); }
       }
@@ -349,11 +368,12 @@ __global__ __launch_bounds__(64 * kGroups) void bn_bwd_finalize(float* __restric
   coef[2 * C + c] = k;
 }
 
-template <bool RELU, bool DRES>
+template <int MASK, bool DRES>
 __global__ __launch_bounds__(NT) void bn_bwd_apply(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
-                                                   const bf16_t* __restrict__ y, const float* __restrict__ coef,
-                                                   bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long M, int C,
-                                                   long chunk, int tpr, int rpi) {
+                                                   const bf16_t* __restrict__ y, const float* __restrict__ ss,
+                                                   const float* __restrict__ coef, bf16_t* __restrict__ dx,
+                                                   bf16_t* __restrict__ dres, long M, int C, long chunk, int tpr,
+                                                   int rpi) {
   const int t = threadIdx.x;
   const int cg = t % tpr, r0 = t / tpr;
   if (r0 >= rpi) return;
@@ -362,18 +382,19 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply(const bf16_t* __restrict__ dy
   const long re = rb + chunk < M ? rb + chunk : M;
   for (int g = cg; g < cv; g += tpr) {
     const int c0 = g * 8;
-    float ca[8], cb[8], ck[8];
+    float ca[8], cb[8], ck[8], sc[8], sf[8];
 #pragma unroll
     for (int j = 0; j < 8; j++) { ca[j] = coef[c0 + j]; cb[j] = coef[C + c0 + j]; ck[j] = coef[2 * C + c0 + j]; }
+    load_ss<MASK>(ss, C, c0, sc, sf);
     for (long r = rb + r0; r < re; r += rpi) {
       const long o = r * C + c0;
       uint4 yv = make_uint4(0, 0, 0, 0);
-      if (RELU) yv = ld16(y + o);
+      if (MASK == 1) yv = ld16(y + o);
       const uint4 dv = ld16(dy + o);
       const uint4 xv = ld16(x + o);
       float dz[8], xf[8], out[8];
-      masked_dy<RELU>(dv, yv, dz);
       unpack8(xv, xf);
+      masked_dy<MASK>(dv, yv, xf, sc, sf, dz);
 #pragma unroll
       for (int j = 0; j < 8; j++) out[j] = fmaf(ca[j], dz[j], fmaf(cb[j], xf[j], ck[j]));
       *reinterpret_cast<uint4*>(dx + o) = pack8(out);
@@ -476,52 +497,67 @@ KFA_API int kfa_bn_fwd_eval(const bf16_t* x, const bf16_t* res, bf16_t* y, const
   return kfa_status();
 }
 
-// y is the forward OUTPUT (ReLU mask source); required when relu != 0.
+template <int MASK>
+static void launch_bwd_apply(const Geom& g, const bf16_t* dy, const bf16_t* x, const bf16_t* y, const float* ss,
+                             const float* coef, bf16_t* dx, bf16_t* dres, long M, int C, hipStream_t s) {
+  if (dres)
+    hipLaunchKernelGGL((bn_bwd_apply<MASK, true>), dim3(g.gx), dim3(NT), 0, s, dy, x, y, ss, coef, dx, dres, M, C,
+                       g.chunk, g.tpr, g.rpi);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply<MASK, false>), dim3(g.gx), dim3(NT), 0, s, dy, x, y, ss, coef, dx, dres, M, C,
+                       g.chunk, g.tpr, g.rpi);
+}
+
+// ReLU mask source when relu != 0: y (the forward OUTPUT) or, with y == nullptr,
+// `ss` = the forward's [scale | shift] (2C floats, no residual in that forward).
+static int mask_mode(int relu, const bf16_t* y, const float* ss) {
+  if (!relu) return 0;
+  if (y) return 1;
+  return ss ? 2 : -1;
+}
+
 // Backward whose partial sums (sum(dz), sum(dz*(x-mean))) were accumulated into
 // `slots` by the dgrad epilogue that produced dy (kfa_conv_igemm with bn_x):
 // finalize + apply only.
 KFA_API int kfa_bn_bwd_prestats(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const float* gamma,
                                 const float* save_mean, const float* save_invstd, bf16_t* dx, bf16_t* dres,
                                 float* dgamma, float* dbeta, float* slots, float* coefws, long M, int C, int relu,
-                                int accumulate, hipStream_t s) {
+                                int accumulate, const float* ss, hipStream_t s) {
   if (!bn_shape_ok(M, C)) return -1;
-  if (relu && !y) return -2;
+  const int mm = mask_mode(relu, y, ss);
+  if (mm < 0) return -2;
   Geom g = geom(M, C, max_row_blocks(C));
   float* coef = coefws;
-  hipLaunchKernelGGL(bn_bwd_finalize, dim3(kfa_ceil_div(C, 64)), dim3(64, kGroups), 0, s, slots, g.gx, M, C, gamma, save_mean,
-                     save_invstd, dgamma, dbeta, coef, accumulate);
-  if (relu && dres)
-    hipLaunchKernelGGL((bn_bwd_apply<true, true>), dim3(g.gx), dim3(NT), 0, s, dy, x, y, coef, dx, dres, M, C, g.chunk, g.tpr, g.rpi);
-  else if (relu)
-    hipLaunchKernelGGL((bn_bwd_apply<true, false>), dim3(g.gx), dim3(NT), 0, s, dy, x, y, coef, dx, dres, M, C, g.chunk, g.tpr, g.rpi);
-  else if (dres)
-    hipLaunchKernelGGL((bn_bwd_apply<false, true>), dim3(g.gx), dim3(NT), 0, s, dy, x, y, coef, dx, dres, M, C, g.chunk, g.tpr, g.rpi);
-  else
-    hipLaunchKernelGGL((bn_bwd_apply<false, false>), dim3(g.gx), dim3(NT), 0, s, dy, x, y, coef, dx, dres, M, C, g.chunk, g.tpr, g.rpi);
+  hipLaunchKernelGGL(bn_bwd_finalize, dim3(kfa_ceil_div(C, 64)), dim3(64, kGroups), 0, s, slots, g.gx, M, C, gamma,
+                     save_mean, save_invstd, dgamma, dbeta, coef, accumulate);
+  if (mm == 2) launch_bwd_apply<2>(g, dy, x, y, ss, coef, dx, dres, M, C, s);
+  else if (mm == 1) launch_bwd_apply<1>(g, dy, x, y, ss, coef, dx, dres, M, C, s);
+  else launch_bwd_apply<0>(g, dy, x, y, ss, coef, dx, dres, M, C, s);
   return kfa_status();
 }
 
 KFA_API int kfa_bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const float* gamma, const float* save_mean,
                        const float* save_invstd, bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta, float* slots,
-                       float* coefws, long M, int C, int relu, int accumulate, hipStream_t s) {
+                       float* coefws, long M, int C, int relu, int accumulate, const float* ss, hipStream_t s) {
   if (!bn_shape_ok(M, C)) return -1;
-  if (relu && !y) return -2;
+  const int mm = mask_mode(relu, y, ss);
+  if (mm < 0) return -2;
   Geom g = geom(M, C, max_row_blocks(C));
   float* part = slots;
   float* coef = coefws;
-  if (relu)
-    hipLaunchKernelGGL(bn_bwd_partial<true>, dim3(g.gx), dim3(NT), 0, s, dy, x, y, save_mean, part, M, C, g.chunk, g.tpr, g.rpi);
+  if (mm == 2)
+    hipLaunchKernelGGL(bn_bwd_partial<2>, dim3(g.gx), dim3(NT), 0, s, dy, x, y, ss, save_mean, part, M, C, g.chunk,
+                       g.tpr, g.rpi);
+  else if (mm == 1)
+    hipLaunchKernelGGL(bn_bwd_partial<1>, dim3(g.gx), dim3(NT), 0, s, dy, x, y, ss, save_mean, part, M, C, g.chunk,
+                       g.tpr, g.rpi);
   else
-    hipLaunchKernelGGL(bn_bwd_partial<false>, dim3(g.gx), dim3(NT), 0, s, dy, x, y, save_mean, part, M, C, g.chunk, g.tpr, g.rpi);
-  hipLaunchKernelGGL(bn_bwd_finalize, dim3(kfa_ceil_div(C, 64)), dim3(64, kGroups), 0, s, part, g.gx, M, C, gamma, save_mean,
-                     save_invstd, dgamma, dbeta, coef, accumulate);
-  if (relu && dres)
-    hipLaunchKernelGGL((bn_bwd_apply<true, true>), dim3(g.gx), dim3(NT), 0, s, dy, x, y, coef, dx, dres, M, C, g.chunk, g.tpr, g.rpi);
-  else if (relu)
-    hipLaunchKernelGGL((bn_bwd_apply<true, false>), dim3(g.gx), dim3(NT), 0, s, dy, x, y, coef, dx, dres, M, C, g.chunk, g.tpr, g.rpi);
-  else if (dres)
-    hipLaunchKernelGGL((bn_bwd_apply<false, true>), dim3(g.gx), dim3(NT), 0, s, dy, x, y, coef, dx, dres, M, C, g.chunk, g.tpr, g.rpi);
-  else
-    hipLaunchKernelGGL((bn_bwd_apply<false, false>), dim3(g.gx), dim3(NT), 0, s, dy, x, y, coef, dx, dres, M, C, g.chunk, g.tpr, g.rpi);
+    hipLaunchKernelGGL(bn_bwd_partial<0>, dim3(g.gx), dim3(NT), 0, s, dy, x, y, ss, save_mean, part, M, C, g.chunk,
+                       g.tpr, g.rpi);
+  hipLaunchKernelGGL(bn_bwd_finalize, dim3(kfa_ceil_div(C, 64)), dim3(64, kGroups), 0, s, part, g.gx, M, C, gamma,
+                     save_mean, save_invstd, dgamma, dbeta, coef, accumulate);
+  if (mm == 2) launch_bwd_apply<2>(g, dy, x, y, ss, coef, dx, dres, M, C, s);
+  else if (mm == 1) launch_bwd_apply<1>(g, dy, x, y, ss, coef, dx, dres, M, C, s);
+  else launch_bwd_apply<0>(g, dy, x, y, ss, coef, dx, dres, M, C, s);
   return kfa_status();
 }

@@ -38,7 +38,8 @@ constexpr int kBnSlots = 64;  // must match batchnorm.hip kSlots (fused statisti
 // that pass.  x == nullptr: forward statistics (sum, sum of squares) instead.
 struct BnBwd {
   const bf16_t* x;
-  const bf16_t* y;
+  const bf16_t* y;   // ReLU mask source (forward output), or nullptr: mask from x with ss
+  const float* ss;   // the BN forward's [scale | shift] (used when relu && !y)
   const float* mean;
   int relu;
 };
@@ -239,11 +240,16 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
     const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
     const int c = lane % CPR;
     const int n = n0 + wn * TN * 16 + c * 8;
-    float mu[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    float mu[8] = {0, 0, 0, 0, 0, 0, 0, 0}, msc[8], msf[8];
     const bool bstat = stats && bnb.x;
+    const bool ymask = bnb.relu && bnb.y;  // else (relu) recompute the mask from x
     if (bstat)
 #pragma unroll
-      for (int j = 0; j < 8; j++) mu[j] = n + j < g.N ? bnb.mean[n + j] : 0.f;
+      for (int j = 0; j < 8; j++) {
+        mu[j] = n + j < g.N ? bnb.mean[n + j] : 0.f;
+        msc[j] = (bnb.relu && !ymask && n + j < g.N) ? bnb.ss[n + j] : 0.f;
+        msf[j] = (bnb.relu && !ymask && n + j < g.N) ? bnb.ss[g.N + n + j] : 0.f;
+      }
     float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // fused BN statistics
     char* stage;
     {
@@ -277,7 +283,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
 #pragma unroll
         for (int it = 0; it < IT; it++) {
           bx[it] = bload16(rBX, offs[it]);
-          if (bnb.relu) by[it] = bload16(rBY, offs[it]);
+          if (ymask) by[it] = bload16(rBY, offs[it]);
         }
 
       if (hh == 0) lds_barrier();  // every wave is done reading `buf`: reuse it as the staging area
@@ -313,11 +319,14 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
           if (bstat) {    // backward statistics of the BN this dgrad feeds
             float xf[8];
             unpack8(bx[it], xf);
-            if (bnb.relu) {
+            if (ymask) {
               float yf[8];
               unpack8(by[it], yf);
 #pragma unroll
               for (int j = 0; j < 8; j++) f[j] = yf[j] > 0.f ? f[j] : 0.f;
+            } else if (bnb.relu) {  // y = relu(fma(x, sc, sh)) exactly as bn_apply evaluated it
+#pragma unroll
+              for (int j = 0; j < 8; j++) f[j] = fmaf(xf[j], msc[j], msf[j]) > 0.f ? f[j] : 0.f;
             }
 #pragma unroll
             for (int j = 0; j < 8; j++) { s1[j] += f[j]; s2[j] += f[j] * (xf[j] - mu[j]); }
@@ -425,8 +434,10 @@ static const bf16_t* zero_page() {
 KFA_API int kfa_conv_igemm(const bf16_t* T, const bf16_t* B, bf16_t* D, const bf16_t* E, int Nb, int H, int W, int C,
                            int P, int Q, int R, int S, int sa, int ra, int oa, int ob, int N, int OH, int OW, int os,
                            int oph, int opw, int ldd, int variant, float* stats, const bf16_t* bn_x,
-                           const bf16_t* bn_y, const float* bn_mean, int bn_relu, hipStream_t st) {
-  const BnBwd bnb{bn_x, bn_y, bn_mean, bn_relu};
+                           const bf16_t* bn_y, const float* bn_mean, int bn_relu, const float* bn_ss,
+                           hipStream_t st) {
+  const BnBwd bnb{bn_x, bn_y, bn_ss, bn_mean, bn_relu};
+  if (bn_x && bn_relu && !bn_y && !bn_ss) return -3;
   if (C % BK != 0 || N % 8 != 0 || ldd % 8 != 0) return -1;
   Geo g{Nb, H, W, C, P, Q, R, S, sa, ra, oa, ob, Nb * P * Q, N, R * S * C, OH, OW, os, oph, opw, ldd, 0, 0, 0};
   if (g.K == 0) g.R = g.S = 1;  // keep index math defined; nk == 0 -> zero/addend-only epilogue
