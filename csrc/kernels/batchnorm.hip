@@ -190,11 +190,27 @@ __global__ void bn_finalize_eval(const float* __restrict__ gamma, const float* _
 }
 
 // ------------------------------------------------------------------ forward apply
-template <bool RELU, bool RES>
+// ReLU bit mask of the output (MB): bit j of byte (row*C + c0)/8 is y[c0+j] > 0
+// (the bf16 value the backward would have read) — for BN+residual+ReLU, whose
+// mask cannot be recomputed from x alone; the backward then reads 1/8 B instead
+// of the 2-B output per element.
+__device__ __forceinline__ unsigned pos_bits(const uint4 v) {
+  const unsigned w[4] = {v.x, v.y, v.z, v.w};
+  unsigned m = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const unsigned lo = w[i] & 0xffffu, hi = w[i] >> 16;
+    m |= (lo != 0u && !(lo & 0x8000u)) ? (1u << (2 * i)) : 0u;
+    m |= (hi != 0u && !(hi & 0x8000u)) ? (1u << (2 * i + 1)) : 0u;
+  }
+  return m;
+}
+
+template <bool RELU, bool RES, bool MB>
 __global__ __launch_bounds__(NT) void bn_apply(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
-                                               bf16_t* __restrict__ y, const float* __restrict__ scale,
-                                               const float* __restrict__ shift, long M, int C, long chunk, int tpr,
-                                               int rpi) {
+                                               bf16_t* __restrict__ y, uint8_t* __restrict__ mb,
+                                               const float* __restrict__ scale, const float* __restrict__ shift,
+                                               long M, int C, long chunk, int tpr, int rpi) {
   const int t = threadIdx.x;
   const int cg = t % tpr, r0 = t / tpr;
   if (r0 >= rpi) return;
@@ -206,46 +222,54 @@ __global__ __launch_bounds__(NT) void bn_apply(const bf16_t* __restrict__ x, con
     float sc[8], sf[8];
 #pragma unroll
     for (int j = 0; j < 8; j++) { sc[j] = scale[c0 + j]; sf[j] = shift[c0 + j]; }
+    auto one = [&](const uint4 v, const uint4 q4, long o) {
+      float f[8], q[8];
+      unpack8(v, f);
+      if (RES) unpack8(q4, q);
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        float z = fmaf(f[j], sc[j], sf[j]);
+        if (RES) z += q[j];
+        f[j] = RELU ? fmaxf(z, 0.f) : z;
+      }
+      const uint4 out = pack8(f);
+      *reinterpret_cast<uint4*>(y + o) = out;
+      if (MB) mb[o >> 3] = (uint8_t)pos_bits(out);
+    };
     long r = rb + r0;
     for (; r + rpi < re; r += 2L * rpi) {
       const long o0 = r * C + c0, o1 = (r + rpi) * C + c0;
-      uint4 v0 = ld16(x + o0), v1 = ld16(x + o1);
-      uint4 q0, q1;
+      const uint4 v0 = ld16(x + o0), v1 = ld16(x + o1);
+      uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;
       if (RES) { q0 = ld16(res + o0); q1 = ld16(res + o1); }
-      float f[8], q[8];
-      unpack8(v0, f);
-      if (RES) unpack8(q0, q);
-#pragma unroll
-      for (int j = 0; j < 8; j++) {
-        float z = fmaf(f[j], sc[j], sf[j]);
-        if (RES) z += q[j];
-        f[j] = RELU ? fmaxf(z, 0.f) : z;
-      }
-      *reinterpret_cast<uint4*>(y + o0) = pack8(f);
-      unpack8(v1, f);
-      if (RES) unpack8(q1, q);
-#pragma unroll
-      for (int j = 0; j < 8; j++) {
-        float z = fmaf(f[j], sc[j], sf[j]);
-        if (RES) z += q[j];
-        f[j] = RELU ? fmaxf(z, 0.f) : z;
-      }
-      *reinterpret_cast<uint4*>(y + o1) = pack8(f);
+      one(v0, q0, o0);
+      one(v1, q1, o1);
     }
     for (; r < re; r += rpi) {
       const long o = r * C + c0;
-      float f[8], q[8];
-      unpack8(ld16(x + o), f);
-      if (RES) unpack8(ld16(res + o), q);
-#pragma unroll
-      for (int j = 0; j < 8; j++) {
-        float z = fmaf(f[j], sc[j], sf[j]);
-        if (RES) z += q[j];
-        f[j] = RELU ? fmaxf(z, 0.f) : z;
-      }
-      *reinterpret_cast<uint4*>(y + o) = pack8(f);
+      one(ld16(x + o), RES ? ld16(res + o) : make_uint4(0, 0, 0, 0), o);
     }
   }
+}
+
+static void launch_apply(int relu, const bf16_t* res, uint8_t* mb, dim3 grid, hipStream_t s, const bf16_t* x,
+                         bf16_t* y, const float* scale, const float* shift, long M, int C, long chunk, int tpr,
+                         int rpi) {
+  if (relu && res && mb)
+    hipLaunchKernelGGL((bn_apply<true, true, true>), grid, dim3(NT), 0, s, x, res, y, mb, scale, shift, M, C, chunk,
+                       tpr, rpi);
+  else if (relu && res)
+    hipLaunchKernelGGL((bn_apply<true, true, false>), grid, dim3(NT), 0, s, x, res, y, mb, scale, shift, M, C, chunk,
+                       tpr, rpi);
+  else if (relu)
+    hipLaunchKernelGGL((bn_apply<true, false, false>), grid, dim3(NT), 0, s, x, res, y, mb, scale, shift, M, C, chunk,
+                       tpr, rpi);
+  else if (res)
+    hipLaunchKernelGGL((bn_apply<false, true, false>), grid, dim3(NT), 0, s, x, res, y, mb, scale, shift, M, C, chunk,
+                       tpr, rpi);
+  else
+    hipLaunchKernelGGL((bn_apply<false, false, false>), grid, dim3(NT), 0, s, x, res, y, mb, scale, shift, M, C,
+                       chunk, tpr, rpi);
 }
 
 // ------------------------------------------------------------------ backward
@@ -254,11 +278,15 @@ __global__ __launch_bounds__(NT) void bn_apply(const bf16_t* __restrict__ x, con
 // scale / shift (relu(fma(x, sc, sh)) > 0 exactly as bn_apply evaluated it), so
 // the bn1 / bn2 backward of a bottleneck never reads y — 2 of its 8 bytes per
 // element (ResNet: 33 BN backward passes per step).
+// MASK 3: from the forward's output bit mask (BN + residual + ReLU, see bn_apply).
 template <int MASK>
 __device__ __forceinline__ void masked_dy(const uint4 dv, const uint4 yv, const float xf[8], const float sc[8],
-                                          const float sf[8], float dz[8]) {
+                                          const float sf[8], unsigned bits, float dz[8]) {
   unpack8(dv, dz);
-  if (MASK == 1) {
+  if (MASK == 3) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) dz[j] = ((bits >> j) & 1u) ? dz[j] : 0.f;
+  } else if (MASK == 1) {
     float yy[8];
     unpack8(yv, yy);
 #pragma unroll
@@ -281,7 +309,8 @@ __device__ __forceinline__ void load_ss(const float* __restrict__ ss, int C, int
 // block sums -> slot accumulators [kSlots][2][C]: sum(dz), sum(dz*(x-mean))
 template <int MASK>
 __global__ __launch_bounds__(NT) void bn_bwd_partial(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
-                                                     const bf16_t* __restrict__ y, const float* __restrict__ ss,
+                                                     const bf16_t* __restrict__ y, const uint8_t* __restrict__ mb,
+                                                     const float* __restrict__ ss,
                                                      const float* __restrict__ mean, float* __restrict__ part, long M,
                                                      int C, long chunk, int tpr, int rpi) {
   __shared__ float sh[2][NT * 8];
@@ -306,13 +335,15 @@ __global__ __launch_bounds__(NT) void bn_bwd_partial(const bf16_t* __restrict__ 
         uint4 x0 = ld16(x + o0), x1 = ld16(x + o1);
         uint4 y0 = make_uint4(0, 0, 0, 0), y1 = y0;
         if (MASK == 1) { y0 = ld16(y + o0); y1 = ld16(y + o1); }
+        unsigned b0 = 0, b1 = 0;
+        if (MASK == 3) { b0 = mb[o0 >> 3]; b1 = mb[o1 >> 3]; }
         float dz[8], xf[8];
         unpack8(x0, xf);
-        masked_dy<MASK>(d0, y0, xf, sc, sf, dz);
+        masked_dy<MASK>(d0, y0, xf, sc, sf, b0, dz);
 #pragma unroll
         for (int j = 0; j < 8; j++) { s1[j] += dz[j]; s2[j] += dz[j] * (xf[j] - mu[j]); }
         unpack8(x1, xf);
-        masked_dy<MASK>(d1, y1, xf, sc, sf, dz);
+        masked_dy<MASK>(d1, y1, xf, sc, sf, b1, dz);
 #pragma unroll
         for (int j = 0; j < 8; j++) { s1[j] += dz[j]; s2[j] += dz[j] * (xf[j] - mu[j]); }
       }
@@ -320,9 +351,10 @@ __global__ __launch_bounds__(NT) void bn_bwd_partial(const bf16_t* __restrict__ 
         const long o = r * C + c0;
         uint4 yv = make_uint4(0, 0, 0, 0);
         if (MASK == 1) yv = ld16(y + o);
+        const unsigned bits = MASK == 3 ? (unsigned)mb[o >> 3] : 0u;
         float dz[8], xf[8];
         unpack8(ld16(x + o), xf);
-        masked_dy<MASK>(ld16(dy + o), yv, xf, sc, sf, dz);
+        masked_dy<MASK>(ld16(dy + o), yv, xf, sc, sf, bits, dz);
 #pragma unroll
         for (int j = 0; j < 8; j++) { s1[j] += dz[j]; s2[j] += dz[j] * (xf[j] - mu[j]); }
       }
@@ -370,7 +402,8 @@ __global__ __launch_bounds__(64 * kGroups) void bn_bwd_finalize(float* __restric
 
 template <int MASK, bool DRES>
 __global__ __launch_bounds__(NT) void bn_bwd_apply(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
-                                                   const bf16_t* __restrict__ y, const float* __restrict__ ss,
+                                                   const bf16_t* __restrict__ y, const uint8_t* __restrict__ mb,
+                                                   const float* __restrict__ ss,
                                                    const float* __restrict__ coef, bf16_t* __restrict__ dx,
                                                    bf16_t* __restrict__ dres, long M, int C, long chunk, int tpr,
                                                    int rpi) {
@@ -390,11 +423,12 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply(const bf16_t* __restrict__ dy
       const long o = r * C + c0;
       uint4 yv = make_uint4(0, 0, 0, 0);
       if (MASK == 1) yv = ld16(y + o);
+      const unsigned bits = MASK == 3 ? (unsigned)mb[o >> 3] : 0u;
       const uint4 dv = ld16(dy + o);
       const uint4 xv = ld16(x + o);
       float dz[8], xf[8], out[8];
       unpack8(xv, xf);
-      masked_dy<MASK>(dv, yv, xf, sc, sf, dz);
+      masked_dy<MASK>(dv, yv, xf, sc, sf, bits, dz);
 #pragma unroll
       for (int j = 0; j < 8; j++) out[j] = fmaf(ca[j], dz[j], fmaf(cb[j], xf[j], ck[j]));
       *reinterpret_cast<uint4*>(dx + o) = pack8(out);
@@ -422,7 +456,8 @@ static bool bn_shape_ok(long M, int C) { return M > 0 && C >= 8 && (C % 8) == 0;
 
 KFA_API int kfa_bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* gamma, const float* beta,
                              float* rmean, float* rvar, float* save_mean, float* save_invstd, float* slots,
-                             float* coefws, long M, int C, float eps, float momentum, int relu, hipStream_t s) {
+                             float* coefws, long M, int C, float eps, float momentum, int relu, uint8_t* mb,
+                             hipStream_t s) {
   if (!bn_shape_ok(M, C)) return -1;
   Geom g = geom(M, C, max_row_blocks(C));
   float* part = slots;
@@ -431,14 +466,7 @@ KFA_API int kfa_bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, cons
   hipLaunchKernelGGL(bn_stats_partial, dim3(g.gx), dim3(NT), 0, s, x, part, M, C, g.chunk, g.tpr, g.rpi);
   hipLaunchKernelGGL(bn_finalize, dim3(kfa_ceil_div(C, 64)), dim3(64, kGroups), 0, s, x, part, g.gx, M, C, gamma, beta, rmean,
                      rvar, save_mean, save_invstd, scale, shift, eps, momentum);
-  if (relu && res)
-    hipLaunchKernelGGL((bn_apply<true, true>), dim3(g.gx), dim3(NT), 0, s, x, res, y, scale, shift, M, C, g.chunk, g.tpr, g.rpi);
-  else if (relu)
-    hipLaunchKernelGGL((bn_apply<true, false>), dim3(g.gx), dim3(NT), 0, s, x, res, y, scale, shift, M, C, g.chunk, g.tpr, g.rpi);
-  else if (res)
-    hipLaunchKernelGGL((bn_apply<false, true>), dim3(g.gx), dim3(NT), 0, s, x, res, y, scale, shift, M, C, g.chunk, g.tpr, g.rpi);
-  else
-    hipLaunchKernelGGL((bn_apply<false, false>), dim3(g.gx), dim3(NT), 0, s, x, res, y, scale, shift, M, C, g.chunk, g.tpr, g.rpi);
+  launch_apply(relu, res, mb, dim3(g.gx), s, x, y, scale, shift, M, C, g.chunk, g.tpr, g.rpi);
   return kfa_status();
 }
 
@@ -459,21 +487,14 @@ KFA_API int kfa_bn_stats_partial(const bf16_t* x, float* slots, long M, int C, h
 KFA_API int kfa_bn_fwd_train_prestats(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* gamma,
                                       const float* beta, float* rmean, float* rvar, float* save_mean,
                                       float* save_invstd, float* slots, float* coefws, long M, int C, float eps,
-                                      float momentum, int relu, hipStream_t s) {
+                                      float momentum, int relu, uint8_t* mb, hipStream_t s) {
   if (!bn_shape_ok(M, C)) return -1;
   Geom g = geom(M, C, max_row_blocks(C));
   float* scale = coefws;
   float* shift = scale + C;
   hipLaunchKernelGGL(bn_finalize, dim3(kfa_ceil_div(C, 64)), dim3(64, kGroups), 0, s, nullptr, slots, g.gx, M, C, gamma, beta,
                      rmean, rvar, save_mean, save_invstd, scale, shift, eps, momentum);
-  if (relu && res)
-    hipLaunchKernelGGL((bn_apply<true, true>), dim3(g.gx), dim3(NT), 0, s, x, res, y, scale, shift, M, C, g.chunk, g.tpr, g.rpi);
-  else if (relu)
-    hipLaunchKernelGGL((bn_apply<true, false>), dim3(g.gx), dim3(NT), 0, s, x, res, y, scale, shift, M, C, g.chunk, g.tpr, g.rpi);
-  else if (res)
-    hipLaunchKernelGGL((bn_apply<false, true>), dim3(g.gx), dim3(NT), 0, s, x, res, y, scale, shift, M, C, g.chunk, g.tpr, g.rpi);
-  else
-    hipLaunchKernelGGL((bn_apply<false, false>), dim3(g.gx), dim3(NT), 0, s, x, res, y, scale, shift, M, C, g.chunk, g.tpr, g.rpi);
+  launch_apply(relu, res, mb, dim3(g.gx), s, x, y, scale, shift, M, C, g.chunk, g.tpr, g.rpi);
   return kfa_status();
 }
 
@@ -486,34 +507,39 @@ KFA_API int kfa_bn_fwd_eval(const bf16_t* x, const bf16_t* res, bf16_t* y, const
   float* shift = ws + C;
   hipLaunchKernelGGL(bn_finalize_eval, dim3(kfa_ceil_div(C, 256)), dim3(256), 0, s, gamma, beta, rmean, rvar, C, eps,
                      scale, shift);
-  if (relu && res)
-    hipLaunchKernelGGL((bn_apply<true, true>), dim3(g.gx), dim3(NT), 0, s, x, res, y, scale, shift, M, C, g.chunk, g.tpr, g.rpi);
-  else if (relu)
-    hipLaunchKernelGGL((bn_apply<true, false>), dim3(g.gx), dim3(NT), 0, s, x, res, y, scale, shift, M, C, g.chunk, g.tpr, g.rpi);
-  else if (res)
-    hipLaunchKernelGGL((bn_apply<false, true>), dim3(g.gx), dim3(NT), 0, s, x, res, y, scale, shift, M, C, g.chunk, g.tpr, g.rpi);
-  else
-    hipLaunchKernelGGL((bn_apply<false, false>), dim3(g.gx), dim3(NT), 0, s, x, res, y, scale, shift, M, C, g.chunk, g.tpr, g.rpi);
+  launch_apply(relu, res, nullptr, dim3(g.gx), s, x, y, scale, shift, M, C, g.chunk, g.tpr, g.rpi);
   return kfa_status();
 }
 
 template <int MASK>
-static void launch_bwd_apply(const Geom& g, const bf16_t* dy, const bf16_t* x, const bf16_t* y, const float* ss,
-                             const float* coef, bf16_t* dx, bf16_t* dres, long M, int C, hipStream_t s) {
+static void launch_bwd_apply(const Geom& g, const bf16_t* dy, const bf16_t* x, const bf16_t* y, const uint8_t* mb,
+                             const float* ss, const float* coef, bf16_t* dx, bf16_t* dres, long M, int C,
+                             hipStream_t s) {
   if (dres)
-    hipLaunchKernelGGL((bn_bwd_apply<MASK, true>), dim3(g.gx), dim3(NT), 0, s, dy, x, y, ss, coef, dx, dres, M, C,
+    hipLaunchKernelGGL((bn_bwd_apply<MASK, true>), dim3(g.gx), dim3(NT), 0, s, dy, x, y, mb, ss, coef, dx, dres, M, C,
                        g.chunk, g.tpr, g.rpi);
   else
-    hipLaunchKernelGGL((bn_bwd_apply<MASK, false>), dim3(g.gx), dim3(NT), 0, s, dy, x, y, ss, coef, dx, dres, M, C,
-                       g.chunk, g.tpr, g.rpi);
+    hipLaunchKernelGGL((bn_bwd_apply<MASK, false>), dim3(g.gx), dim3(NT), 0, s, dy, x, y, mb, ss, coef, dx, dres, M,
+                       C, g.chunk, g.tpr, g.rpi);
 }
 
-// ReLU mask source when relu != 0: y (the forward OUTPUT) or, with y == nullptr,
-// `ss` = the forward's [scale | shift] (2C floats, no residual in that forward).
-static int mask_mode(int relu, const bf16_t* y, const float* ss) {
+// ReLU mask source when relu != 0, first present of: y (the forward OUTPUT), mb
+// (the forward's output bit mask), ss (the forward's [scale | shift], 2C floats,
+// only valid for a forward without residual).
+static int mask_mode(int relu, const bf16_t* y, const uint8_t* mb, const float* ss) {
   if (!relu) return 0;
   if (y) return 1;
+  if (mb) return 3;
   return ss ? 2 : -1;
+}
+
+static void launch_bwd_apply_any(int mm, const Geom& g, const bf16_t* dy, const bf16_t* x, const bf16_t* y,
+                                 const uint8_t* mb, const float* ss, const float* coef, bf16_t* dx, bf16_t* dres,
+                                 long M, int C, hipStream_t s) {
+  if (mm == 3) launch_bwd_apply<3>(g, dy, x, y, mb, ss, coef, dx, dres, M, C, s);
+  else if (mm == 2) launch_bwd_apply<2>(g, dy, x, y, mb, ss, coef, dx, dres, M, C, s);
+  else if (mm == 1) launch_bwd_apply<1>(g, dy, x, y, mb, ss, coef, dx, dres, M, C, s);
+  else launch_bwd_apply<0>(g, dy, x, y, mb, ss, coef, dx, dres, M, C, s);
 }
 
 // Backward whose partial sums (sum(dz), sum(dz*(x-mean))) were accumulated into
@@ -522,42 +548,42 @@ static int mask_mode(int relu, const bf16_t* y, const float* ss) {
 KFA_API int kfa_bn_bwd_prestats(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const float* gamma,
                                 const float* save_mean, const float* save_invstd, bf16_t* dx, bf16_t* dres,
                                 float* dgamma, float* dbeta, float* slots, float* coefws, long M, int C, int relu,
-                                int accumulate, const float* ss, hipStream_t s) {
+                                int accumulate, const float* ss, const uint8_t* mb, hipStream_t s) {
   if (!bn_shape_ok(M, C)) return -1;
-  const int mm = mask_mode(relu, y, ss);
+  const int mm = mask_mode(relu, y, mb, ss);
   if (mm < 0) return -2;
   Geom g = geom(M, C, max_row_blocks(C));
   float* coef = coefws;
   hipLaunchKernelGGL(bn_bwd_finalize, dim3(kfa_ceil_div(C, 64)), dim3(64, kGroups), 0, s, slots, g.gx, M, C, gamma,
                      save_mean, save_invstd, dgamma, dbeta, coef, accumulate);
-  if (mm == 2) launch_bwd_apply<2>(g, dy, x, y, ss, coef, dx, dres, M, C, s);
-  else if (mm == 1) launch_bwd_apply<1>(g, dy, x, y, ss, coef, dx, dres, M, C, s);
-  else launch_bwd_apply<0>(g, dy, x, y, ss, coef, dx, dres, M, C, s);
+  launch_bwd_apply_any(mm, g, dy, x, y, mb, ss, coef, dx, dres, M, C, s);
   return kfa_status();
 }
 
 KFA_API int kfa_bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const float* gamma, const float* save_mean,
                        const float* save_invstd, bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta, float* slots,
-                       float* coefws, long M, int C, int relu, int accumulate, const float* ss, hipStream_t s) {
+                       float* coefws, long M, int C, int relu, int accumulate, const float* ss, const uint8_t* mb,
+                       hipStream_t s) {
   if (!bn_shape_ok(M, C)) return -1;
-  const int mm = mask_mode(relu, y, ss);
+  const int mm = mask_mode(relu, y, mb, ss);
   if (mm < 0) return -2;
   Geom g = geom(M, C, max_row_blocks(C));
   float* part = slots;
   float* coef = coefws;
-  if (mm == 2)
-    hipLaunchKernelGGL(bn_bwd_partial<2>, dim3(g.gx), dim3(NT), 0, s, dy, x, y, ss, save_mean, part, M, C, g.chunk,
-                       g.tpr, g.rpi);
+  if (mm == 3)
+    hipLaunchKernelGGL(bn_bwd_partial<3>, dim3(g.gx), dim3(NT), 0, s, dy, x, y, mb, ss, save_mean, part, M, C,
+                       g.chunk, g.tpr, g.rpi);
+  else if (mm == 2)
+    hipLaunchKernelGGL(bn_bwd_partial<2>, dim3(g.gx), dim3(NT), 0, s, dy, x, y, mb, ss, save_mean, part, M, C,
+                       g.chunk, g.tpr, g.rpi);
   else if (mm == 1)
-    hipLaunchKernelGGL(bn_bwd_partial<1>, dim3(g.gx), dim3(NT), 0, s, dy, x, y, ss, save_mean, part, M, C, g.chunk,
-                       g.tpr, g.rpi);
+    hipLaunchKernelGGL(bn_bwd_partial<1>, dim3(g.gx), dim3(NT), 0, s, dy, x, y, mb, ss, save_mean, part, M, C,
+                       g.chunk, g.tpr, g.rpi);
   else
-    hipLaunchKernelGGL(bn_bwd_partial<0>, dim3(g.gx), dim3(NT), 0, s, dy, x, y, ss, save_mean, part, M, C, g.chunk,
-                       g.tpr, g.rpi);
+    hipLaunchKernelGGL(bn_bwd_partial<0>, dim3(g.gx), dim3(NT), 0, s, dy, x, y, mb, ss, save_mean, part, M, C,
+                       g.chunk, g.tpr, g.rpi);
   hipLaunchKernelGGL(bn_bwd_finalize, dim3(kfa_ceil_div(C, 64)), dim3(64, kGroups), 0, s, part, g.gx, M, C, gamma,
                      save_mean, save_invstd, dgamma, dbeta, coef, accumulate);
-  if (mm == 2) launch_bwd_apply<2>(g, dy, x, y, ss, coef, dx, dres, M, C, s);
-  else if (mm == 1) launch_bwd_apply<1>(g, dy, x, y, ss, coef, dx, dres, M, C, s);
-  else launch_bwd_apply<0>(g, dy, x, y, ss, coef, dx, dres, M, C, s);
+  launch_bwd_apply_any(mm, g, dy, x, y, mb, ss, coef, dx, dres, M, C, s);
   return kfa_status();
 }

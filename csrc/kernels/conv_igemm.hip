@@ -39,7 +39,8 @@ constexpr int kBnSlots = 64;  // must match batchnorm.hip kSlots (fused statisti
 struct BnBwd {
   const bf16_t* x;
   const bf16_t* y;   // ReLU mask source (forward output), or nullptr: mask from x with ss
-  const float* ss;   // the BN forward's [scale | shift] (used when relu && !y)
+  const float* ss;   // the BN forward's [scale | shift] (used when relu && !y && !mb)
+  const uint8_t* mb; // the BN forward's output ReLU bit mask (BN + residual; used when relu && !y)
   const float* mean;
   int relu;
 };
@@ -242,13 +243,15 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
     const int n = n0 + wn * TN * 16 + c * 8;
     float mu[8] = {0, 0, 0, 0, 0, 0, 0, 0}, msc[8], msf[8];
     const bool bstat = stats && bnb.x;
-    const bool ymask = bnb.relu && bnb.y;  // else (relu) recompute the mask from x
+    const bool ymask = bnb.relu && bnb.y;              // mask from the output y
+    const bool bmask = bnb.relu && !bnb.y && bnb.mb;   // from the output bit mask
+    // else (relu) recomputed from x with the saved scale / shift
     if (bstat)
 #pragma unroll
       for (int j = 0; j < 8; j++) {
         mu[j] = n + j < g.N ? bnb.mean[n + j] : 0.f;
-        msc[j] = (bnb.relu && !ymask && n + j < g.N) ? bnb.ss[n + j] : 0.f;
-        msf[j] = (bnb.relu && !ymask && n + j < g.N) ? bnb.ss[g.N + n + j] : 0.f;
+        msc[j] = (bnb.relu && !ymask && !bmask && n + j < g.N) ? bnb.ss[n + j] : 0.f;
+        msf[j] = (bnb.relu && !ymask && !bmask && n + j < g.N) ? bnb.ss[g.N + n + j] : 0.f;
       }
     float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // fused BN statistics
     char* stage;
@@ -276,6 +279,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
         offs[it] = (m >= g.M || n >= g.N) ? kOOB : orow + (unsigned)n * 2u;
       }
       uint4 ev[IT], bx[IT], by[IT];
+      unsigned mbits[IT];
       if (E)
 #pragma unroll
         for (int it = 0; it < IT; it++) ev[it] = bload16(rE, offs[it]);
@@ -284,6 +288,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
         for (int it = 0; it < IT; it++) {
           bx[it] = bload16(rBX, offs[it]);
           if (ymask) by[it] = bload16(rBY, offs[it]);
+          if (bmask) mbits[it] = offs[it] != kOOB ? (unsigned)bnb.mb[offs[it] >> 4] : 0u;  // 8 bf16 = 16 B per bit byte
         }
 
       if (hh == 0) lds_barrier();  // every wave is done reading `buf`: reuse it as the staging area
@@ -324,6 +329,9 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
               unpack8(by[it], yf);
 #pragma unroll
               for (int j = 0; j < 8; j++) f[j] = yf[j] > 0.f ? f[j] : 0.f;
+            } else if (bmask) {
+#pragma unroll
+              for (int j = 0; j < 8; j++) f[j] = ((mbits[it] >> j) & 1u) ? f[j] : 0.f;
             } else if (bnb.relu) {  // y = relu(fma(x, sc, sh)) exactly as bn_apply evaluated it
 #pragma unroll
               for (int j = 0; j < 8; j++) f[j] = fmaf(xf[j], msc[j], msf[j]) > 0.f ? f[j] : 0.f;
@@ -435,9 +443,10 @@ KFA_API int kfa_conv_igemm(const bf16_t* T, const bf16_t* B, bf16_t* D, const bf
                            int P, int Q, int R, int S, int sa, int ra, int oa, int ob, int N, int OH, int OW, int os,
                            int oph, int opw, int ldd, int variant, float* stats, const bf16_t* bn_x,
                            const bf16_t* bn_y, const float* bn_mean, int bn_relu, const float* bn_ss,
-                           hipStream_t st) {
-  const BnBwd bnb{bn_x, bn_y, bn_ss, bn_mean, bn_relu};
-  if (bn_x && bn_relu && !bn_y && !bn_ss) return -3;
+                           const uint8_t* bn_mb, hipStream_t st) {
+  const BnBwd bnb{bn_x, bn_y, bn_ss, bn_mb, bn_mean, bn_relu};
+  if (bn_x && bn_relu && !bn_y && !bn_ss && !bn_mb) return -3;
+  if (bn_mb && ldd != N) return -4;  // the bit mask indexes [M][N] rows
   if (C % BK != 0 || N % 8 != 0 || ldd % 8 != 0) return -1;
   Geo g{Nb, H, W, C, P, Q, R, S, sa, ra, oa, ob, Nb * P * Q, N, R * S * C, OH, OW, os, oph, opw, ldd, 0, 0, 0};
   if (g.K == 0) g.R = g.S = 1;  // keep index math defined; nk == 0 -> zero/addend-only epilogue

@@ -30,9 +30,9 @@ F = ctypes.c_float
 _SIGS = {
     "kfa_bn_slot_floats": [I],
     "kfa_bn_coef_floats": [I],
-    "kfa_bn_fwd_train": [P, P, P, P, P, P, P, P, P, P, P, L, I, F, F, I, P],
+    "kfa_bn_fwd_train": [P, P, P, P, P, P, P, P, P, P, P, L, I, F, F, I, P, P],
     "kfa_bn_fwd_eval": [P, P, P, P, P, P, P, P, L, I, F, I, P],
-    "kfa_bn_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, L, I, I, I, P, P],
+    "kfa_bn_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, L, I, I, I, P, P, P],
 }
 _RESTYPE = {"kfa_bn_slot_floats": L, "kfa_bn_coef_floats": L}
 

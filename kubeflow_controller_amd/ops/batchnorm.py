@@ -7,10 +7,10 @@ with 3 streaming passes forward and 3 backward.
 
 Layout contract: ``x`` is a 4-D bf16 tensor in channels_last memory format (or
 any tensor whose memory is ``[M, C]`` row-major with C innermost); params are
-fp32.  The ReLU mask in backward is read from the saved OUTPUT when the
-forward added a residual; without one it is recomputed from the input and the
-layer's saved [scale | shift] (2C floats), so the backward never reads the
-output (env ``KFA_BN_MASK_FROM_X=0`` reads it instead).  No mask tensor is stored.
+fp32.  Without a residual the backward's ReLU mask is recomputed from the
+input and the layer's saved [scale | shift] (2C floats); with one, the forward
+also writes the mask as bits (1/16 of the output's bytes).  Either way the backward
+never reads the output (env ``KFA_BN_MASK_FROM_X=0`` reads it instead).
 """
 from __future__ import annotations
 
@@ -41,7 +41,7 @@ def _mc(t: torch.Tensor):
     return t.numel() // C, C
 
 
-_lib.register("kfa_bn_fwd_train_prestats", [_lib.P] * 11 + [_lib.L, _lib.I, _lib.F, _lib.F, _lib.I, _lib.P])
+_lib.register("kfa_bn_fwd_train_prestats", [_lib.P] * 11 + [_lib.L, _lib.I, _lib.F, _lib.F, _lib.I, _lib.P, _lib.P])
 _lib.register("kfa_bn_bwd_prestats", [_lib.P] * 12 + [_lib.L, _lib.I, _lib.I, _lib.I, _lib.P, _lib.P])
 
 
@@ -55,10 +55,10 @@ class BnBwdLink:
     epilogue through a ``GradJoin``).  ``convs`` counts the convolutions that
     took the output as input; with more than one, none of them uses the link."""
 
-    __slots__ = ("x", "y", "ss", "mean", "relu", "prestats", "convs")
+    __slots__ = ("x", "y", "ss", "mb", "mean", "relu", "prestats", "convs")
 
     def __init__(self):
-        self.x = self.y = self.ss = self.mean = None
+        self.x = self.y = self.ss = self.mb = self.mean = None
         self.relu = False
         self.prestats = False
         self.convs = 0
@@ -91,7 +91,7 @@ class _BNActFn(torch.autograd.Function):
         y = torch.empty_like(x)
         slots, coef = _workspaces(C, x.device)
         s = _lib.stream()
-        ss = None
+        ss = mb = None
         if training:
             mean = torch.empty(C, dtype=torch.float32, device=x.device)
             invstd = torch.empty_like(mean)
@@ -99,21 +99,26 @@ class _BNActFn(torch.autograd.Function):
                 # keep this layer's [scale | shift]: the backward recomputes the ReLU
                 # mask from x instead of reading y (2 of its 8 bytes per element)
                 ss = torch.empty(2 * C, dtype=torch.float32, device=x.device)
+            elif relu and MASK_FROM_X:
+                # with a residual the mask needs the output: keep it as bits (1/16 of y)
+                mb = torch.empty(M * C // 8, dtype=torch.uint8, device=x.device)
             _lib.call("kfa_bn_fwd_train_prestats" if prestats else "kfa_bn_fwd_train", _lib.ptr(x), _lib.ptr(res),
                       _lib.ptr(y), _lib.ptr(weight), _lib.ptr(bias),
                       _lib.ptr(running_mean), _lib.ptr(running_var), _lib.ptr(mean), _lib.ptr(invstd),
-                      _lib.ptr(slots), _lib.ptr(coef if ss is None else ss), M, C, eps, momentum, int(relu), s)
+                      _lib.ptr(slots), _lib.ptr(coef if ss is None else ss), M, C, eps, momentum, int(relu),
+                      _lib.ptr(mb), s)
         else:
             _lib.call("kfa_bn_fwd_eval", _lib.ptr(x), _lib.ptr(res), _lib.ptr(y), _lib.ptr(weight), _lib.ptr(bias),
                       _lib.ptr(running_mean), _lib.ptr(running_var), _lib.ptr(coef), M, C, eps, int(relu), s)
             var = running_var
             mean = running_mean.clone()
             invstd = torch.rsqrt(var + eps)
-        ymask = y if (relu and ss is None) else None
-        ctx.save_for_backward(x, ymask, ss, weight, mean, invstd)
+        ymask = y if (relu and ss is None and mb is None) else None
+        ctx.save_for_backward(x, ymask, ss, mb, weight, mean, invstd)
         ctx.link = link if training else None
         if ctx.link is not None:
-            link.x, link.y, link.ss, link.mean, link.relu, link.prestats = x, ymask, ss, mean, bool(relu), False
+            link.x, link.y, link.ss, link.mb, link.mean = x, ymask, ss, mb, mean
+            link.relu, link.prestats = bool(relu), False
         ctx.relu = relu
         ctx.has_res = residual is not None
         ctx.params = (weight, bias)
@@ -121,7 +126,7 @@ class _BNActFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, ss, weight, mean, invstd = ctx.saved_tensors
+        x, y, ss, mb, weight, mean, invstd = ctx.saved_tensors
         dy = _as_rows(dy)
         M, C = _mc(x)
         dx = torch.empty_like(x)
@@ -142,11 +147,11 @@ class _BNActFn(torch.autograd.Function):
         pre = lk is not None and lk.prestats
         if lk is not None:
             lk.prestats = False
-            lk.x = lk.y = lk.ss = lk.mean = None
+            lk.x = lk.y = lk.ss = lk.mb = lk.mean = None
         _lib.call("kfa_bn_bwd_prestats" if pre else "kfa_bn_bwd", _lib.ptr(dy), _lib.ptr(x), _lib.ptr(y), _lib.ptr(weight), _lib.ptr(mean),
                   _lib.ptr(invstd), _lib.ptr(dx), _lib.ptr(dres), _lib.ptr(dgamma), _lib.ptr(dbeta), _lib.ptr(slots),
                   _lib.ptr(coef),
-                  M, C, int(ctx.relu), int(direct), _lib.ptr(ss), _lib.stream())
+                  M, C, int(ctx.relu), int(direct), _lib.ptr(ss), _lib.ptr(mb), _lib.stream())
         if direct:
             notify_grad_ready(ctx.params[0])
             notify_grad_ready(ctx.params[1])

@@ -32,7 +32,7 @@ from . import _lib
 from ..parallel.flat import direct_grad_view, notify_grad_ready
 
 P, I = _lib.P, _lib.I
-_lib.register("kfa_conv_igemm", [P, P, P, P] + [I] * 20 + [P, P, P, P, I, P, P])
+_lib.register("kfa_conv_igemm", [P, P, P, P] + [I] * 20 + [P, P, P, P, I, P, P, P])
 _lib.register("kfa_zero_bf16", [P, _lib.L, P])
 _lib.register("kfa_weight_transpose", [P, P] + [I] * 10 + [P])
 _lib.register("kfa_wgrad_part_floats", [I] * 7, _lib.L)
@@ -134,7 +134,7 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, stats=None
     y = torch.empty((Nb, Co, Po, Qo), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
     _lib.call("kfa_conv_igemm", _lib.ptr(x), _lib.ptr(w), _lib.ptr(y), None, Nb, H, W, C, Po, Qo, R, S, stride, 1,
               -pad, -pad, Co, Po, Qo, 1, 0, 0, Co, _variant(Nb * Po * Qo, Co, R * S * C), _lib.ptr(stats), None, None,
-              None, 0, None, _lib.stream())
+              None, 0, None, None, _lib.stream())
     return y
 
 
@@ -158,11 +158,11 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride: int, pad: int
     dx = torch.empty((Nb, Ci, H, W), dtype=dy.dtype, device=dy.device, memory_format=torch.channels_last)
     E = None if addend is None else _cl(addend)
     st = _lib.stream()
-    bn_args = (None, None, None, None, 0, None)
+    bn_args = (None, None, None, None, 0, None, None)
     if bn is not None:
         from .batchnorm import bn_slot_workspace
         bn_args = (_lib.ptr(bn_slot_workspace(Ci, dy.device)), _lib.ptr(bn.x), _lib.ptr(bn.y), _lib.ptr(bn.mean),
-                   int(bn.relu), _lib.ptr(bn.ss))
+                   int(bn.relu), _lib.ptr(bn.ss), _lib.ptr(bn.mb))
         bn.prestats = True
     if stride == 1:
         wt = _transposed_weight(w, 0, 1, R, 0, 1, S)

@@ -55,24 +55,28 @@ def test_bn_act_fwd_bwd(N, C, H, W, relu, res):
         assert (rr.grad.float() - rf.grad).abs().max().item() < 0.02 * max(1.0, rf.grad.abs().max().item())
 
 
+@pytest.mark.parametrize("res", [False, True])
 @pytest.mark.parametrize("N,C,H,W", [(4, 64, 14, 14), (3, 2048, 2, 3), (8, 24, 5, 5)])
-def test_bn_relu_mask_from_input_matches_output_mask(N, C, H, W, monkeypatch):
-    """BN+ReLU without residual recomputes the backward ReLU mask from x and the
-    saved scale/shift; it must reproduce the output-mask backward bit for bit."""
+def test_bn_relu_mask_from_input_matches_output_mask(N, C, H, W, res, monkeypatch):
+    """BN+ReLU recomputes the backward ReLU mask from x and the saved scale/shift
+    (no residual) or reads the forward's bit mask (residual); both must reproduce
+    the output-mask backward bit for bit."""
     from kubeflow_controller_amd.ops import batchnorm as bnmod
     torch.manual_seed(1)
     d = _dev()
     x = (torch.randn(N, C, H, W, device=d) * 2).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     dy = torch.randn_like(x)
+    r = torch.randn_like(x) if res else None
     outs = []
     for from_x in (True, False):
         monkeypatch.setattr(bnmod, "MASK_FROM_X", from_x)
         g = (torch.rand(C, device=d, generator=torch.Generator(d).manual_seed(2)) + 0.5).requires_grad_()
         b = torch.randn(C, device=d, generator=torch.Generator(d).manual_seed(3)).requires_grad_()
         xr = x.detach().clone().requires_grad_()
-        y = bnmod.bn_act(xr, g, b, torch.zeros(C, device=d), torch.ones(C, device=d), None, True, 0.1, 1e-5, True)
+        rr = r.detach().clone().requires_grad_() if res else None
+        y = bnmod.bn_act(xr, g, b, torch.zeros(C, device=d), torch.ones(C, device=d), rr, True, 0.1, 1e-5, True)
         y.backward(dy)
-        outs.append((y, xr.grad, g.grad, b.grad))
+        outs.append((y, xr.grad, g.grad, b.grad) + ((rr.grad,) if res else ()))
     for a, b_ in zip(*outs):
         assert torch.equal(a, b_)
 
