@@ -2,6 +2,8 @@
 // SURVEY §2.6 K7 (ResNet-50 conv2d fwd + dgrad) and K1 (plain GEMM = 1x1 conv).
 //
 // One kernel computes  D[m][n] = sum_k A[m][k] * B[n][k]  (+ E[m][n])  where
+// (with bnb.emb: + E[m][n] * bit(emb, m*N + n), the residual gradient of a
+// BN + residual + ReLU output formed from its raw gradient and ReLU bit mask)
 //   A = implicit im2col of an NHWC tensor T[Nb][H][W][C]:
 //         m = (nb, p, q) in [Nb][P][Q],  k = (r, s, c) in [R][S][C]
 //         A[m][k] = T[nb][p*sa + r*ra + oa][q*sa + s*ra + ob][c]   (0 outside)
@@ -43,6 +45,7 @@ struct BnBwd {
   const uint8_t* mb; // the BN forward's output ReLU bit mask (BN + residual; used when relu && !y)
   const float* mean;
   int relu;
+  const uint8_t* emb;  // addend E masked by these ReLU bits (E = a block output's raw gradient), or nullptr
 };
 
 struct Geo {
@@ -279,10 +282,13 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
         offs[it] = (m >= g.M || n >= g.N) ? kOOB : orow + (unsigned)n * 2u;
       }
       uint4 ev[IT], bx[IT], by[IT];
-      unsigned mbits[IT];
+      unsigned mbits[IT], ebits[IT];
       if (E)
 #pragma unroll
-        for (int it = 0; it < IT; it++) ev[it] = bload16(rE, offs[it]);
+        for (int it = 0; it < IT; it++) {
+          ev[it] = bload16(rE, offs[it]);
+          if (bnb.emb) ebits[it] = offs[it] != kOOB ? (unsigned)bnb.emb[offs[it] >> 4] : 0u;
+        }
       if (bstat)
 #pragma unroll
         for (int it = 0; it < IT; it++) {
@@ -313,8 +319,13 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
           float f[8], h[8];
           unpack8(v, f);
           unpack8(ev[it], h);
+          if (bnb.emb) {  // residual gradient dz = dy * relu-mask, formed here instead of by the BN backward
 #pragma unroll
-          for (int j = 0; j < 8; j++) f[j] += h[j];
+            for (int j = 0; j < 8; j++) f[j] += ((ebits[it] >> j) & 1u) ? h[j] : 0.f;
+          } else {
+#pragma unroll
+            for (int j = 0; j < 8; j++) f[j] += h[j];
+          }
           o = pack8(f);
         }
         __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<decltype(__builtin_amdgcn_raw_buffer_load_b128(rD, 0, 0, 0))*>(&o), rD, off, 0, 0);
@@ -443,10 +454,10 @@ KFA_API int kfa_conv_igemm(const bf16_t* T, const bf16_t* B, bf16_t* D, const bf
                            int P, int Q, int R, int S, int sa, int ra, int oa, int ob, int N, int OH, int OW, int os,
                            int oph, int opw, int ldd, int variant, float* stats, const bf16_t* bn_x,
                            const bf16_t* bn_y, const float* bn_mean, int bn_relu, const float* bn_ss,
-                           const uint8_t* bn_mb, hipStream_t st) {
-  const BnBwd bnb{bn_x, bn_y, bn_ss, bn_mb, bn_mean, bn_relu};
+                           const uint8_t* bn_mb, const uint8_t* add_mb, hipStream_t st) {
+  const BnBwd bnb{bn_x, bn_y, bn_ss, bn_mb, bn_mean, bn_relu, E ? add_mb : nullptr};
   if (bn_x && bn_relu && !bn_y && !bn_ss && !bn_mb) return -3;
-  if (bn_mb && ldd != N) return -4;  // the bit mask indexes [M][N] rows
+  if ((bn_mb || (E && add_mb)) && ldd != N) return -4;  // the bit masks index [M][N] rows
   if (C % BK != 0 || N % 8 != 0 || ldd % 8 != 0) return -1;
   Geo g{Nb, H, W, C, P, Q, R, S, sa, ra, oa, ob, Nb * P * Q, N, R * S * C, OH, OW, os, oph, opw, ldd, 0, 0, 0};
   if (g.K == 0) g.R = g.S = 1;  // keep index math defined; nk == 0 -> zero/addend-only epilogue

@@ -46,14 +46,16 @@ class Bottleneck(nn.Module):
         # bn3's output (the block output) feeds the next block's conv1 (or
         # downsample conv) AND its residual: that conv's dgrad epilogue adds the
         # residual gradient (GradJoin), so it sees the FULL gradient and takes
-        # bn3's backward statistics too.  (The last block feeds the pooling head:
+        # bn3's backward statistics too.  In identity blocks bn3's backward does
+        # not even write the residual gradient: it hands conv1's dgrad epilogue
+        # its raw output gradient + ReLU bits (GradJoin.deposit_masked).  (The last block feeds the pooling head:
         # no conv takes the link, and its BN runs its own statistics pass.)
         join = GradJoin()
         st = self.training
         if self.downsample is None:
             y = self.bn1(self.conv1(x, join=join, bn_stats=st), bwd_link=st)
             y = self.bn2(self.conv2(y, bn_stats=st), bwd_link=st)
-            return self.bn3(self.conv3(y, bn_stats=st), residual=join.branch(x), bwd_link=st)
+            return self.bn3(self.conv3(y, bn_stats=st), residual=join.branch(x), bwd_link=st, res_join=join)
         idn = self.downsample["bn"](self.downsample["conv"](x, join=join, bn_stats=st))
         y = self.bn1(self.conv1(join.branch(x), bn_stats=st), bwd_link=st)
         y = self.bn2(self.conv2(y, bn_stats=st), bwd_link=st)

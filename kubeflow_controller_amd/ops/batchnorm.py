@@ -80,7 +80,7 @@ def _workspaces(C: int, device):
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, residual, training, momentum, eps, relu,
-                prestats=False, link=None):
+                prestats=False, link=None, res_join=None):
         x = _as_rows(x)
         M, C = _mc(x)
         if x.dtype != torch.bfloat16:
@@ -121,6 +121,9 @@ class _BNActFn(torch.autograd.Function):
             link.relu, link.prestats = bool(relu), False
         ctx.relu = relu
         ctx.has_res = residual is not None
+        # residual = a GradJoin branch whose consumer conv can apply the ReLU bits
+        # itself: the backward then skips writing dres (2 of its ~8 bytes per element)
+        ctx.res_join = res_join if (training and mb is not None and residual is not None) else None
         ctx.params = (weight, bias)
         return y
 
@@ -130,7 +133,8 @@ class _BNActFn(torch.autograd.Function):
         dy = _as_rows(dy)
         M, C = _mc(x)
         dx = torch.empty_like(x)
-        dres = torch.empty_like(x) if ctx.has_res else None
+        deposited = ctx.res_join is not None and ctx.res_join.deposit_masked(dy, mb)
+        dres = torch.empty_like(x) if (ctx.has_res and not deposited) else None
         need_w = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
         direct = False
         dgamma = dbeta = None
@@ -155,24 +159,26 @@ class _BNActFn(torch.autograd.Function):
         if direct:
             notify_grad_ready(ctx.params[0])
             notify_grad_ready(ctx.params[1])
-            return dx, None, None, None, None, dres, None, None, None, None, None, None
+            return dx, None, None, None, None, dres, None, None, None, None, None, None, None
         if dgamma is not None and weight is not None and weight.dtype != torch.float32:
             dgamma, dbeta = dgamma.to(weight.dtype), dbeta.to(weight.dtype)
-        return dx, dgamma, dbeta, None, None, dres, None, None, None, None, None, None
+        return dx, dgamma, dbeta, None, None, dres, None, None, None, None, None, None, None
 
 
 def bn_act(x, weight, bias, running_mean, running_var, residual=None, training=True, momentum=0.1, eps=1e-5,
-           relu=True, prestats=False, bwd_link=False):
+           relu=True, prestats=False, bwd_link=False, res_join=None):
     """``prestats``: the statistics of ``x`` already sit in the BN slot workspace
     (accumulated by the producing convolution's epilogue).  ``bwd_link``: the
     output feeds exactly one igemm convolution, whose dgrad epilogue may compute
-    this BN's backward statistics (``BnBwdLink``)."""
+    this BN's backward statistics (``BnBwdLink``).  ``res_join``: the ``ops.conv.GradJoin``
+    whose branch ``residual`` is; the backward then deposits the raw output
+    gradient and the ReLU bits there instead of writing the residual gradient."""
     if prestats and not training:  # never leave the self-cleaning slots dirty
         bn_slot_workspace(x.shape[1], x.device).zero_()
         prestats = False
     link = BnBwdLink() if (bwd_link and training) else None
     y = _BNActFn.apply(x, weight, bias, running_mean, running_var, residual, training, momentum, eps, relu,
-                       prestats, link)
+                       prestats, link, res_join)
     if link is not None:
         y._kfa_bn_link = link
     return y
@@ -205,11 +211,11 @@ class BatchNorm2dAct(nn.Module):
         self.register_buffer("running_mean", torch.zeros(num_features))
         self.register_buffer("running_var", torch.ones(num_features))
 
-    def forward(self, x, residual=None, bwd_link: bool = False):
+    def forward(self, x, residual=None, bwd_link: bool = False, res_join=None):
         if x.is_cuda:
             return bn_act(x, self.weight, self.bias, self.running_mean, self.running_var, residual,
                           self.training, self.momentum, self.eps, self.relu, getattr(x, "_kfa_prestats", False),
-                          bwd_link)
+                          bwd_link, res_join)
         # CPU path (plumbing tests / CPU-only MNIST-style jobs): plain PyTorch.
         y = torch.nn.functional.batch_norm(x, self.running_mean, self.running_var, self.weight.to(x.dtype),
                                            self.bias.to(x.dtype), self.training, self.momentum, self.eps)

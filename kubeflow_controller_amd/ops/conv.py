@@ -32,7 +32,7 @@ from . import _lib
 from ..parallel.flat import direct_grad_view, notify_grad_ready
 
 P, I = _lib.P, _lib.I
-_lib.register("kfa_conv_igemm", [P, P, P, P] + [I] * 20 + [P, P, P, P, I, P, P, P])
+_lib.register("kfa_conv_igemm", [P, P, P, P] + [I] * 20 + [P, P, P, P, I, P, P, P, P])
 _lib.register("kfa_zero_bf16", [P, _lib.L, P])
 _lib.register("kfa_weight_transpose", [P, P] + [I] * 10 + [P])
 _lib.register("kfa_wgrad_part_floats", [I] * 7, _lib.L)
@@ -64,6 +64,9 @@ BIG_MIN_K = int(os.environ.get("KFA_CONV_BIG_MINK", "256"))
 # implicit GEMM.  tools/bench_conv.py shows where MIOpen's forward wins: the
 # compute-heavy 3x3 / K >= 1024 layers of the late stages (e.g. 256->256 3x3 at
 # 14x14: 0.075 vs 0.110 ms), never the memory-bound expand 1x1s.
+# Residual gradient of identity blocks formed in conv1's dgrad epilogue from the raw
+# gradient + ReLU bits (GradJoin.deposit_masked); KFA_MASKED_RESIDUAL=0 writes it instead.
+MASKED_RESIDUAL = os.environ.get("KFA_MASKED_RESIDUAL", "1") != "0"
 TUNE = os.environ.get("KFA_CONV_TUNE", "1") != "0"
 TUNE_LOG = os.environ.get("KFA_CONV_TUNE_LOG", "0") == "1"
 _fwd_plan: dict = {}  # shape key -> True: vendor forward + BN stats pass
@@ -134,7 +137,7 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, stats=None
     y = torch.empty((Nb, Co, Po, Qo), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
     _lib.call("kfa_conv_igemm", _lib.ptr(x), _lib.ptr(w), _lib.ptr(y), None, Nb, H, W, C, Po, Qo, R, S, stride, 1,
               -pad, -pad, Co, Po, Qo, 1, 0, 0, Co, _variant(Nb * Po * Qo, Co, R * S * C), _lib.ptr(stats), None, None,
-              None, 0, None, None, _lib.stream())
+              None, 0, None, None, None, _lib.stream())
     return y
 
 
@@ -148,15 +151,20 @@ def _transposed_weight(w: torch.Tensor, r0: int, dr: int, Rs: int, s0: int, ds: 
 
 
 def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride: int, pad: int, addend=None,
-               bn=None) -> torch.Tensor:
+               bn=None, addend_mask=None) -> torch.Tensor:
     """``bn``: a ``batchnorm.BnBwdLink`` of the BatchNorm whose output is this conv's
-    input — the epilogue then also accumulates that BN's backward statistics."""
+    input — the epilogue then also accumulates that BN's backward statistics.
+    ``addend_mask``: uint8 ReLU bits (one per element of ``addend``, channels-last
+    order, LSB first); the epilogue adds ``addend * mask`` instead of ``addend``."""
     dy, w = _cl(dy), _cl(w)
     Nb, Co, Po, Qo = dy.shape
     _, Ci, R, S = w.shape
     H, W = x_shape[2], x_shape[3]
     dx = torch.empty((Nb, Ci, H, W), dtype=dy.dtype, device=dy.device, memory_format=torch.channels_last)
     E = None if addend is None else _cl(addend)
+    EM = None if E is None else addend_mask
+    if EM is not None and (EM.dtype != torch.uint8 or EM.numel() * 8 != dx.numel()):
+        raise ValueError(f"conv_dgrad: addend mask of {EM.numel()} bytes for {dx.numel()} elements")
     st = _lib.stream()
     bn_args = (None, None, None, None, 0, None, None)
     if bn is not None:
@@ -167,7 +175,8 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride: int, pad: int
     if stride == 1:
         wt = _transposed_weight(w, 0, 1, R, 0, 1, S)
         _lib.call("kfa_conv_igemm", _lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), _lib.ptr(E), Nb, Po, Qo, Co, H, W, R, S,
-                  1, -1, pad, pad, Ci, H, W, 1, 0, 0, Ci, _variant(Nb * H * W, Ci, R * S * Co), *bn_args, st)
+                  1, -1, pad, pad, Ci, H, W, 1, 0, 0, Ci, _variant(Nb * H * W, Ci, R * S * Co), *bn_args,
+                  _lib.ptr(EM), st)
         return dx
     # stride s: output parity classes.  For class (ph, pw) the rows h = s*i + ph
     # receive taps r with (ph + pad - r) % s == 0, from dY row i + (ph + pad - r)/s.
@@ -188,7 +197,7 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride: int, pad: int
             oa_w = (pw + pad - s0) // stride
             _lib.call("kfa_conv_igemm", _lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), _lib.ptr(E), Nb, Po, Qo, Co, Hc, Wc,
                       Rs, Ss, 1, -1, oa_h, oa_w, Ci, H, W, stride, ph, pw, Ci, _variant(Nb * Hc * Wc, Ci, Rs * Ss * Co),
-                      *bn_args, st)
+                      *bn_args, _lib.ptr(EM), st)
     return dx
 
 
@@ -282,10 +291,11 @@ class GradJoin:
     the branch simply returns its gradient to autograd (correct, just unfused).
     """
 
-    __slots__ = ("grad", "state", "fused")
+    __slots__ = ("grad", "mask", "state", "fused")
 
     def __init__(self):
         self.grad = None
+        self.mask = None  # with grad: ReLU bits; the residual gradient is grad * mask (see deposit)
         self.state = "empty"  # empty -> deposited -> empty | consumer-first
         self.fused = False    # set by the consuming conv's forward (HIP path only)
 
@@ -294,16 +304,29 @@ class GradJoin:
             return x
         return _Branch.apply(x, self)
 
+    def deposit_masked(self, grad, mask) -> bool:
+        """Called by the backward of a BN + residual + ReLU whose residual input is
+        this branch: hand over the raw output gradient and the ReLU bits instead of
+        materialising grad * mask (the consuming dgrad epilogue applies the mask).
+        False when the consumer already ran (the caller returns a real gradient)."""
+        if self.state != "empty" or not self.fused or not MASKED_RESIDUAL:
+            return False
+        self.grad, self.mask, self.state = grad, mask, "deposited"
+        return True
+
 
 class _Branch(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, join):
         ctx.join = join
+        ctx.set_materialize_grads(False)  # None = the gradient was deposited (GradJoin.deposit_masked)
         return x.view_as(x)
 
     @staticmethod
     def backward(ctx, g):
         j = ctx.join
+        if g is None:
+            return None, None
         if j.state == "consumer-first":
             j.state = "empty"
             return g, None
@@ -329,26 +352,41 @@ class _ConvFn(torch.autograd.Function):
         x, w = ctx.saved_tensors
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            addend = None
+            addend = addend_mask = None
             bn_link = ctx.bn_link if (ctx.bn_link is not None and ctx.bn_link.convs == 1) else None
             j = ctx.join
             if j is not None:
                 if j.state == "deposited":
-                    addend, j.grad, j.state = j.grad, None, "empty"
+                    addend, addend_mask, j.grad, j.mask, j.state = j.grad, j.mask, None, None, "empty"
                 else:
                     j.state = "consumer-first"
                     # this epilogue sees only part of x's gradient: the BN whose output x
                     # is must compute its backward statistics itself
                     bn_link = None
             if w.shape[0] % 64 == 0 and w.shape[1] % 8 == 0:
-                dx = conv_dgrad(dy, w, x.shape, ctx.stride, ctx.pad, addend, bn_link)
+                dx = conv_dgrad(dy, w, x.shape, ctx.stride, ctx.pad, addend, bn_link, addend_mask)
             else:
                 dx = torch.nn.grad.conv2d_input(x.shape, w, dy, ctx.stride, ctx.pad)
+                if addend is not None and addend_mask is not None:
+                    addend = apply_bit_mask(addend, addend_mask)
                 if addend is not None:
                     dx = dx + addend
         if ctx.needs_input_grad[1]:
             dw = conv_wgrad(x, dy, w, ctx.stride, ctx.pad, ctx.wparam)
         return dx, dw, None, None, None, None, None
+
+
+def apply_bit_mask(t: torch.Tensor, bits: torch.Tensor) -> torch.Tensor:
+    """``t * mask`` for a ReLU bit mask over ``t``'s channels-last elements (LSB first)."""
+    t = _cl(t)
+    shifts = torch.arange(8, device=bits.device, dtype=torch.uint8)
+    m = ((bits.view(-1, 1) >> shifts) & 1).view(-1)
+    flat = t.permute(0, 2, 3, 1).reshape(-1) if t.dim() == 4 else t.reshape(-1)
+    out = torch.where(m.bool(), flat, torch.zeros((), dtype=t.dtype, device=t.device))
+    if t.dim() == 4:
+        n, c, h, w_ = t.shape
+        return out.view(n, h, w_, c).permute(0, 3, 1, 2)
+    return out.view_as(t)
 
 
 def conv2d(x, w, stride: int = 1, pad: int = 0, join: "GradJoin | None" = None, bn_stats: bool = False):

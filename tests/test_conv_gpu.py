@@ -260,3 +260,77 @@ def test_conv_forward_tuner(monkeypatch):
     assert (outs[0] - outs[1]).abs().max().item() < 5e-2
     for a, b in zip(grads[0], grads[1]):
         assert (a - b).abs().max().item() < 5e-2 * max(1.0, b.abs().max().item())
+
+
+@pytest.mark.parametrize("N,C,H,W,Co,k,stride,pad", [(2, 64, 14, 14, 256, 1, 1, 0), (2, 128, 14, 14, 64, 3, 2, 1),
+                                                     (3, 64, 9, 9, 128, 3, 1, 1)])
+def test_dgrad_masked_addend(N, C, H, W, Co, k, stride, pad):
+    """Residual gradient formed in the dgrad epilogue: dx = dgrad(dy) + g * bits
+    (the bits of a BN + residual + ReLU output) equals dgrad(dy) + (g * mask)."""
+    from kubeflow_controller_amd.ops.conv import apply_bit_mask, conv_dgrad
+    torch.manual_seed(0)
+    d = torch.device("cuda")
+    cl = torch.channels_last
+    P = (H + 2 * pad - k) // stride + 1
+    Q = (W + 2 * pad - k) // stride + 1
+    dy = torch.randn(N, Co, P, Q, device=d).to(torch.bfloat16).contiguous(memory_format=cl)
+    w = (torch.randn(Co, C, k, k, device=d) / (C * k * k) ** 0.5).to(torch.bfloat16).contiguous(memory_format=cl)
+    g = torch.randn(N, C, H, W, device=d).to(torch.bfloat16).contiguous(memory_format=cl)
+    bits = torch.randint(0, 256, (N * C * H * W // 8,), device=d, dtype=torch.uint8)
+    got = conv_dgrad(dy, w, (N, C, H, W), stride, pad, g, None, bits)
+    want = conv_dgrad(dy, w, (N, C, H, W), stride, pad, apply_bit_mask(g, bits).contiguous(memory_format=cl))
+    assert torch.equal(got, want)
+    keep = apply_bit_mask(g, bits) != 0
+    assert 0.3 < keep.float().mean().item() < 0.7  # the mask really drops elements
+
+
+def test_resnet_masked_residual_gradient():
+    """Identity blocks hand conv1's dgrad epilogue the raw gradient + ReLU bits
+    (GradJoin.deposit_masked) instead of a written residual gradient: every
+    identity block takes that path, and the gradients are as close to the fp32
+    reference as with the written residual gradient.  (Not bitwise: the fp32
+    BatchNorm statistics atomics make each run's order differ, and small-batch BN
+    backward amplifies that.)"""
+    from kubeflow_controller_amd.models.resnet import ResNet
+    from kubeflow_controller_amd.ops import conv as convmod
+    d = torch.device("cuda")
+    torch.manual_seed(0)
+    m = ResNet((3, 2, 1, 1), num_classes=10, width=64).to(d).to(memory_format=torch.channels_last)
+    for p in m.parameters():
+        if p.dim() >= 2:
+            p.data = p.data.to(torch.bfloat16)
+    for mod in m.modules():
+        if hasattr(mod, "bn3"):
+            torch.nn.init.uniform_(mod.bn3.weight, 0.5, 1.5)
+    x = torch.randn(8, 3, 128, 128, device=d).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    ref = _fp32_reference_grads(x, m)
+    calls = []
+    orig = convmod.GradJoin.deposit_masked
+
+    def counting(self, grad, mask):
+        ok = orig(self, grad, mask)
+        calls.append(ok)
+        return ok
+
+    convmod.GradJoin.deposit_masked = counting
+    try:
+        masked = _stack_grads(True, True, x, m)
+    finally:
+        convmod.GradJoin.deposit_masked = orig
+    assert len(calls) == 3 and all(calls), calls  # 2 identity blocks in layer1, 1 in layer2
+    convmod.GradJoin.deposit_masked = lambda self, grad, mask: False
+    try:
+        plain = _stack_grads(True, True, x, m)
+    finally:
+        convmod.GradJoin.deposit_masked = orig
+    names = ["input"] + [n for n, _ in m.named_parameters()]
+    bad = []
+    for n, a, b, r in zip(names, masked, plain, ref):
+        r = r.to(a.device).float()
+        if r.dim() == 4:
+            r = r.contiguous(memory_format=torch.channels_last)
+        scale = max(1e-4, r.abs().max().item())
+        e_m, e_p = (a - r).abs().max().item(), (b - r).abs().max().item()
+        if e_m > 2.0 * e_p + 0.02 * scale:
+            bad.append((n, e_m, e_p, scale))
+    assert not bad, bad

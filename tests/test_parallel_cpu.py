@@ -217,3 +217,17 @@ def test_async_ps_applies_every_push_exactly_once(tmp_path):
         torch.testing.assert_close(ps["w"], torch.full_like(ps["w"], 0.5 - total))
     steps = sorted(s for w in range(W) for s in torch.load(f"{out}.w{w}", weights_only=True)["steps"])
     assert steps == list(range(1, 7 * W + 1))                  # every push advanced the global step once
+
+
+def test_apply_bit_mask_matches_channels_last_bit_order():
+    """ReLU bit masks cover a tensor's channels-last elements, 8 per byte, LSB first."""
+    import torch
+    from kubeflow_controller_amd.ops.conv import apply_bit_mask
+    torch.manual_seed(0)
+    t = torch.randn(2, 16, 3, 5).contiguous(memory_format=torch.channels_last)
+    keep = torch.rand(2, 3, 5, 16) > 0.5  # NHWC order
+    flat = keep.reshape(-1, 8).to(torch.uint8)
+    bits = (flat << torch.arange(8, dtype=torch.uint8)).sum(1).to(torch.uint8)
+    out = apply_bit_mask(t, bits)
+    want = t * keep.permute(0, 3, 1, 2)
+    assert torch.equal(out, want)

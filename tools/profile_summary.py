@@ -12,6 +12,7 @@ import csv
 import sys
 
 OWN_MARKERS = ("(anonymous namespace)::",)
+ANCHOR = "sgd_kernel"  # one launch per training step (fused SGD over the flat parameter group)
 
 
 def origin(name: str) -> str:
@@ -19,7 +20,7 @@ def origin(name: str) -> str:
         return "own HIP (csrc/kernels)"
     if name.startswith("Cijk_") or name.startswith("Custom_Cijk"):
         return "hipBLASLt"
-    if "igemm_" in name or "ck::" in name or "SubTensor" in name or "MIOpen" in name:
+    if "igemm_" in name or "ck::" in name or name.startswith("_ZN2ck") or "SubTensor" in name or "MIOpen" in name:
         return "MIOpen / CK"
     if "at::native" in name:
         return "PyTorch ATen"
@@ -36,8 +37,15 @@ def short(name: str) -> str:
 def main(path, steps, step_ms, title):
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    end = int(rows[-1]["End_Timestamp"])
-    win = [r for r in rows if int(r["Start_Timestamp"]) > end - steps * step_ms * 1e6]
+    # Anchor on the once-per-step optimizer kernel when present: the window is then exactly
+    # the last STEPS steps (from the end of one optimizer launch to the end of the last).
+    anchors = [i for i, r in enumerate(rows) if ANCHOR in r["Kernel_Name"]]
+    if len(anchors) > steps:
+        win = rows[anchors[-steps - 1] + 1:anchors[-1] + 1]
+        step_ms = (int(win[-1]["End_Timestamp"]) - int(rows[anchors[-steps - 1]]["End_Timestamp"])) / 1e6 / steps
+    else:
+        end = int(rows[-1]["End_Timestamp"])
+        win = [r for r in rows if int(r["Start_Timestamp"]) > end - steps * step_ms * 1e6]
     per = collections.defaultdict(lambda: [0, 0])
     for r in win:
         d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
@@ -60,4 +68,6 @@ def main(path, steps, step_ms, title):
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 5:
+        ANCHOR = sys.argv[5]
     main(sys.argv[1], int(sys.argv[2]), float(sys.argv[3]), sys.argv[4] if len(sys.argv) > 4 else "profile")
