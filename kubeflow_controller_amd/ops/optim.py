@@ -1,10 +1,12 @@
 """Fused SGD(+momentum, weight decay, nesterov) and Adam/AdamW over flat
 parameter groups — ``csrc/kernels/optim.hip``.
 
-One kernel launch per group per step; the gradient average over data-parallel
-ranks (``1/world``) and any loss scale are folded into ``grad_scale`` so no
-separate scaling pass runs.  ``shard`` restricts the update to a slice of the
-group — the parameter-server / ZeRO shard this rank owns (``parallel/ps.py``).
+One kernel launch per optimizer space per step; the gradient average over
+data-parallel ranks (``1/world``) and any loss scale are folded into
+``grad_scale`` so no separate scaling pass runs.  A space is a whole flat group
+or the compact parameter-server / ZeRO shard a rank owns (``parallel/ps.py``):
+the optimizer state is allocated at the space's size, so an owner holds state
+only for what it owns.
 """
 from __future__ import annotations
 
@@ -23,48 +25,70 @@ _lib.register("kfa_f32_to_bf16", [P, P, L, P])
 _lib.register("kfa_sumsq", [P, I, L, P, P])
 
 
-def _slice(t: Optional[torch.Tensor], rng: Optional[Tuple[int, int]]):
-    if t is None or rng is None:
-        return t
-    return t[rng[0]:rng[1]]
+class OptSpace:
+    """One contiguous region a fused optimizer updates in ONE launch: fp32
+    weights ``w`` (updated in place), an optional low-precision compute copy
+    ``wb`` rewritten from ``w`` in the same kernel, and the gradient ``grad``
+    (bf16 or fp32).  A whole flat group (data-parallel all-reduce) or one
+    rank's compact shard of it (parameter-server / ZeRO owner, ``parallel/ps.py``)."""
+
+    __slots__ = ("name", "w", "wb", "_grad")
+
+    def __init__(self, name: str, w: torch.Tensor, wb: Optional[torch.Tensor], grad):
+        self.name = name
+        self.w = w
+        self.wb = wb
+        self._grad = grad
+
+    @classmethod
+    def of_group(cls, g: FlatGroup) -> "OptSpace":
+        return cls(g.name, g.fp32, g.data if g.master is not None else None, lambda: g.opt_grad)
+
+    @property
+    def grad(self) -> torch.Tensor:
+        return self._grad() if callable(self._grad) else self._grad
+
+    @property
+    def numel(self) -> int:
+        return self.w.numel()
+
+    @property
+    def device(self) -> torch.device:
+        return self.w.device
+
+
+def _as_spaces(items) -> List[OptSpace]:
+    return [x if isinstance(x, OptSpace) else OptSpace.of_group(x) for x in items]
 
 
 class _FusedBase:
-    def __init__(self, groups: Sequence[FlatGroup], lr: float, weight_decay: float,
+    def __init__(self, spaces: Sequence, lr: float, weight_decay: float,
                  decay_groups: Optional[Sequence[str]] = None):
-        self.groups: List[FlatGroup] = list(groups)
+        self.spaces: List[OptSpace] = _as_spaces(spaces)
         self.lr = lr
         self.weight_decay = weight_decay
         self.decay_groups = set(decay_groups) if decay_groups is not None else {"weights"}
         self.step_count = 0
-        self.shards: Dict[int, Tuple[int, int]] = {}
 
-    def set_shard(self, group_index: int, start: int, end: int) -> None:
-        self.shards[group_index] = (start, end)
+    def _wd(self, s: OptSpace) -> float:
+        return self.weight_decay if s.name in self.decay_groups or not s.name else 0.0
 
-    def _wd(self, g: FlatGroup) -> float:
-        return self.weight_decay if g.name in self.decay_groups or not g.name else 0.0
-
-    def _cpu_check(self, g: FlatGroup) -> bool:
-        return not g.data.is_cuda
-
-    def sync_compute_copy(self) -> None:
-        """Rewrite bf16 compute weights from the fp32 masters (after a broadcast / load)."""
-        for g in self.groups:
-            if g.master is not None:
-                if g.data.is_cuda:
-                    _lib.call("kfa_f32_to_bf16", _lib.ptr(g.master), _lib.ptr(g.data), g.numel, _lib.stream())
-                else:
-                    g.data.copy_(g.master)
+    @staticmethod
+    def _cpu(s: OptSpace) -> bool:
+        return not s.w.is_cuda
 
     def grad_norm(self, grad_scale: float = 1.0) -> torch.Tensor:
-        out = torch.zeros(1, dtype=torch.float32, device=self.groups[0].device)
-        for g in self.groups:
-            if g.grad.is_cuda:
-                _lib.call("kfa_sumsq", _lib.ptr(g.grad), int(g.grad.dtype == torch.bfloat16), g.numel,
+        """L2 norm of the gradient this rank holds (its shard in the sharded layouts)."""
+        out = torch.zeros(1, dtype=torch.float32, device=self.spaces[0].device)
+        for s in self.spaces:
+            g = s.grad
+            if g.numel() == 0:
+                continue
+            if g.is_cuda:
+                _lib.call("kfa_sumsq", _lib.ptr(g), int(g.dtype == torch.bfloat16), g.numel(),
                           _lib.ptr(out), _lib.stream())
             else:
-                out += g.grad.float().pow(2).sum()
+                out += g.float().pow(2).sum()
         return out.sqrt() * grad_scale
 
 
@@ -75,24 +99,20 @@ class FusedSGD(_FusedBase):
         self.momentum = momentum
         self.dampening = dampening
         self.nesterov = nesterov
-        self.mom = [torch.zeros(g.numel, dtype=torch.float32, device=g.device) if momentum else None
-                    for g in self.groups]
+        self.mom = [torch.zeros(s.numel, dtype=torch.float32, device=s.device) if momentum else None
+                    for s in self.spaces]
 
     @torch.no_grad()
     def step(self, grad_scale: float = 1.0, lr: Optional[float] = None) -> None:
         lr = self.lr if lr is None else lr
         first = int(self.step_count == 0)
-        for gi, g in enumerate(self.groups):
-            rng = self.shards.get(gi)
-            w = _slice(g.fp32, rng)
-            wb = _slice(g.data, rng) if g.master is not None else None
-            gr = _slice(g.grad, rng)
-            mom = _slice(self.mom[gi], rng)
+        for si, s in enumerate(self.spaces):
+            w, wb, gr, mom = s.w, s.wb, s.grad, self.mom[si]
             n = w.numel()
             if n == 0:
                 continue
-            if self._cpu_check(g):
-                d = gr.float() * grad_scale + self._wd(g) * w
+            if self._cpu(s):
+                d = gr.float() * grad_scale + self._wd(s) * w
                 if mom is not None:
                     if first:
                         mom.copy_(d)
@@ -104,7 +124,7 @@ class FusedSGD(_FusedBase):
                     wb.copy_(w)
                 continue
             _lib.call("kfa_sgd_step", _lib.ptr(w), _lib.ptr(wb), _lib.ptr(gr), int(gr.dtype == torch.bfloat16),
-                      _lib.ptr(mom), n, lr, self.momentum, self.dampening, self._wd(g), int(self.nesterov),
+                      _lib.ptr(mom), n, lr, self.momentum, self.dampening, self._wd(s), int(self.nesterov),
                       grad_scale, first, _lib.stream())
         self.step_count += 1
 
@@ -114,8 +134,8 @@ class FusedAdam(_FusedBase):
         super().__init__(groups, lr, weight_decay, decay_groups)
         self.b1, self.b2 = betas
         self.eps = eps
-        self.m = [torch.zeros(g.numel, dtype=torch.float32, device=g.device) for g in self.groups]
-        self.v = [torch.zeros(g.numel, dtype=torch.float32, device=g.device) for g in self.groups]
+        self.m = [torch.zeros(s.numel, dtype=torch.float32, device=s.device) for s in self.spaces]
+        self.v = [torch.zeros(s.numel, dtype=torch.float32, device=s.device) for s in self.spaces]
 
     @torch.no_grad()
     def step(self, grad_scale: float = 1.0, lr: Optional[float] = None) -> None:
@@ -124,17 +144,14 @@ class FusedAdam(_FusedBase):
         t = self.step_count
         bc1 = 1.0 - self.b1 ** t
         bc2 = 1.0 - self.b2 ** t
-        for gi, g in enumerate(self.groups):
-            rng = self.shards.get(gi)
-            w = _slice(g.fp32, rng)
-            wb = _slice(g.data, rng) if g.master is not None else None
-            gr = _slice(g.grad, rng)
-            m, v = _slice(self.m[gi], rng), _slice(self.v[gi], rng)
+        for si, s in enumerate(self.spaces):
+            w, wb, gr = s.w, s.wb, s.grad
+            m, v = self.m[si], self.v[si]
             n = w.numel()
             if n == 0:
                 continue
-            wd = self._wd(g)
-            if self._cpu_check(g):
+            wd = self._wd(s)
+            if self._cpu(s):
                 d = gr.float() * grad_scale
                 m.mul_(self.b1).add_(d, alpha=1 - self.b1)
                 v.mul_(self.b2).addcmul_(d, d, value=1 - self.b2)

@@ -4,21 +4,24 @@ SURVEY §2.4 "Data parallel: all-reduce (no PS)" and §5.8.  Design for the
 MI355X node rather than a DDP clone:
 
 * Gradients already live in flat per-dtype buffers (``parallel/flat.py``), so a
-  bucket is a *slice* of that buffer: no gradient copy into / out of bucket
-  storage.
+  bucket is a *slice* of that buffer (``parallel/buckets.py``): no gradient
+  copy into / out of bucket storage.
 * Buckets are cut in reverse parameter order (the order backward produces
-  them) at ``bucket_mb`` (default 16 MB: large enough to light up RCCL's
-  channels across the 7 xGMI links, small enough that the last bucket's
-  exposed all-reduce after backward stays ~0.1 ms).
-* A post-accumulate-grad hook counts ready tensors per bucket; the bucket's
-  collective is issued the moment its last tensor lands (async, on RCCL's
-  stream, ordered after the producing kernels by torch's stream semantics).
+  them) at ``bucket_mb`` of reduction dtype (default 32 MB, sized for RCCL's
+  channels over the 7 xGMI links, see ``buckets.py``).
+* A post-accumulate-grad hook (or a HIP kernel that wrote the gradient straight
+  into the flat buffer, ``flat.notify_grad_ready``) counts ready tensors per
+  bucket; the bucket's collective is issued the moment its last tensor lands
+  (async, on RCCL's stream, ordered after the producing kernels by torch's
+  stream semantics).
+* **The cross-rank sum runs in fp32** (``reduce_dtype``): a bf16 bucket is
+  widened into the group's fp32 reduction buffer by one cast kernel right
+  before its all-reduce, and the fused optimizer reads that fp32 buffer.  A
+  bf16 ring over 8 ranks rounds every partial sum to 8 significant bits; fp32
+  costs 2x the link bytes, which the overlap with backward hides
+  (``--grad-reduce bf16`` keeps the old behaviour for A/B).
 * The ``1/world`` average is NOT a separate pass: the optimizer kernel takes it
   as ``grad_scale``.
-* ``mode="allreduce"`` (pure DP) or ``mode="reduce_scatter"`` (ZeRO-1 /
-  parameter-server shards: each rank only receives — and only updates — the
-  shard it owns, then ``all_gather`` refreshes the compute weights; see
-  ``parallel/ps.py``).
 """
 from __future__ import annotations
 
@@ -27,80 +30,75 @@ from typing import List, Optional, Sequence, Tuple
 import torch
 import torch.distributed as dist
 
-from .flat import FlatGroup, set_ready_callback
+from .buckets import Bucket, plan_buckets
+from .flat import ALIGN, FlatGroup, set_ready_callback
 
 
-class _Bucket:
-    __slots__ = ("group", "start", "end", "params", "pending", "work")
-
-    def __init__(self, group: int, start: int, end: int):
-        self.group = group
-        self.start = start
-        self.end = end
-        self.params: List[int] = []
-        self.pending = 0
-        self.work = None
+def _join_side_streams(t: torch.Tensor) -> None:
+    if t.is_cuda:  # weight-gradient kernels on the side stream wrote into this bucket
+        from ..ops import streams
+        streams.join(t.device)
 
 
 class GradSync:
-    def __init__(self, groups: Sequence[FlatGroup], process_group=None, bucket_mb: float = 16.0,
-                 overlap: bool = True):
+    def __init__(self, groups: Sequence[FlatGroup], process_group=None, bucket_mb: float = 32.0,
+                 overlap: bool = True, reduce_dtype: Optional[torch.dtype] = torch.float32):
         self.groups = list(groups)
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.overlap = overlap and self.world > 1
-        self.buckets: List[_Bucket] = []
+        self.reduce_dtype = reduce_dtype
+        if self.world > 1 and reduce_dtype is not None:
+            for g in self.groups:
+                if g.grad.dtype != reduce_dtype:
+                    g.grad32 = torch.zeros(g.numel, dtype=reduce_dtype, device=g.device)
+        eb = [(g.grad32 if g.grad32 is not None else g.grad).element_size() for g in self.groups]
+        self.buckets, self._of_param = plan_buckets(self.groups, bucket_mb, ALIGN, eb)
         self._hooks = []
-        self._tensor_bucket = {}
-        for gi, g in enumerate(self.groups):
-            cap = max(int(bucket_mb * (1 << 20)) // g.grad.element_size(), 8)
-            cur: Optional[_Bucket] = None
-            # walk params from last to first (backward order)
-            order = list(range(len(g.params)))[::-1]
-            for pi in order:
-                s, e = g.offsets[pi], g.offsets[pi] + g.params[pi].numel()
-                if cur is None or (cur.end - s) > cap:
-                    end = g.numel if cur is None else cur.start
-                    cur = _Bucket(gi, s, end)
-                    self.buckets.append(cur)
-                cur.start = s
-                cur.params.append(pi)
-                self._tensor_bucket[(gi, pi)] = cur
-            if cur is not None:
-                cur.start = 0
         if self.overlap:
-            for (gi, pi), b in self._tensor_bucket.items():
+            for (gi, pi), bs in self._of_param.items():
                 p = self.groups[gi].params[pi]
-                hook = self._make_hook(b)
+                hook = self._make_hook(bs)
                 # fired either by autograd's AccumulateGrad or by a kernel that wrote
                 # the gradient straight into the flat buffer (flat.notify_grad_ready)
                 self._hooks.append(p.register_post_accumulate_grad_hook(hook))
                 set_ready_callback(p, hook)
         self.reset()
 
-    def _make_hook(self, b: _Bucket):
+    def spaces(self):
+        """What the fused optimizer updates: each whole flat group."""
+        from ..ops.optim import OptSpace
+        return [OptSpace.of_group(g) for g in self.groups]
+
+    def _make_hook(self, bs: List[Bucket]):
         def hook(_p):
-            b.pending -= 1
-            if b.pending == 0:
-                self._launch(b)
+            for b in bs:
+                b.pending -= 1
+                if b.pending == 0:
+                    self._launch(b)
         return hook
 
     def reset(self) -> None:
         for b in self.buckets:
-            # a tied parameter written by several direct-gradient kernels per step
-            # (e.g. BERT's word embedding: lookup + MLM decoder) declares _kfa_uses
-            b.pending = sum(getattr(self.groups[b.group].params[pi], "_kfa_uses", 1) for pi in b.params)
+            b.pending = b.total
             b.work = None
 
-    def _launch(self, b: _Bucket) -> None:
-        view = self.groups[b.group].grad[b.start:b.end]
-        if view.is_cuda:  # weight-gradient kernels on the side stream wrote into this bucket
-            from ..ops import streams
-            streams.join(view.device)
-        b.work = dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+    def _launch(self, b: Bucket) -> None:
+        g = self.groups[b.group]
+        view = g.grad[b.start:b.end]
+        _join_side_streams(view)
+        if g.grad32 is not None:
+            red = g.grad32[b.start:b.end]
+            red.copy_(view)
+        else:
+            red = view
+        b.work = dist.all_reduce(red, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
 
     def finish(self) -> float:
         """Wait for (or issue) every bucket's collective; return the grad scale (1/world)."""
+        if self.groups and self.groups[0].grad.is_cuda:
+            from ..ops import streams
+            streams.join(self.groups[0].grad.device)  # the optimizer reads every weight gradient
         if self.world == 1:
             self.reset()
             return 1.0
@@ -112,14 +110,24 @@ class GradSync:
         self.reset()
         return 1.0 / self.world
 
+    def pull(self) -> None:
+        """No-op: every rank applied the same update to the full weights."""
+
+    def wait_pull(self) -> None:
+        """No-op (see ``ps.ShardedGradSync.wait_pull``)."""
+
     def remove(self) -> None:
         for h in self._hooks:
             h.remove()
         self._hooks.clear()
 
     def describe(self) -> List[Tuple[str, int, float]]:
-        return [(self.groups[b.group].name, len(b.params),
-                 (b.end - b.start) * self.groups[b.group].grad.element_size() / 2 ** 20) for b in self.buckets]
+        out = []
+        for b in self.buckets:
+            g = self.groups[b.group]
+            eb = (g.grad32 if g.grad32 is not None else g.grad).element_size()
+            out.append((g.name, len(b.params), b.numel * eb / 2 ** 20))
+        return out
 
 
 def broadcast_params(groups: Sequence[FlatGroup], src: int = 0, process_group=None) -> None:

@@ -79,11 +79,19 @@ class FlatGroup:
             p._kfa_flat = True
         use_master = (self.dtype != torch.float32) if master is None else master
         self.master: Optional[torch.Tensor] = self.data.float() if use_master else None
+        # fp32 gradient buffer the cross-rank sum runs in when the compute grads are
+        # bf16 (set by ``parallel.ddp.GradSync``); the optimizer then reads it
+        self.grad32: Optional[torch.Tensor] = None
 
     # the fp32 tensor the optimizer updates
     @property
     def fp32(self) -> torch.Tensor:
         return self.master if self.master is not None else self.data
+
+    @property
+    def opt_grad(self) -> torch.Tensor:
+        """The gradient the optimizer consumes (the fp32 reduction buffer if one exists)."""
+        return self.grad32 if self.grad32 is not None else self.grad
 
     def zero_grad(self) -> None:
         self.grad.zero_()

@@ -2,30 +2,42 @@
 
 The reference's PS tasks own round-robin-placed variables
 (``replica_device_setter``, ``mnist_replica.py:137-141``); workers push
-gradients to and pull variables from them over gRPC every step.  On an
-8x MI355X node the same data movement is:
+gradients to and pull variables from them over gRPC every step, and the PS
+applies Adam with the slots it holds (``:170-184``).  On an 8x MI355X node the
+same data movement rides RCCL over xGMI, per gradient bucket
+(``parallel/buckets.py``), overlapped with backward:
 
-* push  = ``reduce_scatter`` of the flat gradient buffer: every owner receives
-  the SUM of all workers' gradients for the shard it owns (the
-  ``SyncReplicasOptimizer`` accumulator of ``replicas_to_aggregate`` grads,
-  K14, folded into the collective);
-* apply = the fused optimizer kernel on the owner's shard only (fp32 master +
-  optimizer state live only on the owner: 1/W of the memory);
-* pull  = ``all_gather`` of the updated bf16 compute weights.
+* **push**  — as soon as a bucket's last gradient lands (backward hook), its
+  gradient is widened to fp32 and summed onto its owner(s):
+  ``placement="ps"``: ``reduce`` to the rank co-located with the PS task the
+  bucket is placed on (round-robin over PS tasks, the ``replica_device_setter``
+  rule at bucket granularity); ``placement="sharded"``: ``reduce_scatter`` so
+  every worker owns ``1/W`` of every bucket (ZeRO-1 balance).  This IS the
+  ``SyncReplicasOptimizer`` accumulator of ``replicas_to_aggregate`` grads
+  (K14), folded into the collective.
+* **apply** — ONE fused optimizer launch per flat group over the rank's
+  compact shard: the fp32 master, the momentum / Adam ``m``/``v`` and the fp32
+  gradient exist ONLY for owned elements (per-rank optimizer memory ``1/W``
+  with ``sharded``, the PS task's share with ``ps``).
+* **pull**  — the updated bf16 weights go back by ``all_gather`` (sharded) /
+  ``broadcast`` from the owner (ps), issued asynchronously right after the
+  optimizer; a forward pre-hook on each module waits only for the buckets
+  holding that module's weights, so the pull of later layers overlaps the
+  forward of earlier ones.
 
-Owners are worker ranks (co-located PS, H1 option a): shard ``r`` of every
-flat group lives on worker ``r``.  ``ps_assignment`` reproduces the reference's
-variable -> PS-task placement (round-robin, or greedy by bytes) for reporting,
-checkpoint manifests and the PS coordinator processes.
+Owners are worker ranks (co-located PS, SURVEY §7.3 H1 option a: RCCL refuses
+two ranks on one GPU, and the PS replicas get no GPU of their own): PS task
+``p`` of ``P`` lives on worker rank ``p * W // P``.
 """
 from __future__ import annotations
 
-from typing import Dict, List, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
 
-from .flat import ALIGN, FlatGroup
+from .buckets import Bucket, plan_buckets
+from .flat import ALIGN, FlatGroup, set_ready_callback
 
 
 def ps_assignment(params: Sequence[Tuple[str, torch.Tensor]], num_ps: int, strategy: str = "round_robin"
@@ -46,54 +58,253 @@ def ps_assignment(params: Sequence[Tuple[str, torch.Tensor]], num_ps: int, strat
     return out
 
 
-def shard_bounds(numel: int, world: int, rank: int) -> Tuple[int, int]:
-    per = numel // world
-    assert per % ALIGN == 0, "flat group must be padded to world*ALIGN elements"
-    return rank * per, (rank + 1) * per
+def ps_owner_ranks(num_workers: int, num_ps: int) -> List[int]:
+    """Worker rank hosting each PS task's variables (spread evenly over the node)."""
+    return [p * num_workers // num_ps for p in range(max(1, num_ps))]
 
 
 class ShardedGradSync:
-    """Push (reduce-scatter) / owner apply / pull (all-gather) for flat groups.
+    """Bucketed push / owner apply / pull for flat groups (see module docstring)."""
 
-    Use with a fused optimizer whose ``set_shard`` restricts the update to the
-    owned slice; call ``push()`` after backward, ``opt.step(grad_scale=...)``,
-    then ``pull()``.
-    """
-
-    def __init__(self, groups: Sequence[FlatGroup], process_group=None):
+    def __init__(self, groups: Sequence[FlatGroup], process_group=None, *, bucket_mb: float = 32.0,
+                 placement: str = "sharded", num_ps: int = 1, reduce_dtype: Optional[torch.dtype] = torch.float32,
+                 model: Optional[torch.nn.Module] = None, overlap: bool = True):
+        if placement not in ("sharded", "ps"):
+            raise ValueError(f"placement must be 'sharded' or 'ps', got {placement!r}")
         self.groups = list(groups)
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(process_group) if dist.is_initialized() else 0
-        self.bounds: List[Tuple[int, int]] = []
-        for g in self.groups:
-            if g.numel % (self.world * ALIGN):
-                raise ValueError(f"{g}: pad the flat group to a multiple of world*{ALIGN} (pad_to)")
-            self.bounds.append(shard_bounds(g.numel, self.world, self.rank))
+        self.placement = placement if self.world > 1 else "sharded"
+        self.num_ps = max(1, num_ps)
+        self.owners = ps_owner_ranks(self.world, self.num_ps) if self.placement == "ps" else []
+        self.reduce_dtype = reduce_dtype
+        self.overlap = overlap and self.world > 1
+        unit = ALIGN * (self.world if self.placement == "sharded" else 1)
+        self.red_dtypes = [reduce_dtype if (reduce_dtype is not None and self.world > 1) else g.grad.dtype
+                           for g in self.groups]
+        eb = [torch.empty(0, dtype=d).element_size() for d in self.red_dtypes]
+        self.buckets, self._of_param = plan_buckets(self.groups, bucket_mb, unit, eb)
+        # ---- ownership + compact shard layout
+        self.shard_numel = [0] * len(self.groups)
+        per_group_idx = [0] * len(self.groups)
+        for b in sorted(self.buckets, key=lambda b: (b.group, b.start)):   # ascending = forward order
+            gi = b.group
+            if self.placement == "sharded":
+                b.owner = -1
+                b.shard_off = b.start // self.world
+                self.shard_numel[gi] += b.numel // self.world
+            else:
+                b.owner = self.owners[per_group_idx[gi] % len(self.owners)]
+                per_group_idx[gi] += 1
+                if b.owner == self.rank:
+                    b.shard_off = self.shard_numel[gi]
+                    self.shard_numel[gi] += b.numel
+        self.w32: List[torch.Tensor] = []
+        self.wb: List[Optional[torch.Tensor]] = []
+        self.gshard: List[torch.Tensor] = []
+        for gi, g in enumerate(self.groups):
+            n = self.shard_numel[gi]
+            full = g.fp32 if g.master is not None else g.data.float()
+            w = torch.empty(n, dtype=torch.float32, device=g.device)
+            for b, s, e, off in self._my_chunks(gi):
+                w[off:off + (e - s)].copy_(full[s:e])
+            self.w32.append(w)
+            self.wb.append(torch.empty(n, dtype=g.dtype, device=g.device) if g.dtype != torch.float32 else None)
+            self.gshard.append(torch.zeros(n, dtype=self.red_dtypes[gi], device=g.device))
+            g.master = None  # the full fp32 master is gone: each rank keeps only what it owns
+        self._hooks = []
+        if self.overlap:
+            for (gi, pi), bs in self._of_param.items():
+                p = self.groups[gi].params[pi]
+                hook = self._make_hook(bs)
+                self._hooks.append(p.register_post_accumulate_grad_hook(hook))
+                set_ready_callback(p, hook)
+        self._pull_hooks = []
+        if model is not None and self.world > 1:
+            self._install_pull_waits(model)
+        self.reset()
 
-    def configure(self, opt) -> None:
-        for gi, (s, e) in enumerate(self.bounds):
-            opt.set_shard(gi, s, e)
+    # ------------------------------------------------------------------ layout
+    def _my_chunks(self, gi: int):
+        """(bucket, flat start, flat end, shard offset) of every chunk this rank owns in group gi."""
+        for b in self.buckets:
+            if b.group != gi:
+                continue
+            if b.owner == -1:
+                c = b.numel // self.world
+                yield b, b.start + self.rank * c, b.start + (self.rank + 1) * c, b.shard_off
+            elif b.owner == self.rank:
+                yield b, b.start, b.end, b.shard_off
+
+    def spaces(self):
+        """What the fused optimizer updates: this rank's compact shard of each group."""
+        from ..ops.optim import OptSpace
+        return [OptSpace(g.name, self.w32[gi], self.wb[gi], self.gshard[gi]) for gi, g in enumerate(self.groups)]
+
+    def layout_signature(self) -> str:
+        """Identifies the shard layout (checkpoints restore shard files only into the same layout)."""
+        parts = [self.placement, str(self.world)]
+        for b in self.buckets:
+            parts.append(f"{b.group}:{b.start}:{b.end}:{b.owner}")
+        return "|".join(parts)
+
+    # ------------------------------------------------------------------ push
+    def _make_hook(self, bs: List[Bucket]):
+        def hook(_p):
+            for b in bs:
+                b.pending -= 1
+                if b.pending == 0:
+                    self._push(b)
+        return hook
+
+    def reset(self) -> None:
+        for b in self.buckets:
+            b.pending = b.total
+            b.work = None
+            b.tmp = None
+
+    def _push(self, b: Bucket) -> None:
+        g = self.groups[b.group]
+        rd = self.red_dtypes[b.group]
+        view = g.grad[b.start:b.end]
+        if view.is_cuda:
+            from ..ops import streams
+            streams.join(view.device)
+        if b.owner == -1:
+            c = b.numel // self.world
+            src = view if view.dtype == rd else view.to(rd)
+            out = self.gshard[b.group][b.shard_off:b.shard_off + c]
+            b.tmp = src
+            b.work = dist.reduce_scatter_tensor(out, src, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+        else:
+            if b.owner == self.rank:
+                buf = self.gshard[b.group][b.shard_off:b.shard_off + b.numel]
+                buf.copy_(view)
+            else:
+                buf = view if view.dtype == rd else view.to(rd)
+            b.tmp = buf
+            b.work = dist.reduce(buf, b.owner, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
 
     def push(self) -> float:
-        """Reduce-scatter every group's gradient into the owned shard; returns 1/world."""
+        """Issue what backward did not, wait for every push; returns the grad scale 1/world."""
+        if self.groups and self.groups[0].grad.is_cuda:
+            from ..ops import streams
+            streams.join(self.groups[0].grad.device)
         if self.world == 1:
+            for gi, g in enumerate(self.groups):   # world 1: the shard is the whole group
+                self.gshard[gi].copy_(g.grad)
+            self.reset()
             return 1.0
-        works = []
-        for g, (s, e) in zip(self.groups, self.bounds):
-            out = g.grad[s:e]
-            works.append(dist.reduce_scatter_tensor(out, g.grad, op=dist.ReduceOp.SUM, group=self.pg,
-                                                    async_op=True))
-        for w in works:
-            w.wait()
+        for b in self.buckets:
+            if b.work is None:
+                self._push(b)
+        for b in self.buckets:
+            b.work.wait()
+        self.reset()
         return 1.0 / self.world
 
+    # ------------------------------------------------------------------ pull
     def pull(self) -> None:
-        """All-gather the updated compute weights (bf16 for mixed precision groups)."""
+        """Start returning the updated weights to every rank (async; see ``wait_pull``)."""
         if self.world == 1:
+            for gi, g in enumerate(self.groups):
+                g.data.copy_(self.wb[gi] if self.wb[gi] is not None else self.w32[gi])
             return
-        works = []
-        for g, (s, e) in zip(self.groups, self.bounds):
-            works.append(dist.all_gather_into_tensor(g.data, g.data[s:e].clone(), group=self.pg, async_op=True))
-        for w in works:
-            w.wait()
+        # forward order: the first layers' buckets first
+        for b in sorted(self.buckets, key=lambda b: (b.group, b.start)):
+            gi = b.group
+            g = self.groups[gi]
+            src_buf = self.wb[gi] if self.wb[gi] is not None else self.w32[gi]
+            out = g.data[b.start:b.end]
+            if b.owner == -1:
+                c = b.numel // self.world
+                b.pull_work = dist.all_gather_into_tensor(out, src_buf[b.shard_off:b.shard_off + c],
+                                                          group=self.pg, async_op=True)
+            else:
+                if b.owner == self.rank:
+                    out.copy_(src_buf[b.shard_off:b.shard_off + b.numel])
+                b.pull_work = dist.broadcast(out, b.owner, group=self.pg, async_op=True)
+        if not self._pull_hooks:
+            self.wait_pull()
+
+    def wait_pull(self, buckets: Optional[Sequence[Bucket]] = None) -> None:
+        for b in (self.buckets if buckets is None else buckets):
+            if b.pull_work is not None:
+                b.pull_work.wait()
+                b.pull_work = None
+
+    def _install_pull_waits(self, model: torch.nn.Module) -> None:
+        """Forward pre-hooks: a module waits only for the pulls of the buckets
+        holding its own parameters.  That is only safe if every module that owns
+        parameters runs its own ``forward`` (a model may read a submodule's
+        weight directly), so the root module waits for EVERY pull until one
+        forward pass has shown that all parameter-owning modules fired their hook."""
+        by_param = {}
+        for gi, g in enumerate(self.groups):
+            for pi, p in enumerate(g.params):
+                by_param[id(p)] = self._of_param.get((gi, pi), [])
+        self._param_modules = set()
+        self._fired = set()
+        self._verified = False
+        for m in model.modules():
+            bs = []
+            for p in m.parameters(recurse=False):
+                for b in by_param.get(id(p), []):
+                    if b not in bs:
+                        bs.append(b)
+            if bs:
+                self._param_modules.add(id(m))
+                self._pull_hooks.append(m.register_forward_pre_hook(
+                    lambda _m, _i, bs=bs: self._module_wait(_m, bs)))
+        self._pull_hooks.append(model.register_forward_pre_hook(lambda _m, _i: self._root_pre()))
+        self._pull_hooks.append(model.register_forward_hook(lambda _m, _i, _o: self._root_post()))
+
+    def _module_wait(self, m, bs) -> None:
+        self._fired.add(id(m))
+        self.wait_pull(bs)
+
+    def _root_pre(self) -> None:
+        if not self._verified:
+            self.wait_pull()
+            self._fired.clear()
+
+    def _root_post(self) -> None:
+        if not self._verified and self._param_modules <= self._fired:
+            self._verified = True
+
+    # ------------------------------------------------------------------ checkpoint helpers
+    def full_master(self, gi: int) -> torch.Tensor:
+        """All ranks: reassemble group ``gi``'s full fp32 master from the owned shards (collective)."""
+        g = self.groups[gi]
+        full = torch.zeros(g.numel, dtype=torch.float32, device=g.device)
+        if self.world == 1:
+            full.copy_(self.w32[gi])
+            return full
+        for b in self.buckets:
+            if b.group != gi:
+                continue
+            out = full[b.start:b.end]
+            if b.owner == -1:
+                c = b.numel // self.world
+                dist.all_gather_into_tensor(out, self.w32[gi][b.shard_off:b.shard_off + c], group=self.pg)
+            else:
+                if b.owner == self.rank:
+                    out.copy_(self.w32[gi][b.shard_off:b.shard_off + b.numel])
+                dist.broadcast(out, b.owner, group=self.pg)
+        return full
+
+    def load_full_master(self, gi: int, full: torch.Tensor) -> None:
+        """Take this rank's chunks of a full fp32 master (resume at another world size)."""
+        full = full.to(self.w32[gi].device)
+        for b, s, e, off in self._my_chunks(gi):
+            self.w32[gi][off:off + (e - s)].copy_(full[s:e])
+
+    def remove(self) -> None:
+        for h in self._hooks + self._pull_hooks:
+            h.remove()
+        self._hooks.clear()
+        self._pull_hooks.clear()
+
+    def describe(self) -> List[Tuple[str, int, float, int]]:
+        return [(self.groups[b.group].name, len(b.params), b.numel * 4 / 2 ** 20, b.owner) for b in self.buckets]

@@ -48,16 +48,25 @@ def _load_opt_state(opt, st: dict) -> None:
 
 
 def save(model_dir: str, step: int, rank: int, world: int, model, groups=(), opt=None, extra: Optional[dict] = None,
-         is_chief: bool = True, keep: int = 2) -> str:
+         is_chief: bool = True, keep: int = 2, full_masters=None, layout: Optional[str] = None) -> str:
+    """Write this rank's file.  ``full_masters`` (sharded layouts, rank 0): every
+    group's full fp32 master, reassembled from the owners' shards, so a resume at
+    a different world size restores exact fp32 weights."""
     os.makedirs(model_dir, exist_ok=True)
+    if full_masters is not None:
+        masters = [m.detach().cpu() for m in full_masters]
+    else:
+        masters = [g.master.detach().cpu() if g.master is not None else torch.empty(0) for g in groups]
     state = {
         "step": step,
         "world": world,
+        "layout": layout or "",
         "model": {k: v.detach().cpu() for k, v in model.state_dict().items()},
-        "masters": [g.master.detach().cpu() if g.master is not None else torch.empty(0) for g in groups],
+        "masters": masters,
     }
     if opt is not None:
         state["opt"] = _opt_state(opt)
+        state["spaces"] = [sp.w.detach().cpu() for sp in getattr(opt, "spaces", [])]
     if extra:
         state["extra"] = extra
     path = os.path.join(model_dir, f"ckpt-{step}.rank{rank}.pt")
@@ -101,8 +110,14 @@ def latest(model_dir: str) -> Optional[dict]:
         return json.load(f)
 
 
-def restore(model_dir: str, rank: int, world: int, model, groups=(), opt=None) -> int:
-    """Load the manifest's step into model/groups/opt; returns the step (0 if none)."""
+def restore(model_dir: str, rank: int, world: int, model, groups=(), opt=None, layout: Optional[str] = None,
+            sync=None) -> int:
+    """Load the manifest's step into model/groups/opt; returns the step (0 if none).
+
+    Same world size and layout: this rank's own file — weights, its fp32 master
+    (shard) and optimizer state, exactly.  Otherwise rank 0's file: the weights
+    and the FULL fp32 masters (each rank takes the part it owns through
+    ``sync.load_full_master`` in the sharded layouts), fresh optimizer state."""
     man = latest(model_dir)
     if man is None:
         return 0
@@ -111,10 +126,27 @@ def restore(model_dir: str, rank: int, world: int, model, groups=(), opt=None) -
     path = own if same_world else os.path.join(model_dir, man["files"][0])
     state = torch.load(path, map_location="cpu", weights_only=True)
     model.load_state_dict(state["model"])
-    for g, m in zip(groups, state.get("masters", [])):
-        if g.master is not None and m.numel() == g.master.numel():
-            g.master.copy_(m.to(g.master.device))
-            g.data.copy_(g.master)
-    if same_world and opt is not None and "opt" in state:
+    exact = (same_world and opt is not None and "opt" in state and "spaces" in state
+             and (layout is None or state.get("layout", "") in ("", layout))
+             and all(a.numel() == b.w.numel() for a, b in zip(state["spaces"], opt.spaces)))
+    if exact:
+        for sp, w in zip(opt.spaces, state["spaces"]):
+            sp.w.copy_(w.to(sp.w.device))
         _load_opt_state(opt, state["opt"])
+        return int(state["step"])
+    chief = os.path.join(model_dir, man["files"][0])
+    if path != chief:  # full masters: rank 0's file (the sharded layouts write them there only)
+        state = torch.load(chief, map_location="cpu", weights_only=True)
+    masters = state.get("masters", [])
+    for gi, g in enumerate(groups):
+        m = masters[gi] if gi < len(masters) else torch.empty(0)
+        full = g.data.detach().float()
+        if m.numel():  # same parameter offsets at any world size; only the tail padding differs
+            k = min(m.numel(), g.numel)
+            full[:k] = m[:k].to(full.device)
+        if sync is not None:
+            sync.load_full_master(gi, full)
+        elif g.master is not None:
+            g.master.copy_(full.to(g.master.device))
+            g.data.copy_(g.master)
     return int(state["step"])

@@ -53,12 +53,21 @@ def init_distributed(backend: Optional[str] = None, prefer_gpu: bool = True) -> 
 
 
 class Engine:
-    """Owns the flat parameter groups, the fused optimizer and the grad sync."""
+    """Owns the flat parameter groups, the gradient sync and the fused optimizer.
+
+    ``ps == 0``: data-parallel all-reduce (``parallel/ddp.py``).  ``ps > 0`` and
+    ``world > 1``: parameter-server push/apply/pull (``parallel/ps.py``) with
+    ``ps_placement`` ``"ps"`` (variables round-robin on the PS tasks'
+    co-located ranks, the reference's ``replica_device_setter``) or
+    ``"sharded"`` (every worker owns 1/W).  In both, gradients are summed
+    across ranks in ``grad_reduce_dtype`` (fp32 by default) and every
+    collective is issued per bucket from backward hooks."""
 
     def __init__(self, model: torch.nn.Module, loss_fn: Callable, *, optimizer: str = "sgd", lr: float = 0.1,
                  momentum: float = 0.9, weight_decay: float = 5e-5, betas=(0.9, 0.999), eps: float = 1e-8,
-                 compute_dtype=torch.bfloat16, bucket_mb: float = 16.0, dist_info: Optional[DistInfo] = None,
-                 channels_last: bool = True, ps: int = 0):
+                 compute_dtype=torch.bfloat16, bucket_mb: float = 32.0, dist_info: Optional[DistInfo] = None,
+                 channels_last: bool = True, ps: int = 0, ps_placement: str = "ps",
+                 grad_reduce_dtype: Optional[torch.dtype] = torch.float32):
         from ..ops.optim import FusedAdam, FusedSGD
         from ..parallel.ddp import GradSync, broadcast_params
 
@@ -69,22 +78,21 @@ class Engine:
         self.loss_fn = loss_fn
         # pad so every group splits evenly into per-rank reduce-scatter shards
         self.groups: List[FlatGroup] = split_params(self.model, compute_dtype, pad_to=8 * max(1, self.info.world))
-        if optimizer == "sgd":
-            self.opt = FusedSGD(self.groups, lr=lr, momentum=momentum, weight_decay=weight_decay)
-        elif optimizer in ("adam", "adamw"):
-            self.opt = FusedAdam(self.groups, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
-        else:
-            raise ValueError(f"unknown optimizer {optimizer!r}")
         broadcast_params(self.groups)
-        # ps > 0: parameter-server layout — shards owned by the
-        # ranks, push = reduce-scatter, owner-side fused optimizer, pull = all-gather
         self.sharded = ps > 0 and self.info.world > 1
         if self.sharded:
             from ..parallel.ps import ShardedGradSync
-            self.sync = ShardedGradSync(self.groups)
-            self.sync.configure(self.opt)
+            self.sync = ShardedGradSync(self.groups, bucket_mb=bucket_mb, placement=ps_placement, num_ps=ps,
+                                        reduce_dtype=grad_reduce_dtype, model=self.model)
         else:
-            self.sync = GradSync(self.groups, bucket_mb=bucket_mb)
+            self.sync = GradSync(self.groups, bucket_mb=bucket_mb, reduce_dtype=grad_reduce_dtype)
+        spaces = self.sync.spaces()
+        if optimizer == "sgd":
+            self.opt = FusedSGD(spaces, lr=lr, momentum=momentum, weight_decay=weight_decay)
+        elif optimizer in ("adam", "adamw"):
+            self.opt = FusedAdam(spaces, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
+        else:
+            raise ValueError(f"unknown optimizer {optimizer!r}")
         self.steps = 0
 
     def zero_grad(self) -> None:
@@ -97,14 +105,51 @@ class Engine:
         loss.backward()
         if self.sharded:
             self.opt.step(grad_scale=self.sync.push())
-            self.sync.pull()
+            self.sync.pull()   # async; forward pre-hooks wait per bucket
         else:
             self.opt.step(grad_scale=self.sync.finish())
         self.steps += 1
         return loss.detach()
 
+    def wait(self) -> None:
+        """Make every rank's compute weights current (after an async pull)."""
+        self.sync.wait_pull()
+
     def num_params(self) -> int:
         return sum(p.numel() for g in self.groups for p in g.params)
+
+    def optimizer_bytes(self) -> int:
+        """Bytes of fp32 master + optimizer state + fp32 reduced gradient this rank keeps."""
+        n = 0
+        for s in self.opt.spaces:
+            n += s.w.numel() * 4 if (s.wb is not None or self.sharded) else 0
+        for name in ("mom", "m", "v"):
+            for b in getattr(self.opt, name, None) or []:
+                n += b.numel() * b.element_size() if b is not None else 0
+        if self.sharded:
+            n += sum(t.numel() * t.element_size() for t in self.sync.gshard)
+        else:
+            n += sum(g.grad32.numel() * 4 for g in self.groups if g.grad32 is not None)
+        return n
+
+    # ------------------------------------------------------------------ checkpoint / resume
+    def save(self, model_dir: str, step: int, *, is_chief: Optional[bool] = None, extra: Optional[dict] = None):
+        from . import checkpoint
+        self.wait()
+        full = None
+        if self.sharded:  # exact fp32 weights for a resume at another world size (collective)
+            full = [self.sync.full_master(gi) for gi in range(len(self.groups))]
+        return checkpoint.save(model_dir, step, self.info.rank, self.info.world, self.model, self.groups, self.opt,
+                               extra=extra, is_chief=self.info.is_chief if is_chief is None else is_chief,
+                               full_masters=full if self.info.is_chief else None, layout=self.layout())
+
+    def restore(self, model_dir: str) -> int:
+        from . import checkpoint
+        return checkpoint.restore(model_dir, self.info.rank, self.info.world, self.model, self.groups, self.opt,
+                                  layout=self.layout(), sync=self.sync if self.sharded else None)
+
+    def layout(self) -> str:
+        return self.sync.layout_signature() if self.sharded else f"allreduce|{self.info.world}"
 
 
 def synchronize(info: DistInfo) -> None:

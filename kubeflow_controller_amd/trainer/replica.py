@@ -248,11 +248,13 @@ def run_ps(spec: ClusterSpec, args) -> int:
 
 
 def run_worker(spec: ClusterSpec, args) -> int:
+    """Worker / Local replica on the shared training engine (``trainer/engine.py``):
+    the same step ``bench.py`` times, plus the reference's logging, global-step
+    bookkeeping, validation and ``spec.modelDir`` checkpoints."""
     from ..ops.loss import accuracy, cross_entropy
-    from ..ops.optim import FusedAdam, FusedSGD
-    from ..parallel.ddp import GradSync, broadcast_params
-    from ..parallel.flat import split_params
-    from ..parallel.ps import ShardedGradSync, ps_assignment
+    from ..parallel.ps import ps_assignment, ps_owner_ranks
+    from . import checkpoint
+    from .engine import DistInfo, Engine
 
     use_gpu = _use_gpu(args)
     device = torch.device("cuda", 0) if use_gpu else torch.device("cpu")
@@ -266,44 +268,38 @@ def run_worker(spec: ClusterSpec, args) -> int:
     store = None
     if not spec.is_local:
         store = _store(spec, spec.is_chief)
-        dist.init_process_group("nccl" if use_gpu else "gloo", store=store, rank=rank, world_size=world,
-                                **({"device_id": device} if use_gpu else {}))
-    torch.manual_seed(args.seed)  # identical init everywhere (+ broadcast below)
-    args.num_ps = 0 if spec.is_local else len(spec.ps)
+        backend = os.environ.get("KFA_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
+        dist.init_process_group(backend, store=store, rank=rank, world_size=world,
+                                **({"device_id": device} if backend == "nccl" else {}))
+    torch.manual_seed(args.seed)  # identical init everywhere (+ broadcast in the engine)
+    num_ps = 0 if spec.is_local else len(spec.ps)
+    args.num_ps = num_ps
     model, data, loss_fn = build(args, device)
     model = model.to(device)
-    if model.__class__.__name__ == "ResNet":
-        model = model.to(memory_format=torch.channels_last)
-    num_ps = len(spec.ps)
-    world_pad = 8 * max(world, 1)
-    groups = split_params(model, torch.bfloat16 if (use_gpu and args.bf16) else None, pad_to=world_pad)
-    if args.optimizer == "adam":
-        opt = FusedAdam(groups, lr=args.learning_rate, weight_decay=args.weight_decay)
-    else:
-        opt = FusedSGD(groups, lr=args.learning_rate, momentum=args.momentum, weight_decay=args.weight_decay)
-    from . import checkpoint
-    resumed = checkpoint.restore(args.model_dir, rank, world, model, groups, opt) if args.model_dir else 0
+    engine = Engine(model, loss_fn, optimizer=args.optimizer, lr=args.learning_rate, momentum=args.momentum,
+                    weight_decay=args.weight_decay, compute_dtype=torch.bfloat16 if (use_gpu and args.bf16) else None,
+                    bucket_mb=args.bucket_mb, dist_info=DistInfo(rank, world, 0, device),
+                    channels_last=model.__class__.__name__ == "ResNet", ps=num_ps, ps_placement=args.ps_placement,
+                    grad_reduce_dtype=None if args.grad_reduce == "bf16" else torch.float32)
+    model = engine.model
+    resumed = engine.restore(args.model_dir) if args.model_dir else 0
     if resumed:
         _log(f"Worker {rank}: resumed from {args.model_dir} at global step {resumed}")
-    broadcast_params(groups)
-    sharded = num_ps > 0 and world > 1
-    if sharded:
-        sync = ShardedGradSync(groups)
-        sync.configure(opt)
+    if engine.sharded and spec.is_chief:
         placement = ps_assignment(list(model.named_parameters()), num_ps)
-        if spec.is_chief:
-            counts = [sum(1 for v in placement.values() if v == p) for p in range(num_ps)]
-            _log(f"PS placement (round-robin over {num_ps} PS tasks): tensors per PS = {counts}; "
-                 f"shards owned by worker ranks 0..{world - 1}")
-    else:
-        sync = GradSync(groups, bucket_mb=args.bucket_mb)
+        counts = [sum(1 for v in placement.values() if v == p) for p in range(num_ps)]
+        where = (f"variables of PS task p on worker rank {ps_owner_ranks(world, num_ps)}[p]"
+                 if args.ps_placement == "ps" else f"shards owned by worker ranks 0..{world - 1}")
+        _log(f"PS placement over {num_ps} PS tasks ({args.ps_placement}): tensors per PS = {counts}; {where}; "
+             f"{len(engine.sync.buckets)} buckets; optimizer state {engine.optimizer_bytes() / 2**20:.1f} MiB "
+             f"on this rank")
 
     inc = 1 if (args.sync_replicas or spec.is_local) else world
     steps_per_worker = max(0, math.ceil((args.train_steps - resumed) / inc))
     fixed = None if data is not None else synthetic_batch(args, model, device, rank)
     _log(f"Worker {rank}: {'local' if spec.is_local else f'{world} workers, {num_ps} ps'}, device {device}, "
          f"model {args.model}, {sum(p.numel() for p in model.parameters())} params, "
-         f"{'sharded push/pull' if sharded else 'all-reduce'}")
+         f"{'push/pull to ' + args.ps_placement + ' owners' if engine.sharded else 'all-reduce'}")
     t_begin = time.time()
     _log(f"Training begins @ {t_begin:f}")
     global_step = resumed
@@ -311,7 +307,7 @@ def run_worker(spec: ClusterSpec, args) -> int:
     loss = None
 
     def _save():
-        checkpoint.save(args.model_dir, global_step, rank, world, model, groups, opt, is_chief=False)
+        engine.save(args.model_dir, global_step, is_chief=False)
         if store is not None:
             dist.barrier()  # every rank's file is on disk before the manifest names the step
         if spec.is_chief:
@@ -323,17 +319,7 @@ def run_worker(spec: ClusterSpec, args) -> int:
             batch = (xb.to(device), yb.to(device))
         else:
             batch = fixed
-        for g in groups:
-            g.zero_grad()
-        loss = loss_fn(model, *batch)
-        loss.backward()
-        if sharded:
-            scale = sync.push()
-            opt.step(grad_scale=scale)
-            sync.pull()
-        else:
-            scale = sync.finish()
-            opt.step(grad_scale=scale)
+        loss = engine.train_step(*batch)
         global_step += inc
         if store is not None and spec.is_chief:
             store.add(STEP_KEY, inc)
@@ -347,6 +333,7 @@ def run_worker(spec: ClusterSpec, args) -> int:
             else:
                 _log(f"{time.time():f}: Worker {rank}: training step {local_step + 1} done "
                      f"(global step: {global_step})")
+    engine.wait()
     if device.type == "cuda":
         torch.cuda.synchronize()
     t_end = time.time()
@@ -403,7 +390,12 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--checkpoint_every", type=int, default=0, help="local steps between checkpoints")
     ap.add_argument("--device", default="auto", choices=["auto", "cpu", "gpu"])
     ap.add_argument("--bf16", type=int, default=1)
-    ap.add_argument("--bucket_mb", type=float, default=16.0)
+    ap.add_argument("--bucket_mb", type=float, default=32.0)
+    ap.add_argument("--ps_placement", default="ps", choices=["ps", "sharded"],
+                    help="collective mode with PS tasks: ps = each gradient bucket owned by one PS task's "
+                         "co-located rank (replica_device_setter round-robin); sharded = every worker owns 1/W")
+    ap.add_argument("--grad_reduce", default="fp32", choices=["fp32", "bf16"],
+                    help="dtype of the cross-rank gradient sum")
     ap.add_argument("--log_every", type=int, default=1)
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--ps_connect_timeout", type=float, default=300.0)

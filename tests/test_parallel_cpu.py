@@ -30,62 +30,86 @@ def _data():
     return torch.randn(16, 12, generator=g), torch.randint(0, 5, (16,), generator=g)
 
 
-def _train(model, groups, opt, sync, x, y, steps, mode):
+def _train(model, opt, sync, x, y, steps, mode):
     import torch.nn.functional as F
     for _ in range(steps):
-        for g in groups:
+        for g in sync.groups:
             g.zero_grad()
         F.cross_entropy(model(x), y).backward()
-        if mode == "sharded":
+        if mode != "allreduce":
             scale = sync.push()
             opt.step(grad_scale=scale)
             sync.pull()
         else:
             opt.step(grad_scale=sync.finish())
+    sync.wait_pull()
+
+
+def _make_sync(mode, groups, model, world):
+    from kubeflow_controller_amd.parallel.ddp import GradSync
+    from kubeflow_controller_amd.parallel.ps import ShardedGradSync
+    if mode == "allreduce":
+        return GradSync(groups, bucket_mb=0.0005)  # several buckets
+    if mode == "sharded":
+        return ShardedGradSync(groups, bucket_mb=0.0005, placement="sharded", model=model)
+    num_ps = int(mode[2:])  # "ps1", "ps2"
+    return ShardedGradSync(groups, bucket_mb=0.0005, placement="ps", num_ps=num_ps, model=model)
 
 
 def _worker(rank, world, port, mode, out):
     sys.path.insert(0, ROOT)
     import torch.distributed as dist
     from kubeflow_controller_amd.ops.optim import FusedAdam
-    from kubeflow_controller_amd.parallel.ddp import GradSync, broadcast_params
+    from kubeflow_controller_amd.parallel.ddp import broadcast_params
     from kubeflow_controller_amd.parallel.flat import split_params
-    from kubeflow_controller_amd.parallel.ps import ShardedGradSync
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     model = _model()
     groups = split_params(model, None, pad_to=8 * world)
-    opt = FusedAdam(groups, lr=0.01)
     broadcast_params(groups)
-    if mode == "sharded":
-        sync = ShardedGradSync(groups)
-        sync.configure(opt)
-    else:
-        sync = GradSync(groups, bucket_mb=0.0005)  # several buckets
+    sync = _make_sync(mode, groups, model, world)
+    opt = FusedAdam(sync.spaces(), lr=0.01)
     x, y = _data()
     n = x.shape[0] // world
-    _train(model, groups, opt, sync, x[rank * n:(rank + 1) * n], y[rank * n:(rank + 1) * n], 5, mode)
-    if rank == 0:
-        torch.save({k: v.clone() for k, v in model.state_dict().items()}, out)
+    _train(model, opt, sync, x[rank * n:(rank + 1) * n], y[rank * n:(rank + 1) * n], 5, mode)
+    state = {"sd": {k: v.clone() for k, v in model.state_dict().items()},
+             "opt_numel": sum(m.numel() for m in opt.m), "buckets": len(sync.buckets)}
+    torch.save(state, f"{out}.{rank}")
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["allreduce", "sharded"])
-def test_dp_matches_single_process(tmp_path, mode):
+def _single_process_reference(steps=5):
     from kubeflow_controller_amd.ops.optim import FusedAdam
     from kubeflow_controller_amd.parallel.ddp import GradSync
     from kubeflow_controller_amd.parallel.flat import split_params
-    out = str(tmp_path / "rank0.pt")
-    mp.start_processes(_worker, args=(2, _free_port(), mode, out), nprocs=2, join=True, start_method="spawn")
-    dist_sd = torch.load(out, weights_only=True)
     model = _model()
     groups = split_params(model, None)
-    opt = FusedAdam(groups, lr=0.01)
+    sync = GradSync(groups)
+    opt = FusedAdam(sync.spaces(), lr=0.01)
     x, y = _data()
-    _train(model, groups, opt, GradSync(groups), x, y, 5, "allreduce")
-    for k, v in model.state_dict().items():
-        torch.testing.assert_close(dist_sd[k], v, atol=2e-5, rtol=1e-4)
+    _train(model, opt, sync, x, y, steps, "allreduce")
+    return model, groups
+
+
+@pytest.mark.parametrize("mode", ["allreduce", "sharded", "ps1", "ps2"])
+def test_dp_matches_single_process(tmp_path, mode):
+    """Every sync mode on 2 gloo ranks (several buckets, parameters straddling
+    bucket boundaries, async pulls waited by forward pre-hooks) reproduces one
+    process on the concatenated batch, on EVERY rank."""
+    out = str(tmp_path / "res")
+    mp.start_processes(_worker, args=(2, _free_port(), mode, out), nprocs=2, join=True, start_method="spawn")
+    model, groups = _single_process_reference()
+    full = sum(g.numel for g in groups)
+    for r in range(2):
+        got = torch.load(f"{out}.{r}", weights_only=True)
+        assert got["buckets"] > 2
+        for k, v in model.state_dict().items():
+            torch.testing.assert_close(got["sd"][k], v, atol=2e-5, rtol=1e-4)
+        if mode == "sharded":  # optimizer state only for the owned half
+            assert got["opt_numel"] * 2 <= full + 16 * 8
+        if mode == "ps1":       # one PS task: its co-located rank 0 owns every variable
+            assert (got["opt_numel"] > 0) == (r == 0)
 
 
 def test_bucket_plan_covers_buffer():
