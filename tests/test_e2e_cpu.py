@@ -228,3 +228,64 @@ def test_fault_injection_restart_and_metrics(node):
         assert 'kfa_children_created_total{kind="Pod",result="success"}' in text
         assert "kfa_sync_duration_seconds_count" in text
         assert 'kfa_replica_exits_total{result="failure",type="Worker"}' in text
+
+
+def _bert_job(name, workers, ps, model_dir, extra=()):
+    cmd = [sys.executable, os.path.join(ROOT, "examples", "workdir", "train.py"), "--model", "bert_tiny",
+           "--train_steps", "3", "--batch_size", "4", "--seq_len", "32", "--optimizer", "adam",
+           "--learning_rate", "0.002", "--sync_replicas", "--log_every", "1", *extra]
+    specs = ([("PS", ps, cmd)] if ps else []) + [("Worker", workers, cmd)]
+    job = _job(name, specs)
+    job.spec.modelDir = model_dir
+    return job
+
+
+def _single_process_bert(steps, world):
+    """One process on the concatenation of every worker's synthetic batch."""
+    import torch
+    from kubeflow_controller_amd.models.bert import BertConfig, BertForPreTraining, bert_loss, synthetic_mlm_batch
+    from kubeflow_controller_amd.trainer.engine import Engine
+    cfg = BertConfig.tiny()
+    torch.manual_seed(1234)
+    m = BertForPreTraining(cfg)
+    eng = Engine(m, bert_loss, optimizer="adam", lr=0.002, weight_decay=0.0, compute_dtype=None,
+                 channels_last=False)
+    parts = [synthetic_mlm_batch(cfg, 4, 32, torch.Generator().manual_seed(1234 + 1000 * r)) for r in range(world)]
+    ids, tt, _, flat, labels, nsp = (list(x) for x in zip(*parts))
+    flat = [f + r * 4 * 32 for r, f in enumerate(flat)]   # positions index the concatenated [B*S] rows
+    batch = (torch.cat(ids), torch.cat(tt), None, torch.cat(flat), torch.cat(labels), torch.cat(nsp))
+    for _ in range(steps):
+        eng.train_step(*batch)
+    return {k: v.detach().clone() for k, v in m.state_dict().items()}
+
+
+def _final_state(model_dir):
+    import json
+    import torch
+    man = json.load(open(os.path.join(model_dir, "manifest.json")))
+    return man, torch.load(os.path.join(model_dir, man["files"][0]), weights_only=True)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("ps", [0, 1])
+def test_multi_worker_tfjob_matches_single_process(node, tmp_path, ps):
+    """A Worker-only 2-replica job (bucketed fp32 all-reduce) and a 2 workers + 1 PS
+    job (``--ps_mode collective``: push to the PS task's co-located owner, owner-side
+    Adam, pull) through controller -> supervisor -> replica runtime both reach
+    Succeeded with the weights of one process trained on the concatenated batch."""
+    import torch
+    st, n, root = node
+    model_dir = str(tmp_path / "model")
+    name = f"bert-2w{ps}ps"
+    st.create(_bert_job(name, 2, ps, model_dir, ["--ps_mode", "collective"] if ps else []))
+    j = wait_for_phase(st, "default", name, {"Succeeded", "Failed"}, 240)
+    assert j.status.phase == "Succeeded", describe_tfjob(st, "default", name)
+    pods = [p for p in st.list("Pod") if p.metadata.labels.get("tf_job_name") == name]
+    w0 = next(p for p in pods if p.metadata.labels["job_type"] == "Worker" and p.metadata.labels["index"] == "0")
+    out = _logs(root, w0)
+    assert ("push/pull to ps owners" if ps else "all-reduce") in out, out
+    man, state = _final_state(model_dir)
+    assert man["step"] == 3 and man["world"] == 2
+    ref = _single_process_bert(3, 2)
+    for k, v in ref.items():
+        torch.testing.assert_close(state["model"][k], v, atol=1e-4, rtol=1e-4)  # Adam: lr 2e-3

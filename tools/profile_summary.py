@@ -39,7 +39,13 @@ def main(path, steps, step_ms, title):
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     # Anchor on the once-per-step optimizer kernel when present: the window is then exactly
     # the last STEPS steps (from the end of one optimizer launch to the end of the last).
-    anchors = [i for i, r in enumerate(rows) if ANCHOR in r["Kernel_Name"]]
+    anchors = []
+    for i, r in enumerate(rows):  # one optimizer launch per flat group: adjacent launches = one step
+        if ANCHOR in r["Kernel_Name"]:
+            if anchors and i - anchors[-1] <= 3:
+                anchors[-1] = i
+            else:
+                anchors.append(i)
     if len(anchors) > steps:
         win = rows[anchors[-steps - 1] + 1:anchors[-1] + 1]
         step_ms = (int(win[-1]["End_Timestamp"]) - int(rows[anchors[-steps - 1]]["End_Timestamp"])) / 1e6 / steps
