@@ -88,7 +88,7 @@ class ResNet(nn.Module):
         nn.init.zeros_(self.fc.bias)
 
     def forward(self, x):
-        x = self.maxpool(self.bn1(self.conv1(x)))
+        x = self.maxpool(self.bn1(self.conv1(x, bn_stats=self.training)))
         x = self.layers(x)
         return self.fc(global_avg_pool(x))
 

@@ -16,7 +16,8 @@
 
 The weight lives as ``[Cout, Cin, kh, kw]`` in channels_last memory, i.e.
 physically ``[Cout][kh][kw][Cin]`` — exactly the K-contiguous B operand.
-Layers the kernel does not cover (the 3-channel stem) use ``F.conv2d``.
+The 3-channel stride-2 stem runs as a stride-1 4x4 conv over its space-to-depth
+input on the same kernels (``csrc/kernels/stem.hip``, ``_StemConvFn``).
 """
 from __future__ import annotations
 
@@ -35,9 +36,13 @@ P, I = _lib.P, _lib.I
 _lib.register("kfa_conv_igemm", [P, P, P, P] + [I] * 20 + [P, P, P, P, I, P, P, P, P])
 _lib.register("kfa_zero_bf16", [P, _lib.L, P])
 _lib.register("kfa_weight_transpose", [P, P] + [I] * 10 + [P])
+_lib.register("kfa_weight_transpose_multi", [P, P, I, I, P])
 _lib.register("kfa_wgrad_part_floats", [I] * 7, _lib.L)
 _lib.register("kfa_conv_wgrad", [P, P, P, I, I, P] + [I] * 11 + [P])
 _lib.register("kfa_bn_stats_partial", [P, P, _lib.L, I, P])
+_lib.register("kfa_stem_s2d", [P, P, I, I, I, I, I, P])
+_lib.register("kfa_stem_weight_s2d", [P, P, I, I, I, I, P])
+_lib.register("kfa_stem_wgrad_fold", [P, P, I, I, I, I, I, I, P])
 
 # Runtime switches (tests compare against the vendor path); env KFA_CONV_IGEMM=0 / KFA_WGRAD=0 disable.
 ENABLED = os.environ.get("KFA_CONV_IGEMM", "1") != "0"
@@ -84,6 +89,19 @@ def _time_ms(fn, reps: int = 5) -> float:
     return s.elapsed_time(e) / reps
 
 
+def _agree(hit: bool, device) -> bool:
+    """Data-parallel ranks must run the same kernels: rank 0's tuning decision wins
+    (every rank reaches each layer's first use in the same order, so this
+    one-element broadcast is matched)."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return hit
+    dev = device if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([1 if hit else 0], dtype=torch.int32, device=dev)
+    dist.broadcast(t, 0)
+    return bool(t.item())
+
+
 def _use_vendor_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, stats) -> bool:
     if not (TUNE and x.is_cuda):
         return False
@@ -104,7 +122,7 @@ def _use_vendor_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, sta
             M, C = y.numel() // y.shape[1], y.shape[1]
             t_vendor += _time_ms(lambda: _lib.call("kfa_bn_stats_partial", _lib.ptr(y), _lib.ptr(scratch), M, C,
                                                    _lib.stream()))
-    hit = _fwd_plan[key] = t_vendor < 0.95 * t_ours
+    hit = _fwd_plan[key] = _agree(t_vendor < 0.95 * t_ours, x.device)
     if TUNE_LOG:
         print(f"[kfa conv tune] x{tuple(x.shape)} w{tuple(w.shape)} s{stride} stats={stats is not None}: "
               f"igemm {t_ours:.3f} ms, vendor{'+stats' if stats is not None else ''} {t_vendor:.3f} ms -> "
@@ -112,10 +130,13 @@ def _use_vendor_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, sta
     return hit
 
 
+NARROW = int(os.environ.get("KFA_CONV_NARROW", "3"))  # tile variant for N <= 64: 1 = 128x64, 3 = 256x64
+
+
 def _variant(M: int, N: int, K: int = 0) -> int:
     """Tile shape of one implicit-GEMM launch: M output pixels x N channels, reduction K."""
     if N <= 64:
-        return 1
+        return NARROW
     if BIG and N % 256 == 0 and K >= BIG_MIN_K:
         return 2
     return 0
@@ -142,12 +163,74 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, stats=None
 
 
 def _transposed_weight(w: torch.Tensor, r0: int, dr: int, Rs: int, s0: int, ds: int, Ss: int) -> torch.Tensor:
+    if Rs * Ss and getattr(w, "_kfa_flat", False) and BATCHED_TRANSPOSE:
+        return _tcache.get(w, r0, dr, Rs, s0, ds, Ss)
     Co, Ci, R, S = w.shape
     wt = torch.empty((Ci, Rs, Ss, Co), dtype=w.dtype, device=w.device)
     if Rs * Ss:
         _lib.call("kfa_weight_transpose", _lib.ptr(w), _lib.ptr(wt), Co, R, S, Ci, r0, dr, Rs, s0, ds, Ss,
                   _lib.stream())
     return wt
+
+
+BATCHED_TRANSPOSE = os.environ.get("KFA_BATCHED_TRANSPOSE", "1") != "0"
+
+
+class _TransposeCache:
+    """The dgrad operand ``W -> [Cin][taps][Cout]`` of every flat-buffer conv weight,
+    refreshed by ONE batched launch at the first dgrad of each backward pass
+    (the forward marks it stale; the weights are final by then).  A transpose
+    met for the first time is computed on its own and joins the batch from the
+    next step on."""
+
+    def __init__(self):
+        self.entries = {}      # key -> (w, wt, args)
+        self.stale = True
+        self._table = None     # (descs uint8 device tensor, first int32 device tensor, n, total)
+
+    def mark_stale(self) -> None:
+        self.stale = True
+
+    def _build_table(self, device) -> None:
+        import struct
+        tdesc = _lib.lib().kfa_tdesc_bytes()
+        blob, first, total = bytearray(), [], 0
+        for w, wt, (Co, R, S, Ci, r0, dr, Rs, s0, ds, Ss) in self.entries.values():
+            gx, gy = -(-Ci // 32), -(-Co // 32)
+            rec = struct.pack("<QQ12i", w.data_ptr(), wt.data_ptr(), Co, R, S, Ci, r0, dr, Rs, s0, ds, Ss, gx, gy)
+            blob += rec + bytes(tdesc - len(rec))
+            first.append(total)
+            total += gx * gy * Rs * Ss
+        descs = torch.frombuffer(blob, dtype=torch.uint8).to(device)
+        firsts = torch.tensor(first, dtype=torch.int32).to(device)
+        self._table = (descs, firsts, len(first), total)
+
+    def refresh(self, device) -> None:
+        self.stale = False
+        if not self.entries:
+            return
+        if self._table is None:
+            self._build_table(device)
+        descs, firsts, n, total = self._table
+        _lib.call("kfa_weight_transpose_multi", _lib.ptr(descs), _lib.ptr(firsts), n, total, _lib.stream())
+
+    def get(self, w, r0, dr, Rs, s0, ds, Ss) -> torch.Tensor:
+        if self.stale:
+            self.refresh(w.device)
+        key = (w.data_ptr(), tuple(w.shape), r0, dr, Rs, s0, ds, Ss)
+        hit = self.entries.get(key)
+        if hit is not None:
+            return hit[1]
+        Co, Ci, R, S = w.shape
+        wt = torch.empty((Ci, Rs, Ss, Co), dtype=w.dtype, device=w.device)
+        _lib.call("kfa_weight_transpose", _lib.ptr(w), _lib.ptr(wt), Co, R, S, Ci, r0, dr, Rs, s0, ds, Ss,
+                  _lib.stream())
+        self.entries[key] = (w, wt, (Co, R, S, Ci, r0, dr, Rs, s0, ds, Ss))
+        self._table = None
+        return wt
+
+
+_tcache = _TransposeCache()
 
 
 def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride: int, pad: int, addend=None,
@@ -244,7 +327,7 @@ def _use_vendor_wgrad(x: torch.Tensor, dy: torch.Tensor, w: torch.Tensor, stride
         t_ours = _time_ms(lambda: wgrad_into(x, dy, acc, Nb, H, W, Ci, dy.shape[2], dy.shape[3], Co, R, S, stride, pad,
                                              True))
         t_vendor = _time_ms(lambda: acc.add_(conv_wgrad_vendor(x, dy, w, stride, pad)))
-    hit = _wgrad_plan[key] = t_vendor < 0.95 * t_ours
+    hit = _wgrad_plan[key] = _agree(t_vendor < 0.95 * t_ours, x.device)
     if TUNE_LOG:
         print(f"[kfa conv tune] wgrad x{tuple(x.shape)} w{tuple(w.shape)} s{stride}: ours {t_ours:.3f} ms, "
               f"vendor {t_vendor:.3f} ms -> {'vendor' if hit else 'ours'}", file=sys.stderr, flush=True)
@@ -343,6 +426,7 @@ class _ConvFn(torch.autograd.Function):
         ctx.bn_link = getattr(x, "_kfa_bn_link", None)  # x = output of a BatchNorm (see conv_dgrad)
         if ctx.bn_link is not None:
             ctx.bn_link.convs += 1
+        _tcache.mark_stale()  # weights may have changed since the last backward
         if vendor:
             return _cl(F.conv2d(_cl(x), _cl(w), None, stride, pad))
         return conv_fwd(x, w, stride, pad, stats)
@@ -389,10 +473,81 @@ def apply_bit_mask(t: torch.Tensor, bits: torch.Tensor) -> torch.Tensor:
     return out.view_as(t)
 
 
+def stem_ok(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int) -> bool:
+    """A few-channel stride-2 conv (the 7x7 ResNet stem) the space-to-depth path covers."""
+    return (ENABLED and x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.dim() == 4
+            and x.shape[1] <= 4 and stride == 2 and w.shape[2] == w.shape[3] and w.shape[2] <= 8
+            and (x.shape[2] + 2 * pad) % 2 == 0 and (x.shape[3] + 2 * pad) % 2 == 0 and w.shape[0] % 64 == 0)
+
+
+def stem_inputs(x: torch.Tensor, w: torch.Tensor, pad: int):
+    """Space-to-depth views of the stem (``csrc/kernels/stem.hip``): xs [N,16,Hs,Ws], ws [Co,16,Rs,Ss]."""
+    x, w = _cl(x), _cl(w)
+    Nb, C, H, W = x.shape
+    Co, _, R, S = w.shape
+    Hs, Ws = (H + 2 * pad) // 2, (W + 2 * pad) // 2
+    Rs, Ss = (R + 1) // 2, (S + 1) // 2
+    xs = torch.empty((Nb, 16, Hs, Ws), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+    ws = torch.empty((Co, 16, Rs, Ss), dtype=w.dtype, device=w.device, memory_format=torch.channels_last)
+    st = _lib.stream()
+    _lib.call("kfa_stem_s2d", _lib.ptr(x), _lib.ptr(xs), Nb, H, W, C, pad, st)
+    _lib.call("kfa_stem_weight_s2d", _lib.ptr(w), _lib.ptr(ws), Co, R, S, C, st)
+    return xs, ws
+
+
+class _StemConvFn(torch.autograd.Function):
+    """The 3-channel stride-2 stem as a stride-1 4x4 conv over the space-to-depth
+    input: forward and weight gradient on the same MFMA kernels as every other
+    conv (no vendor kernel, BatchNorm statistics fused)."""
+
+    @staticmethod
+    def forward(ctx, x, w, stride, pad, stats):
+        xs, ws = stem_inputs(x, w, pad)
+        y = conv_fwd(xs, ws, 1, 0, stats)
+        ctx.save_for_backward(xs, w)
+        ctx.x_shape, ctx.stride, ctx.pad = x.shape, stride, pad
+        ctx.wparam = w
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xs, w = ctx.saved_tensors
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.nn.grad.conv2d_input(ctx.x_shape, w, dy, ctx.stride, ctx.pad)
+        if ctx.needs_input_grad[1]:
+            dy = _cl(dy)
+            Nb, _, Hs, Ws = xs.shape
+            Co, C, R, S = w.shape
+            Rs, Ss = (R + 1) // 2, (S + 1) // 2
+            dws = torch.empty((Co, Rs, Ss, 16), dtype=torch.float32, device=dy.device)
+            wgrad_into(xs, dy, dws, Nb, Hs, Ws, 16, dy.shape[2], dy.shape[3], Co, Rs, Ss, 1, 0, accumulate=False)
+            target = direct_grad_view(ctx.wparam)
+            direct = target is not None and target.dtype in (torch.bfloat16, torch.float32) and \
+                target.is_contiguous(memory_format=torch.channels_last)
+            out = target if direct else torch.empty_like(w, memory_format=torch.channels_last)
+            _lib.call("kfa_stem_wgrad_fold", _lib.ptr(dws), _lib.ptr(out), int(out.dtype == torch.float32),
+                      int(direct), Co, R, S, C, _lib.stream())
+            if direct:
+                notify_grad_ready(ctx.wparam)
+            else:
+                dw = out
+        return dx, dw, None, None, None
+
+
 def conv2d(x, w, stride: int = 1, pad: int = 0, join: "GradJoin | None" = None, bn_stats: bool = False):
     """``bn_stats``: the caller guarantees a training-mode ``BatchNorm2dAct``
     consumes the output next; the epilogue then accumulates its statistics and
     the output is tagged ``_kfa_prestats`` (the BN skips its stats pass)."""
+    if stem_ok(x, w, stride, pad) and join is None:
+        stats = None
+        if bn_stats:
+            from .batchnorm import bn_slot_workspace
+            stats = bn_slot_workspace(w.shape[0], x.device)
+        y = _StemConvFn.apply(x, w, stride, pad, stats)
+        if stats is not None:
+            y._kfa_prestats = True
+        return y
     if igemm_ok(x, w):
         if join is not None:
             join.fused = True

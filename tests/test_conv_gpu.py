@@ -334,3 +334,85 @@ def test_resnet_masked_residual_gradient():
         if e_m > 2.0 * e_p + 0.02 * scale:
             bad.append((n, e_m, e_p, scale))
     assert not bad, bad
+
+
+@pytest.mark.parametrize("N,H,W,C", [(2, 224, 224, 3), (3, 32, 18, 3), (2, 20, 20, 1)])
+def test_stem_space_to_depth_fwd_wgrad(N, H, W, C):
+    """7x7/s2/p3 few-channel stem as a 4x4 stride-1 conv over the space-to-depth
+    input (stem.hip + conv_igemm C=16 + wgrad C=16 + fold) vs fp32 PyTorch;
+    also its fused BatchNorm statistics."""
+    from kubeflow_controller_amd.ops import _lib
+    from kubeflow_controller_amd.ops.conv import conv2d, stem_ok
+    torch.manual_seed(0)
+    d = torch.device("cuda")
+    x = torch.randn(N, C, H, W, device=d).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(64, C, 7, 7, device=d) / (C * 49) ** 0.5).to(torch.bfloat16)
+    w = w.contiguous(memory_format=torch.channels_last)
+    assert stem_ok(x, w, 2, 3)
+    wr = w.clone().requires_grad_()
+    y = conv2d(x, wr, 2, 3)
+    wf = w.float().requires_grad_()
+    yf = torch.nn.functional.conv2d(x.float(), wf, None, 2, 3)
+    assert y.shape == yf.shape and y.is_contiguous(memory_format=torch.channels_last)
+    err = (y.float() - yf).abs().max().item()
+    assert err < 2e-2 * max(1.0, yf.abs().max().item()), err
+    dy = torch.randn_like(yf)
+    y.backward(dy.to(torch.bfloat16))
+    yf.backward(dy)
+    gw = (wr.grad.float() - wf.grad).abs().max().item()
+    assert gw < 3e-2 * max(1.0, wf.grad.abs().max().item()), gw
+    # fused BatchNorm statistics (sum, sum of squares per channel) land in the BN slots
+    from kubeflow_controller_amd.ops.batchnorm import bn_slot_workspace
+    ws = bn_slot_workspace(64, x.device)
+    ws = ws.view(torch.float32) if ws.dtype != torch.float32 else ws
+    torch.cuda.synchronize()
+    ws.zero_()
+    y2 = conv2d(x, w, 2, 3, bn_stats=True)
+    torch.cuda.synchronize()
+    slots = ws[: _lib.lib().kfa_bn_slot_floats(64)].view(-1, 2, 64).sum(0)
+    yb = y2.float().permute(0, 2, 3, 1).reshape(-1, 64)
+    torch.testing.assert_close(slots[0], yb.sum(0), rtol=1e-3, atol=1e-1)
+    torch.testing.assert_close(slots[1], (yb * yb).sum(0), rtol=1e-3, atol=1e-1)
+    ws.zero_()
+
+
+def test_batched_dgrad_weight_transpose_tracks_weight_updates(monkeypatch):
+    """The per-step batched dgrad weight transpose (one launch for every conv,
+    refreshed after each forward) gives bit-identical training to per-call
+    transposes while the optimizer changes the weights every step."""
+    from kubeflow_controller_amd.ops import conv as convmod
+    from kubeflow_controller_amd.ops.conv import Conv2d
+    from kubeflow_controller_amd.trainer.engine import DistInfo, Engine
+
+    class Net(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = Conv2d(64, 64, 3, 1, 1)
+            self.b = Conv2d(64, 128, 3, 2, 1)
+            self.c = Conv2d(128, 128, 1, 2, 0)
+
+        def forward(self, x):
+            return self.c(torch.relu(self.b(torch.relu(self.a(x)))))
+
+    def run(batched):
+        monkeypatch.setattr(convmod, "BATCHED_TRANSPOSE", batched)
+        convmod._tcache = convmod._TransposeCache()
+        torch.manual_seed(0)
+        d = torch.device("cuda")
+        eng = Engine(Net(), lambda m, x: m(x).float().pow(2).mean(), optimizer="sgd", lr=0.5, momentum=0.0,
+                     weight_decay=0.0, dist_info=DistInfo(device=d))
+        x = torch.randn(4, 64, 16, 16, device=d).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        x.requires_grad_()
+        out = []
+        for _ in range(4):
+            x.grad = None
+            out.append(float(eng.train_step(x)))
+            out.append(x.grad.float().sum().item())
+        return out, [g.grad.clone() for g in eng.groups]
+
+    a, ga = run(False)
+    b, gb = run(True)
+    assert a == b
+    for u, v in zip(ga, gb):
+        assert torch.equal(u, v)
+    assert len(convmod._tcache.entries) == 6  # a: 1; b (3x3/s2): 4 parity classes; c (1x1/s2): 1 class with taps

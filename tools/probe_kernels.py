@@ -33,11 +33,19 @@ def main(op: str, iters: int = 5) -> None:
         fn = (lambda: T.attn_fwd(qkv, bqkv, kb, B, S, h, 0.1, 1)) if op == "attn_fwd" else \
             (lambda: T.attn_bwd(qkv, bqkv, kb, out, lse, dout, db, B, S, h, 0.1, 1))
     elif op.startswith("conv_"):
+        # conv_fwd_3x3_14 (legacy name) or conv_{fwd,dgrad}_<Cin>_<H>_<Cout>_<k>_<stride>
         from kubeflow_controller_amd.ops.conv import conv_dgrad, conv_fwd
-        x = bf(256, 256, 14, 14).contiguous(memory_format=torch.channels_last)
-        w = (bf(256, 256, 3, 3) * 0.05).contiguous(memory_format=torch.channels_last)
-        dy = bf(256, 256, 14, 14).contiguous(memory_format=torch.channels_last)
-        fn = (lambda: conv_fwd(x, w, 1, 1)) if "fwd" in op else (lambda: conv_dgrad(dy, w, x.shape, 1, 1))
+        parts = op.split("_")
+        if len(parts) == 7:
+            cin, hh, cout, k, st = (int(v) for v in parts[2:])
+        else:
+            cin, hh, cout, k, st = 256, 14, 256, 3, 1
+        pad = k // 2
+        ho = (hh + 2 * pad - k) // st + 1
+        x = bf(256, cin, hh, hh).contiguous(memory_format=torch.channels_last)
+        w = (bf(cout, cin, k, k) * 0.05).contiguous(memory_format=torch.channels_last)
+        dy = bf(256, cout, ho, ho).contiguous(memory_format=torch.channels_last)
+        fn = (lambda: conv_fwd(x, w, st, pad)) if "fwd" in op else (lambda: conv_dgrad(dy, w, x.shape, st, pad))
     elif op == "gemm_nt":
         from kubeflow_controller_amd.ops import gemm as G
         a, b = bf(32768, 768), bf(3072, 768)
