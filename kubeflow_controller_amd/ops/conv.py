@@ -130,7 +130,7 @@ def _use_vendor_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, sta
     return hit
 
 
-NARROW = int(os.environ.get("KFA_CONV_NARROW", "3"))  # tile variant for N <= 64: 1 = 128x64, 3 = 256x64
+NARROW = int(os.environ.get("KFA_CONV_NARROW", "1"))  # tile variant for N <= 64: 1 = 128x64, 3 = 256x64
 
 
 def _variant(M: int, N: int, K: int = 0) -> int:
