@@ -29,7 +29,21 @@
 // the write-out is 16 B per lane, 8 rows x 128 B per wave instruction.
 #include "common.h"
 
+#include <utility>
+
 namespace {
+
+// Compile-time loop: f(std::integral_constant<int, 0>) ... f(<N-1>) — keeps
+// register-array indices constant where `#pragma unroll` is not honoured
+// (a runtime index sends the whole accumulator array to scratch, rule 20).
+template <class F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
 
 constexpr int GK = 32;     // k per ring slot (one MFMA k-step)
 constexpr int NSLOT = 4;   // ring depth: prefetch distance NSLOT - 1
@@ -279,6 +293,261 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(GemmArgs g, const bf16_t* 
   }
 }
 
+// ---------------------------------------------------------------------------
+// Persistent variant: one 512-thread block per CU sweeps a contiguous range of
+// tiles (XCD-aware, grouped raster) and the 4-slot LDS-DMA ring runs straight
+// across tile boundaries — the next tile's first three k-steps land while the
+// current tile's last MFMAs and its epilogue run, so the per-tile ring fill is
+// paid once per block, not once per tile (the fixed cost that held the
+// per-tile kernel at ~27 % MFMA busy on K = 768, docs/kernels.md).
+// The epilogue stages each wave's rows through a PRIVATE 4 KB LDS area (32
+// rows x 128 B per pass), so it needs no workgroup barrier and never touches
+// the ring.  Its stores are fire-and-forget: the counted vmcnt before each
+// k-step's barrier leaves them (and the younger k-steps) in flight —
+//   N(s) = GL * (k-steps issued after s+1) + XS * (epilogues issued after s+1)
+// with XS = the epilogue's C-store instructions.  Other epilogue VMEM ops
+// (addend / pre-activation / derivative loads and stores, dbias atomics) only
+// make N an under-count of the younger operations: safe, merely slower.
+// Bias values are read with wave-uniform scalar loads (lgkmcnt, not vmcnt).
+template <int BN>
+__global__ __launch_bounds__(512) void gemm_pt_kernel(GemmArgs g, const bf16_t* __restrict__ zp) {
+  constexpr int BM = 256;
+  constexpr int WN = BN / 64, WM = 8 / WN;
+  constexpr int TM = BM / WM / 16, TN = 4;
+  constexpr int A_SLOT = BM * GK, B_SLOT = BN * GK;
+  constexpr int GA = BM / 128, GB = BN / 128;
+  constexpr int GL = GA + GB;
+  constexpr int PASSES = TM / 2;            // 32 staged rows per pass
+  constexpr int XS = PASSES * 4;            // C-store instructions per epilogue (4 per pass per lane)
+  constexpr int STG = 32 * 128;             // bytes of private staging per wave
+  __shared__ __attribute__((aligned(16))) bf16_t smem[NSLOT * (A_SLOT + B_SLOT) + 8 * STG / 2];
+  bf16_t* As = smem;
+  bf16_t* Bs = smem + NSLOT * A_SLOT;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  const int ntn = (g.N + BN - 1) / BN, ntm = (g.M + BM - 1) / BM;
+  const int ntiles = ntm * ntn;
+  // blocks that share an XCD (b % 8) sweep one contiguous range of the tile order
+  const int nwg = gridDim.x;
+  const int G8 = nwg < 8 ? nwg : 8;
+  const int xcd = blockIdx.x % G8, slot = blockIdx.x / G8;
+  const int nslot = (nwg - xcd + G8 - 1) / G8;
+  const int t_lo = (int)((long)ntiles * xcd / G8), t_hi = (int)((long)ntiles * (xcd + 1) / G8);
+  const int my_tiles = t_hi - t_lo > slot ? (t_hi - t_lo - slot + nslot - 1) / nslot : 0;
+  constexpr int GM = 4;
+  auto tile_mn = [&](int i, int& m0, int& n0) __attribute__((always_inline)) {
+    const int wg = t_lo + slot + i * nslot;
+    const int grp = wg / (GM * ntn), gm0 = grp * GM, gmn = min(GM, ntm - gm0), rem = wg - grp * GM * ntn;
+    m0 = (gm0 + rem % gmn) * BM;
+    n0 = (rem / gmn) * BN;
+  };
+
+  const int lrow = lane >> 2, lch = (lane & 3) ^ ((lane >> 4) & 2);
+  const bf16_t* a_src[GA];
+  const bf16_t* b_src[GB];
+  int src_tile = -1;
+  const int nk = (g.K + GK - 1) / GK;
+  const int total = my_tiles * nk;
+  auto issue = [&](int s) __attribute__((always_inline)) {
+    const int ti = s / nk, kt = s - ti * nk;
+    if (ti != src_tile) {
+      int m0, n0;
+      tile_mn(ti, m0, n0);
+#pragma unroll
+      for (int i = 0; i < GA; i++) {
+        const int m = m0 + (wave * GA + i) * 16 + lrow;
+        a_src[i] = m < g.M ? g.A + (long)m * g.lda + lch * 8 : nullptr;
+      }
+#pragma unroll
+      for (int i = 0; i < GB; i++) {
+        const int n = n0 + (wave * GB + i) * 16 + lrow;
+        b_src[i] = n < g.N ? g.B + (long)n * g.ldb + lch * 8 : nullptr;
+      }
+      src_tile = ti;
+    }
+    const int sl = s & (NSLOT - 1), k0 = kt * GK;
+    const bool kin = k0 + lch * 8 < g.K;
+#pragma unroll
+    for (int i = 0; i < GA; i++)
+      lds_dma16((a_src[i] && kin) ? a_src[i] + k0 : zp, As + sl * A_SLOT + (wave * GA + i) * 16 * GK);
+#pragma unroll
+    for (int i = 0; i < GB; i++)
+      lds_dma16((b_src[i] && kin) ? b_src[i] + k0 : zp, Bs + sl * B_SLOT + (wave * GB + i) * 16 * GK);
+  };
+
+  const int fr = lane & 15, fq = lane >> 4;
+  const int loff = fr * GK + ((fq ^ ((fr >> 2) & 2)) << 3);
+  floatx4 acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; i++)
+#pragma unroll
+    for (int j = 0; j < TM; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  char* stage = reinterpret_cast<char*>(smem + NSLOT * (A_SLOT + B_SLOT)) + wave * STG;
+  const int wn_u = __builtin_amdgcn_readfirstlane(wn), wm_u = __builtin_amdgcn_readfirstlane(wm);
+  const __amdgpu_buffer_rsrc_t rC = rsrc(g.C, g.c_bytes);
+  const __amdgpu_buffer_rsrc_t rE = rsrc(g.E ? g.E : g.C, g.E ? g.c_bytes : 0u);
+  const __amdgpu_buffer_rsrc_t rZ = rsrc(g.Z ? g.Z : g.C, g.Z ? g.c_bytes : 0u);
+  const __amdgpu_buffer_rsrc_t rZi = rsrc(g.Zin ? g.Zin : g.C, g.Zin ? g.c_bytes : 0u);
+
+  auto epilogue = [&](int ti) __attribute__((always_inline)) {
+    int m0, n0;
+    tile_mn(ti, m0, n0);
+    const int nw = n0 + wn_u * 64;
+    if (g.bias) {  // wave-uniform scalar loads (constant address space -> s_load) of the wave's 64 bias values
+      const int nb = __builtin_amdgcn_readfirstlane(nw);
+      typedef __attribute__((address_space(4))) const float cfloat;
+      cfloat* cbias = reinterpret_cast<cfloat*>(reinterpret_cast<uintptr_t>(g.bias));
+#pragma unroll
+      for (int ni = 0; ni < TN; ni++) {
+        float b4[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          // column nb + 16 ni + 4 q' + r for this lane's q' = fq: select among the 4 uniform quads
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            const int col = nb + ni * 16 + q * 4 + r;
+            v[r] = col < g.N ? cbias[col] : 0.f;
+          }
+          if (q == 0) { b4[0] = v[0]; b4[1] = v[1]; b4[2] = v[2]; b4[3] = v[3]; }
+          else if (fq == q) { b4[0] = v[0]; b4[1] = v[1]; b4[2] = v[2]; b4[3] = v[3]; }
+        }
+#pragma unroll
+        for (int mi = 0; mi < TM; mi++) {
+          acc[ni][mi][0] += b4[0];
+          acc[ni][mi][1] += b4[1];
+          acc[ni][mi][2] += b4[2];
+          acc[ni][mi][3] += b4[3];
+        }
+      }
+    }
+    const int c = lane & 7;
+    const int n = nw + c * 8;
+    const bool nok = n < g.N;
+    float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    static_for<PASSES>([&](auto psc) {
+      constexpr int ps = decltype(psc)::value;
+#pragma unroll
+      for (int mj = 0; mj < 2; mj++)
+#pragma unroll
+        for (int ni = 0; ni < TN; ni++) {
+          const int mi = ps * 2 + mj;
+          const int row = mj * 16 + fr, col = ni * 16 + fq * 4;
+          *reinterpret_cast<uint2*>(stage + row * 128 + (((col >> 3) ^ (row & 7)) << 4) + (col & 7) * 2) =
+              make_uint2(pack2(acc[ni][mi][0], acc[ni][mi][1]), pack2(acc[ni][mi][2], acc[ni][mi][3]));
+        }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave reads back only its own stage
+      uint4 v[4];
+#pragma unroll
+      for (int it = 0; it < 4; it++) {
+        const int r = it * 8 + (lane >> 3);
+        v[it] = *reinterpret_cast<const uint4*>(stage + r * 128 + ((c ^ (r & 7)) << 4));
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // next pass overwrites the stage
+#pragma unroll
+      for (int it = 0; it < 4; it++) {
+        const int r = it * 8 + (lane >> 3);
+        const int m = m0 + wm_u * (16 * TM) + ps * 32 + r;
+        const unsigned off = (m < g.M && nok) ? ((unsigned)m * (unsigned)g.ldc + (unsigned)n) * 2u : kOOB;
+        float f[8];
+        unpack8(v[it], f);
+        if (g.E) {
+          float h[8];
+          unpack8(bload(rE, off), h);
+#pragma unroll
+          for (int j = 0; j < 8; j++) f[j] += h[j];
+        }
+        if (g.Z) bstore(rZ, off, pack8(f));
+        if (g.act) {
+#pragma unroll
+          for (int j = 0; j < 8; j++) f[j] = act_fwd(f[j], g.act);
+        }
+        if (g.Zin) {
+          float z[8];
+          unpack8(bload(rZi, off), z);
+#pragma unroll
+          for (int j = 0; j < 8; j++) f[j] *= act_bwd(z[j], g.dact);
+        }
+        const uint4 o = pack8(f);
+        bstore(rC, off, o);
+        if (g.dbias && off != kOOB) {
+          float q[8];
+          unpack8(o, q);
+#pragma unroll
+          for (int j = 0; j < 8; j++) cs[j] += q[j];
+        }
+      }
+    });
+    if (g.dbias) {
+#pragma unroll
+      for (int o = 8; o < 64; o <<= 1)
+#pragma unroll
+        for (int j = 0; j < 8; j++) cs[j] += __shfl_xor(cs[j], o, 64);
+      if (lane < 8 && nok)
+#pragma unroll
+        for (int j = 0; j < 8; j++) atomicAdd(g.dbias + n + j, cs[j]);
+    }
+#pragma unroll
+    for (int i = 0; i < TN; i++)
+#pragma unroll
+      for (int j = 0; j < TM; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  };
+
+  if (total == 0) return;
+  issue(0);
+  if (total > 1) issue(1);
+  if (total > 2) issue(2);
+  ring_wait<GL>(total > 2 ? 2 : total - 1);
+  asm volatile("s_barrier" ::: "memory");
+  for (int s = 0; s < total; s++) {
+    if (s + 3 < total) issue(s + 3);  // slot (s+3)&3 = (s-1)&3: every wave passed the barrier after reading it
+    const int kt = s % nk;
+    const bf16_t* At = As + (s & (NSLOT - 1)) * A_SLOT + wm * TM * 16 * GK + loff;
+    const bf16_t* Bt = Bs + (s & (NSLOT - 1)) * B_SLOT + wn * TN * 16 * GK + loff;
+    short8 af[TM], bq[TN];
+#pragma unroll
+    for (int i = 0; i < TN; i++) bq[i] = *reinterpret_cast<const short8*>(Bt + i * 16 * GK);
+#pragma unroll
+    for (int i = 0; i < TM; i++) af[i] = *reinterpret_cast<const short8*>(At + i * 16 * GK);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ni = 0; ni < TN; ni++)
+#pragma unroll
+      for (int mi = 0; mi < TM; mi++)
+        acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[ni], af[mi], acc[ni][mi], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    if (kt == nk - 1) epilogue(s / nk);
+    if (s + 1 < total) {
+      // ops issued after k-step s+1: younger k-steps, plus the stores of epilogues run at
+      // iterations s-2..s (each issued after that iteration's k-step issue)
+      const int steps = min(s + 3, total - 1) - (s + 1);
+      int eps = 0;
+#pragma unroll
+      for (int e = 0; e < 3; e++) {
+        const int ei = s - e;
+        if (ei >= 0 && ei % nk == nk - 1) eps++;
+      }
+      const int nwait = GL * steps + XS * eps;
+      switch (nwait) {
+#define KFA_VMW(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+        KFA_VMW(0) KFA_VMW(1) KFA_VMW(2) KFA_VMW(3) KFA_VMW(4) KFA_VMW(5) KFA_VMW(6) KFA_VMW(7)
+        KFA_VMW(8) KFA_VMW(9) KFA_VMW(10) KFA_VMW(11) KFA_VMW(12) KFA_VMW(13) KFA_VMW(14) KFA_VMW(15)
+        KFA_VMW(16) KFA_VMW(17) KFA_VMW(18) KFA_VMW(19) KFA_VMW(20) KFA_VMW(21) KFA_VMW(22) KFA_VMW(23)
+        KFA_VMW(24) KFA_VMW(25) KFA_VMW(26) KFA_VMW(27) KFA_VMW(28) KFA_VMW(29) KFA_VMW(30) KFA_VMW(31)
+        KFA_VMW(32) KFA_VMW(33) KFA_VMW(34) KFA_VMW(35) KFA_VMW(36) KFA_VMW(37) KFA_VMW(38) KFA_VMW(39)
+        KFA_VMW(40) KFA_VMW(41) KFA_VMW(42) KFA_VMW(43) KFA_VMW(44) KFA_VMW(45) KFA_VMW(46) KFA_VMW(47)
+        KFA_VMW(48) KFA_VMW(49) KFA_VMW(50) KFA_VMW(51) KFA_VMW(52) KFA_VMW(53) KFA_VMW(54) KFA_VMW(55)
+        KFA_VMW(56) KFA_VMW(57) KFA_VMW(58) KFA_VMW(59) KFA_VMW(60) KFA_VMW(61) KFA_VMW(62)
+#undef KFA_VMW
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+  }
+}
+
 }  // namespace
 
 static const bf16_t* gemm_zero_page() {
@@ -312,10 +581,11 @@ KFA_API int kfa_gemm_pick_bn(int M, int N) {
   return (N <= 128 || 0.55 * (double)w128 < (double)w256) ? 128 : 256;
 }
 
-// C = epilogue(A · Bᵀ); see the file comment.  bn: 0 = auto, 128 or 256.
+// C = epilogue(A · Bᵀ); see the file comment.  bn: 0 = auto, 128 or 256;
+// persistent: the tile-sweeping kernel (K >= 64), else one block per tile.
 KFA_API int kfa_gemm_nt(const bf16_t* A, const bf16_t* B, bf16_t* C, const bf16_t* E, const float* bias, bf16_t* Z,
                         const bf16_t* Zin, float* dbias, int M, int N, int K, int lda, int ldb, int ldc, int act,
-                        int dact, int bn, hipStream_t st) {
+                        int dact, int bn, int persistent, hipStream_t st) {
   if (M <= 0 || N <= 0) return 0;
   if (K <= 0 || K % 8 || N % 8 || lda % 8 || ldb % 8 || ldc % 8 || lda < K || ldb < K || ldc < N) return -1;
   if (act < 0 || act > 3 || dact < 0 || dact > 3) return -1;
@@ -325,6 +595,17 @@ KFA_API int kfa_gemm_nt(const bf16_t* A, const bf16_t* B, bf16_t* C, const bf16_
   const long tiles = (long)((M + 255) / 256) * ((N + bn - 1) / bn);
   if (tiles >= (1L << 31)) return -2;
   const GemmArgs g{A, B, C, E, bias, Z, Zin, dbias, M, N, K, lda, ldb, ldc, act, dact, (unsigned)cb};
+  if (persistent && K >= 2 * GK) {
+    const long cus = gemm_cus();
+    const int grid = (int)(tiles < cus ? tiles : cus);
+    if (bn == 256)
+      hipLaunchKernelGGL((gemm_pt_kernel<256>), dim3(grid), dim3(512), 0, st, g, gemm_zero_page());
+    else if (bn == 128)
+      hipLaunchKernelGGL((gemm_pt_kernel<128>), dim3(grid), dim3(512), 0, st, g, gemm_zero_page());
+    else
+      return -1;
+    return kfa_status();
+  }
   if (bn == 256)
     hipLaunchKernelGGL((gemm_nt_kernel<256>), dim3((unsigned)tiles), dim3(512), 0, st, g, gemm_zero_page());
   else if (bn == 128)

@@ -28,7 +28,7 @@ from . import _lib
 from . import conv as _conv  # noqa: F401  (registers kfa_weight_transpose)
 
 P, I = _lib.P, _lib.I
-_lib.register("kfa_gemm_nt", [P] * 8 + [I] * 9 + [P])
+_lib.register("kfa_gemm_nt", [P] * 8 + [I] * 10 + [P])
 _lib.register("kfa_gemm_pick_bn", [I, I])
 
 ACTS = {None: 0, "none": 0, "gelu": 1, "tanh": 2, "relu": 3}
@@ -62,8 +62,11 @@ def _check_vec(t, N, what):
         raise ValueError(f"gemm_nt: {what} must be a contiguous, 16-B aligned fp32 [{N}] vector")
 
 
+PERSISTENT = os.environ.get("KFA_GEMM_PERSIST", "0") == "1"  # measured slower (tools/bench_gemm.py): opt-in
+
+
 def gemm_nt(a, b, *, bias=None, act=None, addend=None, want_z=False, zin=None, dact=None, dbias=None, out=None,
-            bn: int = 0):
+            bn: int = 0, persistent=None):
     """``(C, Z)`` with ``C = epilogue(a @ b.T)`` (see module doc); ``Z`` is None unless ``want_z``."""
     if not gemm_ok(a, b):
         raise ValueError(f"gemm_nt: unsupported operands {tuple(a.shape)}/{a.dtype} x {tuple(b.shape)}/{b.dtype}")
@@ -81,7 +84,7 @@ def gemm_nt(a, b, *, bias=None, act=None, addend=None, want_z=False, zin=None, d
     z = torch.empty_like(c) if want_z else None
     _lib.call("kfa_gemm_nt", _lib.ptr(a), _lib.ptr(b), _lib.ptr(c), _lib.ptr(addend), _lib.ptr(bias), _lib.ptr(z),
               _lib.ptr(zin), _lib.ptr(dbias), M, N, K, a.stride(0), b.stride(0), N, ACTS[act], ACTS[dact], int(bn),
-              _lib.stream())
+              int(PERSISTENT if persistent is None else persistent), _lib.stream())
     return c, z
 
 

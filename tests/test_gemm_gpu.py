@@ -18,6 +18,30 @@ def _bf(*shape, s=1.0):
     return (torch.randn(*shape, device=D) * s).to(torch.bfloat16)
 
 
+@pytest.fixture(params=[True, False], ids=["persistent", "per_tile"], autouse=True)
+def _persistent(request, monkeypatch):
+    """Every test runs on both GEMM kernels: the persistent tile-sweeping one
+    (default) and the one-block-per-tile one."""
+    from kubeflow_controller_amd.ops import gemm as G
+    monkeypatch.setattr(G, "PERSISTENT", request.param)
+    return request.param
+
+
+@pytest.mark.parametrize("M,N,K,bn", [(32768, 768, 768, 256), (20000, 2048, 64, 256), (9000, 1152, 96, 128),
+                                      (65536, 256, 128, 128)])
+def test_gemm_nt_many_tiles_per_block(M, N, K, bn):
+    """More tiles than CUs: the persistent kernel carries its LDS ring across
+    tiles (K = 64 / 96: an epilogue every 2 / 3 k-steps inside the vmcnt window)."""
+    from kubeflow_controller_amd.ops import gemm as G
+    torch.manual_seed(5)
+    a, b = _bf(M, K), _bf(N, K, s=0.05)
+    bias = torch.randn(N, device=D)
+    c, z = G.gemm_nt(a, b, bn=bn, bias=bias, act="gelu", want_z=True)
+    zr = a.float() @ b.float().t() + bias
+    _close(z, zr, 1e-2, f"Z {M}x{N}x{K}")
+    _close(c, torch.nn.functional.gelu(zr), 1e-2, f"C {M}x{N}x{K}")
+
+
 @pytest.mark.parametrize("M,N,K,bn", [(256, 256, 32, 256), (256, 128, 64, 128), (1000, 776, 96, 128),
                                       (333, 2304, 768, 0), (4096, 768, 3072, 128), (2048, 3072, 768, 256),
                                       (513, 136, 1680, 0), (40, 8, 8, 0)])
