@@ -157,6 +157,18 @@ class Supervisor:
         typ = pod.metadata.labels.get("job_type", "")
         return 1 if typ in (v1alpha1.WORKER, v1alpha1.LOCAL, "") else 0
 
+    def _colocated_gpu(self, pod: Pod) -> Optional[List[int]]:
+        """A PS replica whose template sets ``KFA_PS_COLOCATE=1`` shares GPU
+        ``index % num_gpus`` with the worker bound there (not an exclusive
+        binding): the device-resident async parameter server keeps its variables
+        in that GPU's HBM (``parallel/async_ps.py``)."""
+        if pod.metadata.labels.get("job_type", "") != v1alpha1.PS or self.num_gpus == 0:
+            return None
+        env = {e.name: e.value for e in pod.spec.containers[0].env}
+        if env.get("KFA_PS_COLOCATE") != "1":
+            return None
+        return [int(pod.metadata.labels.get("index", "0")) % self.num_gpus]
+
     def _bind_gpus(self, key: str, n: int) -> Optional[List[int]]:
         if n == 0:
             return []
@@ -249,7 +261,9 @@ class Supervisor:
         if not self._hosts_ready(pod, hosts):
             return  # endpoints not allocated yet: stay Pending
         if not p.gpus:
-            g = self._bind_gpus(p.key, self._wants_gpus(pod))
+            g = self._colocated_gpu(pod)
+            if g is None:
+                g = self._bind_gpus(p.key, self._wants_gpus(pod))
             if g is None:
                 return  # wait for free GPUs
             p.gpus = g

@@ -81,7 +81,7 @@ class WideDeep(nn.Module):
         cfg = self.cfg
         B, nf = ids.shape
         gids = (ids + self.offsets.view(1, nf)).reshape(-1)
-        rows = self.tables(gids).view(B, nf, cfg.row_width)               # bf16 [B, nf, E+8]
+        rows = self.tables(gids, getattr(ids, "_kfa_plan", None)).view(B, nf, cfg.row_width)  # [B, nf, E+8]
         deep_emb = rows[:, :, :cfg.embed_dim].reshape(B, nf * cfg.embed_dim)
         wide = rows[:, :, cfg.embed_dim].float().sum(1)
         cdt = self.weights[0].dtype
@@ -102,6 +102,19 @@ class WideDeep(nn.Module):
 
 def wide_deep_loss(model, *batch):
     return model(*batch)
+
+
+def prepare_batch(model: "WideDeep", dense: torch.Tensor, ids: torch.Tensor, labels: torch.Tensor, device):
+    """Host batch -> device batch whose ids carry the embedding exchange's split
+    sizes, computed on the host (``ShardedEmbedding.plan``) before the copy."""
+    plan = None
+    if model.tables.world > 1:
+        gids = ids.cpu() + model.offsets.cpu().view(1, -1)
+        plan = model.tables.plan(gids)
+    ids_d = ids.to(device)
+    if plan is not None:
+        ids_d._kfa_plan = plan
+    return dense.to(device), ids_d, labels.to(device)
 
 
 def synthetic_batch(cfg: WideDeepConfig, batch: int, generator=None, device="cpu"):

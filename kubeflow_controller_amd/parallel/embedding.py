@@ -16,7 +16,10 @@ the PS applies the optimizer (``:184, :256``).  MI355X design:
   that updates only the looked-up rows (``csrc/kernels/sparse.hip``) — applied
   during backward, so no dense gradient or optimizer state is ever touched
   for rows outside the batch;
-* with one rank (or CPU) the same code runs without collectives.
+* with one rank (or CPU) the same code runs without collectives;
+* the split sizes of the two exchanges come from :meth:`ShardedEmbedding.plan`
+  on the host copy of the ids (CPU bincount + a gloo all-to-all of the counts)
+  when the batch carries one, so the step never blocks on a device ``.tolist()``.
 
 Parameters marked ``_kfa_sparse`` are skipped by ``split_params`` (they are not
 part of the dense flat groups / all-reduce).
@@ -45,7 +48,7 @@ def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits: List[int], in_splits:
 
 class _LookupFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, ids, weight, emb: "ShardedEmbedding"):
+    def forward(ctx, ids, weight, emb: "ShardedEmbedding", plan=None):
         ids = ids.reshape(-1)
         n, D = ids.numel(), emb.dim
         comm = emb.world > 1
@@ -53,10 +56,13 @@ class _LookupFn(torch.autograd.Function):
             owner = ids % emb.owners
             order = torch.argsort(owner, stable=True)
             sorted_ids = ids.index_select(0, order)
-            send = torch.bincount(owner, minlength=emb.world)
-            recv = torch.empty_like(send)
-            dist.all_to_all_single(recv, send, group=emb.pg)
-            send_l, recv_l = send.tolist(), recv.tolist()
+            if plan is not None:   # split sizes known on the host already: no device sync
+                send_l, recv_l = plan
+            else:                  # derive them on the device (one D2H sync per lookup)
+                send = torch.bincount(owner, minlength=emb.world)
+                recv = torch.empty_like(send)
+                dist.all_to_all_single(recv, send, group=emb.pg)
+                send_l, recv_l = send.tolist(), recv.tolist()
             req = torch.empty(sum(recv_l), dtype=ids.dtype, device=ids.device)
             _a2a(req, sorted_ids, recv_l, send_l, emb.pg)
         else:
@@ -88,7 +94,7 @@ class _LookupFn(torch.autograd.Function):
         else:
             g = dout
         emb.apply_sparse(local, g)
-        return None, None, None
+        return None, None, None, None
 
 
 class ShardedEmbedding(nn.Module):
@@ -191,8 +197,28 @@ class ShardedEmbedding(nn.Module):
         else:
             w.index_add_(0, uniq, -self.lr * gs)
 
-    def forward(self, ids: torch.Tensor) -> torch.Tensor:
-        out = _LookupFn.apply(ids, self.weight, self)
+    def plan(self, ids_cpu: torch.Tensor):
+        """Host-side split sizes for a lookup of ``ids_cpu`` (a CPU tensor, e.g. the
+        data loader's batch before its H2D copy): the per-owner counts come from a
+        CPU bincount and the receive counts from an all-to-all on a gloo (host)
+        group, so the lookup itself never waits for the GPU (``.tolist()`` of a
+        device tensor would drain the stream every step)."""
+        if self.world == 1:
+            return None
+        ids_cpu = ids_cpu.reshape(-1).cpu()
+        send = torch.bincount(ids_cpu % self.owners, minlength=self.world)
+        recv = torch.empty_like(send)
+        dist.all_to_all_single(recv, send, group=self._meta_group())
+        return send.tolist(), recv.tolist()
+
+    def _meta_group(self):
+        if getattr(self, "_meta", None) is None:
+            backend = dist.get_backend(self.pg)
+            self._meta = self.pg if backend == "gloo" else dist.new_group(backend="gloo")
+        return self._meta
+
+    def forward(self, ids: torch.Tensor, plan=None) -> torch.Tensor:
+        out = _LookupFn.apply(ids, self.weight, self, plan)
         return out.view(*ids.shape, self.dim)
 
     def full_table(self) -> torch.Tensor:

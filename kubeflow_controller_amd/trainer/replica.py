@@ -89,8 +89,10 @@ def build(args, device):
     if name in ("wide_deep", "wide_deep_tiny"):
         from ..models.wide_deep import WideDeep, WideDeepConfig, wide_deep_loss
         cfg = WideDeepConfig() if name == "wide_deep" else WideDeepConfig.tiny()
-        # tables live on the ranks co-located with the PS replicas
-        cfg.owners = getattr(args, "num_ps", 0) or None
+        # table rows interleave over every worker rank (balanced sparse-update work);
+        # --embedding_owners ps keeps them on the ranks co-located with the PS tasks
+        cfg.owners = (getattr(args, "num_ps", 0) or None) if getattr(args, "embedding_owners", "all") == "ps" \
+            else None
         return WideDeep(cfg, device=device), None, wide_deep_loss
     raise SystemExit(f"unknown --model {name}")
 
@@ -109,23 +111,35 @@ def synthetic_batch(args, model, device, rank: int):
         from ..models.bert import synthetic_mlm_batch
         return synthetic_mlm_batch(model.cfg, B, args.seq_len, g, device)
     if args.model.startswith("wide_deep"):
+        from ..models.wide_deep import prepare_batch
         from ..models.wide_deep import synthetic_batch as wd_batch
-        return wd_batch(model.cfg, B, g, device)
+        return prepare_batch(model, *wd_batch(model.cfg, B, g, "cpu"), device)
     raise ValueError(args.model)
 
 
 def _async_mode(spec: ClusterSpec, args) -> bool:
     if spec.is_local or not spec.ps:
         return False
-    if args.ps_mode == "auto":
-        return not args.sync_replicas and args.model.startswith("mnist")
+    if args.ps_mode == "auto":  # the reference's default update mode is async (no --sync_replicas)
+        return not args.sync_replicas and (args.model.startswith("mnist") or args.ps_transport == "device")
     return args.ps_mode == "async"
 
 
 # ------------------------------------------------------------------ roles
+TRANSPORT_KEY = "kfa/async_ps/transport"
+
+
+def _ps_transport(args, has_gpu: bool) -> str:
+    if args.ps_transport == "auto":
+        return "device" if has_gpu else "host"
+    if args.ps_transport == "device" and not has_gpu:
+        raise SystemExit("--ps_transport device: this PS replica has no GPU (set KFA_PS_COLOCATE=1 in its template)")
+    return args.ps_transport
+
+
 def run_ps_async(spec: ClusterSpec, args) -> int:
     """PS task of the async mode: own the round-robin-placed variables, serve pulls/pushes."""
-    from ..parallel.async_ps import AsyncPSServer
+    from ..parallel.async_ps import AsyncPSServer, DeviceAsyncPSServer
     W, P = spec.num_workers, len(spec.ps)
     rank = W + spec.task_index
     _log(f"PS {spec.task_index}: async parameter server, rank {rank} of {W} workers + {P} ps at "
@@ -142,10 +156,20 @@ def run_ps_async(spec: ClusterSpec, args) -> int:
             time.sleep(0.5)
     dist.init_process_group("gloo", store=store, rank=rank, world_size=W + P)
     torch.manual_seed(args.seed)  # same initial values as every worker's model
+    use_gpu = _use_gpu(args)
+    transport = _ps_transport(args, use_gpu)
+    if spec.task_index == 0:
+        store.set(TRANSPORT_KEY, transport)
     model, _, _ = build(args, torch.device("cpu"))
-    server = AsyncPSServer(list(model.named_parameters()), W, P, spec.task_index, lr=args.learning_rate,
-                           optimizer=args.optimizer)
-    _log(f"PS {spec.task_index}: serving {len(server.names)} variables ({server.w.numel()} values)")
+    if transport == "device":
+        torch.cuda.set_device(0)
+        server = DeviceAsyncPSServer(list(model.named_parameters()), W, P, spec.task_index, store,
+                                     torch.device("cuda", 0), lr=args.learning_rate, optimizer=args.optimizer)
+    else:
+        server = AsyncPSServer(list(model.named_parameters()), W, P, spec.task_index, lr=args.learning_rate,
+                               optimizer=args.optimizer)
+    _log(f"PS {spec.task_index}: serving {len(server.names)} variables ({server.w.numel()} values), "
+         f"{transport}-resident ({'GPU HBM, HIP IPC pull/push' if transport == 'device' else 'host memory, gloo'})")
     pushes = server.serve(log=_log)
     _log(f"PS {spec.task_index}: all {W} workers done after {pushes} updates; exiting")
     dist.destroy_process_group()
@@ -155,7 +179,7 @@ def run_ps_async(spec: ClusterSpec, args) -> int:
 def run_worker_async(spec: ClusterSpec, args) -> int:
     """Between-graph replicated async training against the PS tasks (``mnist_replica.py:251-264``)."""
     from ..ops.loss import accuracy, cross_entropy
-    from ..parallel.async_ps import AsyncPSClient
+    from ..parallel.async_ps import AsyncPSClient, DeviceAsyncPSClient
     W, P = spec.num_workers, len(spec.ps)
     use_gpu = _use_gpu(args)
     device = torch.device("cuda", 0) if use_gpu else torch.device("cpu")
@@ -169,9 +193,21 @@ def run_worker_async(spec: ClusterSpec, args) -> int:
     args.num_ps = P
     model, data, loss_fn = build(args, device)
     model = model.to(device)
-    client = AsyncPSClient(list(model.named_parameters()), W, P)
+    if use_gpu and args.bf16:  # the compute copy: bf16 matrices, fp32 vectors (the PS keeps fp32 masters)
+        for p in model.parameters():
+            if p.dim() >= 2:
+                p.data = p.data.to(torch.bfloat16)
+        if model.__class__.__name__ == "ResNet":
+            model = model.to(memory_format=torch.channels_last)
+    transport = store.get(TRANSPORT_KEY).decode()  # PS 0 decides (waits for it to come up)
+    if transport == "device" and not use_gpu:
+        raise SystemExit("device-resident async PS needs GPU workers")
+    if transport == "device":
+        client = DeviceAsyncPSClient(list(model.named_parameters()), W, P, spec.task_index, store)
+    else:
+        client = AsyncPSClient(list(model.named_parameters()), W, P)
     _log(f"Worker {spec.task_index}: {W} workers, {P} ps, device {device}, model {args.model}, "
-         f"{sum(p.numel() for p in model.parameters())} params, async parameter server")
+         f"{sum(p.numel() for p in model.parameters())} params, async parameter server ({transport} transport)")
     fixed = None if data is not None else synthetic_batch(args, model, device, spec.task_index)
     t_begin = time.time()
     _log(f"Training begins @ {t_begin:f}")
@@ -382,6 +418,9 @@ def build_parser() -> argparse.ArgumentParser:
                     help="async: PS tasks own variables + Adam (reference default); collective: RCCL "
                          "reduce-scatter/all-gather on the workers; auto: async for MNIST without "
                          "--sync_replicas, collective otherwise")
+    ap.add_argument("--ps_transport", default="auto", choices=["auto", "host", "device"],
+                    help="async PS payloads: device = variables in the co-located GPU's HBM, pulled / pushed by "
+                         "HIP IPC device copies; host = CPU tensors over gloo; auto = device when the PS has a GPU")
     ap.add_argument("--replicas_to_aggregate", type=int, default=None, help="accepted; = #workers")
     ap.add_argument("--num_gpus", type=int, default=1, help="accepted (one GPU per replica)")
     ap.add_argument("--data_dir", default="", help="accepted (synthetic data; no network)")
@@ -394,6 +433,8 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--ps_placement", default="ps", choices=["ps", "sharded"],
                     help="collective mode with PS tasks: ps = each gradient bucket owned by one PS task's "
                          "co-located rank (replica_device_setter round-robin); sharded = every worker owns 1/W")
+    ap.add_argument("--embedding_owners", default="all", choices=["all", "ps"],
+                    help="Wide&Deep table rows: interleaved over all workers, or only the PS-co-located ranks")
     ap.add_argument("--grad_reduce", default="fp32", choices=["fp32", "bf16"],
                     help="dtype of the cross-rank gradient sum")
     ap.add_argument("--log_every", type=int, default=1)

@@ -141,6 +141,27 @@ def test_delete_tfjob_kills_replicas(node):
         assert not _alive(p)
 
 
+def test_ps_colocated_gpu_binding(tmp_path):
+    """A PS template with KFA_PS_COLOCATE=1 (device-resident async PS) shares GPU
+    index % num_gpus with the worker bound there; workers keep exclusive GPUs."""
+    st = ObjectStore()
+    n = Node(st, kubelet=True, root_dir=str(tmp_path), num_gpus=2, resync=30).start()
+    try:
+        cmd = [sys.executable, "-c", "import os; print('HIP=' + os.environ['HIP_VISIBLE_DEVICES'])"]
+        job = _job("colo", [("PS", 2, cmd), ("Worker", 2, cmd)])
+        from kubeflow_controller_amd.api.core import EnvVar
+        job.spec.specs[0].template.spec.containers[0].env = [EnvVar(name="KFA_PS_COLOCATE", value="1")]
+        st.create(job)
+        wait_for_phase(st, "default", "colo", {"Succeeded"}, 60)
+        pods = st.list("Pod")
+        ps = sorted((p.metadata.labels["index"], p.status.gpus) for p in pods if p.metadata.labels["job_type"] == "PS")
+        assert ps == [("0", [0]), ("1", [1])], ps
+        w = sorted(p.status.gpus[0] for p in pods if p.metadata.labels["job_type"] == "Worker")
+        assert w == [0, 1]
+    finally:
+        n.shutdown()
+
+
 def test_gpu_binding_policy(tmp_path):
     """Workers get one GPU each (HIP_VISIBLE_DEVICES), PS none; binding released on exit."""
     st = ObjectStore()

@@ -151,8 +151,12 @@ def _wd_worker(rank, world, port, owners, out):
     dense, ids, labels = synthetic_batch(cfg, 64, torch.Generator().manual_seed(5))
     n = 64 // world
     sl = slice(rank * n, (rank + 1) * n)
-    for _ in range(4):
-        eng.train_step(dense[sl], ids[sl], labels[sl])
+    from kubeflow_controller_amd.models.wide_deep import prepare_batch
+    for step in range(4):
+        if step % 2:   # host-planned split sizes (no device sync) on odd steps, device-derived on even
+            eng.train_step(*prepare_batch(m, dense[sl], ids[sl], labels[sl], "cpu"))
+        else:
+            eng.train_step(dense[sl], ids[sl], labels[sl])
     table = m.tables.full_table()
     if rank == 0:
         sd = {k: v.clone() for k, v in m.state_dict().items() if not k.startswith("tables.")}

@@ -49,10 +49,11 @@ def main(argv=None) -> int:
         loss_fn, unit, flops = bert_loss, "sequences/sec", flops_per_step(cfg, args.batch, args.seq)
         metric = f"{args.model} pre-training sequences/sec (seq {args.seq}, whole node)"
     else:
-        from kubeflow_controller_amd.models.wide_deep import WideDeep, WideDeepConfig, synthetic_batch, wide_deep_loss
+        from kubeflow_controller_amd.models.wide_deep import (WideDeep, WideDeepConfig, prepare_batch, synthetic_batch,
+                                                              wide_deep_loss)
         cfg = WideDeepConfig() if args.model == "wide_deep" else WideDeepConfig.tiny()
         model = WideDeep(cfg, device=info.device)
-        batch = synthetic_batch(cfg, args.batch, g, info.device)
+        batch = prepare_batch(model, *synthetic_batch(cfg, args.batch, g, "cpu"), info.device)
         loss_fn, unit, flops = wide_deep_loss, "examples/sec", None
         metric = f"{args.model} training examples/sec (whole node)"
     engine = Engine(model, loss_fn, optimizer="adam", lr=args.lr, weight_decay=0.01, bucket_mb=args.bucket_mb,
