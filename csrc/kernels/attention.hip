@@ -32,6 +32,8 @@
 // most 2-way).
 #include "common.h"
 
+#include <stdlib.h>
+
 namespace {
 
 constexpr int AS = 128;  // sequence length
@@ -525,6 +527,437 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(const bf16_t* __restri
   }
 }
 
+// ============================================================================
+// Long sequences, S = 128·n (BERT pre-training phase 2: S = 512).  The same
+// lane layouts and LDS images as the S = 128 kernels, tiled over 128-key /
+// 128-query blocks:
+//   forward   one workgroup per (sequence, head, 128-query block); key blocks
+//             streamed through LDS with an online softmax (running max / sum per
+//             query, held by the lane that owns the query column; O rescaled in
+//             registers), so no S x S tensor exists;
+//   backward  D = rowsum(dO∘O) by a small pre-pass, then two kernels that both
+//             recompute P and dS for their tiles (no atomics, no S x S buffer):
+//             key-owner dK / dV (the S = 128 kernel's phase A over every query
+//             block) and query-owner dQ = dS·K.
+// Dropout uses the same counter hash of (bh, query, key) as the S = 128 path.
+constexpr int BLK = 128;
+
+__global__ __launch_bounds__(256, 2) void attn_fwd_long_kernel(const bf16_t* __restrict__ qkv,
+                                                               const float* __restrict__ bqkv,
+                                                               const float* __restrict__ kbias, bf16_t* __restrict__ out,
+                                                               float* __restrict__ lse, int heads, int S, float qscale,
+                                                               uint32_t thresh, float dscale, uint64_t seed) {
+  __shared__ __attribute__((aligned(16))) char sm[3 * 16384 + 4 * 8192];  // 80 KiB
+  char* Qi = sm;
+  char* Ki = sm + 16384;
+  char* Vi = sm + 32768;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
+  char* Pw = sm + 49152 + wave * 8192;
+  const int nb = S / BLK;
+  const int qblk = blockIdx.x % nb, bh = blockIdx.x / nb, b = bh / heads, h = bh - b * heads, H = heads * AD;
+  const long seq0 = (long)b * S, q0 = seq0 + (long)qblk * BLK;
+  const int qb = wave * 32;
+  {
+    const int col[1] = {h * AD};
+    const bool ub[1] = {true}, tf[1] = {true};
+    const float sc[1] = {qscale};
+    char* const img[1] = {Qi};
+    const bf16_t* const src[1] = {qkv};
+    const long ld[1] = {3L * H};
+    ImageLoad<1> L;
+    images_issue<1>(L, src, ld, q0, col, bqkv, ub, tid);
+    images_commit<1>(L, tf, sc, img, tid);
+  }
+  float m[2] = {-3.0e38f, -3.0e38f}, l[2] = {0.f, 0.f};
+  floatx4 o[4][2];
+#pragma unroll
+  for (int dt = 0; dt < 4; dt++) o[dt][0] = o[dt][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < nb; j++) {
+    const long k0 = seq0 + (long)j * BLK;
+    if (j > 0) __syncthreads();  // every wave is done with key block j-1
+    const int col[2] = {H + h * AD, 2 * H + h * AD};
+    const bool ub[2] = {true, true}, tf[2] = {true, true};
+    const float sc[2] = {1.f, 1.f};
+    char* const img[2] = {Ki, Vi};
+    const bf16_t* const src[2] = {qkv, qkv};
+    const long ld[2] = {3L * H, 3L * H};
+    ImageLoad<2> L;
+    images_issue<2>(L, src, ld, k0, col, bqkv, ub, tid);
+    float kb[8][4];
+    load_key_bias(kbias, k0, fq, kb);
+    images_commit<2>(L, tf, sc, img, tid);
+    __syncthreads();
+    floatx4 s[8][2];
+    scores_t(Qi, Ki, qb, fr, fq, s);
+#pragma unroll
+    for (int qt = 0; qt < 2; qt++) {
+      const int q = qblk * BLK + qb + qt * 16 + fr;
+      float mx = -3.0e38f;
+#pragma unroll
+      for (int kt = 0; kt < 8; kt++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          s[kt][qt][r] += kb[kt][r];
+          mx = fmaxf(mx, s[kt][qt][r]);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mn = fmaxf(m[qt], mx);
+      const float alpha = __expf(m[qt] - mn);
+      float sum = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 8; kt++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const float e = __expf(s[kt][qt][r] - mn);
+          s[kt][qt][r] = e;
+          sum += e;
+        }
+      sum += __shfl_xor(sum, 16, 64);
+      sum += __shfl_xor(sum, 32, 64);
+      l[qt] = l[qt] * alpha + sum;
+      m[qt] = mn;
+#pragma unroll
+      for (int dt = 0; dt < 4; dt++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) o[dt][qt][r] *= alpha;
+#pragma unroll
+      for (int kt = 0; kt < 8; kt++) {
+        float pp[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          float v = s[kt][qt][r];
+          if (thresh)
+            v = drop_hash(seed, ((uint64_t)bh * S + q) * S + j * BLK + kt * 16 + 4 * fq + r) >= thresh ? v * dscale
+                                                                                                       : 0.f;
+          pp[r] = v;
+        }
+        *reinterpret_cast<uint2*>(Pw + off128(qt * 16 + fr, kt * 16 + 4 * fq)) = pack4(pp[0], pp[1], pp[2], pp[3]);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // only this wave reads its P rows
+#pragma unroll
+    for (int ks = 0; ks < 4; ks++) {
+      const short8 b0 = rd_row<128>(Pw, fr, ks * 32 + fq * 8);
+      const short8 b1 = rd_row<128>(Pw, 16 + fr, ks * 32 + fq * 8);
+#pragma unroll
+      for (int dt = 0; dt < 4; dt++) {
+        const short8 a = rd_tr<64>(Vi, ks * 32, dt * 16, lane);
+        o[dt][0] = mma(a, b0, o[dt][0]);
+        o[dt][1] = mma(a, b1, o[dt][1]);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // Pw is rewritten next block
+  }
+#pragma unroll
+  for (int qt = 0; qt < 2; qt++) {
+    const float inv = 1.f / l[qt];
+    if (fq == 0) lse[(long)bh * S + qblk * BLK + qb + qt * 16 + fr] = m[qt] + __logf(l[qt]);
+#pragma unroll
+    for (int dt = 0; dt < 4; dt++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) o[dt][qt][r] *= inv;
+  }
+#pragma unroll
+  for (int dt = 0; dt < 4; dt++)
+#pragma unroll
+    for (int qt = 0; qt < 2; qt++)
+      *reinterpret_cast<uint2*>(Pw + off64(qt * 16 + fr, dt * 16 + 4 * fq)) =
+          pack4(o[dt][qt][0], o[dt][qt][1], o[dt][qt][2], o[dt][qt][3]);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int it = 0; it < 4; it++) {
+    const int r = it * 8 + (lane >> 3), c = lane & 7;
+    *reinterpret_cast<uint4*>(out + (q0 + qb + r) * H + h * AD + c * 8) =
+        *reinterpret_cast<const uint4*>(Pw + off64(r, c * 8));
+  }
+}
+
+// D[bh][s] = Σ_d dO[token][h·64 + d]·O[token][h·64 + d]  (token = b·S + s), one thread per (token, head)
+__global__ void attn_rowdot_kernel(const bf16_t* __restrict__ dout, const bf16_t* __restrict__ out,
+                                   float* __restrict__ D, long tokens, int heads, int S) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= tokens * heads) return;
+  const long tok = t / heads;
+  const int h = (int)(t - tok * heads), H = heads * AD;
+  const uint4* g = reinterpret_cast<const uint4*>(dout + tok * H + h * AD);
+  const uint4* o = reinterpret_cast<const uint4*>(out + tok * H + h * AD);
+  float acc = 0.f;
+#pragma unroll
+  for (int c = 0; c < 8; c++) {
+    float a[8], b[8];
+    unpack8(g[c], a);
+    unpack8(o[c], b);
+#pragma unroll
+    for (int e = 0; e < 8; e++) acc += a[e] * b[e];
+  }
+  const long b = tok / S;
+  D[(b * heads + h) * S + (tok - b * S)] = acc;
+}
+
+// stage a wave's [32 rows][64] fp32 tiles t[dt][t2] (rows 16·t2 + fr, cols 16·dt + 4fq + r), scaled, as bf16
+__device__ __forceinline__ void stage_tile(char* st, const floatx4 (&t)[4][2], float scale, int fr, int fq) {
+#pragma unroll
+  for (int dt = 0; dt < 4; dt++)
+#pragma unroll
+    for (int t2 = 0; t2 < 2; t2++)
+      *reinterpret_cast<uint2*>(st + off64(t2 * 16 + fr, dt * 16 + 4 * fq)) =
+          pack4(t[dt][t2][0] * scale, t[dt][t2][1] * scale, t[dt][t2][2] * scale, t[dt][t2][3] * scale);
+}
+
+// write a staged [32 rows][64] tile to rows row0.. of dqkv column block colb; column sums -> dbias[colb..]
+__device__ __forceinline__ void store_tile(const char* st, bf16_t* __restrict__ dqkv, long row0, long W3, int colb,
+                                           float* __restrict__ dbias, int lane) {
+  const int c = lane & 7;
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int it = 0; it < 4; it++) {
+    const int r = it * 8 + (lane >> 3);
+    const uint4 v = *reinterpret_cast<const uint4*>(st + off64(r, c * 8));
+    *reinterpret_cast<uint4*>(dqkv + (row0 + r) * W3 + colb + c * 8) = v;
+    float f[8];
+    unpack8(v, f);
+#pragma unroll
+    for (int e = 0; e < 8; e++) cs[e] += f[e];
+  }
+  if (dbias) {
+#pragma unroll
+    for (int o = 8; o < 64; o <<= 1)
+#pragma unroll
+      for (int e = 0; e < 8; e++) cs[e] += __shfl_xor(cs[e], o, 64);
+    if (lane < 8)
+#pragma unroll
+      for (int e = 0; e < 8; e++) atomicAdd(dbias + colb + c * 8 + e, cs[e]);
+  }
+}
+
+// key-owner dK / dV: workgroup per (sequence, head, 128-key block); wave w owns keys 32w.. of the block
+__global__ __launch_bounds__(256, 2) void attn_bwd_kv_long_kernel(
+    const bf16_t* __restrict__ qkv, const float* __restrict__ bqkv, const float* __restrict__ kbias,
+    const float* __restrict__ lse, const float* __restrict__ Dq, const bf16_t* __restrict__ dout,
+    bf16_t* __restrict__ dqkv, float* __restrict__ dbqkv, int heads, int S, float qscale, uint32_t thresh,
+    float dscale, uint64_t seed) {
+  __shared__ __attribute__((aligned(16))) char sm[3 * 16384];  // Q, K, dO images (48 KiB)
+  char* Qi = sm;
+  char* Ki = sm + 16384;
+  char* Gi = sm + 32768;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
+  const int nb = S / BLK;
+  const int kblk = blockIdx.x % nb, bh = blockIdx.x / nb, b = bh / heads, h = bh - b * heads, H = heads * AD;
+  const long seq0 = (long)b * S, k0 = seq0 + (long)kblk * BLK, W3 = 3L * H;
+  const int kw = wave * 32;
+  {
+    const int col[1] = {H + h * AD};
+    const bool ub[1] = {true}, tf[1] = {true};
+    const float sc[1] = {1.f};
+    char* const img[1] = {Ki};
+    const bf16_t* const src[1] = {qkv};
+    const long ld[1] = {W3};
+    ImageLoad<1> L;
+    images_issue<1>(L, src, ld, k0, col, bqkv, ub, tid);
+    images_commit<1>(L, tf, sc, img, tid);
+  }
+  short8 vreg[2][2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ks++) {
+    const int col = 2 * H + h * AD + ks * 32 + fq * 8;
+    const float4 b0 = *reinterpret_cast<const float4*>(bqkv + col), b1 = *reinterpret_cast<const float4*>(bqkv + col + 4);
+    const float vb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+    for (int kt = 0; kt < 2; kt++) {
+      float f[8];
+      unpack8(*reinterpret_cast<const uint4*>(qkv + (k0 + kw + kt * 16 + fr) * W3 + col), f);
+#pragma unroll
+      for (int e = 0; e < 8; e++) f[e] += vb[e];
+      const uint4 u = pack8(f);
+      vreg[kt][ks] = *reinterpret_cast<const short8*>(&u);
+    }
+  }
+  float kbv[2];
+#pragma unroll
+  for (int kt = 0; kt < 2; kt++) kbv[kt] = kbias[k0 + kw + kt * 16 + fr];
+  __syncthreads();
+  short8 kreg[2][2];
+#pragma unroll
+  for (int kt = 0; kt < 2; kt++)
+#pragma unroll
+    for (int ks = 0; ks < 2; ks++) kreg[kt][ks] = rd_row<64>(Ki, kw + kt * 16 + fr, ks * 32 + fq * 8);
+  floatx4 dvT[4][2], dkT[4][2];
+#pragma unroll
+  for (int dt = 0; dt < 4; dt++) dvT[dt][0] = dvT[dt][1] = dkT[dt][0] = dkT[dt][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < nb; i++) {
+    const long qrow0 = seq0 + (long)i * BLK;
+    if (i > 0) __syncthreads();  // every wave is done with the previous Q / dO images
+    const int col[2] = {h * AD, h * AD};
+    const bool ub[2] = {true, false}, tf[2] = {true, false};
+    const float sc[2] = {qscale, 1.f};
+    char* const img[2] = {Qi, Gi};
+    const bf16_t* const src[2] = {qkv, dout};
+    const long ld[2] = {W3, (long)H};
+    ImageLoad<2> L;
+    images_issue<2>(L, src, ld, qrow0, col, bqkv, ub, tid);
+    const float2 lse2 = *reinterpret_cast<const float2*>(lse + (long)bh * S + i * BLK + 2 * lane);
+    const float2 dd2 = *reinterpret_cast<const float2*>(Dq + (long)bh * S + i * BLK + 2 * lane);
+    images_commit<2>(L, tf, sc, img, tid);
+    __syncthreads();
+    for (int j = 0; j < 4; j++) {
+      floatx4 s[2][2], dp[2][2];
+#pragma unroll
+      for (int qt = 0; qt < 2; qt++) s[qt][0] = s[qt][1] = dp[qt][0] = dp[qt][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ks++)
+#pragma unroll
+        for (int qt = 0; qt < 2; qt++) {
+          const short8 aq = rd_row<64>(Qi, 32 * j + 16 * qt + fr, ks * 32 + fq * 8);
+          const short8 ag = rd_row<64>(Gi, 32 * j + 16 * qt + fr, ks * 32 + fq * 8);
+#pragma unroll
+          for (int kt = 0; kt < 2; kt++) {
+            s[qt][kt] = mma(aq, kreg[kt][ks], s[qt][kt]);
+            dp[qt][kt] = mma(ag, vreg[kt][ks], dp[qt][kt]);
+          }
+        }
+      floatx4 pd[2][2], ds[2][2];
+#pragma unroll
+      for (int qt = 0; qt < 2; qt++) {
+        const int qb4 = 32 * j + 16 * qt + 4 * fq;  // query within the block
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const float D = __shfl(r & 1 ? dd2.y : dd2.x, (qb4 + r) >> 1, 64);
+          const float lq = __shfl(r & 1 ? lse2.y : lse2.x, (qb4 + r) >> 1, 64);
+#pragma unroll
+          for (int kt = 0; kt < 2; kt++) {
+            const float p = __expf(s[qt][kt][r] + kbv[kt] - lq);
+            float g = dp[qt][kt][r], pv = p;
+            if (thresh) {
+              const bool keep = drop_hash(seed, ((uint64_t)bh * S + i * BLK + qb4 + r) * S + kblk * BLK + kw +
+                                                    kt * 16 + fr) >= thresh;
+              pv = keep ? p * dscale : 0.f;
+              g = keep ? g * dscale : 0.f;
+            }
+            pd[qt][kt][r] = pv;
+            ds[qt][kt][r] = p * (g - D);
+          }
+        }
+      }
+      const int ra = 32 * j + 4 * fq, rb = ra + 16;
+      short8 gtr[4], qtr[4];
+#pragma unroll
+      for (int dt = 0; dt < 4; dt++) {
+        gtr[dt] = rd_tr2<64>(Gi, ra, rb, dt * 16, lane);
+        qtr[dt] = rd_tr2<64>(Qi, ra, rb, dt * 16, lane);
+      }
+#pragma unroll
+      for (int kt = 0; kt < 2; kt++) {
+        const short8 bp = pack_pair(pd[0][kt], pd[1][kt]);
+        const short8 bs = pack_pair(ds[0][kt], ds[1][kt]);
+#pragma unroll
+        for (int dt = 0; dt < 4; dt++) {
+          dvT[dt][kt] = mma(gtr[dt], bp, dvT[dt][kt]);
+          dkT[dt][kt] = mma(qtr[dt], bs, dkT[dt][kt]);
+        }
+      }
+    }
+  }
+  __syncthreads();  // the images become the output stage
+  char* st = sm + wave * 8192;
+  stage_tile(st, dkT, 1.f, fr, fq);
+  stage_tile(st + 4096, dvT, 1.f, fr, fq);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  store_tile(st, dqkv, k0 + kw, W3, H + h * AD, dbqkv, lane);
+  store_tile(st + 4096, dqkv, k0 + kw, W3, 2 * H + h * AD, dbqkv, lane);
+}
+
+// query-owner dQ = dS·K: workgroup per (sequence, head, 128-query block); wave w owns queries 32w..
+__global__ __launch_bounds__(256, 2) void attn_bwd_q_long_kernel(
+    const bf16_t* __restrict__ qkv, const float* __restrict__ bqkv, const float* __restrict__ kbias,
+    const float* __restrict__ lse, const float* __restrict__ Dq, const bf16_t* __restrict__ dout,
+    bf16_t* __restrict__ dqkv, float* __restrict__ dbqkv, int heads, int S, float qscale, uint32_t thresh,
+    float dscale, uint64_t seed) {
+  __shared__ __attribute__((aligned(16))) char sm[4 * 16384];  // Q, dO, K, V images (64 KiB)
+  char* Qi = sm;
+  char* Gi = sm + 16384;
+  char* Ki = sm + 32768;
+  char* Vi = sm + 49152;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
+  const int nb = S / BLK;
+  const int qblk = blockIdx.x % nb, bh = blockIdx.x / nb, b = bh / heads, h = bh - b * heads, H = heads * AD;
+  const long seq0 = (long)b * S, q0 = seq0 + (long)qblk * BLK, W3 = 3L * H;
+  const int qb = wave * 32;
+  {
+    const int col[2] = {h * AD, h * AD};
+    const bool ub[2] = {true, false}, tf[2] = {true, false};
+    const float sc[2] = {qscale, 1.f};
+    char* const img[2] = {Qi, Gi};
+    const bf16_t* const src[2] = {qkv, dout};
+    const long ld[2] = {W3, (long)H};
+    ImageLoad<2> L;
+    images_issue<2>(L, src, ld, q0, col, bqkv, ub, tid);
+    images_commit<2>(L, tf, sc, img, tid);
+  }
+  float lq[2], Dv[2];
+#pragma unroll
+  for (int qt = 0; qt < 2; qt++) {
+    const long qi = (long)bh * S + qblk * BLK + qb + qt * 16 + fr;
+    lq[qt] = lse[qi];
+    Dv[qt] = Dq[qi];
+  }
+  floatx4 dqT[4][2];
+#pragma unroll
+  for (int dt = 0; dt < 4; dt++) dqT[dt][0] = dqT[dt][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < nb; j++) {
+    const long k0 = seq0 + (long)j * BLK;
+    if (j > 0) __syncthreads();  // every wave is done with key block j-1
+    const int col[2] = {H + h * AD, 2 * H + h * AD};
+    const bool ub[2] = {true, true}, tf[2] = {true, true};
+    const float sc[2] = {1.f, 1.f};
+    char* const img[2] = {Ki, Vi};
+    const bf16_t* const src[2] = {qkv, qkv};
+    const long ld[2] = {W3, W3};
+    ImageLoad<2> L;
+    images_issue<2>(L, src, ld, k0, col, bqkv, ub, tid);
+    float kb[8][4];
+    load_key_bias(kbias, k0, fq, kb);
+    images_commit<2>(L, tf, sc, img, tid);
+    __syncthreads();
+    floatx4 s[8][2], dp[8][2];
+    scores_t(Qi, Ki, qb, fr, fq, s);   // (q = qb + 16qt + fr, key = 16kt + 4fq + r)
+    scores_t(Gi, Vi, qb, fr, fq, dp);  // dP(q, key) = dO[q]·V[key]
+#pragma unroll
+    for (int qt = 0; qt < 2; qt++) {
+      const int q = qblk * BLK + qb + qt * 16 + fr;
+#pragma unroll
+      for (int kt = 0; kt < 8; kt++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const float p = __expf(s[kt][qt][r] + kb[kt][r] - lq[qt]);
+          float g = dp[kt][qt][r];
+          if (thresh)
+            g = drop_hash(seed, ((uint64_t)bh * S + q) * S + j * BLK + kt * 16 + 4 * fq + r) >= thresh ? g * dscale
+                                                                                                       : 0.f;
+          s[kt][qt][r] = p * (g - Dv[qt]);  // dS
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const int ra = 32 * c + 4 * fq, rb = ra + 16;
+      short8 ktr[4];
+#pragma unroll
+      for (int dt = 0; dt < 4; dt++) ktr[dt] = rd_tr2<64>(Ki, ra, rb, dt * 16, lane);
+#pragma unroll
+      for (int qt = 0; qt < 2; qt++) {
+        const short8 bs = pack_pair(s[2 * c][qt], s[2 * c + 1][qt]);
+#pragma unroll
+        for (int dt = 0; dt < 4; dt++) dqT[dt][qt] = mma(ktr[dt], bs, dqT[dt][qt]);
+      }
+    }
+  }
+  __syncthreads();
+  char* st = sm + wave * 4096;
+  stage_tile(st, dqT, qscale, fr, fq);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  store_tile(st, dqkv, q0 + qb, W3, h * AD, dbqkv, lane);
+}
+
 uint32_t attn_drop_thresh(float p) {
   if (p <= 0.f) return 0u;
   const double t = (double)p * 4294967296.0;
@@ -533,29 +966,57 @@ uint32_t attn_drop_thresh(float p) {
 
 }  // namespace
 
+static bool attn_long_forced() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("KFA_ATTN_LONG");
+    v = (e && e[0] == '1') ? 1 : 0;
+  }
+  return v == 1;
+}
+
 // ctx [B*S, heads*64] = attention(qkv [B*S, 3*heads*64] (+ bqkv), key_bias [B, S]); lse [B*heads, S]
+// S = 128: one workgroup per (sequence, head); S = 128·n: per 128-query block, online softmax.
 KFA_API int kfa_attn_fwd(const void* qkv, const float* bqkv, const float* key_bias, void* out, float* lse, int B, int S,
                          int heads, int d, float qscale, float p, unsigned long long seed, hipStream_t st) {
   if (!bqkv || !key_bias) return -1;  // the caller passes zeros: no branches around the prologue loads
-  if (B <= 0 || heads <= 0 || S != AS || d != AD || (long)B * heads >= (1L << 31)) return -1;
+  if (B <= 0 || heads <= 0 || S <= 0 || S % BLK || S > 8192 || d != AD || (long)B * heads * (S / BLK) >= (1L << 31))
+    return -1;
   const uint32_t th = attn_drop_thresh(p);
   const float ds = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  hipLaunchKernelGGL(attn_fwd_kernel, dim3((unsigned)(B * heads)), dim3(256), 0, st, (const bf16_t*)qkv, bqkv, key_bias,
-                     (bf16_t*)out, lse, heads, qscale, th, ds, (uint64_t)seed);
+  if (S == AS && !attn_long_forced())
+    hipLaunchKernelGGL(attn_fwd_kernel, dim3((unsigned)(B * heads)), dim3(256), 0, st, (const bf16_t*)qkv, bqkv,
+                       key_bias, (bf16_t*)out, lse, heads, qscale, th, ds, (uint64_t)seed);
+  else
+    hipLaunchKernelGGL(attn_fwd_long_kernel, dim3((unsigned)((long)B * heads * (S / BLK))), dim3(256), 0, st,
+                       (const bf16_t*)qkv, bqkv, key_bias, (bf16_t*)out, lse, heads, S, qscale, th, ds, (uint64_t)seed);
   return kfa_status();
 }
 
 // dqkv [B*S, 3H] (overwritten); dbqkv [3H] fp32 (+)= bias gradient (nullable)
-// (out = the forward's ctx: D = rowsum(dO∘O) is formed from it)
+// (out = the forward's ctx: D = rowsum(dO∘O) is formed from it).  work: B*heads*S floats (S > 128 only)
 KFA_API int kfa_attn_bwd(const void* qkv, const float* bqkv, const float* key_bias, const void* out, const float* lse,
                          const void* dout, void* dqkv, float* dbqkv, int B, int S, int heads, int d, float qscale,
-                         float p, unsigned long long seed, hipStream_t st) {
+                         float p, unsigned long long seed, float* work, hipStream_t st) {
   if (!bqkv || !key_bias) return -1;
-  if (B <= 0 || heads <= 0 || S != AS || d != AD || (long)B * heads >= (1L << 31)) return -1;
+  if (B <= 0 || heads <= 0 || S <= 0 || S % BLK || S > 8192 || d != AD || (long)B * heads * (S / BLK) >= (1L << 31))
+    return -1;
   const uint32_t th = attn_drop_thresh(p);
   const float ds = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  hipLaunchKernelGGL(attn_bwd_kernel, dim3((unsigned)(B * heads)), dim3(256), 0, st, (const bf16_t*)qkv, bqkv, key_bias,
-                     (const bf16_t*)out, lse, (const bf16_t*)dout, (bf16_t*)dqkv, dbqkv, heads, qscale, th, ds,
-                     (uint64_t)seed);
+  if (S == AS && !attn_long_forced()) {
+    hipLaunchKernelGGL(attn_bwd_kernel, dim3((unsigned)(B * heads)), dim3(256), 0, st, (const bf16_t*)qkv, bqkv,
+                       key_bias, (const bf16_t*)out, lse, (const bf16_t*)dout, (bf16_t*)dqkv, dbqkv, heads, qscale, th,
+                       ds, (uint64_t)seed);
+    return kfa_status();
+  }
+  if (!work) return -3;
+  const long tokens = (long)B * S;
+  hipLaunchKernelGGL(attn_rowdot_kernel, dim3((unsigned)((tokens * heads + 255) / 256)), dim3(256), 0, st,
+                     (const bf16_t*)dout, (const bf16_t*)out, work, tokens, heads, S);
+  const dim3 grid((unsigned)((long)B * heads * (S / BLK)));
+  hipLaunchKernelGGL(attn_bwd_kv_long_kernel, grid, dim3(256), 0, st, (const bf16_t*)qkv, bqkv, key_bias, lse, work,
+                     (const bf16_t*)dout, (bf16_t*)dqkv, dbqkv, heads, S, qscale, th, ds, (uint64_t)seed);
+  hipLaunchKernelGGL(attn_bwd_q_long_kernel, grid, dim3(256), 0, st, (const bf16_t*)qkv, bqkv, key_bias, lse, work,
+                     (const bf16_t*)dout, (bf16_t*)dqkv, dbqkv, heads, S, qscale, th, ds, (uint64_t)seed);
   return kfa_status();
 }

@@ -53,7 +53,7 @@ _lib.register("kfa_embed_fwd", [P, P, P, P, P, P, I, P, L, I, L, P])
 _lib.register("kfa_embed_bwd", [P, P, L, P, P, I, L, I, I, P])
 _lib.register("kfa_colsum", [P, P, P, L, I, I, P])
 _lib.register("kfa_attn_fwd", [P, P, P, P, P, I, I, I, I, Fl, Fl, U64, P])
-_lib.register("kfa_attn_bwd", [P, P, P, P, P, P, P, P, I, I, I, I, Fl, Fl, U64, P])
+_lib.register("kfa_attn_bwd", [P, P, P, P, P, P, P, P, I, I, I, I, Fl, Fl, U64, P, P])
 
 # env KFA_FUSED_ATTN=0 falls back to the split kernels + batched library GEMMs
 FUSED_ATTN = os.environ.get("KFA_FUSED_ATTN", "1") != "0"
@@ -334,8 +334,9 @@ def embedding_sum(tables, ids):
 
 # ----------------------------------------------------------------------------- fused attention
 def fused_attention_ok(S: int, d: int) -> bool:
-    """``csrc/kernels/attention.hip`` covers sequence 128 x head dim 64 (BERT-base/large phase 1)."""
-    return FUSED_ATTN and S == 128 and d == 64
+    """``csrc/kernels/attention.hip`` covers head dim 64 at S = 128 (one workgroup per
+    head) and S = 128·n up to 8192 (128-query blocks, online softmax; BERT phase 2: 512)."""
+    return FUSED_ATTN and S % 128 == 0 and 0 < S <= 8192 and d == 64
 
 
 def _attn_biases(bqkv, key_bias, W3, T_, dev):
@@ -381,9 +382,10 @@ def attn_bwd(qkv, bqkv, key_bias, out, lse, dout, dbqkv, B, S, heads, p=0.0, see
         raise ValueError("attn_bwd: out must be the contiguous bf16 [B*S, H] forward output")
     bqkv, key_bias = _attn_biases(bqkv, key_bias, W3, B * S, qkv.device)
     dqkv = torch.empty_like(qkv)
+    work = _lib.workspace(B * heads * S * 4, qkv.device, "attn_rowdot")  # D = rowsum(dO∘O) (S > 128)
     _lib.call("kfa_attn_bwd", _lib.ptr(qkv), _lib.ptr(bqkv), _lib.ptr(key_bias), _lib.ptr(out), _lib.ptr(lse),
               _lib.ptr(dout), _lib.ptr(dqkv), _lib.ptr(dbqkv), B, S, heads, d, 1.0 / math.sqrt(d), float(p),
-              int(seed) & _MASK64, _lib.stream())
+              int(seed) & _MASK64, _lib.ptr(work), _lib.stream())
     return dqkv
 
 

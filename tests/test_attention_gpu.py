@@ -44,16 +44,19 @@ def _reference(qkv, bqkv, kb, B, S, heads, d, mask, p):
     return (pr @ v).permute(0, 2, 1, 3).reshape(B * S, heads * d)
 
 
+@pytest.mark.parametrize("S", [128, 256, 512])
 @pytest.mark.parametrize("p", [0.0, 0.1])
-def test_fused_attention_fwd_bwd(p):
+def test_fused_attention_fwd_bwd(p, S):
+    """S = 128: one workgroup per head; S = 256 / 512: the 128-block kernels
+    (online-softmax forward, key-owner dK/dV + query-owner dQ backward)."""
     from kubeflow_controller_amd.ops import transformer as T
     torch.manual_seed(0)
-    B, S, heads, d = 3, 128, 4, 64
+    B, heads, d = (3, 4, 64) if S == 128 else (2, 2, 64)
     H = heads * d
     qkv = torch.randn(B * S, 3 * H, device=D).to(torch.bfloat16)
     bqkv = torch.randn(3 * H, device=D) * 0.1
     m = torch.ones(B, S, device=D)
-    m[1, 90:] = 0
+    m[1, S - 38:] = 0   # masked tail, crossing a 128-key block boundary for S > 128
     kb = ((1 - m) * -10000.0).contiguous()
     seed = 987654321
     out, lse = T.attn_fwd(qkv, bqkv, kb, B, S, heads, p, seed)

@@ -111,13 +111,14 @@ def _layer_params(H, I, dev):
     return out
 
 
-@pytest.mark.parametrize("route_gemm,fused_attn", [(False, True), (True, True), (False, False)])
-def test_encoder_layer_vs_reference(monkeypatch, route_gemm, fused_attn):
+@pytest.mark.parametrize("route_gemm,fused_attn,S", [(False, True, 128), (True, True, 128), (False, False, 128),
+                                                     (False, True, 512)])
+def test_encoder_layer_vs_reference(monkeypatch, route_gemm, fused_attn, S):
     from kubeflow_controller_amd.ops import gemm as G
     from kubeflow_controller_amd.ops import transformer as T
     monkeypatch.setattr(G, "ROUTE_LAYERS", route_gemm)
     monkeypatch.setattr(T, "FUSED_ATTN", fused_attn)
-    B, S, heads, H, I = 4, 128, 4, 256, 1024
+    B, heads, H, I = (4, 4, 256, 1024) if S == 128 else (2, 4, 256, 1024)
     params = _layer_params(H, I, D)
     x = _bf(torch.randn(B * S, H)).requires_grad_()
     mask = torch.ones(B, S, device=D)
