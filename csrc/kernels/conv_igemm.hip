@@ -94,7 +94,14 @@ __device__ __forceinline__ int swz(int row, int chunk) { return row * BK + ((chu
 // (8 waves: 256 x 256 tiles of 128 x 64 per wave, one block per CU — half the
 // operand bytes per MFMA of the 4-wave 128 x 128 tile; the epilogue then stages
 // the wave tile in NHALF passes so it fits the one ring buffer it may use.)
-template <int WM, int WN, int TM, int TN>
+// EPI: epilogue features compiled in (kEpiE addend, kEpiStats fused BN statistics,
+// kEpiBnBwd backward statistics of the BN this dgrad feeds, kEpiEmb ReLU-bit-masked
+// addend).  A feature's runtime pointer may still be null; features not compiled in
+// cost no registers — the all-features build spilled (256 VGPRs) and serialised the
+// main loop's LDS fragment reads on a reused register.
+constexpr unsigned kEpiE = 1, kEpiStats = 2, kEpiBnBwd = 4, kEpiEmb = 8, kEpiAll = 15;
+
+template <int WM, int WN, int TM, int TN, unsigned EPI>
 __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_t* __restrict__ T,
                                                                      const bf16_t* __restrict__ B,
                                                                      bf16_t* __restrict__ D, const bf16_t* __restrict__ E,
@@ -245,7 +252,8 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
     const int c = lane % CPR;
     const int n = n0 + wn * TN * 16 + c * 8;
     float mu[8] = {0, 0, 0, 0, 0, 0, 0, 0}, msc[8], msf[8];
-    const bool bstat = stats && bnb.x;
+    constexpr bool kE = EPI & kEpiE, kST = EPI & kEpiStats, kBS = EPI & kEpiBnBwd, kEM = EPI & kEpiEmb;
+    const bool bstat = kBS && kST && stats && bnb.x;
     const bool ymask = bnb.relu && bnb.y;              // mask from the output y
     const bool bmask = bnb.relu && !bnb.y && bnb.mb;   // from the output bit mask
     // else (relu) recomputed from x with the saved scale / shift
@@ -283,11 +291,11 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
       }
       uint4 ev[IT], bx[IT], by[IT];
       unsigned mbits[IT], ebits[IT];
-      if (E)
+      if (kE && E)
 #pragma unroll
         for (int it = 0; it < IT; it++) {
           ev[it] = bload16(rE, offs[it]);
-          if (bnb.emb) ebits[it] = offs[it] != kOOB ? (unsigned)bnb.emb[offs[it] >> 4] : 0u;
+          if (kEM && bnb.emb) ebits[it] = offs[it] != kOOB ? (unsigned)bnb.emb[offs[it] >> 4] : 0u;
         }
       if (bstat)
 #pragma unroll
@@ -315,11 +323,11 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
         const uint4 v = *reinterpret_cast<const uint4*>(stage + r * RB + ((c ^ (r & (CPR - 1))) << 4));
         const unsigned off = offs[it];
         uint4 o = v;
-        if (E) {  // wave-uniform branch
+        if (kE && E) {  // wave-uniform branch
           float f[8], h[8];
           unpack8(v, f);
           unpack8(ev[it], h);
-          if (bnb.emb) {  // residual gradient dz = dy * relu-mask, formed here instead of by the BN backward
+          if (kEM && bnb.emb) {  // residual gradient dz = dy * relu-mask, formed here instead of by the BN backward
 #pragma unroll
             for (int j = 0; j < 8; j++) f[j] += ((ebits[it] >> j) & 1u) ? h[j] : 0.f;
           } else {
@@ -329,7 +337,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
           o = pack8(f);
         }
         __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<decltype(__builtin_amdgcn_raw_buffer_load_b128(rD, 0, 0, 0))*>(&o), rD, off, 0, 0);
-        if (stats && off != kOOB) {  // wave-uniform pointer test; per-lane row mask
+        if (kST && stats && off != kOOB) {  // wave-uniform pointer test; per-lane row mask
           float f[8];
           unpack8(o, f);  // the bf16-rounded values the BatchNorm will see
           if (bstat) {    // backward statistics of the BN this dgrad feeds
@@ -356,7 +364,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
         }
       }
     }
-    if (stats) {
+    if (kST && stats) {
       // Butterfly-reduce over the lanes sharing channel chunk c = lane % CPR (xor
       // 8, 16, 32): every lane ends with its chunk's wave totals.  Lane L then
       // publishes channel (L % 8) * 8 + L / 8 — its own chunk, register L / 8
@@ -499,6 +507,44 @@ static const bf16_t* zero_page() {
   return z;
 }
 
+// smallest compiled epilogue configuration covering `need` (see conv_igemm_kernel's EPI)
+static unsigned pick_epi(unsigned need) {
+  static const unsigned have[] = {0u, kEpiStats, kEpiE, kEpiE | kEpiEmb, kEpiStats | kEpiBnBwd,
+                                  kEpiE | kEpiStats | kEpiBnBwd};
+  for (unsigned h : have)
+    if ((need & ~h) == 0) return h;
+  return kEpiAll;
+}
+
+template <int WM, int WN, int TM, int TN>
+static void launch_igemm(unsigned epi, dim3 grid, dim3 block, int lds, hipStream_t st, const bf16_t* T, const bf16_t* B,
+                         bf16_t* D, const bf16_t* E, float* stats, const BnBwd& bnb, const Geo& g) {
+#define KFA_IG(EP)                                                                                                   \
+  case EP:                                                                                                           \
+    if (lds > 65536) {                                                                                               \
+      static bool attr = false;                                                                                      \
+      if (!attr) {                                                                                                   \
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_igemm_kernel<WM, WN, TM, TN, EP>),             \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);                                  \
+        attr = true;                                                                                                 \
+      }                                                                                                              \
+    }                                                                                                                \
+    hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, TM, TN, EP>), grid, block, lds, st, T, B, D, E, zero_page(), stats, \
+                       bnb, g);                                                                                      \
+    break;
+  switch (pick_epi(epi)) {
+    KFA_IG(0u)
+    KFA_IG(kEpiStats)
+    KFA_IG(kEpiE)
+    KFA_IG(kEpiE | kEpiEmb)
+    KFA_IG(kEpiStats | kEpiBnBwd)
+    KFA_IG(kEpiE | kEpiStats | kEpiBnBwd)
+    default:
+      KFA_IG(kEpiAll)
+  }
+#undef KFA_IG
+}
+
 // variant: 0 = 128x128 tile, 1 = 128x64 tile (N <= 64), 2 = 256x256 tile (8 waves), 3 = 256x64 (N <= 64)
 KFA_API int kfa_conv_igemm(const bf16_t* T, const bf16_t* B, bf16_t* D, const bf16_t* E, int Nb, int H, int W, int C,
                            int P, int Q, int R, int S, int sa, int ra, int oa, int ob, int N, int OH, int OW, int os,
@@ -534,38 +580,22 @@ KFA_API int kfa_conv_igemm(const bf16_t* T, const bf16_t* B, bf16_t* D, const bf
   }
   const int slots = 2 * cus;  // 2 resident blocks per CU (64 KB LDS, <=256 VGPR/2 waves)
   auto pgrid = [&](long tiles) { return (int)(tiles < slots ? tiles : slots); };
+  const unsigned epi = (E ? kEpiE : 0u) | (stats ? kEpiStats : 0u) | (bn_x ? kEpiBnBwd : 0u) |
+                       ((E && add_mb) ? kEpiEmb : 0u);
   if (variant == 3) {  // 256 x 64 tile (Cout <= 64): 4 waves of 64x64, 80 KB LDS -> 2 blocks / CU
     const int grid = pgrid((long)kfa_ceil_div(g.M, 256) * kfa_ceil_div(N, 64));
-    const int lds = 2 * (256 + 64) * BK * 2;
-    static bool attr3 = false;
-    if (!attr3) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_igemm_kernel<4, 1, 4, 4>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-      attr3 = true;
-    }
-    hipLaunchKernelGGL((conv_igemm_kernel<4, 1, 4, 4>), dim3(grid), dim3(256), lds, st, T, B, D, E, zero_page(), stats,
-                       bnb, g);
+    launch_igemm<4, 1, 4, 4>(epi, dim3(grid), dim3(256), 2 * (256 + 64) * BK * 2, st, T, B, D, E, stats, bnb, g);
   } else if (variant == 1) {  // 128 x 64 tile (Cout <= 64): 4 waves of 32x64
     const long tiles = (long)kfa_ceil_div(g.M, 128) * kfa_ceil_div(N, 64);
-    const int grid = (int)(tiles < 3L * cus ? tiles : 3L * cus);  // 160 VGPR, 48 KB LDS: 3 blocks / CU
-    hipLaunchKernelGGL((conv_igemm_kernel<4, 1, 2, 4>), dim3(grid), dim3(256), 2 * (128 + 64) * BK * 2, st, T, B, D,
-                       E, zero_page(), stats, bnb, g);
+    const int grid = (int)(tiles < 3L * cus ? tiles : 3L * cus);  // 48 KB LDS: up to 3 blocks / CU
+    launch_igemm<4, 1, 2, 4>(epi, dim3(grid), dim3(256), 2 * (128 + 64) * BK * 2, st, T, B, D, E, stats, bnb, g);
   } else if (variant == 2) {  // 256 x 256 tile: 2x4 waves of 128x64, one block per CU (128 KiB LDS)
     const long tiles = (long)kfa_ceil_div(g.M, 256) * kfa_ceil_div(N, 256);
     const int grid = (int)(tiles < cus ? tiles : cus);
-    const int lds = 2 * (256 + 256) * BK * 2;
-    static bool attr = false;
-    if (!attr) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_igemm_kernel<2, 4, 8, 4>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-      attr = true;
-    }
-    hipLaunchKernelGGL((conv_igemm_kernel<2, 4, 8, 4>), dim3(grid), dim3(512), lds, st, T, B, D, E, zero_page(), stats,
-                       bnb, g);
+    launch_igemm<2, 4, 8, 4>(kEpiAll, dim3(grid), dim3(512), 2 * (256 + 256) * BK * 2, st, T, B, D, E, stats, bnb, g);
   } else {  // 128 x 128 tile: 2x2 waves of 64x64
     const int grid = pgrid((long)kfa_ceil_div(g.M, 128) * kfa_ceil_div(N, 128));
-    hipLaunchKernelGGL((conv_igemm_kernel<2, 2, 4, 4>), dim3(grid), dim3(256), 2 * (128 + 128) * BK * 2, st, T, B, D,
-                       E, zero_page(), stats, bnb, g);
+    launch_igemm<2, 2, 4, 4>(epi, dim3(grid), dim3(256), 2 * (128 + 128) * BK * 2, st, T, B, D, E, stats, bnb, g);
   }
   return kfa_status();
 }

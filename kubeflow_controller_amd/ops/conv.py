@@ -72,7 +72,7 @@ BIG_MIN_K = int(os.environ.get("KFA_CONV_BIG_MINK", "256"))
 # Residual gradient of identity blocks formed in conv1's dgrad epilogue from the raw
 # gradient + ReLU bits (GradJoin.deposit_masked); KFA_MASKED_RESIDUAL=0 writes it instead.
 MASKED_RESIDUAL = os.environ.get("KFA_MASKED_RESIDUAL", "1") != "0"
-TUNE = os.environ.get("KFA_CONV_TUNE", "1") != "0"
+TUNE = os.environ.get("KFA_CONV_TUNE", "0") == "1"  # opt-in: the own kernels win every ResNet-50 shape (10,003 vs 10,099 img/s with the vendor race on)
 TUNE_LOG = os.environ.get("KFA_CONV_TUNE_LOG", "0") == "1"
 _fwd_plan: dict = {}  # shape key -> True: vendor forward + BN stats pass
 
