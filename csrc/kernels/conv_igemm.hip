@@ -99,7 +99,7 @@ __device__ __forceinline__ int swz(int row, int chunk) { return row * BK + ((chu
 // addend).  A feature's runtime pointer may still be null; features not compiled in
 // cost no registers — the all-features build spilled (256 VGPRs) and serialised the
 // main loop's LDS fragment reads on a reused register.
-constexpr unsigned kEpiE = 1, kEpiStats = 2, kEpiBnBwd = 4, kEpiEmb = 8, kEpiAll = 15;
+constexpr unsigned kEpiE = 1, kEpiStats = 2, kEpiBnBwd = 4, kEpiEmb = 8, kEpiYMask = 16, kEpiAll = 31;
 
 template <int WM, int WN, int TM, int TN, unsigned EPI>
 __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_t* __restrict__ T,
@@ -253,8 +253,9 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
     const int n = n0 + wn * TN * 16 + c * 8;
     float mu[8] = {0, 0, 0, 0, 0, 0, 0, 0}, msc[8], msf[8];
     constexpr bool kE = EPI & kEpiE, kST = EPI & kEpiStats, kBS = EPI & kEpiBnBwd, kEM = EPI & kEpiEmb;
+    constexpr bool kYM = EPI & kEpiYMask;  // ReLU mask read from the BN output (else bits / recomputed from x)
     const bool bstat = kBS && kST && stats && bnb.x;
-    const bool ymask = bnb.relu && bnb.y;              // mask from the output y
+    const bool ymask = kYM && bnb.relu && bnb.y;       // mask from the output y
     const bool bmask = bnb.relu && !bnb.y && bnb.mb;   // from the output bit mask
     // else (relu) recomputed from x with the saved scale / shift
     if (bstat)
@@ -510,7 +511,7 @@ static const bf16_t* zero_page() {
 // smallest compiled epilogue configuration covering `need` (see conv_igemm_kernel's EPI)
 static unsigned pick_epi(unsigned need) {
   static const unsigned have[] = {0u, kEpiStats, kEpiE, kEpiE | kEpiEmb, kEpiStats | kEpiBnBwd,
-                                  kEpiE | kEpiStats | kEpiBnBwd};
+                                  kEpiE | kEpiStats | kEpiBnBwd, kEpiE | kEpiEmb | kEpiStats | kEpiBnBwd};
   for (unsigned h : have)
     if ((need & ~h) == 0) return h;
   return kEpiAll;
@@ -539,6 +540,7 @@ static void launch_igemm(unsigned epi, dim3 grid, dim3 block, int lds, hipStream
     KFA_IG(kEpiE | kEpiEmb)
     KFA_IG(kEpiStats | kEpiBnBwd)
     KFA_IG(kEpiE | kEpiStats | kEpiBnBwd)
+    KFA_IG(kEpiE | kEpiEmb | kEpiStats | kEpiBnBwd)
     default:
       KFA_IG(kEpiAll)
   }
@@ -581,7 +583,7 @@ KFA_API int kfa_conv_igemm(const bf16_t* T, const bf16_t* B, bf16_t* D, const bf
   const int slots = 2 * cus;  // 2 resident blocks per CU (64 KB LDS, <=256 VGPR/2 waves)
   auto pgrid = [&](long tiles) { return (int)(tiles < slots ? tiles : slots); };
   const unsigned epi = (E ? kEpiE : 0u) | (stats ? kEpiStats : 0u) | (bn_x ? kEpiBnBwd : 0u) |
-                       ((E && add_mb) ? kEpiEmb : 0u);
+                       ((E && add_mb) ? kEpiEmb : 0u) | ((bn_x && bn_y && bn_relu) ? kEpiYMask : 0u);
   if (variant == 3) {  // 256 x 64 tile (Cout <= 64): 4 waves of 64x64, 80 KB LDS -> 2 blocks / CU
     const int grid = pgrid((long)kfa_ceil_div(g.M, 256) * kfa_ceil_div(N, 64));
     launch_igemm<4, 1, 4, 4>(epi, dim3(grid), dim3(256), 2 * (256 + 64) * BK * 2, st, T, B, D, E, stats, bnb, g);
