@@ -53,7 +53,7 @@ enum Act { kNone = 0, kGelu = 1, kTanh = 2, kRelu = 3 };
 
 __device__ __forceinline__ float act_fwd(float z, int act) {
   switch (act) {
-    case kGelu: return 0.5f * z * (1.f + erff(z * 0.70710678118654752f));
+    case kGelu: return gelu_f(z);
     case kTanh: return tanhf(z);
     case kRelu: return fmaxf(z, 0.f);
     default: return z;
@@ -62,10 +62,7 @@ __device__ __forceinline__ float act_fwd(float z, int act) {
 
 __device__ __forceinline__ float act_bwd(float z, int act) {
   switch (act) {
-    case kGelu: {
-      const float cdf = 0.5f * (1.f + erff(z * 0.70710678118654752f));
-      return cdf + z * 0.39894228040143268f * __expf(-0.5f * z * z);
-    }
+    case kGelu: return gelu_grad(z);
     case kTanh: {
       const float t = tanhf(z);
       return 1.f - t * t;
@@ -84,6 +81,7 @@ struct GemmArgs {
   bf16_t* Z;           // pre-activation out [M][ldc] or null
   const bf16_t* Zin;   // activation-derivative input [M][ldc] or null
   float* dbias;        // column sums [N] (atomic) or null
+  float* dpart;        // with dbias: per-wave-row-block partial column sums [ceil(M / rows)][N] (plain stores)
   int M, N, K, lda, ldb, ldc, act, dact;
   unsigned c_bytes;    // extent of C / E / Z / Zin
 };
@@ -114,6 +112,7 @@ __device__ __forceinline__ void vm_wait() {
   else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
   else static_assert(N < 0, "vm_wait: add the literal");
 }
 
@@ -125,17 +124,17 @@ __device__ __forceinline__ void ring_wait(int ahead) {
   else vm_wait<0>();
 }
 
-template <int BN>
-__global__ __launch_bounds__(512) void gemm_nt_kernel(GemmArgs g, const bf16_t* __restrict__ zp) {
+template <int BN, int NS = NSLOT, int NW = 8>
+__global__ __launch_bounds__(NW * 64, 8 / NW) void gemm_nt_kernel(GemmArgs g, const bf16_t* __restrict__ zp) {
   constexpr int BM = 256;
-  constexpr int WN = BN / 64, WM = 8 / WN;           // waves along N / M
+  constexpr int WN = BN / 64, WM = NW / WN;          // waves along N / M
   constexpr int TM = BM / WM / 16, TN = 4;           // wave tile: 16*TM rows x 64 columns
   constexpr int A_SLOT = BM * GK, B_SLOT = BN * GK;  // elements per ring slot
-  constexpr int GA = BM / 128, GB = BN / 128;        // LDS-DMA instructions per wave per k-step (16 rows each)
+  constexpr int GA = BM / (16 * NW), GB = BN / (16 * NW);  // LDS-DMA instructions per wave per k-step (16 rows each)
   constexpr int GL = GA + GB;
-  __shared__ __attribute__((aligned(16))) bf16_t smem[NSLOT * (A_SLOT + B_SLOT)];
+  __shared__ __attribute__((aligned(16))) bf16_t smem[NS * (A_SLOT + B_SLOT)];
   bf16_t* As = smem;
-  bf16_t* Bs = smem + NSLOT * A_SLOT;
+  bf16_t* Bs = smem + NS * A_SLOT;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM;
@@ -168,7 +167,7 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(GemmArgs g, const bf16_t* 
     b_src[i] = n < g.N ? g.B + (long)n * g.ldb + lch * 8 : nullptr;
   }
   auto issue = [&](int kt) {
-    const int slot = kt & (NSLOT - 1), k0 = kt * GK;
+    const int slot = kt % NS, k0 = kt * GK;
     const bool kin = k0 + lch * 8 < g.K;  // K tail (K % 8 == 0): chunks past K read the zero page
 #pragma unroll
     for (int i = 0; i < GA; i++)
@@ -188,15 +187,17 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(GemmArgs g, const bf16_t* 
     for (int j = 0; j < TM; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = (g.K + GK - 1) / GK;
-  issue(0);
-  if (nk > 1) issue(1);
-  if (nk > 2) issue(2);
-  ring_wait<GL>(nk > 2 ? 2 : nk - 1);
+  // NS-slot ring: k-step t+NS-1 is issued while t multiplies (slot of t-1:
+  // every wave passed the barrier after reading it); the barrier closing t
+  // waits for t+1 with min(NS-2, ...) younger k-steps left in flight.
+  for (int i = 0; i < NS - 1; i++)
+    if (i < nk) issue(i);
+  ring_wait<GL>(min(NS - 2, nk - 1));
   asm volatile("s_barrier" ::: "memory");
   for (int t = 0; t < nk; t++) {
-    if (t + 3 < nk) issue(t + 3);  // slot (t+3)&3 = (t-1)&3: every wave passed the barrier after reading it
-    const bf16_t* At = As + (t & (NSLOT - 1)) * A_SLOT + wm * TM * 16 * GK + loff;
-    const bf16_t* Bt = Bs + (t & (NSLOT - 1)) * B_SLOT + wn * TN * 16 * GK + loff;
+    if (t + NS - 1 < nk) issue(t + NS - 1);
+    const bf16_t* At = As + (t % NS) * A_SLOT + wm * TM * 16 * GK + loff;
+    const bf16_t* Bt = Bs + (t % NS) * B_SLOT + wn * TN * 16 * GK + loff;
     short8 af[TM], bq[TN];
 #pragma unroll
     for (int i = 0; i < TN; i++) bq[i] = *reinterpret_cast<const short8*>(Bt + i * 16 * GK);
@@ -209,7 +210,7 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(GemmArgs g, const bf16_t* 
       for (int mi = 0; mi < TM; mi++)
         acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[ni], af[mi], acc[ni][mi], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
-    ring_wait<GL>((t + 3 < nk ? t + 3 : nk - 1) - (t + 1));
+    ring_wait<GL>((t + NS - 1 < nk ? t + NS - 1 : nk - 1) - (t + 1));
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
 
@@ -287,9 +288,16 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(GemmArgs g, const bf16_t* 
     for (int o = 8; o < 64; o <<= 1)
 #pragma unroll
       for (int j = 0; j < 8; j++) cs[j] += __shfl_xor(cs[j], o, 64);
-    if (lane < 8 && nok)
+    if (lane < 8 && nok) {
+      if (g.dpart) {  // M / ROWS partials per column, summed by gemm_dbias_reduce: no L2-serialised atomics
+        float* pp = g.dpart + (long)((m0 + wm * ROWS) / ROWS) * g.N + n;
+        *reinterpret_cast<float4*>(pp) = make_float4(cs[0], cs[1], cs[2], cs[3]);
+        *reinterpret_cast<float4*>(pp + 4) = make_float4(cs[4], cs[5], cs[6], cs[7]);
+      } else {
 #pragma unroll
-      for (int j = 0; j < 8; j++) atomicAdd(g.dbias + n + j, cs[j]);
+        for (int j = 0; j < 8; j++) atomicAdd(g.dbias + n + j, cs[j]);
+      }
+    }
   }
 }
 
@@ -550,6 +558,25 @@ __global__ __launch_bounds__(512) void gemm_pt_kernel(GemmArgs g, const bf16_t* 
 
 }  // namespace
 
+namespace {
+// dbias[n] += Σ_p part[p][n]: blockIdx.y takes every RS-th partial row of 256
+// columns (8 independent loads in flight per thread), then one atomic per
+// column per row split — RS adds per address instead of P.
+constexpr int kDbRS = 16;
+__global__ __launch_bounds__(256) void gemm_dbias_reduce(const float* __restrict__ part, float* __restrict__ dbias,
+                                                        int P, int N) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int p = blockIdx.y;
+  for (; p + 7 * kDbRS < P; p += 8 * kDbRS)
+#pragma unroll
+    for (int j = 0; j < 8; j++) a[j] += part[(long)(p + j * kDbRS) * N + n];
+  for (; p < P; p += kDbRS) a[0] += part[(long)p * N + n];
+  atomicAdd(dbias + n, ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7])));
+}
+}  // namespace
+
 static const bf16_t* gemm_zero_page() {
   static bf16_t* z = nullptr;
   if (!z) {
@@ -583,19 +610,44 @@ KFA_API int kfa_gemm_pick_bn(int M, int N) {
 
 // C = epilogue(A · Bᵀ); see the file comment.  bn: 0 = auto, 128 or 256;
 // persistent: the tile-sweeping kernel (K >= 64), else one block per tile.
+// Rows per dbias partial (one wave's M extent) of the kernel kfa_gemm_nt picks; 0 =
+// the kernel keeps per-column atomics (persistent variant).
+static int gemm_part_rows(int M, int N, int bn, int persistent) {
+  if (bn == 0) bn = kfa_gemm_pick_bn(M, N);
+  if (persistent == 1) return 0;
+  if (persistent == 3) return 64;             // <128, 3, 8>: 4 x 2 waves of 64 x 64
+  if (persistent == 4) return 128;            // <128, 3, 4>: 2 x 2 waves of 128 x 64
+  return bn == 256 ? 128 : 64;                // <256>: 2 x 4 waves of 128 x 64; <128>: 4 x 2 of 64 x 64
+}
+
+// Floats of the dbias partial workspace kfa_gemm_nt needs (0: none).
+KFA_API long kfa_gemm_dpart_floats(int M, int N, int bn, int persistent) {
+  const int r = gemm_part_rows(M, N, bn, persistent);
+  return r ? (long)((M + r - 1) / r) * N : 0;
+}
+
+// C = epilogue(A · Bᵀ); see the file comment.  bn: 0 = auto, 128 or 256;
+// persistent: 0 = one block per tile, 1 = the tile-sweeping kernel (K >= 64),
+// 3 / 4 = 256 x 128 tiles on a 3-slot ring, two blocks per CU (8 / 4 waves).
+// dbias with dpart (kfa_gemm_dpart_floats floats): per-wave partial column sums
+// + one reduce launch instead of M / rows atomics per column.
 KFA_API int kfa_gemm_nt(const bf16_t* A, const bf16_t* B, bf16_t* C, const bf16_t* E, const float* bias, bf16_t* Z,
-                        const bf16_t* Zin, float* dbias, int M, int N, int K, int lda, int ldb, int ldc, int act,
-                        int dact, int bn, int persistent, hipStream_t st) {
+                        const bf16_t* Zin, float* dbias, float* dpart, int M, int N, int K, int lda, int ldb, int ldc,
+                        int act, int dact, int bn, int persistent, hipStream_t st) {
   if (M <= 0 || N <= 0) return 0;
   if (K <= 0 || K % 8 || N % 8 || lda % 8 || ldb % 8 || ldc % 8 || lda < K || ldb < K || ldc < N) return -1;
   if (act < 0 || act > 3 || dact < 0 || dact > 3) return -1;
+  if (persistent == 1 && K < 2 * GK) persistent = 0;
   const long cb = (long)M * ldc * 2;
   if (cb >= (long)kOOB) return -2;  // 32-bit buffer offsets in the epilogue
+  const int prow = gemm_part_rows(M, N, bn, persistent);
   if (bn == 0) bn = kfa_gemm_pick_bn(M, N);
+  if (persistent == 3 || persistent == 4) bn = 128;
   const long tiles = (long)((M + 255) / 256) * ((N + bn - 1) / bn);
   if (tiles >= (1L << 31)) return -2;
-  const GemmArgs g{A, B, C, E, bias, Z, Zin, dbias, M, N, K, lda, ldb, ldc, act, dact, (unsigned)cb};
-  if (persistent && K >= 2 * GK) {
+  if (!dbias || !prow) dpart = nullptr;
+  const GemmArgs g{A, B, C, E, bias, Z, Zin, dbias, dpart, M, N, K, lda, ldb, ldc, act, dact, (unsigned)cb};
+  if (persistent == 1) {
     const long cus = gemm_cus();
     const int grid = (int)(tiles < cus ? tiles : cus);
     if (bn == 256)
@@ -604,13 +656,19 @@ KFA_API int kfa_gemm_nt(const bf16_t* A, const bf16_t* B, bf16_t* C, const bf16_
       hipLaunchKernelGGL((gemm_pt_kernel<128>), dim3(grid), dim3(512), 0, st, g, gemm_zero_page());
     else
       return -1;
-    return kfa_status();
-  }
-  if (bn == 256)
+  } else if (persistent == 4) {
+    hipLaunchKernelGGL((gemm_nt_kernel<128, 3, 4>), dim3((unsigned)tiles), dim3(256), 0, st, g, gemm_zero_page());
+  } else if (persistent == 3) {
+    hipLaunchKernelGGL((gemm_nt_kernel<128, 3>), dim3((unsigned)tiles), dim3(512), 0, st, g, gemm_zero_page());
+  } else if (bn == 256) {
     hipLaunchKernelGGL((gemm_nt_kernel<256>), dim3((unsigned)tiles), dim3(512), 0, st, g, gemm_zero_page());
-  else if (bn == 128)
+  } else if (bn == 128) {
     hipLaunchKernelGGL((gemm_nt_kernel<128>), dim3((unsigned)tiles), dim3(512), 0, st, g, gemm_zero_page());
-  else
+  } else {
     return -1;
+  }
+  if (dpart)
+    hipLaunchKernelGGL(gemm_dbias_reduce, dim3((N + 255) / 256, kDbRS), dim3(256), 0, st, dpart, dbias,
+                       (M + prow - 1) / prow, N);
   return kfa_status();
 }

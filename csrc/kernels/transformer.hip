@@ -228,7 +228,7 @@ enum Act { kNone = 0, kGelu = 1, kTanh = 2, kRelu = 3 };
 
 __device__ __forceinline__ float act_f(float z, int act) {
   switch (act) {
-    case kGelu: return 0.5f * z * (1.f + erff(z * 0.70710678118654752f));
+    case kGelu: return gelu_f(z);
     case kTanh: return tanhf(z);
     case kRelu: return fmaxf(z, 0.f);
     default: return z;
@@ -237,11 +237,7 @@ __device__ __forceinline__ float act_f(float z, int act) {
 
 __device__ __forceinline__ float act_grad(float z, int act) {
   switch (act) {
-    case kGelu: {
-      const float cdf = 0.5f * (1.f + erff(z * 0.70710678118654752f));
-      const float pdf = 0.39894228040143268f * __expf(-0.5f * z * z);
-      return cdf + z * pdf;
-    }
+    case kGelu: return gelu_grad(z);
     case kTanh: { const float t = tanhf(z); return 1.f - t * t; }
     case kRelu: return z > 0.f ? 1.f : 0.f;
     default: return 1.f;

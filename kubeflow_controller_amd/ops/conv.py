@@ -372,6 +372,12 @@ class GradJoin:
     the separate add kernel.  Autograd's ready-queue order (latest-created node
     first) runs the branch's backward before the conv's; if it ever does not,
     the branch simply returns its gradient to autograd (correct, just unfused).
+
+    A join lives for ONE forward/backward: models create a fresh one per forward
+    (``models/resnet.py``), so no deposit can leak into the next step.  Its
+    backward runs once: ``retain_graph=True`` re-runs and partial
+    ``torch.autograd.grad`` calls over the block are not supported (a second
+    pass would find the state already consumed).
     """
 
     __slots__ = ("grad", "mask", "state", "fused")

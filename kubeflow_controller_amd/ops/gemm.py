@@ -28,16 +28,21 @@ from . import _lib
 from . import conv as _conv  # noqa: F401  (registers kfa_weight_transpose)
 
 P, I = _lib.P, _lib.I
-_lib.register("kfa_gemm_nt", [P] * 8 + [I] * 10 + [P])
+_lib.register("kfa_gemm_nt", [P] * 9 + [I] * 10 + [P])
+_lib.register("kfa_gemm_dpart_floats", [I, I, I, I], restype=_lib.L)
 _lib.register("kfa_gemm_pick_bn", [I, I])
 
 ACTS = {None: 0, "none": 0, "gelu": 1, "tanh": 2, "relu": 3}
-# Dense layers route their projections through this kernel only with KFA_GEMM=1.
-# Measured on MI355X (tools/bench_gemm.py, profiles/r1_gemm_attention.md):
-# hipBLASLt runs the plain BERT / Wide&Deep projections at 800-1250 TFLOP/s vs
-# 550-830 here, and the fused epilogue does not make up the difference, so the
-# default keeps plain GEMMs on the library (the one place it is allowed).
-ROUTE_LAYERS = os.environ.get("KFA_GEMM", "0") == "1"
+# Which dense-layer GEMMs run on this kernel (KFA_GEMM):
+#   "1"      every projection (forward and dgrad);
+#   "fused"  only the ones whose epilogue replaces a separate pass: the FFN-up
+#            forward (bias + GELU + pre-activation) and its dgrad (GELU' +
+#            bias-gradient column sums);
+#   "0"      none (hipBLASLt via torch.mm / addmm for all of them).
+# Measured on MI355X (tools/bench_gemm.py, tools/gpu_bert_gemm.sh; docs/kernels.md).
+_ROUTE = os.environ.get("KFA_GEMM", "0")
+ROUTE_LAYERS = _ROUTE == "1"
+ROUTE_FUSED = _ROUTE in ("1", "fused")
 
 
 def gemm_ok(a: torch.Tensor, b: torch.Tensor) -> bool:
@@ -62,7 +67,12 @@ def _check_vec(t, N, what):
         raise ValueError(f"gemm_nt: {what} must be a contiguous, 16-B aligned fp32 [{N}] vector")
 
 
-PERSISTENT = os.environ.get("KFA_GEMM_PERSIST", "0") == "1"  # measured slower (tools/bench_gemm.py): opt-in
+# Kernel variant: 0 = one 8-wave block per 256 x bn tile (128 KB ring: one block
+# per CU), 1 = persistent blocks carrying the LDS ring across tiles, 3 = 256 x 128
+# blocks on a 3-slot ring (72 KB: two blocks per CU, so one block's barriers and
+# epilogue run under the other's MFMAs — the fastest, default), 4 = as 3 with
+# four 128 x 64 waves.  KFA_GEMM_VARIANT overrides; tools/bench_gemm.py compares.
+PERSISTENT = int(os.environ.get("KFA_GEMM_VARIANT", "3"))
 
 
 def gemm_nt(a, b, *, bias=None, act=None, addend=None, want_z=False, zin=None, dact=None, dbias=None, out=None,
@@ -82,9 +92,14 @@ def gemm_nt(a, b, *, bias=None, act=None, addend=None, want_z=False, zin=None, d
     if (zin is None) != (dact in (None, "none")):
         raise ValueError("gemm_nt: zin and dact go together")
     z = torch.empty_like(c) if want_z else None
+    variant = int(PERSISTENT if persistent is None else persistent)
+    dpart = None
+    if dbias is not None:  # partial column sums + one reduce (no per-column atomics)
+        nf = _lib.lib().kfa_gemm_dpart_floats(M, N, int(bn), variant)
+        dpart = _lib.workspace(4 * nf, a.device, "gemm_dbias") if nf else None
     _lib.call("kfa_gemm_nt", _lib.ptr(a), _lib.ptr(b), _lib.ptr(c), _lib.ptr(addend), _lib.ptr(bias), _lib.ptr(z),
-              _lib.ptr(zin), _lib.ptr(dbias), M, N, K, a.stride(0), b.stride(0), N, ACTS[act], ACTS[dact], int(bn),
-              int(PERSISTENT if persistent is None else persistent), _lib.stream())
+              _lib.ptr(zin), _lib.ptr(dbias), _lib.ptr(dpart), M, N, K, a.stride(0), b.stride(0), N, ACTS[act],
+              ACTS[dact], int(bn), variant, _lib.stream())
     return c, z
 
 

@@ -32,7 +32,6 @@ import torch
 
 ENABLED = os.environ.get("KFA_SIDE_STREAM", "1") != "0"
 _side: Dict[int, torch.cuda.Stream] = {}
-_callback_queued = False
 
 
 def enabled(t: torch.Tensor) -> bool:
@@ -57,14 +56,11 @@ def join(dev=None) -> None:
 
 
 def _end_of_backward() -> None:
-    global _callback_queued
-    _callback_queued = False
     join()
 
 
 def run_on_side(fn: Callable, device: torch.device, tensors: Iterable[torch.Tensor] = ()):
     """``fn()`` on the side stream of ``device``, after the current stream's queued work."""
-    global _callback_queued
     main = torch.cuda.current_stream(device)
     side = side_stream(device)
     side.wait_stream(main)
@@ -73,10 +69,12 @@ def run_on_side(fn: Callable, device: torch.device, tensors: Iterable[torch.Tens
     for t in tensors:
         if t is not None and t.is_cuda:
             t.record_stream(side)
-    if not _callback_queued:
-        try:  # join at the end of this backward pass
-            torch.autograd.Variable._execution_engine.queue_callback(_end_of_backward)
-            _callback_queued = True
-        except RuntimeError:  # not inside a backward pass: join right away
-            main.wait_stream(side)
+    # One join per side-stream launch, queued on THIS backward's graph task: no
+    # process-wide "already queued" flag that a backward which raised (and so
+    # never ran its callbacks) could leave set for the next one.  A join is an
+    # event record + wait, so the extra ones cost nothing measurable.
+    try:
+        torch.autograd.Variable._execution_engine.queue_callback(_end_of_backward)
+    except RuntimeError:  # not inside a backward pass: join right away
+        main.wait_stream(side)
     return out

@@ -86,9 +86,11 @@ def _grad_target(p: torch.Tensor):
 
 
 def _finish(p, buf, direct):
-    if direct:
+    if direct:  # the bucket launch joins the side stream (parallel/ddp.py, ps.py)
         notify_grad_ready(p)
         return None
+    if buf.is_cuda:  # the weight gradient may still be in flight on the side stream
+        _streams.join(buf.device)
     return buf.to(p.dtype)
 
 
@@ -211,7 +213,7 @@ class DenseFn(torch.autograd.Function):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
         has_act = act not in (None, "none")
-        fused = p == 0 and _gemm.ROUTE_LAYERS and _gemm.gemm_ok(x2, weight) and (
+        fused = p == 0 and (_gemm.ROUTE_LAYERS or (_gemm.ROUTE_FUSED and has_act)) and _gemm.gemm_ok(x2, weight) and (
             bias is None or (bias.dtype == torch.float32 and bias.is_contiguous() and bias.data_ptr() % 16 == 0))
         if fused:
             y, z = _gemm.gemm_nt(x2, weight, bias=bias, act=act, want_z=has_act)  # z includes the bias
@@ -241,7 +243,7 @@ class DenseFn(torch.autograd.Function):
             dz = dy2
         dx = None
         if ctx.needs_input_grad[0]:
-            wt = _gemm.transpose(weight) if (fused and weight.shape[1] % 8 == 0) else None
+            wt = _gemm.transpose(weight) if (fused and _gemm.ROUTE_LAYERS and weight.shape[1] % 8 == 0) else None
             if wt is not None and _gemm.gemm_ok(dz, wt):
                 dx = _gemm.gemm_nt(dz, wt)[0].view(shp)
             else:
@@ -414,6 +416,7 @@ class EncoderLayerFn(torch.autograd.Function):
         dev = x.device
         s_attn, s_h1, s_h2 = mix_seed(seed, 1), mix_seed(seed, 2), mix_seed(seed, 3)
         use_g = _gemm.ROUTE_LAYERS and _gemm.gemm_ok(x, wqkv) and _gemm.gemm_ok(x, w1) and w2.shape[0] % 8 == 0 and w2.shape[1] % 8 == 0
+        use_f = use_g or (_gemm.ROUTE_FUSED and _gemm.gemm_ok(x, w1) and w2.shape[0] % 8 == 0 and w2.shape[1] % 8 == 0)
         mm = (lambda a, w: _gemm.gemm_nt(a, w)[0]) if use_g else (lambda a, w: torch.mm(a, w.t()))  # noqa: E731
         fused = fused_attention_ok(S, d)
         # attention
@@ -441,7 +444,7 @@ class EncoderLayerFn(torch.autograd.Function):
         h1, h1s, m1, r1 = ln_fwd(ao, g1, be1, res=x, bias=bo, eps=eps, p=ph, seed=s_h1)
         del ao
         # feed-forward; f1 = pre-activation (GEMM path: bias included)
-        if use_g:
+        if use_f:
             f1a, f1 = _gemm.gemm_nt(h1, w1, bias=b1, act="gelu", want_z=True)
         else:
             f1 = torch.mm(h1, w1.t())                                      # [T, I]
@@ -450,7 +453,7 @@ class EncoderLayerFn(torch.autograd.Function):
         h2, h2s, m2, r2 = ln_fwd(f2, g2, be2, res=h1, bias=b2, eps=eps, p=ph, seed=s_h2)
         ctx.save_for_backward(x, ctxr, h1, h1s, m1, r1, f1, f1a, h2s, m2, r2, *att)
         ctx.params = (wqkv, bqkv, wo, bo, g1, be1, w1, b1, w2, b2, g2, be2)
-        ctx.cfg = (B, S, heads, ph, pa, (s_attn, s_h1, s_h2), qscale, use_g, fused)
+        ctx.cfg = (B, S, heads, ph, pa, (s_attn, s_h1, s_h2), qscale, use_g, use_f, fused)
         ctx.key_bias = key_bias
         return h2
 
@@ -458,7 +461,7 @@ class EncoderLayerFn(torch.autograd.Function):
     def backward(ctx, dy):
         (x, ctxr, h1, h1s, m1, r1, f1, f1a, h2s, m2, r2, *att) = ctx.saved_tensors
         wqkv, bqkv, wo, bo, g1, be1, w1, b1, w2, b2, g2, be2 = ctx.params
-        B, S, heads, ph, pa, (s_attn, s_h1, s_h2), qscale, use_g, fused = ctx.cfg
+        B, S, heads, ph, pa, (s_attn, s_h1, s_h2), qscale, use_g, use_f, fused = ctx.cfg
         key_bias = ctx.key_bias
         T, H = x.shape
         d = H // heads
@@ -469,7 +472,7 @@ class EncoderLayerFn(torch.autograd.Function):
         # LN2 (+ FFN2 bias grad, hidden dropout): dres -> h1, dbranch -> f2
         dh1_res, df2 = ln_bwd(dy, h2s, m2, r2, g2, G(g2), G(be2), G(b2), p=ph, seed=s_h2, want_branch=True)
         _wgrad_side_(G(w2), df2, f1a)
-        if use_g:   # df1 = (df2 · W2) * gelu'(z1), db1 += colsum(df1): one GEMM launch
+        if use_f:   # df1 = (df2 · W2) * gelu'(z1), db1 += colsum(df1): one GEMM launch
             df1 = _gemm.gemm_nt(df2, _gemm.transpose(w2), zin=f1, dact="gelu", dbias=G(b1))[0]
         else:
             df1 = bias_act_bwd(torch.mm(df2, w2), f1, b1, "gelu", G(b1))

@@ -18,10 +18,10 @@ def _bf(*shape, s=1.0):
     return (torch.randn(*shape, device=D) * s).to(torch.bfloat16)
 
 
-@pytest.fixture(params=[True, False], ids=["persistent", "per_tile"], autouse=True)
+@pytest.fixture(params=[1, 0, 2], ids=["persistent", "per_tile", "four_wave"], autouse=True)
 def _persistent(request, monkeypatch):
-    """Every test runs on both GEMM kernels: the persistent tile-sweeping one
-    (default) and the one-block-per-tile one."""
+    """Every test runs on all three GEMM kernels: the persistent tile-sweeping
+    one, the one-8-wave-block-per-tile one and the 4-wave 128 x 128-wave-tile one."""
     from kubeflow_controller_amd.ops import gemm as G
     monkeypatch.setattr(G, "PERSISTENT", request.param)
     return request.param

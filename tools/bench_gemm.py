@@ -46,8 +46,10 @@ def dense():
         t_mm = timeit(lambda: torch.mm(x, w.t()))
         t_128 = timeit(lambda: G.gemm_nt(x, w, bn=128))
         t_256 = timeit(lambda: G.gemm_nt(x, w, bn=256))
-        t_128o = timeit(lambda: G.gemm_nt(x, w, bn=128, persistent=False))
-        t_256o = timeit(lambda: G.gemm_nt(x, w, bn=256, persistent=False))
+        t_128o = timeit(lambda: G.gemm_nt(x, w, bn=128, persistent=1))
+        t_256o = timeit(lambda: G.gemm_nt(x, w, bn=256, persistent=1))
+        t_2cu = timeit(lambda: G.gemm_nt(x, w, persistent=3))
+        t_2cu4 = timeit(lambda: G.gemm_nt(x, w, persistent=4))
         t_ep = timeit(lambda: G.gemm_nt(x, w, bias=b, act="gelu", want_z=True))
         gw = torch.zeros(N, K, device=d, dtype=torch.bfloat16)
         t_wm = timeit(lambda: gw.addmm_(dy.t(), x))
@@ -55,7 +57,8 @@ def dense():
         tf = lambda t: fl / t / 1e9  # noqa: E731
         print(f"{M:6d} {N:5d} {K:5d} | {t_mm:7.3f} {tf(t_mm):5.0f} | {t_128:7.3f} {tf(t_128):5.0f} | "
               f"{t_256:7.3f} {tf(t_256):5.0f} | {t_ep:7.3f} | {t_wm:7.3f} {tf(t_wm):5.0f} | {t_wk:7.3f} {tf(t_wk):5.0f}"
-              f" | per-tile kernel: g128 {tf(t_128o):5.0f} g256 {tf(t_256o):5.0f} TF/s", flush=True)
+              f" | persistent: g128 {tf(t_128o):5.0f} g256 {tf(t_256o):5.0f} | 2/CU g128 {tf(t_2cu):5.0f} 4w {tf(t_2cu4):5.0f} TF/s",
+              flush=True)
 
 
 def attention():
