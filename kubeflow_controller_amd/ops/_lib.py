@@ -56,7 +56,9 @@ def lib():
         if _lib is not None:
             return _lib
         path = _build.kernels_target()
-        if not os.path.exists(path) or os.environ.get("KFA_REBUILD_KERNELS") == "1":
+        if os.environ.get("KFA_KERNELS_SO"):  # A/B experiments: another in-tree build of the same sources
+            path = os.path.join(os.path.dirname(path), os.environ["KFA_KERNELS_SO"])
+        elif not os.path.exists(path) or os.environ.get("KFA_REBUILD_KERNELS") == "1":
             _build.build_kernels()
         h = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
         for name, args in _SIGS.items():

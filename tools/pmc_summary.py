@@ -26,7 +26,7 @@ def main(path, title):
             d["n"] += 1
     print(f"# {title}\n\nSource: `{path}` (rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE "
           f"SQ_INSTS_VALU_MFMA_MOPS_BF16 --kernel-trace).  TFLOP/s = MOPS_BF16 x 512 / dispatch time "
-          f"(dense bf16 peak ~2500).  Includes MIOpen's one-off autotuning dispatches for the 3-channel stem.\n")
+          f"(dense bf16 peak ~2500).\n")
     print("| kernel | dispatches | time ms | MFMA TFLOP/s (bf16) |\n|---|---|---|---|")
     for k, d in sorted(per.items(), key=lambda kv: -kv[1]["ns"])[:20]:
         tf = d["mops"] * 512 / max(d["ns"], 1) / 1e3
