@@ -124,6 +124,98 @@ __device__ __forceinline__ void ring_wait(int ahead) {
   else vm_wait<0>();
 }
 
+// Write-out of one wave tile (acc[ni][mi][r] = C(m = mw + 16mi + fr, n = nw + 16ni + 4fq + r)):
+// bias, addend, pre-activation, activation (forward or backward), dbias column
+// sums, staged through the wave's private LDS area `stage` (16TM rows x 32TN
+// bytes) so every store is 16 B per lane, 8 rows x 128 B per wave instruction.
+template <int TM, int TN>
+__device__ __forceinline__ void tile_epilogue(const GemmArgs& g, floatx4 (&acc)[TN][TM], char* stage, int lane, int mw,
+                                              int nw) {
+  const int fr = lane & 15, fq = lane >> 4;
+  constexpr int ROWS = 16 * TM, RB = 32 * TN, IT = ROWS / 8;  // staged rows, bytes per row, row groups per lane
+  if (g.bias) {
+#pragma unroll
+    for (int ni = 0; ni < TN; ni++) {
+      const int n = nw + ni * 16 + fq * 4;
+      const float4 bb = n < g.N ? *reinterpret_cast<const float4*>(g.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int mi = 0; mi < TM; mi++) {
+        acc[ni][mi][0] += bb.x;
+        acc[ni][mi][1] += bb.y;
+        acc[ni][mi][2] += bb.z;
+        acc[ni][mi][3] += bb.w;
+      }
+    }
+  }
+#pragma unroll
+  for (int mi = 0; mi < TM; mi++)
+#pragma unroll
+    for (int ni = 0; ni < TN; ni++) {
+      const int row = mi * 16 + fr, col = ni * 16 + fq * 4;
+      *reinterpret_cast<uint2*>(stage + row * RB + (((col >> 3) ^ (row & 7)) << 4) + (col & 7) * 2) =
+          make_uint2(pack2(acc[ni][mi][0], acc[ni][mi][1]), pack2(acc[ni][mi][2], acc[ni][mi][3]));
+    }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave reads back only its own stage
+
+  const int c = lane & 7;
+  const int n = nw + c * 8;
+  const bool nok = n < g.N;
+  const __amdgpu_buffer_rsrc_t rC = rsrc(g.C, g.c_bytes);
+  const __amdgpu_buffer_rsrc_t rE = rsrc(g.E ? g.E : g.C, g.E ? g.c_bytes : 0u);
+  const __amdgpu_buffer_rsrc_t rZ = rsrc(g.Z ? g.Z : g.C, g.Z ? g.c_bytes : 0u);
+  const __amdgpu_buffer_rsrc_t rZi = rsrc(g.Zin ? g.Zin : g.C, g.Zin ? g.c_bytes : 0u);
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int it = 0; it < IT; it++) {
+    const int r = it * 8 + (lane >> 3);
+    const int m = mw + r;
+    const unsigned off = (m < g.M && nok) ? ((unsigned)m * (unsigned)g.ldc + (unsigned)n) * 2u : kOOB;
+    float f[8];
+    unpack8(*reinterpret_cast<const uint4*>(stage + r * RB + ((c ^ (r & 7)) << 4)), f);
+    if (g.E) {
+      float h[8];
+      unpack8(bload(rE, off), h);
+#pragma unroll
+      for (int j = 0; j < 8; j++) f[j] += h[j];
+    }
+    if (g.Z) bstore(rZ, off, pack8(f));
+    if (g.act) {
+#pragma unroll
+      for (int j = 0; j < 8; j++) f[j] = act_fwd(f[j], g.act);
+    }
+    if (g.Zin) {
+      float z[8];
+      unpack8(bload(rZi, off), z);
+#pragma unroll
+      for (int j = 0; j < 8; j++) f[j] *= act_bwd(z[j], g.dact);
+    }
+    const uint4 o = pack8(f);
+    bstore(rC, off, o);
+    if (g.dbias && off != kOOB) {
+      float q[8];
+      unpack8(o, q);  // the bf16-rounded values the next layer sees
+#pragma unroll
+      for (int j = 0; j < 8; j++) cs[j] += q[j];
+    }
+  }
+  if (g.dbias) {
+#pragma unroll
+    for (int o = 8; o < 64; o <<= 1)
+#pragma unroll
+      for (int j = 0; j < 8; j++) cs[j] += __shfl_xor(cs[j], o, 64);
+    if (lane < 8 && nok) {
+      if (g.dpart) {  // M / ROWS partials per column, summed by gemm_dbias_reduce: no L2-serialised atomics
+        float* pp = g.dpart + (long)(mw / ROWS) * g.N + n;
+        *reinterpret_cast<float4*>(pp) = make_float4(cs[0], cs[1], cs[2], cs[3]);
+        *reinterpret_cast<float4*>(pp + 4) = make_float4(cs[4], cs[5], cs[6], cs[7]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; j++) atomicAdd(g.dbias + n + j, cs[j]);
+      }
+    }
+  }
+}
+
 template <int BN, int NS = NSLOT, int NW = 8>
 __global__ __launch_bounds__(NW * 64, 8 / NW) void gemm_nt_kernel(GemmArgs g, const bf16_t* __restrict__ zp) {
   constexpr int BM = 256;
@@ -215,90 +307,9 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void gemm_nt_kernel(GemmArgs g, co
   }
 
   // ---- epilogue: acc[ni][mi][r] = C(m = m0 + wm*16TM + 16mi + fr, n = n0 + wn*64 + 16ni + 4fq + r)
-  constexpr int ROWS = 16 * TM, RB = 32 * TN, IT = ROWS / 8;  // staged rows, bytes per row, row groups per lane
-  char* stage = reinterpret_cast<char*>(smem) + wave * ROWS * RB;  // ring is idle: every wave passed the last barrier
-  const int nw = n0 + wn * 64;
-  if (g.bias) {
-#pragma unroll
-    for (int ni = 0; ni < TN; ni++) {
-      const int n = nw + ni * 16 + fq * 4;
-      const float4 bb = n < g.N ? *reinterpret_cast<const float4*>(g.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-      for (int mi = 0; mi < TM; mi++) {
-        acc[ni][mi][0] += bb.x;
-        acc[ni][mi][1] += bb.y;
-        acc[ni][mi][2] += bb.z;
-        acc[ni][mi][3] += bb.w;
-      }
-    }
-  }
-#pragma unroll
-  for (int mi = 0; mi < TM; mi++)
-#pragma unroll
-    for (int ni = 0; ni < TN; ni++) {
-      const int row = mi * 16 + fr, col = ni * 16 + fq * 4;
-      *reinterpret_cast<uint2*>(stage + row * RB + (((col >> 3) ^ (row & 7)) << 4) + (col & 7) * 2) =
-          make_uint2(pack2(acc[ni][mi][0], acc[ni][mi][1]), pack2(acc[ni][mi][2], acc[ni][mi][3]));
-    }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave reads back only its own stage
-
-  const int c = lane & 7;
-  const int n = nw + c * 8;
-  const bool nok = n < g.N;
-  const __amdgpu_buffer_rsrc_t rC = rsrc(g.C, g.c_bytes);
-  const __amdgpu_buffer_rsrc_t rE = rsrc(g.E ? g.E : g.C, g.E ? g.c_bytes : 0u);
-  const __amdgpu_buffer_rsrc_t rZ = rsrc(g.Z ? g.Z : g.C, g.Z ? g.c_bytes : 0u);
-  const __amdgpu_buffer_rsrc_t rZi = rsrc(g.Zin ? g.Zin : g.C, g.Zin ? g.c_bytes : 0u);
-  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-  for (int it = 0; it < IT; it++) {
-    const int r = it * 8 + (lane >> 3);
-    const int m = m0 + wm * ROWS + r;
-    const unsigned off = (m < g.M && nok) ? ((unsigned)m * (unsigned)g.ldc + (unsigned)n) * 2u : kOOB;
-    float f[8];
-    unpack8(*reinterpret_cast<const uint4*>(stage + r * RB + ((c ^ (r & 7)) << 4)), f);
-    if (g.E) {
-      float h[8];
-      unpack8(bload(rE, off), h);
-#pragma unroll
-      for (int j = 0; j < 8; j++) f[j] += h[j];
-    }
-    if (g.Z) bstore(rZ, off, pack8(f));
-    if (g.act) {
-#pragma unroll
-      for (int j = 0; j < 8; j++) f[j] = act_fwd(f[j], g.act);
-    }
-    if (g.Zin) {
-      float z[8];
-      unpack8(bload(rZi, off), z);
-#pragma unroll
-      for (int j = 0; j < 8; j++) f[j] *= act_bwd(z[j], g.dact);
-    }
-    const uint4 o = pack8(f);
-    bstore(rC, off, o);
-    if (g.dbias && off != kOOB) {
-      float q[8];
-      unpack8(o, q);  // the bf16-rounded values the next layer sees
-#pragma unroll
-      for (int j = 0; j < 8; j++) cs[j] += q[j];
-    }
-  }
-  if (g.dbias) {
-#pragma unroll
-    for (int o = 8; o < 64; o <<= 1)
-#pragma unroll
-      for (int j = 0; j < 8; j++) cs[j] += __shfl_xor(cs[j], o, 64);
-    if (lane < 8 && nok) {
-      if (g.dpart) {  // M / ROWS partials per column, summed by gemm_dbias_reduce: no L2-serialised atomics
-        float* pp = g.dpart + (long)((m0 + wm * ROWS) / ROWS) * g.N + n;
-        *reinterpret_cast<float4*>(pp) = make_float4(cs[0], cs[1], cs[2], cs[3]);
-        *reinterpret_cast<float4*>(pp + 4) = make_float4(cs[4], cs[5], cs[6], cs[7]);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; j++) atomicAdd(g.dbias + n + j, cs[j]);
-      }
-    }
-  }
+  // ring is idle: every wave passed the last barrier
+  tile_epilogue<TM, TN>(g, acc, reinterpret_cast<char*>(smem) + wave * (16 * TM) * (32 * TN), lane, m0 + wm * 16 * TM,
+                        n0 + wn * 64);
 }
 
 // ---------------------------------------------------------------------------
@@ -556,6 +567,224 @@ __global__ __launch_bounds__(512) void gemm_pt_kernel(GemmArgs g, const bf16_t* 
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Ping-pong 256x256 kernel (cdna_hip_programming.md §5, "The 256² 8-phase
+// template"): 512 threads = two wave GROUPS (waves 0-3 own output rows
+// 0-127, waves 4-7 rows 128-255; wave w owns the 128 x 64 tile at
+// (w >> 2, w & 3)), one block per CU, BK = 64, two LDS buffers of 64 KB.
+// Each k-tile is split into four 16 KB PIECES (128 rows x 64 k), ordered by
+// when the waves first need them:
+//   piece 0 "A0": A rows {0-63, 128-191}   (each group's first 64 rows)
+//   piece 1 "B0": B rows {64c + 0..31}      (each wave's first 32 columns)
+//   piece 2 "B1": B rows {64c + 32..63}
+//   piece 3 "A1": A rows {64-127, 192-255}
+// and the k-tile runs in four PHASES of 16 MFMAs per wave (one 64 x 32
+// quadrant of the wave tile, K = 64):
+//   s0: read A0 (8 x ds_read_b128) + B0 (4) -> rows 0-63  x cols 0-31
+//   s1: read B1 (4)                         -> rows 0-63  x cols 32-63
+//   s2: read A1 (8)                         -> rows 64-127 x cols 32-63
+//   s3: (registers only)                    -> rows 64-127 x cols 0-31
+// Phase = { ds_reads + one piece's LDS-DMA (2 buffer_load ... lds per lane)
+// ; counted vmcnt ; s_barrier ; lgkmcnt(0) ; 16 MFMAs ; s_barrier }.  Group 1
+// runs ONE barrier behind group 0 (an extra s_barrier before its first phase),
+// so on every SIMD (one wave of each group) one wave's MFMAs overlap the other
+// wave's LDS reads and DMA issue — the MFMA pipe never waits for the reads.
+// Hazards (P = global phase 4u + s; a piece read in phase Q is free for a DMA
+// from phase Q + 2; a DMA retired by the vmcnt of phase W is readable from
+// phase W + 1):
+//   phase 4u+0 issues B1(u+1), 4u+1 A1(u+1), 4u+2 A0(u+2), 4u+3 B0(u+2)
+// — the piece of phase P belongs to k-tile (P + 6) >> 2 — and the vmcnt of
+// phase P retires the piece of phase P - 4: four pieces (8 DMAs/lane, ~2000
+// cycles) stay in flight across the barriers, never vmcnt(0) in steady state.
+// Operand rows go through 32-bit buffer offsets (rows past M / N read as 0 by
+// the buffer range check); the k-tile advances in the scalar offset.  LDS
+// image: 128-B rows, 16-B chunk c of row r stored at c ^ ((r >> 1) & 7) via the
+// per-lane SOURCE address (rule 21): conflict-free for the 16x16x32 fragment
+// reads (ds_read_b128 lane groups, MI355X_MICROARCH.md §LDS).
+constexpr int PP_BK = 64;
+constexpr int PP_PIECE = 128 * PP_BK * 2;  // bytes per piece
+
+__device__ __forceinline__ void pp_dma(__amdgpu_buffer_rsrc_t r, char* lds, int voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void pp_vmcnt() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+}
+// retire every DMA except the pieces issued in the `younger` (0..4) most recent phases
+__device__ __forceinline__ void pp_retire(int younger) {
+  if (younger >= 4) pp_vmcnt<8>();
+  else if (younger == 3) pp_vmcnt<6>();
+  else if (younger == 2) pp_vmcnt<4>();
+  else if (younger == 1) pp_vmcnt<2>();
+  else pp_vmcnt<0>();
+}
+
+__global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
+  constexpr int TM = 8, TN = 4;
+  __shared__ __attribute__((aligned(16))) char smem[2 * 4 * PP_PIECE];  // 128 KB
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  // T1 XCD remap + grouped raster (as gemm_nt_kernel)
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q8 = nwg >> 3, r8 = nwg & 7, x8 = bid & 7;
+  const int wg = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + (bid >> 3);
+  const int ntn = (g.N + 255) / 256, ntm = (g.M + 255) / 256;
+  constexpr int GM = 4;
+  const int grp = wg / (GM * ntn), gm0 = grp * GM, gmn = min(GM, ntm - gm0), rem = wg - grp * GM * ntn;
+  const int m0 = (gm0 + rem % gmn) * 256, n0 = (rem / gmn) * 256;
+
+  const __amdgpu_buffer_rsrc_t rA = rsrc(g.A, (unsigned)(((long)(g.M - 1) * g.lda + g.K) * 2));
+  const __amdgpu_buffer_rsrc_t rB = rsrc(g.B, (unsigned)(((long)(g.N - 1) * g.ldb + g.K) * 2));
+  // DMA plan: instruction j of wave w fills piece rows j*64 + w*8 + lane/8,
+  // physical chunk lane&7 <- logical chunk (lane&7) ^ ((row >> 1) & 7)
+  const int prow = wave * 8 + (lane >> 3);
+  const int lc = (lane & 7) ^ ((prow >> 1) & 7);
+  int voff[4][2];
+#pragma unroll
+  for (int j = 0; j < 2; j++) {
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int m = m0 + j * 128 + h * 64 + prow;
+      voff[h ? 3 : 0][j] = m < g.M ? (m * g.lda + lc * 8) * 2 : (int)kOOB;
+      const int n = n0 + (2 * j + (prow >> 5)) * 64 + h * 32 + (prow & 31);
+      voff[h ? 2 : 1][j] = n < g.N ? (n * g.ldb + lc * 8) * 2 : (int)kOOB;
+    }
+  }
+  const int nk = g.K / PP_BK;
+  const int plast = 4 * nk - 7;  // last phase that issues a piece
+  // STEADY (compile-time): the phase is known to issue its piece (k-tile < nk)
+  // and to retire with vmcnt(8) — no runtime count in the main loop.
+  auto issue = [&](int P, auto pc, auto steady) __attribute__((always_inline)) {
+    constexpr int p = decltype(pc)::value;
+    const int kt = (P + 6) >> 2;
+    if (decltype(steady)::value || kt < nk) {
+      char* dst = smem + (kt & 1) * (4 * PP_PIECE) + p * PP_PIECE + wave * 8 * 128;
+      const __amdgpu_buffer_rsrc_t r = (p == 0 || p == 3) ? rA : rB;
+      pp_dma(r, dst, voff[p][0], kt * PP_BK * 2);
+      pp_dma(r, dst + 64 * 128, voff[p][1], kt * PP_BK * 2);
+    }
+  };
+  auto retire = [&](int P, auto steady) __attribute__((always_inline)) {
+    if constexpr (decltype(steady)::value) {
+      pp_vmcnt<8>();
+    } else {
+      const int younger = min(P, plast) - (P - 3) + 1;
+      pp_retire(younger < 0 ? 0 : younger);
+    }
+  };
+
+  // this lane's fragment read offsets in a piece: row fr, logical chunk 4 ks + fq
+  const int fr = lane & 15, fq = lane >> 4;
+  const int ro0 = fr * 128 + ((fq ^ (fr >> 1)) << 4), ro1 = fr * 128 + (((4 + fq) ^ (fr >> 1)) << 4);
+  floatx4 acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; i++)
+#pragma unroll
+    for (int j = 0; j < TM; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  short8 a[4][2], b0[2][2], b1[2][2];
+
+  // prologue: pieces of phases -6..-1 (A0 B0 B1 A1 of k-tile 0, A0 B0 of k-tile 1)
+  issue(-6, std::integral_constant<int, 0>{}, std::false_type{});
+  issue(-5, std::integral_constant<int, 1>{}, std::false_type{});
+  issue(-4, std::integral_constant<int, 2>{}, std::false_type{});
+  issue(-3, std::integral_constant<int, 3>{}, std::false_type{});
+  issue(-2, std::integral_constant<int, 0>{}, std::false_type{});
+  issue(-1, std::integral_constant<int, 1>{}, std::false_type{});
+  retire(-1, std::false_type{});
+  asm volatile("s_barrier" ::: "memory");
+  if (wr) asm volatile("s_barrier" ::: "memory");  // group 1 runs one barrier behind
+
+  auto mfma_q = [&](short8 (&bb)[2][2], int mh, int nh) __attribute__((always_inline)) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ks++)
+#pragma unroll
+      for (int ni = 0; ni < 2; ni++)
+#pragma unroll
+        for (int mi = 0; mi < 4; mi++)
+          acc[nh * 2 + ni][mh * 4 + mi] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[ni][ks], a[mi][ks], acc[nh * 2 + ni][mh * 4 + mi], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto rd = [&](const char* p) -> short8 { return *reinterpret_cast<const short8*>(p); };
+
+  // one k-tile = four phases (st: std::true_type when every phase of k-tile u
+  // issues a piece, i.e. u + 2 < nk)
+  auto ktile = [&](int u, auto st) __attribute__((always_inline)) {
+    const char* buf = smem + (u & 1) * (4 * PP_PIECE);
+    const int P = 4 * u;
+    // s0: A0 + B0
+    {
+      const char* pa = buf + wr * 64 * 128;
+      const char* pb = buf + PP_PIECE + wc * 32 * 128;
+#pragma unroll
+      for (int ni = 0; ni < 2; ni++) {
+        b0[ni][0] = rd(pb + ni * 16 * 128 + ro0);
+        b0[ni][1] = rd(pb + ni * 16 * 128 + ro1);
+      }
+#pragma unroll
+      for (int mi = 0; mi < 4; mi++) {
+        a[mi][0] = rd(pa + mi * 16 * 128 + ro0);
+        a[mi][1] = rd(pa + mi * 16 * 128 + ro1);
+      }
+      issue(P, std::integral_constant<int, 2>{}, st);
+      retire(P, st);
+      asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      mfma_q(b0, 0, 0);
+      asm volatile("s_barrier" ::: "memory");
+    }
+    // s1: B1
+    {
+      const char* pb = buf + 2 * PP_PIECE + wc * 32 * 128;
+#pragma unroll
+      for (int ni = 0; ni < 2; ni++) {
+        b1[ni][0] = rd(pb + ni * 16 * 128 + ro0);
+        b1[ni][1] = rd(pb + ni * 16 * 128 + ro1);
+      }
+      issue(P + 1, std::integral_constant<int, 3>{}, st);
+      retire(P + 1, st);
+      asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      mfma_q(b1, 0, 1);
+      asm volatile("s_barrier" ::: "memory");
+    }
+    // s2: A1
+    {
+      const char* pa = buf + 3 * PP_PIECE + wr * 64 * 128;
+#pragma unroll
+      for (int mi = 0; mi < 4; mi++) {
+        a[mi][0] = rd(pa + mi * 16 * 128 + ro0);
+        a[mi][1] = rd(pa + mi * 16 * 128 + ro1);
+      }
+      issue(P + 2, std::integral_constant<int, 0>{}, st);
+      retire(P + 2, st);
+      asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      mfma_q(b1, 1, 1);
+      asm volatile("s_barrier" ::: "memory");
+    }
+    // s3: registers only
+    {
+      issue(P + 3, std::integral_constant<int, 1>{}, st);
+      retire(P + 3, st);
+      asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      mfma_q(b0, 1, 0);
+      asm volatile("s_barrier" ::: "memory");
+    }
+  };
+  int u = 0;
+  for (; u + 2 < nk; u++) ktile(u, std::true_type{});
+  for (; u < nk; u++) ktile(u, std::false_type{});
+  if (!wr) asm volatile("s_barrier" ::: "memory");  // both groups at the same barrier count: the ring is idle
+  tile_epilogue<TM, TN>(g, acc, smem + wave * (16 * TM) * (32 * TN), lane, m0 + wr * 128, n0 + wc * 64);
+}
+
 }  // namespace
 
 namespace {
@@ -617,6 +846,7 @@ static int gemm_part_rows(int M, int N, int bn, int persistent) {
   if (persistent == 1) return 0;
   if (persistent == 3) return 64;             // <128, 3, 8>: 4 x 2 waves of 64 x 64
   if (persistent == 4) return 128;            // <128, 3, 4>: 2 x 2 waves of 128 x 64
+  if (persistent == 5) return 128;            // ping-pong 256 x 256: 2 x 4 waves of 128 x 64
   return bn == 256 ? 128 : 64;                // <256>: 2 x 4 waves of 128 x 64; <128>: 4 x 2 of 64 x 64
 }
 
@@ -638,11 +868,14 @@ KFA_API int kfa_gemm_nt(const bf16_t* A, const bf16_t* B, bf16_t* C, const bf16_
   if (K <= 0 || K % 8 || N % 8 || lda % 8 || ldb % 8 || ldc % 8 || lda < K || ldb < K || ldc < N) return -1;
   if (act < 0 || act > 3 || dact < 0 || dact > 3) return -1;
   if (persistent == 1 && K < 2 * GK) persistent = 0;
+  // ping-pong kernel: K in whole 64-deep k-tiles, operand extents within 31-bit buffer offsets
+  if (persistent == 5 && (K % PP_BK || (long)M * lda * 2 >= (long)kOOB || (long)N * ldb * 2 >= (long)kOOB)) persistent = 4;  // same dbias partial rows (128)
   const long cb = (long)M * ldc * 2;
   if (cb >= (long)kOOB) return -2;  // 32-bit buffer offsets in the epilogue
   const int prow = gemm_part_rows(M, N, bn, persistent);
   if (bn == 0) bn = kfa_gemm_pick_bn(M, N);
   if (persistent == 3 || persistent == 4) bn = 128;
+  if (persistent == 5) bn = 256;
   const long tiles = (long)((M + 255) / 256) * ((N + bn - 1) / bn);
   if (tiles >= (1L << 31)) return -2;
   if (!dbias || !prow) dpart = nullptr;
@@ -656,6 +889,8 @@ KFA_API int kfa_gemm_nt(const bf16_t* A, const bf16_t* B, bf16_t* C, const bf16_
       hipLaunchKernelGGL((gemm_pt_kernel<128>), dim3(grid), dim3(512), 0, st, g, gemm_zero_page());
     else
       return -1;
+  } else if (persistent == 5) {
+    hipLaunchKernelGGL(gemm_pp_kernel, dim3((unsigned)tiles), dim3(512), 0, st, g);
   } else if (persistent == 4) {
     hipLaunchKernelGGL((gemm_nt_kernel<128, 3, 4>), dim3((unsigned)tiles), dim3(256), 0, st, g, gemm_zero_page());
   } else if (persistent == 3) {

@@ -18,10 +18,12 @@ def _bf(*shape, s=1.0):
     return (torch.randn(*shape, device=D) * s).to(torch.bfloat16)
 
 
-@pytest.fixture(params=[1, 0, 2], ids=["persistent", "per_tile", "four_wave"], autouse=True)
+@pytest.fixture(params=[1, 0, 2, 3, 5], ids=["persistent", "per_tile", "four_wave", "two_per_cu", "pingpong"], autouse=True)
 def _persistent(request, monkeypatch):
-    """Every test runs on all three GEMM kernels: the persistent tile-sweeping
-    one, the one-8-wave-block-per-tile one and the 4-wave 128 x 128-wave-tile one."""
+    """Every test runs on every GEMM kernel: the persistent tile-sweeping one,
+    the one-8-wave-block-per-tile one, the 4-wave 128 x 128-wave-tile one, the
+    two-blocks-per-CU 256 x 128 one and the 256 x 256 ping-pong one (which
+    falls back to variant 4 when K % 64 != 0)."""
     from kubeflow_controller_amd.ops import gemm as G
     monkeypatch.setattr(G, "PERSISTENT", request.param)
     return request.param
@@ -114,3 +116,19 @@ def test_dense_layer_uses_fused_gemm_and_matches_reference(monkeypatch):
     _close(x.grad, xr.grad, 3e-2, "dx")
     _close(w.grad, wr.grad, 3e-2, "dw")
     _close(b.grad, br.grad, 3e-2, "db")
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (300, 520, 128), (4096, 4096, 3072), (33000, 776, 768),
+                                   (777, 2304, 192), (32768, 3072, 768)])
+def test_gemm_pingpong_shapes(M, N, K):
+    """Ping-pong kernel: one k-tile (prologue + tail only), M / N tails (rows
+    past the operand read as zero by the buffer range check), deep K (many
+    steady-state k-tiles), BERT shapes; bias + GELU + pre-activation epilogue."""
+    from kubeflow_controller_amd.ops import gemm as G
+    torch.manual_seed(7)
+    a, b = _bf(M, K), _bf(N, K, s=0.05)
+    bias = torch.randn(N, device=D)
+    c, z = G.gemm_nt(a, b, bias=bias, act="gelu", want_z=True, persistent=5)
+    zr = a.float() @ b.float().t() + bias
+    _close(z, zr, 1e-2, f"Z {M}x{N}x{K}")
+    _close(c, torch.nn.functional.gelu(zr), 1e-2, f"C {M}x{N}x{K}")

@@ -34,7 +34,7 @@ def timeit(fn, iters=20):
 def dense():
     d = torch.device("cuda")
     shapes = [(32768, 2304, 768), (32768, 768, 768), (32768, 3072, 768), (32768, 768, 3072),
-              (8192, 2304, 768), (8192, 768, 3072), (65536, 1024, 1680), (65536, 512, 1024)]
+              (8192, 2304, 768), (8192, 768, 3072), (65536, 1024, 1680), (65536, 512, 1024), (8192, 8192, 8192)]
     print(f"{'M':>6} {'N':>5} {'K':>5} | {'mm ms':>7} {'TF/s':>5} | {'g128':>7} {'TF/s':>5} | {'g256':>7} {'TF/s':>5}"
           f" | {'gelu+z':>7} | {'wg mm':>7} {'TF/s':>5} | {'wg kfa':>7} {'TF/s':>5}")
     for M, N, K in shapes:
@@ -50,6 +50,7 @@ def dense():
         t_256o = timeit(lambda: G.gemm_nt(x, w, bn=256, persistent=1))
         t_2cu = timeit(lambda: G.gemm_nt(x, w, persistent=3))
         t_2cu4 = timeit(lambda: G.gemm_nt(x, w, persistent=4))
+        t_pp = timeit(lambda: G.gemm_nt(x, w, persistent=5))
         t_ep = timeit(lambda: G.gemm_nt(x, w, bias=b, act="gelu", want_z=True))
         gw = torch.zeros(N, K, device=d, dtype=torch.bfloat16)
         t_wm = timeit(lambda: gw.addmm_(dy.t(), x))
@@ -57,7 +58,7 @@ def dense():
         tf = lambda t: fl / t / 1e9  # noqa: E731
         print(f"{M:6d} {N:5d} {K:5d} | {t_mm:7.3f} {tf(t_mm):5.0f} | {t_128:7.3f} {tf(t_128):5.0f} | "
               f"{t_256:7.3f} {tf(t_256):5.0f} | {t_ep:7.3f} | {t_wm:7.3f} {tf(t_wm):5.0f} | {t_wk:7.3f} {tf(t_wk):5.0f}"
-              f" | persistent: g128 {tf(t_128o):5.0f} g256 {tf(t_256o):5.0f} | 2/CU g128 {tf(t_2cu):5.0f} 4w {tf(t_2cu4):5.0f} TF/s",
+              f" | persistent: g128 {tf(t_128o):5.0f} g256 {tf(t_256o):5.0f} | 2/CU g128 {tf(t_2cu):5.0f} 4w {tf(t_2cu4):5.0f} | pingpong {tf(t_pp):5.0f} TF/s",
               flush=True)
 
 
