@@ -93,9 +93,11 @@ __device__ __forceinline__ uint4 bload(__amdgpu_buffer_rsrc_t r, unsigned off) {
   auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
   return *reinterpret_cast<uint4*>(&v);
 }
-__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, unsigned off, uint4 v) {
+// aux: cache policy (2 = non-temporal: streamed past the caches)
+__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, unsigned off, uint4 v, int aux = 0) {
   using V = decltype(__builtin_amdgcn_raw_buffer_load_b128(r, 0, 0, 0));
-  __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<V*>(&v), r, off, 0, 0);
+  if (aux == 2) __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<V*>(&v), r, off, 0, 2);
+  else __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<V*>(&v), r, off, 0, 0);
 }
 
 // 16 B per lane HBM/L2 -> LDS.  A plain device function: the builtin named
@@ -124,15 +126,52 @@ __device__ __forceinline__ void ring_wait(int ahead) {
   else vm_wait<0>();
 }
 
+// acc[ni][mi][r] += bias[nw + 16 ni + 4 fq + r] from wave-uniform SCALAR loads
+// (constant address space -> s_load) of the wave's 64 bias values: no VGPR-
+// destination global load, so hipcc does not drain vmcnt(0) (and with it the
+// LDS-DMA pieces in flight) before the bias is used.
+template <int TM, int TN>
+__device__ __forceinline__ void add_bias_scalar(const GemmArgs& g, floatx4 (&acc)[TN][TM], int nw, int fq) {
+  const int nb = __builtin_amdgcn_readfirstlane(nw);
+  typedef __attribute__((address_space(4))) const float cfloat;
+  cfloat* cbias = reinterpret_cast<cfloat*>(reinterpret_cast<uintptr_t>(g.bias));
+#pragma unroll
+  for (int ni = 0; ni < TN; ni++) {
+    float b4[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      // column nb + 16 ni + 4 q' + r for this lane's q' = fq: select among the 4 uniform quads
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int col = nb + ni * 16 + q * 4 + r;
+        v[r] = col < g.N ? cbias[col] : 0.f;
+      }
+      if (q == 0) { b4[0] = v[0]; b4[1] = v[1]; b4[2] = v[2]; b4[3] = v[3]; }
+      else if (fq == q) { b4[0] = v[0]; b4[1] = v[1]; b4[2] = v[2]; b4[3] = v[3]; }
+    }
+#pragma unroll
+    for (int mi = 0; mi < TM; mi++) {
+      acc[ni][mi][0] += b4[0];
+      acc[ni][mi][1] += b4[1];
+      acc[ni][mi][2] += b4[2];
+      acc[ni][mi][3] += b4[3];
+    }
+  }
+}
+
 // Write-out of one wave tile (acc[ni][mi][r] = C(m = mw + 16mi + fr, n = nw + 16ni + 4fq + r)):
 // bias, addend, pre-activation, activation (forward or backward), dbias column
 // sums, staged through the wave's private LDS area `stage` (16TM rows x 32TN
 // bytes) so every store is 16 B per lane, 8 rows x 128 B per wave instruction.
-template <int TM, int TN>
+// NTST: non-temporal C / Z stores.
+template <int TM, int TN, int PTM = TM, bool NTST = false>
 __device__ __forceinline__ void tile_epilogue(const GemmArgs& g, floatx4 (&acc)[TN][TM], char* stage, int lane, int mw,
                                               int nw) {
   const int fr = lane & 15, fq = lane >> 4;
-  constexpr int ROWS = 16 * TM, RB = 32 * TN, IT = ROWS / 8;  // staged rows, bytes per row, row groups per lane
+  // ROWS: the wave tile's rows; staged PTM m-tiles (16 PTM rows) per pass
+  constexpr int ROWS = 16 * TM, RB = 32 * TN, IT = 16 * PTM / 8;  // rows, bytes per staged row, row groups per lane per pass
+  static_assert(TM % PTM == 0, "whole passes");
   if (g.bias) {
 #pragma unroll
     for (int ni = 0; ni < TN; ni++) {
@@ -147,16 +186,6 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& g, floatx4 (&acc)[
       }
     }
   }
-#pragma unroll
-  for (int mi = 0; mi < TM; mi++)
-#pragma unroll
-    for (int ni = 0; ni < TN; ni++) {
-      const int row = mi * 16 + fr, col = ni * 16 + fq * 4;
-      *reinterpret_cast<uint2*>(stage + row * RB + (((col >> 3) ^ (row & 7)) << 4) + (col & 7) * 2) =
-          make_uint2(pack2(acc[ni][mi][0], acc[ni][mi][1]), pack2(acc[ni][mi][2], acc[ni][mi][3]));
-    }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave reads back only its own stage
-
   const int c = lane & 7;
   const int n = nw + c * 8;
   const bool nok = n < g.N;
@@ -165,10 +194,24 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& g, floatx4 (&acc)[
   const __amdgpu_buffer_rsrc_t rZ = rsrc(g.Z ? g.Z : g.C, g.Z ? g.c_bytes : 0u);
   const __amdgpu_buffer_rsrc_t rZi = rsrc(g.Zin ? g.Zin : g.C, g.Zin ? g.c_bytes : 0u);
   float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  static_for<TM / PTM>([&](auto pc) {
+    constexpr int pass = decltype(pc)::value;
+    if (pass) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave read back its previous pass
+#pragma unroll
+    for (int mj = 0; mj < PTM; mj++)
+#pragma unroll
+      for (int ni = 0; ni < TN; ni++) {
+        const int mi = pass * PTM + mj;
+        const int row = mj * 16 + fr, col = ni * 16 + fq * 4;
+        char* dst = stage + row * RB + (((col >> 3) ^ (row & 7)) << 4) + (col & 7) * 2;
+        const uint2 v = make_uint2(pack2(acc[ni][mi][0], acc[ni][mi][1]), pack2(acc[ni][mi][2], acc[ni][mi][3]));
+        *reinterpret_cast<uint2*>(dst) = v;
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave reads back only its own stage
 #pragma unroll 4
   for (int it = 0; it < IT; it++) {
     const int r = it * 8 + (lane >> 3);
-    const int m = mw + r;
+    const int m = mw + pass * 16 * PTM + r;
     const unsigned off = (m < g.M && nok) ? ((unsigned)m * (unsigned)g.ldc + (unsigned)n) * 2u : kOOB;
     float f[8];
     unpack8(*reinterpret_cast<const uint4*>(stage + r * RB + ((c ^ (r & 7)) << 4)), f);
@@ -178,7 +221,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& g, floatx4 (&acc)[
 #pragma unroll
       for (int j = 0; j < 8; j++) f[j] += h[j];
     }
-    if (g.Z) bstore(rZ, off, pack8(f));
+    if (g.Z) bstore(rZ, off, pack8(f), NTST ? 2 : 0);
     if (g.act) {
 #pragma unroll
       for (int j = 0; j < 8; j++) f[j] = act_fwd(f[j], g.act);
@@ -190,7 +233,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& g, floatx4 (&acc)[
       for (int j = 0; j < 8; j++) f[j] *= act_bwd(z[j], g.dact);
     }
     const uint4 o = pack8(f);
-    bstore(rC, off, o);
+    bstore(rC, off, o, NTST ? 2 : 0);
     if (g.dbias && off != kOOB) {
       float q[8];
       unpack8(o, q);  // the bf16-rounded values the next layer sees
@@ -198,6 +241,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& g, floatx4 (&acc)[
       for (int j = 0; j < 8; j++) cs[j] += q[j];
     }
   }
+  });
   if (g.dbias) {
 #pragma unroll
     for (int o = 8; o < 64; o <<= 1)
@@ -414,34 +458,7 @@ __global__ __launch_bounds__(512) void gemm_pt_kernel(GemmArgs g, const bf16_t* 
     int m0, n0;
     tile_mn(ti, m0, n0);
     const int nw = n0 + wn_u * 64;
-    if (g.bias) {  // wave-uniform scalar loads (constant address space -> s_load) of the wave's 64 bias values
-      const int nb = __builtin_amdgcn_readfirstlane(nw);
-      typedef __attribute__((address_space(4))) const float cfloat;
-      cfloat* cbias = reinterpret_cast<cfloat*>(reinterpret_cast<uintptr_t>(g.bias));
-#pragma unroll
-      for (int ni = 0; ni < TN; ni++) {
-        float b4[4];
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-          // column nb + 16 ni + 4 q' + r for this lane's q' = fq: select among the 4 uniform quads
-          float v[4];
-#pragma unroll
-          for (int r = 0; r < 4; r++) {
-            const int col = nb + ni * 16 + q * 4 + r;
-            v[r] = col < g.N ? cbias[col] : 0.f;
-          }
-          if (q == 0) { b4[0] = v[0]; b4[1] = v[1]; b4[2] = v[2]; b4[3] = v[3]; }
-          else if (fq == q) { b4[0] = v[0]; b4[1] = v[1]; b4[2] = v[2]; b4[3] = v[3]; }
-        }
-#pragma unroll
-        for (int mi = 0; mi < TM; mi++) {
-          acc[ni][mi][0] += b4[0];
-          acc[ni][mi][1] += b4[1];
-          acc[ni][mi][2] += b4[2];
-          acc[ni][mi][3] += b4[3];
-        }
-      }
-    }
+    if (g.bias) add_bias_scalar<TM, TN>(g, acc, nw, fq);
     const int c = lane & 7;
     const int n = nw + c * 8;
     const bool nok = n < g.N;
@@ -626,6 +643,7 @@ __device__ __forceinline__ void pp_retire(int younger) {
   else pp_vmcnt<0>();
 }
 
+template <bool PROBE_NO_EPI = false, bool NTST = false>
 __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
   constexpr int TM = 8, TN = 4;
   __shared__ __attribute__((aligned(16))) char smem[2 * 4 * PP_PIECE];  // 128 KB
@@ -782,8 +800,10 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs g) {
   for (; u + 2 < nk; u++) ktile(u, std::true_type{});
   for (; u < nk; u++) ktile(u, std::false_type{});
   if (!wr) asm volatile("s_barrier" ::: "memory");  // both groups at the same barrier count: the ring is idle
-  tile_epilogue<TM, TN>(g, acc, smem + wave * (16 * TM) * (32 * TN), lane, m0 + wr * 128, n0 + wc * 64);
+  if (PROBE_NO_EPI && g.M >= 0) return;  // timing probe (tools/bench_gemm.py): main loop only
+  tile_epilogue<TM, TN, TM, NTST>(g, acc, smem + wave * (16 * TM) * (32 * TN), lane, m0 + wr * 128, n0 + wc * 64);
 }
+
 
 }  // namespace
 
@@ -846,7 +866,7 @@ static int gemm_part_rows(int M, int N, int bn, int persistent) {
   if (persistent == 1) return 0;
   if (persistent == 3) return 64;             // <128, 3, 8>: 4 x 2 waves of 64 x 64
   if (persistent == 4) return 128;            // <128, 3, 4>: 2 x 2 waves of 128 x 64
-  if (persistent == 5) return 128;            // ping-pong 256 x 256: 2 x 4 waves of 128 x 64
+  if (persistent == 5 || persistent == 6) return 128;  // ping-pong 256 x 256: 2 x 4 waves of 128 x 64
   return bn == 256 ? 128 : 64;                // <256>: 2 x 4 waves of 128 x 64; <128>: 4 x 2 of 64 x 64
 }
 
@@ -869,13 +889,13 @@ KFA_API int kfa_gemm_nt(const bf16_t* A, const bf16_t* B, bf16_t* C, const bf16_
   if (act < 0 || act > 3 || dact < 0 || dact > 3) return -1;
   if (persistent == 1 && K < 2 * GK) persistent = 0;
   // ping-pong kernel: K in whole 64-deep k-tiles, operand extents within 31-bit buffer offsets
-  if (persistent == 5 && (K % PP_BK || (long)M * lda * 2 >= (long)kOOB || (long)N * ldb * 2 >= (long)kOOB)) persistent = 4;  // same dbias partial rows (128)
+  if ((persistent == 5 || persistent == 6 || persistent == 7) && (K % PP_BK || (long)M * lda * 2 >= (long)kOOB || (long)N * ldb * 2 >= (long)kOOB)) persistent = 4;  // same dbias partial rows (128)
   const long cb = (long)M * ldc * 2;
   if (cb >= (long)kOOB) return -2;  // 32-bit buffer offsets in the epilogue
   const int prow = gemm_part_rows(M, N, bn, persistent);
   if (bn == 0) bn = kfa_gemm_pick_bn(M, N);
   if (persistent == 3 || persistent == 4) bn = 128;
-  if (persistent == 5) bn = 256;
+  if (persistent == 5 || persistent == 6 || persistent == 7) bn = 256;
   const long tiles = (long)((M + 255) / 256) * ((N + bn - 1) / bn);
   if (tiles >= (1L << 31)) return -2;
   if (!dbias || !prow) dpart = nullptr;
@@ -889,8 +909,12 @@ KFA_API int kfa_gemm_nt(const bf16_t* A, const bf16_t* B, bf16_t* C, const bf16_
       hipLaunchKernelGGL((gemm_pt_kernel<128>), dim3(grid), dim3(512), 0, st, g, gemm_zero_page());
     else
       return -1;
+  } else if (persistent == 7) {  // probe: ping-pong main loop without the epilogue (C untouched)
+    hipLaunchKernelGGL((gemm_pp_kernel<true, false>), dim3((unsigned)tiles), dim3(512), 0, st, g);
+  } else if (persistent == 6) {  // ping-pong with non-temporal C / Z stores
+    hipLaunchKernelGGL((gemm_pp_kernel<false, true>), dim3((unsigned)tiles), dim3(512), 0, st, g);
   } else if (persistent == 5) {
-    hipLaunchKernelGGL(gemm_pp_kernel, dim3((unsigned)tiles), dim3(512), 0, st, g);
+    hipLaunchKernelGGL((gemm_pp_kernel<false, false>), dim3((unsigned)tiles), dim3(512), 0, st, g);
   } else if (persistent == 4) {
     hipLaunchKernelGGL((gemm_nt_kernel<128, 3, 4>), dim3((unsigned)tiles), dim3(256), 0, st, g, gemm_zero_page());
   } else if (persistent == 3) {

@@ -70,9 +70,21 @@ def _check_vec(t, N, what):
 # Kernel variant: 0 = one 8-wave block per 256 x bn tile (128 KB ring: one block
 # per CU), 1 = persistent blocks carrying the LDS ring across tiles, 3 = 256 x 128
 # blocks on a 3-slot ring (72 KB: two blocks per CU, so one block's barriers and
-# epilogue run under the other's MFMAs — the fastest, default), 4 = as 3 with
+# epilogue run under the other's MFMAs — the pick for short k-loops), 4 = as 3 with
 # four 128 x 64 waves.  KFA_GEMM_VARIANT overrides; tools/bench_gemm.py compares.
-PERSISTENT = int(os.environ.get("KFA_GEMM_VARIANT", "3"))
+# 5 / 6 = 256 x 256 ping-pong (two wave groups one barrier apart; 6 with
+# non-temporal C stores), K % 64 == 0: the fastest main loop (1.1-1.4 PFLOP/s
+# without its epilogue), but its C write is not overlapped with MFMA work, so
+# it wins only where the k-loop is long or the output wide (K >= 2048 or
+# N >= 3072; tools/bench_gemm.py, docs/kernels.md).  None = pick per shape.
+_VAR_ENV = os.environ.get("KFA_GEMM_VARIANT")
+PERSISTENT = int(_VAR_ENV) if _VAR_ENV else None
+
+
+def pick_variant(M: int, N: int, K: int) -> int:
+    if K % 64 == 0 and (K >= 2048 or N >= 3072):
+        return 6
+    return 3
 
 
 def gemm_nt(a, b, *, bias=None, act=None, addend=None, want_z=False, zin=None, dact=None, dbias=None, out=None,
@@ -92,7 +104,8 @@ def gemm_nt(a, b, *, bias=None, act=None, addend=None, want_z=False, zin=None, d
     if (zin is None) != (dact in (None, "none")):
         raise ValueError("gemm_nt: zin and dact go together")
     z = torch.empty_like(c) if want_z else None
-    variant = int(PERSISTENT if persistent is None else persistent)
+    variant = persistent if persistent is not None else PERSISTENT
+    variant = pick_variant(M, N, K) if variant is None else int(variant)
     dpart = None
     if dbias is not None:  # partial column sums + one reduce (no per-column atomics)
         nf = _lib.lib().kfa_gemm_dpart_floats(M, N, int(bn), variant)

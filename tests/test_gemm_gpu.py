@@ -18,12 +18,13 @@ def _bf(*shape, s=1.0):
     return (torch.randn(*shape, device=D) * s).to(torch.bfloat16)
 
 
-@pytest.fixture(params=[1, 0, 2, 3, 5], ids=["persistent", "per_tile", "four_wave", "two_per_cu", "pingpong"], autouse=True)
+@pytest.fixture(params=[1, 0, 2, 3, 5, 6], ids=["persistent", "per_tile", "four_wave", "two_per_cu", "pingpong",
+                                          "pingpong_nt"], autouse=True)
 def _persistent(request, monkeypatch):
     """Every test runs on every GEMM kernel: the persistent tile-sweeping one,
     the one-8-wave-block-per-tile one, the 4-wave 128 x 128-wave-tile one, the
-    two-blocks-per-CU 256 x 128 one and the 256 x 256 ping-pong one (which
-    falls back to variant 4 when K % 64 != 0)."""
+    two-blocks-per-CU 256 x 128 one and the 256 x 256 ping-pong one, with plain
+    and non-temporal stores (both fall back to variant 4 when K % 64 != 0)."""
     from kubeflow_controller_amd.ops import gemm as G
     monkeypatch.setattr(G, "PERSISTENT", request.param)
     return request.param
@@ -120,7 +121,8 @@ def test_dense_layer_uses_fused_gemm_and_matches_reference(monkeypatch):
 
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (300, 520, 128), (4096, 4096, 3072), (33000, 776, 768),
                                    (777, 2304, 192), (32768, 3072, 768)])
-def test_gemm_pingpong_shapes(M, N, K):
+@pytest.mark.parametrize("variant", [5, 6])
+def test_gemm_pingpong_shapes(M, N, K, variant, _persistent):
     """Ping-pong kernel: one k-tile (prologue + tail only), M / N tails (rows
     past the operand read as zero by the buffer range check), deep K (many
     steady-state k-tiles), BERT shapes; bias + GELU + pre-activation epilogue."""
@@ -128,7 +130,37 @@ def test_gemm_pingpong_shapes(M, N, K):
     torch.manual_seed(7)
     a, b = _bf(M, K), _bf(N, K, s=0.05)
     bias = torch.randn(N, device=D)
-    c, z = G.gemm_nt(a, b, bias=bias, act="gelu", want_z=True, persistent=5)
+    if _persistent != 0:
+        pytest.skip("shape sweep runs once (explicit variant)")
+    c, z = G.gemm_nt(a, b, bias=bias, act="gelu", want_z=True, persistent=variant)
     zr = a.float() @ b.float().t() + bias
     _close(z, zr, 1e-2, f"Z {M}x{N}x{K}")
     _close(c, torch.nn.functional.gelu(zr), 1e-2, f"C {M}x{N}x{K}")
+
+
+@pytest.mark.parametrize("route", [False, True])
+def test_linear_module_runs_hip_dense_and_matches_fp32(route, monkeypatch, _persistent):
+    """ops.linear.Linear (ResNet FC, MNIST hidden layer) on bf16 CUDA input goes
+    through DenseFn: own GEMM + fused bias epilogue (route) or library GEMM +
+    the fused bias pass; dW by wgrad_kernel, db by column sums — vs fp32."""
+    if _persistent != 0:
+        pytest.skip("runs once")
+    from kubeflow_controller_amd.ops import gemm as G
+    from kubeflow_controller_amd.ops.linear import Linear
+    monkeypatch.setattr(G, "ROUTE_LAYERS", route)
+    torch.manual_seed(11)
+    lin = Linear(2048, 1000).to(D)
+    x = _bf(256, 2048).requires_grad_()
+    y = lin(x)
+    assert y.dtype == torch.bfloat16 and y.shape == (256, 1000)
+    dy = torch.randn(256, 1000, device=D)
+    y.backward(dy.to(torch.bfloat16))
+    xr = x.detach().float().requires_grad_()
+    wr = lin.weight.detach().to(torch.bfloat16).float().requires_grad_()
+    br = lin.bias.detach().float().requires_grad_()
+    yr = torch.nn.functional.linear(xr, wr, br)
+    yr.backward(dy)
+    _close(y, yr, 2e-2, "y")
+    _close(x.grad, xr.grad, 3e-2, "dx")
+    _close(lin.weight.grad, wr.grad, 3e-2, "dw")
+    _close(lin.bias.grad, br.grad, 3e-2, "db")

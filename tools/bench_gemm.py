@@ -51,6 +51,9 @@ def dense():
         t_2cu = timeit(lambda: G.gemm_nt(x, w, persistent=3))
         t_2cu4 = timeit(lambda: G.gemm_nt(x, w, persistent=4))
         t_pp = timeit(lambda: G.gemm_nt(x, w, persistent=5))
+        t_ppp = timeit(lambda: G.gemm_nt(x, w, persistent=6))
+        t_noepi = timeit(lambda: G.gemm_nt(x, w, persistent=7))
+        t_pppe = timeit(lambda: G.gemm_nt(x, w, bias=b, act="gelu", want_z=True, persistent=6))
         t_ep = timeit(lambda: G.gemm_nt(x, w, bias=b, act="gelu", want_z=True))
         gw = torch.zeros(N, K, device=d, dtype=torch.bfloat16)
         t_wm = timeit(lambda: gw.addmm_(dy.t(), x))
@@ -58,7 +61,7 @@ def dense():
         tf = lambda t: fl / t / 1e9  # noqa: E731
         print(f"{M:6d} {N:5d} {K:5d} | {t_mm:7.3f} {tf(t_mm):5.0f} | {t_128:7.3f} {tf(t_128):5.0f} | "
               f"{t_256:7.3f} {tf(t_256):5.0f} | {t_ep:7.3f} | {t_wm:7.3f} {tf(t_wm):5.0f} | {t_wk:7.3f} {tf(t_wk):5.0f}"
-              f" | persistent: g128 {tf(t_128o):5.0f} g256 {tf(t_256o):5.0f} | 2/CU g128 {tf(t_2cu):5.0f} 4w {tf(t_2cu4):5.0f} | pingpong {tf(t_pp):5.0f} TF/s",
+              f" | persistent: g128 {tf(t_128o):5.0f} g256 {tf(t_256o):5.0f} | 2/CU g128 {tf(t_2cu):5.0f} 4w {tf(t_2cu4):5.0f} | pingpong {tf(t_pp):5.0f} nt-stores {tf(t_ppp):5.0f} (+bias/gelu/z {t_pppe:.3f} ms) | pp main loop only {tf(t_noepi):5.0f} TF/s",
               flush=True)
 
 
