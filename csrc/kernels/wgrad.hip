@@ -96,8 +96,16 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_kernel(const bf16_t* __
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM;
   const int ntn = (g.N + BN - 1) / BN;
-  const int m0 = (blockIdx.x / ntn) * BM, n0 = (blockIdx.x % ntn) * BN;
-  const int split = blockIdx.y;
+  // XCD-aware order (T1, bijective remap): the hardware deals block ids round-
+  // robin over the 8 XCDs; renumber so the blocks an XCD runs together are the
+  // weight tiles of ONE pixel split — they re-read the same dY rows and
+  // overlapping X windows (one per tap), which then hit that XCD's L2 instead
+  // of HBM (a 3x3 layer's 5-9 tiles otherwise read each split from HBM 5-9x).
+  const int nwg = gridDim.x * gridDim.y, bid = blockIdx.x + blockIdx.y * gridDim.x;
+  const int q8 = nwg >> 3, r8 = nwg & 7, x8 = bid & 7;
+  const int ord = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + (bid >> 3);
+  const int tile = ord % gridDim.x, split = ord / gridDim.x;
+  const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
   const int kb = split * g.kchunk;
   const int ke = min(g.K, kb + g.kchunk);
   if (kb >= ke) return;
