@@ -206,11 +206,16 @@ __device__ __forceinline__ unsigned pos_bits(const uint4 v) {
   return m;
 }
 
-template <bool RELU, bool RES, bool MB>
+// RAFF: the residual is itself a BatchNorm's RAW input r, normalised here with
+// that BN's [scale | shift] (rss, 2C floats): z = x*sc + sh + (r*rsc + rsh) —
+// a ResNet downsample block's two BNs in one pass (the downsample BN's output
+// is never written or re-read).
+template <bool RELU, bool RES, bool MB, bool RAFF = false>
 __global__ __launch_bounds__(NT) void bn_apply(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
                                                bf16_t* __restrict__ y, uint8_t* __restrict__ mb,
                                                const float* __restrict__ scale, const float* __restrict__ shift,
-                                               long M, int C, long chunk, int tpr, int rpi) {
+                                               long M, int C, long chunk, int tpr, int rpi,
+                                               const float* __restrict__ rss = nullptr) {
   const int t = threadIdx.x;
   const int cg = t % tpr, r0 = t / tpr;
   if (r0 >= rpi) return;
@@ -219,9 +224,14 @@ __global__ __launch_bounds__(NT) void bn_apply(const bf16_t* __restrict__ x, con
   const long re = rb + chunk < M ? rb + chunk : M;
   for (int g = cg; g < cv; g += tpr) {
     const int c0 = g * 8;
-    float sc[8], sf[8];
+    float sc[8], sf[8], rsc[8], rsf[8];
 #pragma unroll
-    for (int j = 0; j < 8; j++) { sc[j] = scale[c0 + j]; sf[j] = shift[c0 + j]; }
+    for (int j = 0; j < 8; j++) {
+      sc[j] = scale[c0 + j];
+      sf[j] = shift[c0 + j];
+      rsc[j] = RAFF ? rss[c0 + j] : 1.f;
+      rsf[j] = RAFF ? rss[C + c0 + j] : 0.f;
+    }
     auto one = [&](const uint4 v, const uint4 q4, long o) {
       float f[8], q[8];
       unpack8(v, f);
@@ -229,7 +239,7 @@ __global__ __launch_bounds__(NT) void bn_apply(const bf16_t* __restrict__ x, con
 #pragma unroll
       for (int j = 0; j < 8; j++) {
         float z = fmaf(f[j], sc[j], sf[j]);
-        if (RES) z += q[j];
+        if (RES) z += RAFF ? fmaf(q[j], rsc[j], rsf[j]) : q[j];
         f[j] = RELU ? fmaxf(z, 0.f) : z;
       }
       const uint4 out = pack8(f);
@@ -254,8 +264,17 @@ __global__ __launch_bounds__(NT) void bn_apply(const bf16_t* __restrict__ x, con
 
 static void launch_apply(int relu, const bf16_t* res, uint8_t* mb, dim3 grid, hipStream_t s, const bf16_t* x,
                          bf16_t* y, const float* scale, const float* shift, long M, int C, long chunk, int tpr,
-                         int rpi) {
-  if (relu && res && mb)
+                         int rpi, const float* rss = nullptr) {
+  if (rss && relu && res && mb)
+    hipLaunchKernelGGL((bn_apply<true, true, true, true>), grid, dim3(NT), 0, s, x, res, y, mb, scale, shift, M, C,
+                       chunk, tpr, rpi, rss);
+  else if (rss && relu && res)
+    hipLaunchKernelGGL((bn_apply<true, true, false, true>), grid, dim3(NT), 0, s, x, res, y, mb, scale, shift, M, C,
+                       chunk, tpr, rpi, rss);
+  else if (rss && res)
+    hipLaunchKernelGGL((bn_apply<false, true, false, true>), grid, dim3(NT), 0, s, x, res, y, mb, scale, shift, M, C,
+                       chunk, tpr, rpi, rss);
+  else if (relu && res && mb)
     hipLaunchKernelGGL((bn_apply<true, true, true>), grid, dim3(NT), 0, s, x, res, y, mb, scale, shift, M, C, chunk,
                        tpr, rpi);
   else if (relu && res)
@@ -437,6 +456,77 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply(const bf16_t* __restrict__ dy
   }
 }
 
+// bn_bwd_apply for a BN whose residual input r is another BatchNorm's RAW input
+// (the bn_apply RAFF forward): instead of writing the residual-branch gradient
+// dres = dz, accumulate THAT BN's backward statistics sum(dz), sum(dz*(r - rmean))
+// into its slot workspace (rslots); its own backward then re-derives dz from dy
+// and the ReLU mask (kfa_bn_bwd_prestats, mask mode 3).  Same channel-group
+// loop and LDS block reduction as bn_bwd_partial.
+template <int MASK>
+__global__ __launch_bounds__(NT) void bn_bwd_apply_rstats(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                                                          const bf16_t* __restrict__ y, const uint8_t* __restrict__ mb,
+                                                          const float* __restrict__ ss, const float* __restrict__ coef,
+                                                          bf16_t* __restrict__ dx, const bf16_t* __restrict__ r,
+                                                          const float* __restrict__ rmean, float* __restrict__ rslots,
+                                                          long M, int C, long chunk, int tpr, int rpi) {
+  __shared__ float sh[2][NT * 8];
+  const int t = threadIdx.x;
+  const int cg = t % tpr, r0 = t / tpr;
+  const bool active = r0 < rpi;
+  const int cv = C / 8;
+  const long rb = (long)blockIdx.x * chunk;
+  const long re = rb + chunk < M ? rb + chunk : M;
+  for (int g0 = 0; g0 < cv; g0 += tpr) {
+    const int c0 = (g0 + cg) * 8;
+    float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (active && g0 + cg < cv) {
+      float ca[8], cb[8], ck[8], sc[8], sf[8], mu[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        ca[j] = coef[c0 + j];
+        cb[j] = coef[C + c0 + j];
+        ck[j] = coef[2 * C + c0 + j];
+        mu[j] = rmean[c0 + j];
+      }
+      load_ss<MASK>(ss, C, c0, sc, sf);
+      for (long row = rb + r0; row < re; row += rpi) {
+        const long o = row * C + c0;
+        uint4 yv = make_uint4(0, 0, 0, 0);
+        if (MASK == 1) yv = ld16(y + o);
+        const unsigned bits = MASK == 3 ? (unsigned)mb[o >> 3] : 0u;
+        const uint4 dv = ld16(dy + o), xv = ld16(x + o), rv = ld16(r + o);
+        float dz[8], xf[8], rf[8], out[8];
+        unpack8(xv, xf);
+        unpack8(rv, rf);
+        masked_dy<MASK>(dv, yv, xf, sc, sf, bits, dz);
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+          out[j] = fmaf(ca[j], dz[j], fmaf(cb[j], xf[j], ck[j]));
+          s1[j] += dz[j];
+          s2[j] += dz[j] * (rf[j] - mu[j]);
+        }
+        *reinterpret_cast<uint4*>(dx + o) = pack8(out);
+      }
+    }
+    if (active) {
+#pragma unroll
+      for (int j = 0; j < 8; j++) { sh[0][r0 * tpr * 8 + cg * 8 + j] = s1[j]; sh[1][r0 * tpr * 8 + cg * 8 + j] = s2[j]; }
+    }
+    __syncthreads();
+    const int width = tpr * 8;
+    for (int idx = t; idx < 2 * width; idx += NT) {
+      const int a = idx / width, c = idx % width;
+      if (g0 * 8 + c < C) {
+        float acc = 0.f;
+        for (int rr = 0; rr < rpi; rr++) acc += sh[a][rr * width + c];
+        __hip_atomic_fetch_add(&rslots[((long)(blockIdx.x % kSlots) * 2 + a) * C + g0 * 8 + c], acc,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace
 
 // ====================================================================== C ABI
@@ -585,5 +675,80 @@ KFA_API int kfa_bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const
   hipLaunchKernelGGL(bn_bwd_finalize, dim3(kfa_ceil_div(C, 64)), dim3(64, kGroups), 0, s, part, g.gx, M, C, gamma,
                      save_mean, save_invstd, dgamma, dbeta, coef, accumulate);
   launch_bwd_apply_any(mm, g, dy, x, y, mb, ss, coef, dx, dres, M, C, s);
+  return kfa_status();
+}
+
+// ---------------------------------------------------------------- downsample-block pair
+// A ResNet downsample block ends in relu(bn3(x) + bn_ds(r)): r (the downsample
+// conv's output) is normalised inside bn3's apply pass (bn_apply RAFF) instead
+// of by a pass of its own, and bn_ds's backward statistics are gathered by
+// bn3's backward apply pass instead of a partial pass over a written dres.
+
+// Forward finalize alone (bn_ds): scale / shift into ss = [scale | shift] (2C),
+// batch mean / invstd, running statistics.  prestats = 0: the statistics pass
+// over x runs first (else the producing conv's epilogue accumulated them).
+KFA_API int kfa_bn_finalize(const bf16_t* x, float* slots, long M, int C, const float* gamma, const float* beta,
+                            float* rmean, float* rvar, float* save_mean, float* save_invstd, float* ss, float eps,
+                            float momentum, int prestats, hipStream_t s) {
+  if (!bn_shape_ok(M, C)) return -1;
+  Geom g = geom(M, C, max_row_blocks(C));
+  if (!prestats)
+    hipLaunchKernelGGL(bn_stats_partial, dim3(g.gx), dim3(NT), 0, s, x, slots, M, C, g.chunk, g.tpr, g.rpi);
+  hipLaunchKernelGGL(bn_finalize, dim3(kfa_ceil_div(C, 64)), dim3(64, kGroups), 0, s, prestats ? nullptr : x, slots,
+                     g.gx, M, C, gamma, beta, rmean, rvar, save_mean, save_invstd, ss, ss + C, eps, momentum);
+  return kfa_status();
+}
+
+// bn3 forward with the residual r normalised by rss (bn_ds's [scale | shift]).
+KFA_API int kfa_bn_fwd_train_dual(const bf16_t* x, const bf16_t* r, bf16_t* y, const float* gamma, const float* beta,
+                                  float* rmean, float* rvar, float* save_mean, float* save_invstd, float* slots,
+                                  float* ss, long M, int C, float eps, float momentum, int relu, uint8_t* mb,
+                                  const float* rss, int prestats, hipStream_t s) {
+  if (!bn_shape_ok(M, C) || !r || !rss) return -1;
+  if (kfa_bn_finalize(x, slots, M, C, gamma, beta, rmean, rvar, save_mean, save_invstd, ss, eps, momentum, prestats,
+                      s))
+    return -1;
+  Geom g = geom(M, C, max_row_blocks(C));
+  launch_apply(relu, r, mb, dim3(g.gx), s, x, y, ss, ss + C, M, C, g.chunk, g.tpr, g.rpi, rss);
+  return kfa_status();
+}
+
+// bn3 backward (statistics from `slots`, accumulated by the consuming dgrad
+// epilogue when prestats, else by its own partial pass) whose apply pass also
+// accumulates bn_ds's backward statistics into rslots (see bn_bwd_apply_rstats);
+// no residual gradient is written.
+KFA_API int kfa_bn_bwd_rstats(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const float* gamma,
+                              const float* save_mean, const float* save_invstd, bf16_t* dx, float* dgamma,
+                              float* dbeta, float* slots, float* coefws, long M, int C, int relu, int accumulate,
+                              const float* ss, const uint8_t* mb, const bf16_t* r, const float* rmean, float* rslots,
+                              int prestats, hipStream_t s) {
+  if (!bn_shape_ok(M, C) || !r || !rmean || !rslots) return -1;
+  const int mm = mask_mode(relu, y, mb, ss);
+  if (mm < 0 || mm == 2) return -2;  // a mask recomputed from x alone is wrong with a residual
+  Geom g = geom(M, C, max_row_blocks(C));
+  if (!prestats) {
+    if (mm == 3)
+      hipLaunchKernelGGL(bn_bwd_partial<3>, dim3(g.gx), dim3(NT), 0, s, dy, x, y, mb, ss, save_mean, slots, M, C,
+                         g.chunk, g.tpr, g.rpi);
+    else if (mm == 1)
+      hipLaunchKernelGGL(bn_bwd_partial<1>, dim3(g.gx), dim3(NT), 0, s, dy, x, y, mb, ss, save_mean, slots, M, C,
+                         g.chunk, g.tpr, g.rpi);
+    else if (mm == 0)
+      hipLaunchKernelGGL(bn_bwd_partial<0>, dim3(g.gx), dim3(NT), 0, s, dy, x, y, mb, ss, save_mean, slots, M, C,
+                         g.chunk, g.tpr, g.rpi);
+    else
+      return -2;  // mask from x is invalid with a residual
+  }
+  hipLaunchKernelGGL(bn_bwd_finalize, dim3(kfa_ceil_div(C, 64)), dim3(64, kGroups), 0, s, slots, g.gx, M, C, gamma,
+                     save_mean, save_invstd, dgamma, dbeta, coefws, accumulate);
+  if (mm == 3)
+    hipLaunchKernelGGL(bn_bwd_apply_rstats<3>, dim3(g.gx), dim3(NT), 0, s, dy, x, y, mb, ss, coefws, dx, r, rmean,
+                       rslots, M, C, g.chunk, g.tpr, g.rpi);
+  else if (mm == 1)
+    hipLaunchKernelGGL(bn_bwd_apply_rstats<1>, dim3(g.gx), dim3(NT), 0, s, dy, x, y, mb, ss, coefws, dx, r, rmean,
+                       rslots, M, C, g.chunk, g.tpr, g.rpi);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply_rstats<0>, dim3(g.gx), dim3(NT), 0, s, dy, x, y, mb, ss, coefws, dx, r, rmean,
+                       rslots, M, C, g.chunk, g.tpr, g.rpi);
   return kfa_status();
 }

@@ -9,14 +9,18 @@ The last BN of each block is zero-initialised (standard large-batch recipe).
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn as nn
 
-from ..ops.batchnorm import BatchNorm2dAct
+from ..ops.batchnorm import DS_SLOTS, BatchNorm2dAct, bn_act_dual
 from ..ops.conv import Conv2d, GradJoin
 from ..ops.linear import Linear
 from ..ops.pool import MaxPool2d, global_avg_pool
+
+
+DUAL_BN = os.environ.get("KFA_BN_DUAL", "1") != "0"
 
 
 class Bottleneck(nn.Module):
@@ -56,9 +60,16 @@ class Bottleneck(nn.Module):
             y = self.bn1(self.conv1(x, join=join, bn_stats=st), bwd_link=st)
             y = self.bn2(self.conv2(y, bn_stats=st), bwd_link=st)
             return self.bn3(self.conv3(y, bn_stats=st), residual=join.branch(x), bwd_link=st, res_join=join)
-        idn = self.downsample["bn"](self.downsample["conv"](x, join=join, bn_stats=st))
+        # downsample block: relu(bn3(.) + bn_ds(.)) in ONE apply pass each way
+        # (ops.batchnorm.bn_act_dual): the downsample conv's statistics wait in
+        # their own slot workspace while conv1..conv3 fill the shared one.
+        dual = DUAL_BN and st and x.is_cuda
+        r = self.downsample["conv"](x, join=join, bn_stats=(DS_SLOTS if dual else st))
+        idn = None if dual else self.downsample["bn"](r)
         y = self.bn1(self.conv1(join.branch(x), bn_stats=st), bwd_link=st)
         y = self.bn2(self.conv2(y, bn_stats=st), bwd_link=st)
+        if dual:
+            return bn_act_dual(self.bn3, self.conv3(y, bn_stats=st), self.downsample["bn"], r, bwd_link=st)
         return self.bn3(self.conv3(y, bn_stats=st), residual=idn, bwd_link=st)
 
 

@@ -42,7 +42,11 @@ def _mc(t: torch.Tensor):
 
 
 _lib.register("kfa_bn_fwd_train_prestats", [_lib.P] * 11 + [_lib.L, _lib.I, _lib.F, _lib.F, _lib.I, _lib.P, _lib.P])
-_lib.register("kfa_bn_bwd_prestats", [_lib.P] * 12 + [_lib.L, _lib.I, _lib.I, _lib.I, _lib.P, _lib.P])
+_lib.register("kfa_bn_bwd_prestats", [_lib.P] * 12 + [_lib.L, _lib.I, _lib.I, _lib.I, _lib.P, _lib.P, _lib.P])
+_lib.register("kfa_bn_finalize", [_lib.P, _lib.P, _lib.L, _lib.I] + [_lib.P] * 7 + [_lib.F, _lib.F, _lib.I, _lib.P])
+_lib.register("kfa_bn_fwd_train_dual", [_lib.P] * 11 + [_lib.L, _lib.I, _lib.F, _lib.F, _lib.I, _lib.P, _lib.P,
+                                                        _lib.I, _lib.P])
+_lib.register("kfa_bn_bwd_rstats", [_lib.P] * 11 + [_lib.L, _lib.I, _lib.I, _lib.I] + [_lib.P] * 5 + [_lib.I, _lib.P])
 
 
 class BnBwdLink:
@@ -64,10 +68,15 @@ class BnBwdLink:
         self.convs = 0
 
 
-def bn_slot_workspace(C: int, device) -> torch.Tensor:
+def bn_slot_workspace(C: int, device, tag: str = "bn_slots") -> torch.Tensor:
     """The zero-initialised, self-cleaning statistics slots shared by every BN
-    (and by convolutions that accumulate a BN's statistics in their epilogue)."""
-    return _lib.workspace(_lib.lib().kfa_bn_slot_floats(C) * 4, device, "bn_slots")
+    (and by convolutions that accumulate a BN's statistics in their epilogue).
+    ``DS_SLOTS``: a second set for the downsample BN of :func:`bn_act_dual`,
+    whose statistics wait there while the block's other BNs use the first."""
+    return _lib.workspace(_lib.lib().kfa_bn_slot_floats(C) * 4, device, tag)
+
+
+DS_SLOTS = "bn_slots_ds"
 
 
 def _workspaces(C: int, device):
@@ -184,6 +193,120 @@ def bn_act(x, weight, bias, running_mean, running_var, residual=None, training=T
     return y
 
 
+def _param_grads(weight, bias, C, device):
+    """(dgamma, dbeta, direct): views into the flat fp32 gradient bucket when the
+    params live there (the kernel then accumulates), else fresh fp32 vectors."""
+    wv, bv = direct_grad_view(weight), direct_grad_view(bias)
+    if wv is not None and bv is not None and wv.dtype == torch.float32 and bv.dtype == torch.float32:
+        return wv, bv, True
+    return (torch.empty(C, dtype=torch.float32, device=device), torch.empty(C, dtype=torch.float32, device=device),
+            False)
+
+
+class _BNDualFn(torch.autograd.Function):
+    """``relu(bn(x) + bn_r(r))`` in training — a ResNet downsample block's tail
+    (bn3 of the main branch plus the downsample BN of the shortcut).
+
+    Forward: bn_r's statistics (accumulated by the downsample conv's epilogue
+    into the ``DS_SLOTS`` workspace) are finalized into its [scale | shift];
+    bn's apply pass normalises r itself (``bn_apply`` RAFF), so bn_r's output is
+    never written or re-read.  Backward: bn's apply pass accumulates bn_r's
+    statistics (``bn_bwd_apply_rstats``) instead of writing the shortcut
+    gradient; bn_r's backward then re-derives that gradient from dy and the
+    block output's ReLU bits.  Saves, per block, bn_r's forward apply pass and
+    its backward statistics pass over a written residual gradient."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, r, rweight, rbias, rrunning_mean, rrunning_var,
+                momentum, eps, relu, prestats, rprestats, link):
+        x, r = _as_rows(x), _as_rows(r)
+        M, C = _mc(x)
+        if x.dtype != torch.bfloat16 or r.dtype != torch.bfloat16 or r.shape != x.shape:
+            raise ValueError(f"bn_act_dual: bf16 x {tuple(x.shape)} and r {tuple(r.shape)} of one shape required")
+        dev = x.device
+        s = _lib.stream()
+        slots, coef = _workspaces(C, dev)
+        rslots = bn_slot_workspace(C, dev, DS_SLOTS)
+        f32 = dict(dtype=torch.float32, device=dev)
+        rmean, rinv, rss = torch.empty(C, **f32), torch.empty(C, **f32), torch.empty(2 * C, **f32)
+        _lib.call("kfa_bn_finalize", _lib.ptr(r), _lib.ptr(rslots), M, C, _lib.ptr(rweight), _lib.ptr(rbias),
+                  _lib.ptr(rrunning_mean), _lib.ptr(rrunning_var), _lib.ptr(rmean), _lib.ptr(rinv), _lib.ptr(rss),
+                  eps, momentum, int(rprestats), s)
+        y = torch.empty_like(x)
+        mean, invstd = torch.empty(C, **f32), torch.empty(C, **f32)
+        mb = torch.empty(M * C // 8, dtype=torch.uint8, device=dev) if relu else None
+        _lib.call("kfa_bn_fwd_train_dual", _lib.ptr(x), _lib.ptr(r), _lib.ptr(y), _lib.ptr(weight), _lib.ptr(bias),
+                  _lib.ptr(running_mean), _lib.ptr(running_var), _lib.ptr(mean), _lib.ptr(invstd), _lib.ptr(slots),
+                  _lib.ptr(coef), M, C, eps, momentum, int(relu), _lib.ptr(mb), _lib.ptr(rss), int(prestats), s)
+        ctx.save_for_backward(x, r, mb, weight, rweight, mean, invstd, rmean, rinv)
+        ctx.link = link
+        if link is not None:
+            link.x, link.y, link.ss, link.mb, link.mean = x, None, None, mb, mean
+            link.relu, link.prestats = bool(relu), False
+        ctx.relu = relu
+        ctx.params = (weight, bias, rweight, rbias)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, r, mb, weight, rweight, mean, invstd, rmean, rinv = ctx.saved_tensors
+        dy = _as_rows(dy)
+        M, C = _mc(x)
+        dev = x.device
+        s = _lib.stream()
+        w, b, rw, rb = ctx.params
+        dg, db, direct = _param_grads(w, b, C, dev)
+        rdg, rdb, rdirect = _param_grads(rw, rb, C, dev)
+        slots, coef = _workspaces(C, dev)
+        rslots = bn_slot_workspace(C, dev, DS_SLOTS)
+        lk = ctx.link
+        pre = lk is not None and lk.prestats
+        if lk is not None:
+            lk.prestats = False
+            lk.x = lk.y = lk.ss = lk.mb = lk.mean = None
+        dx, dr = torch.empty_like(x), torch.empty_like(r)
+        _lib.call("kfa_bn_bwd_rstats", _lib.ptr(dy), _lib.ptr(x), None, _lib.ptr(weight), _lib.ptr(mean),
+                  _lib.ptr(invstd), _lib.ptr(dx), _lib.ptr(dg), _lib.ptr(db), _lib.ptr(slots), _lib.ptr(coef), M, C,
+                  int(ctx.relu), int(direct), None, _lib.ptr(mb), _lib.ptr(r), _lib.ptr(rmean), _lib.ptr(rslots),
+                  int(pre), s)
+        # bn_r: statistics now in rslots; dz = dy * (block output > 0) from the bits
+        _lib.call("kfa_bn_bwd_prestats", _lib.ptr(dy), _lib.ptr(r), None, _lib.ptr(rweight), _lib.ptr(rmean),
+                  _lib.ptr(rinv), _lib.ptr(dr), None, _lib.ptr(rdg), _lib.ptr(rdb), _lib.ptr(rslots), _lib.ptr(coef),
+                  M, C, int(ctx.relu), int(rdirect), None, _lib.ptr(mb), s)
+        out = []
+        for p, g, d in ((w, dg, direct), (b, db, direct), (rw, rdg, rdirect), (rb, rdb, rdirect)):
+            if d:
+                notify_grad_ready(p)
+                out.append(None)
+            else:
+                out.append(g if p.dtype == torch.float32 else g.to(p.dtype))
+        return (dx, out[0], out[1], None, None, dr, out[2], out[3], None, None, None, None, None, None, None, None)
+
+
+def bn_act_dual(bn: "BatchNorm2dAct", x: torch.Tensor, bn_r: "BatchNorm2dAct", r: torch.Tensor,
+                bwd_link: bool = False) -> torch.Tensor:
+    """``act(bn(x) + bn_r(r))`` with one apply pass each way (training, CUDA);
+    ``bn_r`` must not have a ReLU of its own.  ``r``'s statistics may sit in the
+    ``DS_SLOTS`` workspace (its conv ran with ``bn_stats=DS_SLOTS``).  Other
+    cases run the two BNs separately."""
+    if not (x.is_cuda and bn.training and bn_r.training and not bn_r.relu and bn.eps == bn_r.eps
+            and bn.momentum == bn_r.momentum):
+        if getattr(r, "_kfa_prestats_tag", None) == DS_SLOTS:  # never leave the slots dirty
+            bn_slot_workspace(r.shape[1], r.device, DS_SLOTS).zero_()
+            r._kfa_prestats = False  # bn_r runs its own statistics pass
+        return bn(x, residual=bn_r(r), bwd_link=bwd_link)
+    link = BnBwdLink() if bwd_link else None
+    rpre = getattr(r, "_kfa_prestats", False) and getattr(r, "_kfa_prestats_tag", None) == DS_SLOTS
+    if getattr(r, "_kfa_prestats", False) and not rpre:
+        raise ValueError("bn_act_dual: r's statistics must be accumulated into the DS_SLOTS workspace")
+    y = _BNDualFn.apply(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, r, bn_r.weight, bn_r.bias,
+                        bn_r.running_mean, bn_r.running_var, bn.momentum, bn.eps, bn.relu,
+                        getattr(x, "_kfa_prestats", False), rpre, link)
+    if link is not None:
+        y._kfa_bn_link = link
+    return y
+
+
 def bn_act_reference(x, weight, bias, running_mean, running_var, residual=None, training=True, momentum=0.1,
                      eps=1e-5, relu=True):
     """Plain PyTorch fp32 reference of the same op (used by the numerics tests)."""
@@ -213,9 +336,9 @@ class BatchNorm2dAct(nn.Module):
 
     def forward(self, x, residual=None, bwd_link: bool = False, res_join=None):
         if x.is_cuda:
+            pre = getattr(x, "_kfa_prestats", False) and getattr(x, "_kfa_prestats_tag", "bn_slots") == "bn_slots"
             return bn_act(x, self.weight, self.bias, self.running_mean, self.running_var, residual,
-                          self.training, self.momentum, self.eps, self.relu, getattr(x, "_kfa_prestats", False),
-                          bwd_link, res_join)
+                          self.training, self.momentum, self.eps, self.relu, pre, bwd_link, res_join)
         # CPU path (plumbing tests / CPU-only MNIST-style jobs): plain PyTorch.
         y = torch.nn.functional.batch_norm(x, self.running_mean, self.running_var, self.weight.to(x.dtype),
                                            self.bias.to(x.dtype), self.training, self.momentum, self.eps)

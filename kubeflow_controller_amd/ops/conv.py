@@ -541,18 +541,23 @@ class _StemConvFn(torch.autograd.Function):
         return dx, dw, None, None, None
 
 
-def conv2d(x, w, stride: int = 1, pad: int = 0, join: "GradJoin | None" = None, bn_stats: bool = False):
+def conv2d(x, w, stride: int = 1, pad: int = 0, join: "GradJoin | None" = None, bn_stats=False):
     """``bn_stats``: the caller guarantees a training-mode ``BatchNorm2dAct``
     consumes the output next; the epilogue then accumulates its statistics and
-    the output is tagged ``_kfa_prestats`` (the BN skips its stats pass)."""
+    the output is tagged ``_kfa_prestats`` (the BN skips its stats pass).  A
+    string names the slot workspace (``ops.batchnorm.bn_slot_workspace`` tag)
+    for a BN whose finalize runs later than the next BN's (the downsample BN of
+    ``bn_act_dual``); True = the shared one."""
+    tag = bn_stats if isinstance(bn_stats, str) else "bn_slots"
     if stem_ok(x, w, stride, pad) and join is None:
         stats = None
         if bn_stats:
             from .batchnorm import bn_slot_workspace
-            stats = bn_slot_workspace(w.shape[0], x.device)
+            stats = bn_slot_workspace(w.shape[0], x.device, tag)
         y = _StemConvFn.apply(x, w, stride, pad, stats)
         if stats is not None:
             y._kfa_prestats = True
+            y._kfa_prestats_tag = tag
         return y
     if igemm_ok(x, w):
         if join is not None:
@@ -560,13 +565,14 @@ def conv2d(x, w, stride: int = 1, pad: int = 0, join: "GradJoin | None" = None, 
         stats = None
         if bn_stats:
             from .batchnorm import bn_slot_workspace
-            stats = bn_slot_workspace(w.shape[0], x.device)
+            stats = bn_slot_workspace(w.shape[0], x.device, tag)
         vendor = _use_vendor_fwd(x, w, stride, pad, stats)
         if vendor:
             stats = None  # the BN runs its own statistics pass
         y = _ConvFn.apply(x, w, stride, pad, join, stats, vendor)
         if stats is not None:
             y._kfa_prestats = True
+            y._kfa_prestats_tag = tag
         return y
     return F.conv2d(x, w, None, stride, pad)  # unfused: join.branch() is a no-op alias
 
@@ -585,9 +591,9 @@ class Conv2d(nn.Module):
         self.weight = nn.Parameter(w.contiguous(memory_format=torch.channels_last))
         self.bias = nn.Parameter(torch.zeros(out_channels)) if bias else None
 
-    def forward(self, x, join: "GradJoin | None" = None, bn_stats: bool = False):
+    def forward(self, x, join: "GradJoin | None" = None, bn_stats=False):
         w = self.weight if self.weight.dtype == x.dtype else self.weight.to(x.dtype)
-        y = conv2d(x, w, self.stride, self.padding, join, bn_stats and self.bias is None)
+        y = conv2d(x, w, self.stride, self.padding, join, bn_stats if self.bias is None else False)
         if self.bias is not None:
             y = y + self.bias.to(y.dtype).view(1, -1, 1, 1)
         return y

@@ -195,3 +195,64 @@ def test_maxpool_fwd_bwd(N, C, H, W, k, s, p):
     y.backward(dy)
     yf.backward(dy.float())
     torch.testing.assert_close(xr.grad.float(), xf.grad, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("N,C,H,W", [(4, 256, 14, 14), (2, 2048, 7, 7), (8, 24, 5, 5)])
+@pytest.mark.parametrize("conv_stats", [False, True])
+def test_bn_act_dual_downsample_pair_matches_fp32(N, C, H, W, conv_stats):
+    """relu(bn(x) + bn_r(r)) in one apply pass each way (ops.batchnorm.bn_act_dual)
+    vs two fp32 batch_norms: output, running stats, dx, dr, both BNs' dgamma /
+    dbeta.  conv_stats: x / r come from convs whose epilogues accumulated the
+    statistics (x into the shared slots, r into DS_SLOTS).  Both slot
+    workspaces must be clean (all zero) afterwards."""
+    _native_loaded()
+    from kubeflow_controller_amd.ops import conv as CV
+    from kubeflow_controller_amd.ops.batchnorm import DS_SLOTS, BatchNorm2dAct, bn_act_dual, bn_slot_workspace
+    torch.manual_seed(3)
+    d = _dev()
+    cl = torch.channels_last
+    bn, bnr = BatchNorm2dAct(C, relu=True).to(d), BatchNorm2dAct(C, relu=False).to(d)
+    for m in (bn, bnr):
+        with torch.no_grad():
+            m.weight.copy_(torch.rand(C, device=d) + 0.5)
+            m.bias.copy_(torch.randn(C, device=d) * 0.3)
+    if conv_stats and C % 64 == 0:
+        xin = (torch.randn(N, 64, H, W, device=d)).to(torch.bfloat16).contiguous(memory_format=cl)
+        w1 = (torch.randn(C, 64, 1, 1, device=d) * 0.2).to(torch.bfloat16).contiguous(memory_format=cl)
+        w2 = (torch.randn(C, 64, 1, 1, device=d) * 0.2).to(torch.bfloat16).contiguous(memory_format=cl)
+        with torch.no_grad():
+            r0 = CV.conv2d(xin, w2, bn_stats=DS_SLOTS)
+            x0 = CV.conv2d(xin, w1, bn_stats=True)
+        assert getattr(x0, "_kfa_prestats", False) and getattr(r0, "_kfa_prestats_tag", None) == DS_SLOTS
+    else:
+        x0 = (torch.randn(N, C, H, W, device=d) * 2 + 1).to(torch.bfloat16).contiguous(memory_format=cl)
+        r0 = (torch.randn(N, C, H, W, device=d) - 0.5).to(torch.bfloat16).contiguous(memory_format=cl)
+    x = x0.detach().requires_grad_()
+    r = r0.detach().requires_grad_()
+    for t, t0 in ((x, x0), (r, r0)):  # keep the conv's statistics tags on the leaf copies
+        for a in ("_kfa_prestats", "_kfa_prestats_tag"):
+            if hasattr(t0, a):
+                setattr(t, a, getattr(t0, a))
+    y = bn_act_dual(bn, x, bnr, r)
+    xf, rf = x0.float().detach().requires_grad_(), r0.float().detach().requires_grad_()
+    g1, b1 = bn.weight.detach().clone().requires_grad_(), bn.bias.detach().clone().requires_grad_()
+    g2, b2 = bnr.weight.detach().clone().requires_grad_(), bnr.bias.detach().clone().requires_grad_()
+    rm1, rv1, rm2, rv2 = (torch.zeros(C, device=d), torch.ones(C, device=d), torch.zeros(C, device=d),
+                          torch.ones(C, device=d))
+    F = torch.nn.functional
+    yf = torch.relu(F.batch_norm(xf, rm1, rv1, g1, b1, True, 0.1, 1e-5) + F.batch_norm(rf, rm2, rv2, g2, b2, True, 0.1,
+                                                                                         1e-5))
+    assert (y.float() - yf).abs().max().item() < 0.05 * max(1.0, yf.abs().max().item() / 8)
+    for a, b_ in ((bn.running_mean, rm1), (bn.running_var, rv1), (bnr.running_mean, rm2), (bnr.running_var, rv2)):
+        torch.testing.assert_close(a, b_, atol=3e-3, rtol=3e-3)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    yf.backward(dy.float())
+    for got, want in ((x.grad, xf.grad), (r.grad, rf.grad)):
+        assert (got.float() - want).abs().max().item() < 0.05 * max(1.0, want.abs().max().item())
+    for got, want in ((bn.weight.grad, g1.grad), (bn.bias.grad, b1.grad), (bnr.weight.grad, g2.grad),
+                      (bnr.bias.grad, b2.grad)):
+        torch.testing.assert_close(got, want, atol=0.05 * max(1.0, want.abs().max().item()), rtol=0.02)
+    torch.cuda.synchronize()
+    for tag in ("bn_slots", DS_SLOTS):
+        assert bn_slot_workspace(C, d, tag).abs().max().item() == 0, f"{tag} left dirty"
