@@ -94,9 +94,14 @@ __global__ __launch_bounds__(256) void maxpool_bwd(const bf16_t* __restrict__ dy
 // used — the generic loops' bounds `continue`s serialised the 9 (fwd) / 4 (bwd)
 // loads of a thread, leaving the pool latency-bound at 2-3 TB/s.  Out-of-range
 // taps load a clamped (valid) address and are masked afterwards.
+// BN: x is the PRE-BatchNorm tensor; every window element is first mapped to
+// the bf16 value the BN + ReLU apply pass would have written,
+// bf16(relu(fma(x, scale[c], shift[c]))) (ss = [scale | shift]), so the stem's
+// BN output is never materialised (its backward recomputes the mask from x).
+template <bool BN>
 __global__ __launch_bounds__(256) void maxpool3s2_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
                                                       uint8_t* __restrict__ idx, int N, int H, int W, int C, int Ho,
-                                                      int Wo, int p) {
+                                                      int Wo, int p, const float* __restrict__ ss) {
   const unsigned cv = C / 8;
   const unsigned total = (unsigned)N * Ho * Wo * cv;
   const unsigned v = blockIdx.x * blockDim.x + threadIdx.x;
@@ -119,15 +124,24 @@ __global__ __launch_bounds__(256) void maxpool3s2_fwd(const bf16_t* __restrict__
       const int ch = min(max(ih, 0), H - 1), cw = min(max(iw, 0), W - 1);
       in[kh * 3 + kw] = *reinterpret_cast<const uint4*>(xb + ((long)ch * W + cw) * C);
     }
-  float best[8];
+  float best[8], sc[8], sf[8];
   int bi[8];
 #pragma unroll
-  for (int j = 0; j < 8; j++) { best[j] = -INFINITY; bi[j] = 0; }
+  for (int j = 0; j < 8; j++) {
+    best[j] = -INFINITY;
+    bi[j] = 0;
+    sc[j] = BN ? ss[cg * 8 + j] : 1.f;
+    sf[j] = BN ? ss[C + cg * 8 + j] : 0.f;
+  }
 #pragma unroll
   for (int pos = 0; pos < 9; pos++) {
     if (!ok[pos]) continue;
     float f[8];
     unpack8(in[pos], f);
+    if (BN) {
+#pragma unroll
+      for (int j = 0; j < 8; j++) f[j] = bf2f(f2bf(fmaxf(fmaf(f[j], sc[j], sf[j]), 0.f)));
+    }
 #pragma unroll
     for (int j = 0; j < 8; j++)
       if (f[j] > best[j] || (f[j] != f[j] && best[j] == best[j])) { best[j] = f[j]; bi[j] = pos; }
@@ -200,8 +214,8 @@ KFA_API int kfa_maxpool_fwd(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int
   if (C % 8 || k > 15) return -1;
   const long work = (long)N * Ho * Wo * (C / 8);
   if (k == 3 && s == 2 && p <= 1 && work < (1L << 31) && (long)N * H * W * C < (1L << 40))
-    hipLaunchKernelGGL(maxpool3s2_fwd, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, st, x, y, idx, N, H, W, C,
-                       Ho, Wo, p);
+    hipLaunchKernelGGL(maxpool3s2_fwd<false>, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, st, x, y, idx, N, H,
+                       W, C, Ho, Wo, p, nullptr);
   else if (work < (1L << 31))
     hipLaunchKernelGGL(maxpool_fwd<unsigned>, dim3(grid_for(work)), dim3(256), 0, st, x, y, idx, N, H, W, C, Ho, Wo, k,
                        s, p);
@@ -224,5 +238,16 @@ KFA_API int kfa_maxpool_bwd(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, in
   else
     hipLaunchKernelGGL(maxpool_bwd<long>, dim3(grid_for(work)), dim3(256), 0, st, dy, idx, dx, N, H, W, C, Ho, Wo, k,
                        s, p);
+  return kfa_status();
+}
+
+// Stem BatchNorm + ReLU + 3x3/s2 max pool in one pass over the PRE-BN tensor
+// (see maxpool3s2_fwd<true>); ss = the BN's [scale | shift] (kfa_bn_finalize).
+KFA_API int kfa_maxpool_fwd_bn(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H, int W, int C, int Ho, int Wo,
+                               int k, int s, int p, const float* ss, hipStream_t st) {
+  const long work = (long)N * Ho * Wo * (C / 8);
+  if (C % 8 || k != 3 || s != 2 || p > 1 || !ss || work >= (1L << 31) || (long)N * H * W * C >= (1L << 40)) return -1;
+  hipLaunchKernelGGL(maxpool3s2_fwd<true>, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, st, x, y, idx, N, H, W,
+                     C, Ho, Wo, p, ss);
   return kfa_status();
 }

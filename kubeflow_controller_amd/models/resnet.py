@@ -14,13 +14,14 @@ import os
 import torch
 import torch.nn as nn
 
-from ..ops.batchnorm import DS_SLOTS, BatchNorm2dAct, bn_act_dual
+from ..ops.batchnorm import DS_SLOTS, BatchNorm2dAct, bn_act_dual, bn_relu_maxpool
 from ..ops.conv import Conv2d, GradJoin
 from ..ops.linear import Linear
 from ..ops.pool import MaxPool2d, global_avg_pool
 
 
 DUAL_BN = os.environ.get("KFA_BN_DUAL", "1") != "0"
+FUSED_STEM_POOL = os.environ.get("KFA_STEM_POOL_FUSED", "1") != "0"
 
 
 class Bottleneck(nn.Module):
@@ -99,7 +100,9 @@ class ResNet(nn.Module):
         nn.init.zeros_(self.fc.bias)
 
     def forward(self, x):
-        x = self.maxpool(self.bn1(self.conv1(x, bn_stats=self.training)))
+        x = self.conv1(x, bn_stats=self.training)
+        # stem BN + ReLU + 3x3/s2 max pool: one pass over the conv output in training
+        x = bn_relu_maxpool(self.bn1, x) if FUSED_STEM_POOL else self.maxpool(self.bn1(x))
         x = self.layers(x)
         return self.fc(global_avg_pool(x))
 

@@ -307,6 +307,77 @@ def bn_act_dual(bn: "BatchNorm2dAct", x: torch.Tensor, bn_r: "BatchNorm2dAct", r
     return y
 
 
+_lib.register("kfa_maxpool_fwd_bn", [_lib.P, _lib.P, _lib.P] + [_lib.I] * 9 + [_lib.P, _lib.P])
+_lib.register("kfa_maxpool_bwd", [_lib.P, _lib.P, _lib.P] + [_lib.I] * 9 + [_lib.P])
+
+
+class _BNReluPoolFn(torch.autograd.Function):
+    """``maxpool(relu(bn(x)))`` for the ResNet stem (training): BN finalize, then
+    ONE pass that normalises each window element and pools it (``kfa_maxpool_fwd_bn``)
+    — the 4x larger BN output is never written or re-read.  Backward: the pool's
+    gradient scatter, then the BN backward with the ReLU mask recomputed from x
+    and the saved [scale | shift] (exactly what the unfused pair runs)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, prestats, k, s, p):
+        x = _as_rows(x)
+        N, C, H, W = x.shape
+        M = N * H * W
+        dev = x.device
+        Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+        slots, _ = _workspaces(C, dev)
+        f32 = dict(dtype=torch.float32, device=dev)
+        mean, invstd, ss = torch.empty(C, **f32), torch.empty(C, **f32), torch.empty(2 * C, **f32)
+        st = _lib.stream()
+        _lib.call("kfa_bn_finalize", _lib.ptr(x), _lib.ptr(slots), M, C, _lib.ptr(weight), _lib.ptr(bias),
+                  _lib.ptr(running_mean), _lib.ptr(running_var), _lib.ptr(mean), _lib.ptr(invstd), _lib.ptr(ss),
+                  eps, momentum, int(prestats), st)
+        cl = torch.channels_last
+        y = torch.empty((N, C, Ho, Wo), dtype=x.dtype, device=dev, memory_format=cl)
+        idx = torch.empty((N, C, Ho, Wo), dtype=torch.uint8, device=dev, memory_format=cl)
+        _lib.call("kfa_maxpool_fwd_bn", _lib.ptr(x), _lib.ptr(y), _lib.ptr(idx), N, H, W, C, Ho, Wo, k, s, p,
+                  _lib.ptr(ss), st)
+        ctx.save_for_backward(x, ss, idx, weight, mean, invstd)
+        ctx.meta = (N, C, H, W, Ho, Wo, k, s, p)
+        ctx.params = (weight, bias)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, ss, idx, weight, mean, invstd = ctx.saved_tensors
+        N, C, H, W, Ho, Wo, k, s, p = ctx.meta
+        dev = x.device
+        st = _lib.stream()
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dbn = torch.empty_like(x)
+        _lib.call("kfa_maxpool_bwd", _lib.ptr(dy), _lib.ptr(idx), _lib.ptr(dbn), N, H, W, C, Ho, Wo, k, s, p, st)
+        w, b = ctx.params
+        dg, db, direct = _param_grads(w, b, C, dev)
+        slots, coef = _workspaces(C, dev)
+        dx = torch.empty_like(x)
+        _lib.call("kfa_bn_bwd", _lib.ptr(dbn), _lib.ptr(x), None, _lib.ptr(weight), _lib.ptr(mean), _lib.ptr(invstd),
+                  _lib.ptr(dx), None, _lib.ptr(dg), _lib.ptr(db), _lib.ptr(slots), _lib.ptr(coef), N * H * W, C, 1,
+                  int(direct), _lib.ptr(ss), None, st)
+        if direct:
+            notify_grad_ready(w)
+            notify_grad_ready(b)
+            return dx, None, None, None, None, None, None, None, None, None, None
+        return (dx, dg if w.dtype == torch.float32 else dg.to(w.dtype), db if b.dtype == torch.float32 else db.to(b.dtype),
+                None, None, None, None, None, None, None, None)
+
+
+def bn_relu_maxpool(bn: "BatchNorm2dAct", x: torch.Tensor, k: int = 3, s: int = 2, p: int = 1) -> torch.Tensor:
+    """``max_pool2d(bn(x), k, s, p)`` for a BN with ReLU; fused in training on the
+    GPU for the 3x3/s2 pool (:class:`_BNReluPoolFn`), else the two ops."""
+    if (x.is_cuda and bn.training and bn.relu and MASK_FROM_X and k == 3 and s == 2 and p <= 1 and x.dim() == 4
+            and x.dtype == torch.bfloat16 and x.shape[1] % 8 == 0):
+        pre = getattr(x, "_kfa_prestats", False) and getattr(x, "_kfa_prestats_tag", "bn_slots") == "bn_slots"
+        return _BNReluPoolFn.apply(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.momentum, bn.eps, pre,
+                                   k, s, p)
+    from .pool import max_pool2d
+    return max_pool2d(bn(x), k, s, p)
+
+
 def bn_act_reference(x, weight, bias, running_mean, running_var, residual=None, training=True, momentum=0.1,
                      eps=1e-5, relu=True):
     """Plain PyTorch fp32 reference of the same op (used by the numerics tests)."""

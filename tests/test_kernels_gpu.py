@@ -256,3 +256,38 @@ def test_bn_act_dual_downsample_pair_matches_fp32(N, C, H, W, conv_stats):
     torch.cuda.synchronize()
     for tag in ("bn_slots", DS_SLOTS):
         assert bn_slot_workspace(C, d, tag).abs().max().item() == 0, f"{tag} left dirty"
+
+
+@pytest.mark.parametrize("N,C,H,W", [(4, 64, 112, 112), (2, 16, 9, 7)])
+def test_bn_relu_maxpool_fused_matches_fp32(N, C, H, W):
+    """Stem BN + ReLU + 3x3/s2 max pool in one pass (ops.batchnorm.bn_relu_maxpool)
+    vs fp32 batch_norm -> relu -> max_pool2d: output, running stats, dx, dgamma,
+    dbeta."""
+    _native_loaded()
+    from kubeflow_controller_amd.ops.batchnorm import BatchNorm2dAct, bn_relu_maxpool
+    torch.manual_seed(9)
+    d = _dev()
+    bn = BatchNorm2dAct(C, relu=True).to(d)
+    with torch.no_grad():
+        bn.weight.copy_(torch.rand(C, device=d) + 0.5)
+        bn.bias.copy_(torch.randn(C, device=d) * 0.3)
+    x0 = (torch.randn(N, C, H, W, device=d) * 2 + 0.5).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x = x0.detach().requires_grad_()
+    y = bn_relu_maxpool(bn, x)
+    xf = x0.float().detach().requires_grad_()
+    g, b = bn.weight.detach().clone().requires_grad_(), bn.bias.detach().clone().requires_grad_()
+    rm, rv = torch.zeros(C, device=d), torch.ones(C, device=d)
+    F = torch.nn.functional
+    yf = F.max_pool2d(torch.relu(F.batch_norm(xf, rm, rv, g, b, True, 0.1, 1e-5)), 3, 2, 1)
+    assert y.shape == yf.shape
+    assert (y.float() - yf).abs().max().item() < 0.02 * max(1.0, yf.abs().max().item())
+    torch.testing.assert_close(bn.running_mean, rm, atol=2e-3, rtol=2e-3)
+    torch.testing.assert_close(bn.running_var, rv, atol=2e-3, rtol=2e-3)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    yf.backward(dy.float())
+    # argmax ties between bf16-rounded window values may route a gradient to a different tap
+    err = (x.grad.float() - xf.grad).abs()
+    assert (err > 0.05 * max(1.0, xf.grad.abs().max().item())).float().mean().item() < 1e-3
+    torch.testing.assert_close(bn.weight.grad, g.grad, atol=0.05 * max(1.0, g.grad.abs().max().item()), rtol=0.03)
+    torch.testing.assert_close(bn.bias.grad, b.grad, atol=0.05 * max(1.0, b.grad.abs().max().item()), rtol=0.03)
