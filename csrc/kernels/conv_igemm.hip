@@ -88,6 +88,14 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+template <int N>
+__device__ __forceinline__ void lgkm_wait() {
+  if constexpr (N == 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
+  else static_assert(N < 0, "lgkm_wait: add the literal");
+}
+
 __device__ __forceinline__ int swz(int row, int chunk) { return row * BK + ((chunk ^ ((row >> 1) & 7)) << 3); }
 
 // WM x WN waves, each owning TM x TN MFMA 16x16 tiles (wave tile 16TM x 16TN)
@@ -214,23 +222,59 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
     for (int j = 0; j < TM; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fq = lane >> 4;
+  // Fragment reads ahead of the MFMAs that use them: k-half 0's A and B plus
+  // k-half 1's B fragments are issued before k-half 0's MFMAs, k-half 1's A
+  // fragments between the two MFMA groups, each group preceded by a counted
+  // lgkmcnt.  The reads are inline asm: with compiler-visible ds_reads hipcc
+  // re-used a few fragment registers and waited lgkmcnt(0) between small MFMA
+  // groups (its wait pass does not count these reads exactly), exposing the LDS
+  // latency several times per k-step.  sched_barrier after each wait keeps the
+  // MFMAs behind it (rule 18).  TM + 2 TN <= 15 reads in flight (4-bit counter);
+  // the 8-wave 256x256 variant keeps the plain form.
   auto compute = [&](int buf) {
     const bf16_t* Ab = As + buf * BM * BK;
     const bf16_t* Bb = Bs + buf * BN * BK;
-#pragma unroll
-    for (int ks = 0; ks < 2; ks++) {
-      short8 af[TM], bf[TN];
-#pragma unroll
-      for (int i = 0; i < TM; i++)
-        af[i] = *reinterpret_cast<const short8*>(Ab + swz(wm * TM * 16 + i * 16 + fr, ks * 4 + fq));
-#pragma unroll
-      for (int i = 0; i < TN; i++)
-        bf[i] = *reinterpret_cast<const short8*>(Bb + swz(wn * TN * 16 + i * 16 + fr, ks * 4 + fq));
+    short8 af[2][TM], bf[2][TN];
+    auto mfma = [&](int ks) {
 #pragma unroll
       for (int ni = 0; ni < TN; ni++)
 #pragma unroll
         for (int mi = 0; mi < TM; mi++)
-          acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[ni], af[mi], acc[ni][mi], 0, 0, 0);
+          acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[ks][ni], af[ks][mi], acc[ni][mi], 0, 0, 0);
+    };
+    if constexpr (TM + 2 * TN <= 15) {
+      auto rd = [&](const bf16_t* p) {
+        short8 v;
+        const unsigned la = (unsigned)(uintptr_t)(__attribute__((address_space(3))) const bf16_t*)p;
+        asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(la) : "memory");
+        return v;
+      };
+#pragma unroll
+      for (int i = 0; i < TN; i++) bf[0][i] = rd(Bb + swz(wn * TN * 16 + i * 16 + fr, fq));
+#pragma unroll
+      for (int i = 0; i < TM; i++) af[0][i] = rd(Ab + swz(wm * TM * 16 + i * 16 + fr, fq));
+#pragma unroll
+      for (int i = 0; i < TN; i++) bf[1][i] = rd(Bb + swz(wn * TN * 16 + i * 16 + fr, 4 + fq));
+      lgkm_wait<TN>();  // k-half 0's fragments landed; k-half 1's B reads may still be in flight
+      __builtin_amdgcn_sched_barrier(0);
+      mfma(0);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < TM; i++) af[1][i] = rd(Ab + swz(wm * TM * 16 + i * 16 + fr, 4 + fq));
+      lgkm_wait<0>();
+      __builtin_amdgcn_sched_barrier(0);
+      mfma(1);
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < 2; ks++) {
+#pragma unroll
+        for (int i = 0; i < TM; i++)
+          af[ks][i] = *reinterpret_cast<const short8*>(Ab + swz(wm * TM * 16 + i * 16 + fr, ks * 4 + fq));
+#pragma unroll
+        for (int i = 0; i < TN; i++)
+          bf[ks][i] = *reinterpret_cast<const short8*>(Bb + swz(wn * TN * 16 + i * 16 + fr, ks * 4 + fq));
+        mfma(ks);
+      }
     }
   };
   // Epilogue through LDS: MFMA leaves each lane 4 consecutive channels of one
