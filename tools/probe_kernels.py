@@ -33,7 +33,7 @@ def main(op: str, iters: int = 5) -> None:
         fn = (lambda: T.attn_fwd(qkv, bqkv, kb, B, S, h, 0.1, 1)) if op == "attn_fwd" else \
             (lambda: T.attn_bwd(qkv, bqkv, kb, out, lse, dout, db, B, S, h, 0.1, 1))
     elif op.startswith("conv_"):
-        # conv_fwd_3x3_14 (legacy name) or conv_{fwd,dgrad}_<Cin>_<H>_<Cout>_<k>_<stride>
+        # conv_fwd_3x3_14 (legacy name) or conv_{fwd,dgrad,wgrad}_<Cin>_<H>_<Cout>_<k>_<stride>
         from kubeflow_controller_amd.ops.conv import conv_dgrad, conv_fwd
         parts = op.split("_")
         if len(parts) == 7:
@@ -45,7 +45,12 @@ def main(op: str, iters: int = 5) -> None:
         x = bf(256, cin, hh, hh).contiguous(memory_format=torch.channels_last)
         w = (bf(cout, cin, k, k) * 0.05).contiguous(memory_format=torch.channels_last)
         dy = bf(256, cout, ho, ho).contiguous(memory_format=torch.channels_last)
-        fn = (lambda: conv_fwd(x, w, st, pad)) if "fwd" in op else (lambda: conv_dgrad(dy, w, x.shape, st, pad))
+        if "wgrad" in op:  # conv_wgrad_<Cin>_<H>_<Cout>_<k>_<stride>: dW into a bf16 gradient
+            from kubeflow_controller_amd.ops.conv import wgrad_into
+            gw = torch.zeros_like(w)
+            fn = lambda: wgrad_into(x, dy, gw, 256, hh, hh, cin, ho, ho, cout, k, k, st, pad, True)  # noqa: E731
+        else:
+            fn = (lambda: conv_fwd(x, w, st, pad)) if "fwd" in op else (lambda: conv_dgrad(dy, w, x.shape, st, pad))
     elif op == "gemm_nt":
         from kubeflow_controller_amd.ops import gemm as G
         a, b = bf(32768, 768), bf(3072, 768)
