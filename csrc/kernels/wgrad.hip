@@ -144,6 +144,23 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_kernel(const bf16_t* __
   const int PQ = g.P * g.Q;
   const float rPQ = 1.f / (float)PQ, rQ = 1.f / (float)g.Q;
   const bool lin_b = g.R == 1 && g.S == 1 && g.st == 1 && g.pad == 0;  // X row k is pixel k
+  // gathered X rows: each B instruction's pixel k = kb + step*BKW + b_row advances by
+  // BKW per k-step, so its (image, p, q) is carried incrementally (a few adds and
+  // compares per step) instead of two divisions per instruction per k-step
+  // (not in the 8-wave variant: it is at the VGPR limit, and the three carried
+  // digits per instruction turned into scratch spills there: -4 % ResNet-50)
+  constexpr bool INC = NW < 8;
+  constexpr int NI = INC ? B_IPW : 1;
+  int b_img[NI], b_p[NI], b_q[NI];
+  const int dq = BKW % g.Q, dp = (BKW / g.Q) % g.P, dimg = BKW / PQ;  // BKW pixels in (img, p, q) digits
+#pragma unroll
+  for (int i = 0; i < (INC ? B_IPW : 0); i++) {
+    const int k = kb + b_row[i];
+    const int img = fdiv(k, PQ, rPQ), rem = k - img * PQ;
+    b_img[i] = img;
+    b_p[i] = fdiv(rem, g.Q, rQ);
+    b_q[i] = rem - b_p[i] * g.Q;
+  }
 
   auto issue = [&](int step, int buf) {
     const int k0 = kb + step * BKW;
@@ -161,6 +178,10 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_kernel(const bf16_t* __
       if (k < ke && b_ok[i]) {
         if (lin_b) {
           sb = X + (long)k * g.Ci + b_ci[i];
+        } else if constexpr (INC) {
+          const int h = b_p[i] * g.st - g.pad + b_r[i], w = b_q[i] * g.st - g.pad + b_s[i];
+          if ((unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W)
+            sb = X + (((long)b_img[i] * g.H + h) * g.W + w) * g.Ci + b_ci[i];
         } else {
           const int img = fdiv(k, PQ, rPQ), rem = k - img * PQ;
           const int p = fdiv(rem, g.Q, rQ), q = rem - p * g.Q;
@@ -171,6 +192,14 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_kernel(const bf16_t* __
       }
       __builtin_amdgcn_global_load_lds(sb, (__attribute__((address_space(3))) void*)(Bs + buf * BKW * BN + b_lds[i]),
                                        16, 0, 0);
+      if (INC && !lin_b) {  // advance this row's pixel by BKW (issue() runs once per step, in order)
+        int q = b_q[i] + dq, p = b_p[i] + dp, img = b_img[i] + dimg;
+        if (q >= g.Q) { q -= g.Q; p++; }
+        if (p >= g.P) { p -= g.P; img++; }
+        b_q[i] = q;
+        b_p[i] = p;
+        b_img[i] = img;
+      }
     }
   };
 
