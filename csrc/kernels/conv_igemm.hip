@@ -71,6 +71,14 @@ __device__ __forceinline__ uint4 bload16(__amdgpu_buffer_rsrc_t r, unsigned off)
   return *reinterpret_cast<uint4*>(&v);
 }
 
+// 16 B per lane buffer -> LDS DMA (buffer_load_dwordx4 ... lds): voff per lane,
+// soff wave-uniform.  A plain device function: the builtin named directly inside
+// the templated kernel's lambdas stops clang's host pass from emitting the
+// kernels' launch stubs.
+__device__ __forceinline__ void buf_dma16(__amdgpu_buffer_rsrc_t r, bf16_t* lds, int voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
+}
+
 // x / d for 0 <= x < 2^24 via an fp32 reciprocal + one correction step
 // (hipcc's int32 division is a ~40-instruction sequence; these run per row).
 __device__ __forceinline__ int fdiv(int x, int d, float rcp) {
@@ -146,7 +154,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
   // pointwise fast paths: A row m is T[m] (1x1 / stride 1 / no pad) and/or D row m is D[m]
   const bool lin_a = g.R == 1 && g.S == 1 && g.sa == 1 && g.oa == 0 && g.ob == 0 && g.H == g.P && g.W == g.Q;
   const bool lin_d = g.os == 1 && g.oph == 0 && g.opw == 0 && g.OH == g.P && g.OW == g.Q;
-  int a_hb[AR], a_wb[AR], a_base[AR];  // element offsets fit in 32 bits (checked on the host)
+  int a_hb[AR], a_wb[AR], a_vo[AR];  // a_vo: byte offset of the row's image + swizzled chunk (< 2^31, host-checked)
   unsigned b_off[BR];
   const __amdgpu_buffer_rsrc_t rT = rsrc(T, g.t_bytes), rB = rsrc(B, g.b_bytes), rD = rsrc(D, g.d_bytes);
   const __amdgpu_buffer_rsrc_t rE = rsrc(E ? E : D, E ? g.d_bytes : 0u);
@@ -157,37 +165,44 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
 #pragma unroll
     for (int i = 0; i < AR; i++) {
       const int m = m0 + rbase + RPP * i;
+      const int cs = (kc ^ ((((i * RPP) + rbase) >> 1) & 7)) * 8;  // this lane's swizzled source chunk
       if (m < g.M && lin_a) {
         a_hb[i] = 0;
         a_wb[i] = 0;
-        a_base[i] = m * g.C;
+        a_vo[i] = (m * g.C + cs) * 2;
       } else if (m < g.M) {
         const int nb = fdiv(m, PQ, rPQ), rem = m - nb * PQ;
         const int p = fdiv(rem, g.Q, rQ), q = rem - p * g.Q;
         a_hb[i] = p * g.sa + g.oa;
         a_wb[i] = q * g.sa + g.ob;
-        a_base[i] = nb * g.H * g.W * g.C;
+        a_vo[i] = (nb * g.H * g.W * g.C + cs) * 2;
       } else {
         a_hb[i] = -(1 << 28);  // forces out-of-range
         a_wb[i] = 0;
-        a_base[i] = 0;
+        a_vo[i] = (int)kOOB;
       }
     }
 #pragma unroll
     for (int i = 0; i < BR; i++) {
       const int n = n0 + rbase + RPP * i;
-      b_off[i] = n < g.N ? (unsigned)(n * g.K + kc * 8) * 2u : kOOB;
+      const int cs = (kc ^ ((((i * RPP) + rbase) >> 1) & 7)) * 8;
+      b_off[i] = n < g.N ? (unsigned)(n * g.K + cs) * 2u : kOOB;
     }
   };
 
   // Operand staging: LDS-DMA (global_load_lds_dwordx4).  Each wave-instruction
   // writes 1 KiB = 8 tile rows lane-linearly; the XOR swizzle is applied on the
-  // per-lane SOURCE address (rule 21), padding taps / tails read a zero page.
+  // per-lane SOURCE address (rule 21); padding taps / tails read as zero (range check).
   // No staging VGPRs, no ds_write pass; waits are counted by hand.
   const int nk = g.K / BK;
   const int total = my_tiles * nk;
   int setup_tile = -1;
   const int l8 = lane >> 3, pos = lane & 7;
+  // DMA sources as 32-bit buffer offsets (buffer_load ... lds): the per-lane part
+  // is fixed per tile (the swizzled chunk included), the k-slice's channel offset
+  // goes in the SCALAR offset, padding taps / tails get an offset past the
+  // buffer (read as 0 by the range check).  1x1 stride-1 layers then issue
+  // their DMAs with no per-step vector math at all.
   auto issue = [&](int st, int buf) {
     const int ti = st / nk, kt = st - ti * nk;
     if (ti != setup_tile) { setup(tile_of(ti)); setup_tile = ti; }
@@ -195,26 +210,23 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
     const int tap = k0 / g.C, c0 = k0 - tap * g.C;
     const int r = tap / g.S, s = tap - r * g.S;
     const int dh = r * g.ra, dw = s * g.ra;
+    if (lin_a) {  // the whole offset but the slice's is fixed per tile (a_vo, setup)
 #pragma unroll
-    for (int i = 0; i < AR; i++) {
-      const int row = i * RPP + wave * 8 + l8;
-      const int c = pos ^ ((row >> 1) & 7);
-      const int ih = a_hb[i] + dh, iw = a_wb[i] + dw;
-      const bool ok = (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
-      const bf16_t* src = ok ? T + (unsigned)(a_base[i] + (ih * g.W + iw) * g.C + c0 + c * 8) : Z;
-      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(As + buf * BM * BK + (i * RPP + wave * 8) * BK),
-                                       16, 0, 0);
+      for (int i = 0; i < AR; i++)
+        buf_dma16(rT, As + buf * BM * BK + (i * RPP + wave * 8) * BK, a_vo[i], k0 * 2);
+    } else {
+#pragma unroll
+      for (int i = 0; i < AR; i++) {
+        const int ih = a_hb[i] + dh, iw = a_wb[i] + dw;
+        const bool ok = (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+        const int vo = ok ? a_vo[i] + (ih * g.W + iw) * g.C * 2 : (int)kOOB;
+        buf_dma16(rT, As + buf * BM * BK + (i * RPP + wave * 8) * BK, vo, c0 * 2);
+      }
     }
 #pragma unroll
-    for (int i = 0; i < BR; i++) {
-      const int row = i * RPP + wave * 8 + l8;
-      const int c = pos ^ ((row >> 1) & 7);
-      const bf16_t* src = b_off[i] == kOOB ? Z : B + b_off[i] / 2 + k0 + (c - pos) * 8;
-      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(Bs + buf * BN * BK + (i * RPP + wave * 8) * BK),
-                                       16, 0, 0);
-    }
+    for (int i = 0; i < BR; i++)
+      buf_dma16(rB, Bs + buf * BN * BK + (i * RPP + wave * 8) * BK, (int)b_off[i], k0 * 2);
   };
-
   floatx4 acc[TN][TM];
 #pragma unroll
   for (int i = 0; i < TN; i++)
