@@ -31,6 +31,7 @@ struct WGeo {
   int N;        // R*S*Ci
   int K;        // Nb*P*Q  (pixels)
   int kchunk;   // pixels per split (multiple of BKW)
+  unsigned x_bytes;  // extent of X (buffer range)
 };
 
 __device__ __forceinline__ int fdiv(int x, int d, float rcp) {
@@ -41,6 +42,16 @@ __device__ __forceinline__ int fdiv(int x, int d, float rcp) {
 }
 
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+constexpr unsigned kOOB = 0x80000000u;  // a buffer offset past every extent: the load returns 0
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wrsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+// 16 B per lane buffer -> LDS DMA; a plain device function (the builtin inside the
+// templated kernel's lambda stops clang's host pass from emitting launch stubs)
+__device__ __forceinline__ void buf_dma16(__amdgpu_buffer_rsrc_t r, bf16_t* lds, int voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
+}
 
 typedef short v4i16 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
@@ -144,6 +155,13 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_kernel(const bf16_t* __
   const int PQ = g.P * g.Q;
   const float rPQ = 1.f / (float)PQ, rQ = 1.f / (float)g.Q;
   const bool lin_b = g.R == 1 && g.S == 1 && g.st == 1 && g.pad == 0;  // X row k is pixel k
+  const __amdgpu_buffer_rsrc_t rA = wrsrc(dY, (unsigned)g.K * (unsigned)g.Co * 2u);
+  const __amdgpu_buffer_rsrc_t rX = wrsrc(X, g.x_bytes);
+  int a_vo[A_IPW], b_vo[B_IPW];
+#pragma unroll
+  for (int i = 0; i < A_IPW; i++) a_vo[i] = a_ok[i] ? (a_row[i] * g.Co + a_m[i]) * 2 : (int)kOOB;
+#pragma unroll
+  for (int i = 0; i < B_IPW; i++) b_vo[i] = b_ok[i] ? (b_row[i] * g.Ci + b_ci[i]) * 2 : (int)kOOB;
   // gathered X rows: each B instruction's pixel k = kb + step*BKW + b_row advances by
   // BKW per k-step, so its (image, p, q) is carried incrementally (a few adds and
   // compares per step) instead of two divisions per instruction per k-step
@@ -162,37 +180,41 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_kernel(const bf16_t* __
     b_q[i] = rem - b_p[i] * g.Q;
   }
 
+  // DMA sources as 32-bit buffer offsets (buffer_load ... lds): dY rows and
+  // pointwise X rows are fixed per lane with the k-step in the SCALAR offset
+  // (splits are whole k-steps, so only the tensor's end is partial: the range
+  // check reads it as 0); gathered X rows compute their offset per step.
   auto issue = [&](int step, int buf) {
     const int k0 = kb + step * BKW;
 #pragma unroll
-    for (int i = 0; i < A_IPW; i++) {
-      const int k = k0 + a_row[i];
-      const bf16_t* sa = (k < ke && a_ok[i]) ? dY + (long)k * g.Co + a_m[i] : Z;
-      __builtin_amdgcn_global_load_lds(sa, (__attribute__((address_space(3))) void*)(As + buf * BKW * BM + a_lds[i]),
-                                       16, 0, 0);
+    for (int i = 0; i < A_IPW; i++) buf_dma16(rA, As + buf * BKW * BM + a_lds[i], a_vo[i], k0 * g.Co * 2);
+    if (lin_b) {
+#pragma unroll
+      for (int i = 0; i < B_IPW; i++) buf_dma16(rX, Bs + buf * BKW * BN + b_lds[i], b_vo[i], k0 * g.Ci * 2);
+      return;
     }
 #pragma unroll
     for (int i = 0; i < B_IPW; i++) {
       const int k = k0 + b_row[i];
-      const bf16_t* sb = Z;
+      int vo = (int)kOOB;
       if (k < ke && b_ok[i]) {
-        if (lin_b) {
-          sb = X + (long)k * g.Ci + b_ci[i];
-        } else if constexpr (INC) {
-          const int h = b_p[i] * g.st - g.pad + b_r[i], w = b_q[i] * g.st - g.pad + b_s[i];
-          if ((unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W)
-            sb = X + (((long)b_img[i] * g.H + h) * g.W + w) * g.Ci + b_ci[i];
+        int img, p, q;
+        if constexpr (INC) {
+          img = b_img[i];
+          p = b_p[i];
+          q = b_q[i];
         } else {
-          const int img = fdiv(k, PQ, rPQ), rem = k - img * PQ;
-          const int p = fdiv(rem, g.Q, rQ), q = rem - p * g.Q;
-          const int h = p * g.st - g.pad + b_r[i], w = q * g.st - g.pad + b_s[i];
-          if ((unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W)
-            sb = X + (((long)img * g.H + h) * g.W + w) * g.Ci + b_ci[i];
+          img = fdiv(k, PQ, rPQ);
+          const int rem = k - img * PQ;
+          p = fdiv(rem, g.Q, rQ);
+          q = rem - p * g.Q;
         }
+        const int h = p * g.st - g.pad + b_r[i], w = q * g.st - g.pad + b_s[i];
+        if ((unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W)
+          vo = ((((img * g.H + h) * g.W) + w) * g.Ci + b_ci[i]) * 2;
       }
-      __builtin_amdgcn_global_load_lds(sb, (__attribute__((address_space(3))) void*)(Bs + buf * BKW * BN + b_lds[i]),
-                                       16, 0, 0);
-      if (INC && !lin_b) {  // advance this row's pixel by BKW (issue() runs once per step, in order)
+      buf_dma16(rX, Bs + buf * BKW * BN + b_lds[i], vo, 0);
+      if constexpr (INC) {  // advance this row's pixel by BKW (issue() runs once per step, in order)
         int q = b_q[i] + dq, p = b_p[i] + dp, img = b_img[i] + dimg;
         if (q >= g.Q) { q -= g.Q; p++; }
         if (p >= g.P) { p -= g.P; img++; }
@@ -373,7 +395,9 @@ KFA_API int kfa_conv_wgrad(const bf16_t* dY, const bf16_t* X, void* grad, int gr
   if (Ci % 8 || Co % 8) return -1;
   const long K = (long)Nb * P * Q;
   if (K >= (1L << 24)) return -2;  // fp32-reciprocal pixel division is exact below 2^24
-  WGeo g{H, W, Ci, P, Q, Co, R, S, st, pad, R * S * Ci, (int)K, 0};
+  // 32-bit buffer offsets (dY rows, X pixels; the scalar k offset included)
+  if (K * Co * 2 >= (long)kOOB || (long)Nb * H * W * Ci * 2 >= (long)kOOB) return -2;
+  WGeo g{H, W, Ci, P, Q, Co, R, S, st, pad, R * S * Ci, (int)K, 0, (unsigned)((long)Nb * H * W * Ci * 2)};
   const WPlan p = plan(K, Co, g.N);
   g.kchunk = p.kchunk;
   const size_t lds = (size_t)2 * BKW * (p.BM + p.BN) * sizeof(bf16_t);
