@@ -251,3 +251,74 @@ KFA_API int kfa_maxpool_fwd_bn(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, 
                      C, Ho, Wo, p, ss);
   return kfa_status();
 }
+
+// ---------------------------------------------------------------- global average pool
+// NHWC [N][HW][C] bf16 -> [N][C] bf16 (fp32 sums) and its backward
+// dx[n][hw][c] = dy[n][c] / HW written straight in NHWC — the ResNet head (the
+// ATen mean backward expanded, scaled, converted and re-laid-out the 51 MB
+// gradient in four passes, ~0.13 ms per step).  One thread per 8 channels.
+namespace {
+__global__ __launch_bounds__(256) void gap_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int N, int HW,
+                                                      int C) {
+  const int cv = C / 8;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= N * cv) return;
+  const int n = t / cv, c8 = t - n * cv;
+  const bf16_t* p = x + (long)n * HW * C + c8 * 8;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int i = 0;
+  for (; i + 3 < HW; i += 4) {  // four rows in flight
+    uint4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) v[u] = *reinterpret_cast<const uint4*>(p + (long)(i + u) * C);
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      float f[8];
+      unpack8(v[u], f);
+#pragma unroll
+      for (int j = 0; j < 8; j++) s[j] += f[j];
+    }
+  }
+  for (; i < HW; i++) {
+    float f[8];
+    unpack8(*reinterpret_cast<const uint4*>(p + (long)i * C), f);
+#pragma unroll
+    for (int j = 0; j < 8; j++) s[j] += f[j];
+  }
+  const float r = 1.f / (float)HW;
+#pragma unroll
+  for (int j = 0; j < 8; j++) s[j] *= r;
+  *reinterpret_cast<uint4*>(y + (long)n * C + c8 * 8) = pack8(s);
+}
+
+__global__ __launch_bounds__(256) void gap_bwd_kernel(const bf16_t* __restrict__ dy, bf16_t* __restrict__ dx, int N,
+                                                      int HW, int C) {
+  const int cv = C / 8;
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long)N * HW * cv) return;
+  const int c8 = (int)(t % cv);
+  const long nhw = t / cv;
+  const int n = (int)(nhw / HW);
+  float f[8];
+  unpack8(*reinterpret_cast<const uint4*>(dy + (long)n * C + c8 * 8), f);
+  const float r = 1.f / (float)HW;
+#pragma unroll
+  for (int j = 0; j < 8; j++) f[j] *= r;
+  *reinterpret_cast<uint4*>(dx + t * 8) = pack8(f);
+}
+}  // namespace
+
+KFA_API int kfa_gap_fwd(const bf16_t* x, bf16_t* y, int N, int HW, int C, hipStream_t st) {
+  if (C % 8 || N <= 0 || HW <= 0) return -1;
+  const int th = N * (C / 8);
+  hipLaunchKernelGGL(gap_fwd_kernel, dim3((th + 255) / 256), dim3(256), 0, st, x, y, N, HW, C);
+  return kfa_status();
+}
+
+KFA_API int kfa_gap_bwd(const bf16_t* dy, bf16_t* dx, int N, int HW, int C, hipStream_t st) {
+  if (C % 8 || N <= 0 || HW <= 0) return -1;
+  const long th = (long)N * HW * (C / 8);
+  if (th >= (1L << 31)) return -2;
+  hipLaunchKernelGGL(gap_bwd_kernel, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, st, dy, dx, N, HW, C);
+  return kfa_status();
+}

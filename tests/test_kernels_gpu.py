@@ -291,3 +291,23 @@ def test_bn_relu_maxpool_fused_matches_fp32(N, C, H, W):
     assert (err > 0.05 * max(1.0, xf.grad.abs().max().item())).float().mean().item() < 1e-3
     torch.testing.assert_close(bn.weight.grad, g.grad, atol=0.05 * max(1.0, g.grad.abs().max().item()), rtol=0.03)
     torch.testing.assert_close(bn.bias.grad, b.grad, atol=0.05 * max(1.0, b.grad.abs().max().item()), rtol=0.03)
+
+
+@pytest.mark.parametrize("N,C,H,W", [(256, 2048, 7, 7), (3, 16, 5, 3)])
+def test_global_avg_pool_fwd_bwd(N, C, H, W):
+    """ops.pool.global_avg_pool (kfa_gap_fwd / kfa_gap_bwd) vs fp32 mean."""
+    _native_loaded()
+    from kubeflow_controller_amd.ops.pool import global_avg_pool
+    torch.manual_seed(2)
+    d = _dev()
+    x0 = torch.randn(N, C, H, W, device=d).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x = x0.detach().requires_grad_()
+    y = global_avg_pool(x)
+    xf = x0.float().detach().requires_grad_()
+    yf = xf.mean((2, 3))
+    torch.testing.assert_close(y.float(), yf, atol=1e-2, rtol=1e-2)
+    dy = torch.randn(N, C, device=d).to(torch.bfloat16)
+    y.backward(dy)
+    yf.backward(dy.float())
+    assert x.grad.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(x.grad.float(), xf.grad, atol=1e-3, rtol=1e-2)
