@@ -107,6 +107,11 @@ __device__ __forceinline__ void lds_dma16(const bf16_t* src, bf16_t* dst) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
 }
 
+// 16 B per lane buffer -> LDS DMA (buffer_load_dwordx4 ... lds), soff wave-uniform
+__device__ __forceinline__ void pp_dma(__amdgpu_buffer_rsrc_t r, char* lds, int voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
+}
+
 template <int N>
 __device__ __forceinline__ void vm_wait() {
   if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -290,27 +295,32 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void gemm_nt_kernel(GemmArgs g, co
   // LDS-DMA plan: instruction i of wave w fills rows (w*G + i)*16 + lane/4, physical
   // chunk lane&3, from logical chunk (lane&3) ^ swz(row), swz(row) = (row >> 2) & 2
   const int lrow = lane >> 2, lch = (lane & 3) ^ ((lane >> 4) & 2);
-  const bf16_t* a_src[GA];
-  const bf16_t* b_src[GB];
+  // sources as 32-bit buffer offsets, k-step in the scalar offset; rows past M / N
+  // (and chunks past K) get an offset past the buffer: read as 0 by the range check
+  const __amdgpu_buffer_rsrc_t rA = rsrc(g.A, (unsigned)(((long)(g.M - 1) * g.lda + g.K) * 2));
+  const __amdgpu_buffer_rsrc_t rB = rsrc(g.B, (unsigned)(((long)(g.N - 1) * g.ldb + g.K) * 2));
+  int a_vo[GA], b_vo[GB];
 #pragma unroll
   for (int i = 0; i < GA; i++) {
     const int m = m0 + (wave * GA + i) * 16 + lrow;
-    a_src[i] = m < g.M ? g.A + (long)m * g.lda + lch * 8 : nullptr;
+    a_vo[i] = m < g.M ? (m * g.lda + lch * 8) * 2 : (int)kOOB;
   }
 #pragma unroll
   for (int i = 0; i < GB; i++) {
     const int n = n0 + (wave * GB + i) * 16 + lrow;
-    b_src[i] = n < g.N ? g.B + (long)n * g.ldb + lch * 8 : nullptr;
+    b_vo[i] = n < g.N ? (n * g.ldb + lch * 8) * 2 : (int)kOOB;
   }
   auto issue = [&](int kt) {
     const int slot = kt % NS, k0 = kt * GK;
-    const bool kin = k0 + lch * 8 < g.K;  // K tail (K % 8 == 0): chunks past K read the zero page
+    const bool kin = k0 + lch * 8 < g.K;  // K tail (K % 8 == 0): chunks past K read as 0
 #pragma unroll
     for (int i = 0; i < GA; i++)
-      lds_dma16((a_src[i] && kin) ? a_src[i] + k0 : zp, As + slot * A_SLOT + (wave * GA + i) * 16 * GK);
+      pp_dma(rA, reinterpret_cast<char*>(As + slot * A_SLOT + (wave * GA + i) * 16 * GK), kin ? a_vo[i] : (int)kOOB,
+             k0 * 2);
 #pragma unroll
     for (int i = 0; i < GB; i++)
-      lds_dma16((b_src[i] && kin) ? b_src[i] + k0 : zp, Bs + slot * B_SLOT + (wave * GB + i) * 16 * GK);
+      pp_dma(rB, reinterpret_cast<char*>(Bs + slot * B_SLOT + (wave * GB + i) * 16 * GK), kin ? b_vo[i] : (int)kOOB,
+             k0 * 2);
   };
 
   // this lane's 16-B operand piece of a 16-row tile: row fr, logical chunk fq
@@ -622,9 +632,6 @@ __global__ __launch_bounds__(512) void gemm_pt_kernel(GemmArgs g, const bf16_t* 
 constexpr int PP_BK = 64;
 constexpr int PP_PIECE = 128 * PP_BK * 2;  // bytes per piece
 
-__device__ __forceinline__ void pp_dma(__amdgpu_buffer_rsrc_t r, char* lds, int voff, int soff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
-}
 
 template <int N>
 __device__ __forceinline__ void pp_vmcnt() {
@@ -892,6 +899,7 @@ KFA_API int kfa_gemm_nt(const bf16_t* A, const bf16_t* B, bf16_t* C, const bf16_
   if ((persistent == 5 || persistent == 6 || persistent == 7) && (K % PP_BK || (long)M * lda * 2 >= (long)kOOB || (long)N * ldb * 2 >= (long)kOOB)) persistent = 4;  // same dbias partial rows (128)
   const long cb = (long)M * ldc * 2;
   if (cb >= (long)kOOB) return -2;  // 32-bit buffer offsets in the epilogue
+  if ((long)M * lda * 2 >= (long)kOOB || (long)N * ldb * 2 >= (long)kOOB) return -2;  // ... and the operand DMA
   const int prow = gemm_part_rows(M, N, bn, persistent);
   if (bn == 0) bn = kfa_gemm_pick_bn(M, N);
   if (persistent == 3 || persistent == 4) bn = 128;

@@ -47,12 +47,14 @@ ROUTE_FUSED = _ROUTE in ("1", "fused")
 
 def gemm_ok(a: torch.Tensor, b: torch.Tensor) -> bool:
     """Operands the kernel takes: bf16 CUDA matrices, K-contiguous, K / N / row
-    strides multiples of 8 (16-B LDS-DMA pieces), 16-B aligned."""
+    strides multiples of 8 (16-B LDS-DMA pieces), 16-B aligned, every operand
+    within 32-bit buffer offsets."""
     return (a.is_cuda and b.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16
             and a.dim() == 2 and b.dim() == 2 and a.shape[1] == b.shape[1] and a.shape[1] % 8 == 0
             and b.shape[0] % 8 == 0 and a.shape[0] > 0 and a.stride(1) == 1 and b.stride(1) == 1
             and a.stride(0) % 8 == 0 and b.stride(0) % 8 == 0 and a.data_ptr() % 16 == 0
-            and b.data_ptr() % 16 == 0 and a.shape[0] * b.shape[0] * 2 < (1 << 31))
+            and b.data_ptr() % 16 == 0 and a.shape[0] * b.shape[0] * 2 < (1 << 31)
+            and a.shape[0] * a.stride(0) * 2 < (1 << 31) and b.shape[0] * b.stride(0) * 2 < (1 << 31))
 
 
 def _check_mn(t, M, N, what):
