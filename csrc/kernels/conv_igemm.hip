@@ -203,13 +203,21 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
   // goes in the SCALAR offset, padding taps / tails get an offset past the
   // buffer (read as 0 by the range check).  1x1 stride-1 layers then issue
   // their DMAs with no per-step vector math at all.
+  // issue() runs for st = 0, 1, 2, ... in order: the (tile, k-slice, channel
+  // offset, tap) of the next slice is carried incrementally (wave-uniform) instead
+  // of four scalar divisions per k-step
+  int nx_ti = 0, nx_kt = 0, nx_c0 = 0, nx_r = 0, nx_s = 0;
   auto issue = [&](int st, int buf) {
-    const int ti = st / nk, kt = st - ti * nk;
+    (void)st;
+    const int ti = nx_ti, k0 = nx_kt * BK, c0 = nx_c0;
     if (ti != setup_tile) { setup(tile_of(ti)); setup_tile = ti; }
-    const int k0 = kt * BK;
-    const int tap = k0 / g.C, c0 = k0 - tap * g.C;
-    const int r = tap / g.S, s = tap - r * g.S;
-    const int dh = r * g.ra, dw = s * g.ra;
+    const int dh = nx_r * g.ra, dw = nx_s * g.ra;
+    nx_c0 += BK;  // advance to the next slice: BK channels of one tap, or BK / C whole taps (C < BK)
+    while (nx_c0 >= g.C) {
+      nx_c0 -= g.C;
+      if (++nx_s == g.S) { nx_s = 0; nx_r++; }
+    }
+    if (++nx_kt == nk) { nx_kt = 0; nx_ti++; nx_c0 = 0; nx_r = 0; nx_s = 0; }
     if (lin_a) {  // the whole offset but the slice's is fixed per tile (a_vo, setup)
 #pragma unroll
       for (int i = 0; i < AR; i++)
