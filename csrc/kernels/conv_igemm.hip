@@ -131,7 +131,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
   bf16_t* Bs = smem + 2 * BM * BK;    // [2][BN][BK]
 
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: LDS-DMA bases in SGPRs
   const int wm = wave % WM, wn = wave / WM;
   const int ntn = (g.N + BN - 1) / BN;
   const int ntiles = ((g.M + BM - 1) / BM) * ntn;

@@ -277,7 +277,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void gemm_nt_kernel(GemmArgs g, co
   bf16_t* As = smem;
   bf16_t* Bs = smem + NS * A_SLOT;
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: LDS-DMA bases in SGPRs
   const int wm = wave % WM, wn = wave / WM;
   // T1: blocks that share an XCD (blockIdx % 8) take consecutive tiles (bijective remap)
   const int nwg = gridDim.x, bid = blockIdx.x;
@@ -397,7 +397,7 @@ __global__ __launch_bounds__(512) void gemm_pt_kernel(GemmArgs g, const bf16_t* 
   bf16_t* As = smem;
   bf16_t* Bs = smem + NSLOT * A_SLOT;
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: LDS-DMA bases in SGPRs
   const int wm = wave % WM, wn = wave / WM;
   const int ntn = (g.N + BN - 1) / BN, ntm = (g.M + BM - 1) / BM;
   const int ntiles = ntm * ntn;

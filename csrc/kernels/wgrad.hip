@@ -104,7 +104,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_kernel(const bf16_t* __
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
   bf16_t* As = smem;                    // [2][BM / WA][BKW][WA]
   bf16_t* Bs = smem + 2 * BKW * BM;     // [2][BN / WB][BKW][WB]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: LDS-DMA bases in SGPRs
   const int wm = wave % WM, wn = wave / WM;
   const int ntn = (g.N + BN - 1) / BN;
   // XCD-aware order (T1, bijective remap): the hardware deals block ids round-
