@@ -56,6 +56,9 @@ def parse_args(argv=None):
                     help="resnet_tiny only for the launcher's CPU/plumbing test")
     ap.add_argument("--device", choices=["auto", "cpu"], default="auto")
     ap.add_argument("--port", type=int, default=0, help="rendezvous port for the self-launch (0 = pick one)")
+    ap.add_argument("--graph", choices=["auto", "on", "off"], default=os.environ.get("KFA_GRAPH", "off"),
+                    help="replay the whole step as one HIP graph after the warm-up (Engine.capture); "
+                         "auto/on: where Engine.graph_ok allows it (1 rank, SGD)")
     return ap.parse_args(argv)
 
 
@@ -130,7 +133,7 @@ def run_rank(args) -> int:
     x = x.contiguous(memory_format=torch.channels_last)
     y = torch.randint(0, ncls, (B,), device=info.device)
 
-    r = timed_steps(engine, (x, y), args.steps, args.warmup)
+    r = timed_steps(engine, (x, y), args.steps, args.warmup, graph=args.graph != "off")
     ms = r["elapsed"] / args.steps * 1e3
     ips = B * info.world * args.steps / r["elapsed"]
     if info.rank == 0:
@@ -155,6 +158,7 @@ def run_rank(args) -> int:
                        "backend": (torch.distributed.get_backend() if torch.distributed.is_initialized()
                                    else None),
                        "optimizer": "SGD momentum 0.9 (fused HIP), fp32 master",
+                       "hip_graph": engine._graph is not None,
                        "loss": r["loss"]},
         }
         print(json.dumps(out), flush=True)

@@ -20,6 +20,8 @@
 // weight has too few tiles to fill the chip: each block
 // writes an fp32 partial tile; a second kernel sums the partials and adds them
 // (converted) straight into the flat gradient buffer (bf16 or fp32).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -236,7 +238,8 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_kernel(const bf16_t* __
     const int buf = st & 1;
     if (st + 1 < nsteps) {
       issue(st + 1, buf ^ 1);
-      if constexpr (A_IPW + B_IPW == 8) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+      if constexpr (A_IPW + B_IPW == 10) asm volatile("s_waitcnt vmcnt(10)\n\ts_barrier" ::: "memory");
+      else if constexpr (A_IPW + B_IPW == 8) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
       else if constexpr (A_IPW + B_IPW == 6) asm volatile("s_waitcnt vmcnt(6)\n\ts_barrier" ::: "memory");
       else if constexpr (A_IPW + B_IPW == 4) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
@@ -352,8 +355,19 @@ int num_cus() {
   return cached;
 }
 
+// 64x256 tiles for the Co = 64 weights (stem, 256->64 1x1s): KFA_WGRAD_WIDE64=0 keeps 64x128
+bool wide64() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("KFA_WGRAD_WIDE64");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+
 struct WPlan {
-  int variant;   // 0: 128x128, 1: 64x128 (Co <= 64), 2: 128x64 (N <= 64), 3: 64x64 (both), 4: 256x256 (8 waves)
+  int variant;   // 0: 128x128, 1: 64x128 (Co <= 64), 2: 128x64 (N <= 64), 3: 64x64 (both), 4: 256x256 (8 waves),
+                 // 5: 64x256 (Co <= 64, N % 256 == 0: 64x64 wave tiles instead of 64x32)
   int BM, BN, tiles, splits, kchunk, threads, blocks_per_cu;
 };
 
@@ -362,9 +376,10 @@ WPlan plan(long K, int Co, int N) {
   // 256x256 (8 waves of 128x64, one block per CU): half the operand bytes per
   // MFMA of the 128x128 tile — for the long reductions of big weights
   if (Co % 256 == 0 && N % 256 == 0 && K >= 8192) p.variant = 4;
+  else if (Co <= 64 && N % 256 == 0 && wide64()) p.variant = 5;
   else p.variant = Co <= 64 ? (N <= 64 ? 3 : 1) : (N <= 64 ? 2 : 0);
-  p.BM = p.variant == 4 ? 256 : ((p.variant == 1 || p.variant == 3) ? 64 : 128);
-  p.BN = p.variant == 4 ? 256 : ((p.variant == 2 || p.variant == 3) ? 64 : 128);
+  p.BM = p.variant == 4 ? 256 : ((p.variant == 1 || p.variant == 3 || p.variant == 5) ? 64 : 128);
+  p.BN = (p.variant == 4 || p.variant == 5) ? 256 : ((p.variant == 2 || p.variant == 3) ? 64 : 128);
   p.threads = p.variant == 4 ? 512 : 256;
   p.blocks_per_cu = p.variant == 4 ? 1 : 2;
   p.tiles = ((Co + p.BM - 1) / p.BM) * ((N + p.BN - 1) / p.BN);
@@ -416,6 +431,16 @@ KFA_API int kfa_conv_wgrad(const bf16_t* dY, const bf16_t* X, void* grad, int gr
   else if (p.variant == 3)
     hipLaunchKernelGGL((wgrad_kernel<2, 2, 2, 2>), grid, dim3(256), lds, s, dY, X, pp, grad, grad_f32, accumulate,
                        zero_page(), g);
+  else if (p.variant == 5) {
+    static bool attr = false;  // 80 KiB of dynamic LDS (2 blocks / CU)
+    if (!attr) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_kernel<1, 4, 4, 4>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      attr = true;
+    }
+    hipLaunchKernelGGL((wgrad_kernel<1, 4, 4, 4>), grid, dim3(256), lds, s, dY, X, pp, grad, grad_f32, accumulate,
+                       zero_page(), g);
+  }
   else {
     static bool attr = false;  // 128 KiB of dynamic LDS
     if (!attr) {

@@ -94,12 +94,18 @@ class Engine:
         else:
             raise ValueError(f"unknown optimizer {optimizer!r}")
         self.steps = 0
+        self._graph = None  # (hipGraph, captured inputs, captured loss) once capture() ran
 
     def zero_grad(self) -> None:
         for g in self.groups:
             g.zero_grad()
 
     def train_step(self, *batch) -> torch.Tensor:
+        if self._graph is not None:
+            return self._replay(batch)
+        return self._eager_step(*batch)
+
+    def _eager_step(self, *batch) -> torch.Tensor:
         self.zero_grad()
         loss = self.loss_fn(self.model, *batch)
         loss.backward()
@@ -110,6 +116,66 @@ class Engine:
             self.opt.step(grad_scale=self.sync.finish())
         self.steps += 1
         return loss.detach()
+
+    # ------------------------------------------------------------------ HIP graph replay
+    def graph_ok(self) -> Optional[str]:
+        """None if the whole step can be one HIP graph, else why not.
+
+        Every kernel argument is frozen at capture, so what changes per step
+        must live in device memory or not change at all: SGD's lr / momentum
+        / decay are constants, Adam's bias corrections are not (host scalars
+        per step).  Collectives stay eager (world > 1): RCCL work issued from
+        backward hooks is not replayed through this path.  The conv tuner and
+        every lazily-created workspace are settled by the eager warm-up steps
+        before capture."""
+        from ..ops.optim import FusedSGD
+        if self.info.device.type != "cuda":
+            return "not on a GPU"
+        if self.info.world > 1:
+            return "world > 1 (bucket collectives stay eager)"
+        if not isinstance(self.opt, FusedSGD):
+            return "optimizer has per-step host scalars (Adam bias correction)"
+        if self.opt.step_count == 0:
+            return "capture needs one eager step first (momentum init, lazy workspaces)"
+        return None
+
+    def capture(self, *batch) -> None:
+        """Record one whole training step — zero-grad, forward, loss, backward,
+        fused optimizer — as a HIP graph (``torch.cuda.CUDAGraph`` is
+        hipGraph on ROCm).  ``train_step`` then copies its batch into the
+        captured input buffers (skipped when it passes those same tensors) and
+        replays the graph: one launch per step instead of ~470 kernel launches
+        through Python, ctypes and autograd."""
+        why = self.graph_ok()
+        if why is not None:
+            raise RuntimeError(f"Engine.capture: {why}")
+        static = tuple(batch)
+        # warm-up on a side stream first (torch's capture recipe): autograd /
+        # allocator state of the capture stream settles before recording
+        side = torch.cuda.Stream(self.info.device)
+        side.wait_stream(torch.cuda.current_stream(self.info.device))
+        with torch.cuda.stream(side):
+            self._eager_step(*static)
+        torch.cuda.current_stream(self.info.device).wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            loss = self._eager_step(*static)
+        self.steps -= 1  # recorded, not executed: each replay counts its step
+        self.opt.step_count -= 1
+        self._graph = (g, static, loss)
+
+    def _replay(self, batch) -> torch.Tensor:
+        g, static, loss = self._graph
+        for s, b in zip(static, batch):
+            if isinstance(s, torch.Tensor) and b is not s:
+                s.copy_(b, non_blocking=True)
+        g.replay()
+        self.opt.step_count += 1
+        self.steps += 1
+        return loss
+
+    def release_graph(self) -> None:
+        self._graph = None
 
     def wait(self) -> None:
         """Make every rank's compute weights current (after an async pull)."""
@@ -161,11 +227,17 @@ def synchronize(info: DistInfo) -> None:
             torch.cuda.synchronize()
 
 
-def timed_steps(engine: Engine, batch, steps: int, warmup: int) -> Dict[str, float]:
+def timed_steps(engine: Engine, batch, steps: int, warmup: int, graph: bool = False) -> Dict[str, float]:
     """W untimed warmup steps, then EXACTLY ``steps`` timed steps bracketed by a
-    barrier + device sync on both sides; returns the MAX elapsed over ranks."""
+    barrier + device sync on both sides; returns the MAX elapsed over ranks.
+
+    ``graph``: after the warm-up, capture the step as a HIP graph
+    (``Engine.capture``) when ``Engine.graph_ok`` allows it, and time replays."""
     for _ in range(warmup):
         engine.train_step(*batch)
+    if graph and engine._graph is None and engine.graph_ok() is None:
+        synchronize(engine.info)
+        engine.capture(*batch)
     synchronize(engine.info)
     t0 = time.perf_counter()
     loss = None

@@ -113,7 +113,9 @@ def test_resnet_block_grads_igemm_vs_vendor():
     assert not bad, bad
 
 
-@pytest.mark.parametrize("rows,out_f,in_f", [(8192, 2304, 768), (4096, 768, 3072), (1000, 64, 136)])
+@pytest.mark.parametrize("rows,out_f,in_f", [(8192, 2304, 768), (4096, 768, 3072), (1000, 64, 136),
+                                             # 64x256 tiles (Co <= 64, N % 256 == 0), split-K, tail rows
+                                             (20000, 64, 256), (3001, 48, 512)])
 def test_wgrad_dense_shapes(rows, out_f, in_f):
     """dW = dYᵀ·X through the wgrad kernel as a 1x1 conv over `rows` pixels."""
     from kubeflow_controller_amd.ops.conv import wgrad_into
@@ -130,6 +132,34 @@ def test_wgrad_dense_shapes(rows, out_f, in_f):
     wgrad_into(x, dy, outb, 1, 1, rows, in_f, 1, rows, out_f, 1, 1, 1, 0, accumulate=False)
     err = (outb.float() - ref).abs().max().item()
     assert err < 2e-2 * ref.abs().max().item(), err
+
+
+@pytest.mark.parametrize("wide", ["1", "0"])
+def test_wgrad_co64_gathered_taps(wide, monkeypatch):
+    """Co = 64 weight gradients (1x1, gathered 3x3 / strided taps; N = R*S*Ci a
+    multiple of 256) on the 64x256 tile and on the 64x128 one, both vs fp32.
+    Own process per setting: the tile choice is read once from the env."""
+    import subprocess, sys, os
+    code = (
+        "import torch, torch.nn.functional as F\n"
+        "from kubeflow_controller_amd.ops.conv import wgrad_into\n"
+        "torch.manual_seed(0); d = torch.device('cuda')\n"
+        "for (N, Ci, H, k, s, p) in [(4, 256, 14, 1, 1, 0), (3, 256, 13, 3, 2, 1), (2, 512, 9, 3, 1, 1)]:\n"
+        "    x = torch.randn(N, Ci, H, H, device=d).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)\n"
+        "    w = torch.randn(64, Ci, k, k, device=d)\n"
+        "    y = F.conv2d(x.float(), w, None, s, p)\n"
+        "    dy = torch.randn_like(y).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)\n"
+        "    ref = torch.ops.aten.convolution_backward(dy.float(), x.float(), w, None, [s, s], [p, p], [1, 1], False, [0, 0], 1, [False, True, False])[1]\n"
+        "    P, Q = y.shape[2], y.shape[3]\n"
+        "    out = torch.zeros(64, k, k, Ci, device=d)\n"
+        "    wgrad_into(x, dy, out, N, H, H, Ci, P, Q, 64, k, k, s, p, accumulate=False)\n"
+        "    err = (out.permute(0, 3, 1, 2) - ref).abs().max().item()\n"
+        "    assert err < 1e-2 * ref.abs().max().item(), (N, Ci, H, k, s, err)\n"
+        "print('ok')\n")
+    env = dict(os.environ, KFA_WGRAD_WIDE64=wide)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-3000:]
 
 
 @pytest.mark.parametrize("vendor", [False, True])

@@ -23,6 +23,10 @@ if [[ $what == bench || $what == all ]]; then
   KFA_CONV_TUNE_LOG=1 timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 \
     > gpurun_out/bench1.log 2> gpurun_out/bench1.err || { tail -30 gpurun_out/bench1.err; exit 1; }
   tail -1 gpurun_out/bench1.log
+  step "bench 1 GPU, whole step as one HIP graph"
+  timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --graph on \
+    > gpurun_out/bench1_graph.log 2> gpurun_out/bench1_graph.err || { tail -30 gpurun_out/bench1_graph.err; exit 1; }
+  tail -1 gpurun_out/bench1_graph.log
   step "bench --gpus 2 (gloo rehearsal on one GPU)"
   KFA_DIST_BACKEND=gloo timeout -k 10 300 python -u bench.py --gpus 2 --steps 3 --warmup 1 --batch 64 \
     > gpurun_out/bench2_gloo.log 2> gpurun_out/bench2_gloo.err || { tail -30 gpurun_out/bench2_gloo.err; exit 1; }
