@@ -658,7 +658,7 @@ KFA_API int kfa_conv_igemm(const bf16_t* T, const bf16_t* B, bf16_t* D, const bf
   } else if (variant == 2) {  // 256 x 256 tile: 2x4 waves of 128x64, one block per CU (128 KiB LDS)
     const long tiles = (long)kfa_ceil_div(g.M, 256) * kfa_ceil_div(N, 256);
     const int grid = (int)(tiles < cus ? tiles : cus);
-    launch_igemm<2, 4, 8, 4>(kEpiAll, dim3(grid), dim3(512), 2 * (256 + 256) * BK * 2, st, T, B, D, E, stats, bnb, g);
+    launch_igemm<2, 4, 8, 4>(epi, dim3(grid), dim3(512), 2 * (256 + 256) * BK * 2, st, T, B, D, E, stats, bnb, g);
   } else {  // 128 x 128 tile: 2x2 waves of 64x64
     const int grid = pgrid((long)kfa_ceil_div(g.M, 128) * kfa_ceil_div(N, 128));
     launch_igemm<2, 2, 4, 4>(epi, dim3(grid), dim3(256), 2 * (128 + 128) * BK * 2, st, T, B, D, E, stats, bnb, g);

@@ -133,11 +133,21 @@ def _use_vendor_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, sta
 NARROW = int(os.environ.get("KFA_CONV_NARROW", "1"))  # tile variant for N <= 64: 1 = 128x64, 3 = 256x64
 
 
+# 256x256 tiles where they win per shape (tools/bench_conv_tiles.py, bs 256): the
+# memory-bound short reductions over many pixels (K <= 128, M >= 200704: the 56x56
+# 64->256 expand forward, the 256->64 / 256->128 data gradients) — one block per CU
+# streaming a 256-wide output tile keeps more of the epilogue's stores in flight
+# (0.176 -> 0.163 ms, 0.283 -> 0.236 ms); every compute-bound shape loses there.
+BIG_AUTO = os.environ.get("KFA_CONV_BIG_AUTO", "1") != "0"
+
+
 def _variant(M: int, N: int, K: int = 0) -> int:
     """Tile shape of one implicit-GEMM launch: M output pixels x N channels, reduction K."""
     if N <= 64:
         return NARROW
     if BIG and N % 256 == 0 and K >= BIG_MIN_K:
+        return 2
+    if BIG_AUTO and N % 256 == 0 and 0 < K <= 128 and M >= 200704:
         return 2
     return 0
 

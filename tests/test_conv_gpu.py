@@ -106,10 +106,13 @@ def test_resnet_block_grads_igemm_vs_vendor():
         r = r.to(f.device).float()
         if r.dim() == 4:
             r = r.contiguous(memory_format=torch.channels_last)
-        scale = max(1e-4, r.abs().max().item())
-        e_f, e_u, e_v = ((t - r).abs().max().item() for t in (f, u, v))
-        if e_f > 2.0 * e_v + 0.02 * scale or e_u > 2.0 * e_v + 0.02 * scale:
-            bad.append((n, e_f, e_u, e_v, scale))
+        # relative Frobenius error: the max-abs error of a tiny, rounding-dominated
+        # gradient (e.g. the last stage's conv3 weight at 4x4 pixels) varies run to
+        # run with the order of the BN-statistics atomics
+        rn = max(1e-12, r.norm().item())
+        e_f, e_u, e_v = ((t.float() - r).norm().item() / rn for t in (f, u, v))
+        if e_f > 1.5 * e_v + 0.01 or e_u > 1.5 * e_v + 0.01:
+            bad.append((n, e_f, e_u, e_v))
     assert not bad, bad
 
 
