@@ -70,7 +70,12 @@ template <bool GBF16>
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ w, bf16_t* __restrict__ wb,
                                                    const void* __restrict__ g, float* __restrict__ m_,
                                                    float* __restrict__ v_, long n8, float lr, float b1, float b2,
-                                                   float eps, float wd, float bc1, float bc2, float gscale) {
+                                                   float eps, float wd, float bc1, float bc2, float gscale,
+                                                   const float* __restrict__ dbc) {
+  if (dbc) {  // bias corrections produced on the device (adam_bc_kernel): replayable in a HIP graph
+    bc1 = dbc[0];
+    bc2 = dbc[1];
+  }
   const float step = lr / bc1;
   const float rbc2 = rsqrtf(bc2);
   for (long v = (long)blockIdx.x * blockDim.x + threadIdx.x; v < n8; v += (long)gridDim.x * blockDim.x) {
@@ -91,6 +96,17 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ w, bf16_t
     store8(v_ + i, s);
     store8(w + i, p);
     if (wb) *reinterpret_cast<uint4*>(wb + i) = pack8(p);
+  }
+}
+
+// t += 1; bc = (1 - b1^t, 1 - b2^t): the per-step scalars of Adam kept on the
+// device, so a captured step needs no host value that changes per step
+__global__ void adam_bc_kernel(int* __restrict__ t, float* __restrict__ bc, float b1, float b2) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    const int s = t[0] + 1;
+    t[0] = s;
+    bc[0] = 1.f - powf(b1, (float)s);
+    bc[1] = 1.f - powf(b2, (float)s);
   }
 }
 
@@ -142,16 +158,23 @@ KFA_API int kfa_sgd_step(float* w, bf16_t* wb, const void* g, int g_is_bf16, flo
   return kfa_status();
 }
 
+// dbc: nullptr (bc1 / bc2 as given) or the device pair written by kfa_adam_bc
 KFA_API int kfa_adam_step(float* w, bf16_t* wb, const void* g, int g_is_bf16, float* m, float* v, long n, float lr,
-                          float b1, float b2, float eps, float wd, float bc1, float bc2, float gscale, hipStream_t s) {
+                          float b1, float b2, float eps, float wd, float bc1, float bc2, float gscale, const float* dbc,
+                          hipStream_t s) {
   if (n % 8) return -1;
   const long n8 = n / 8;
   if (g_is_bf16)
     hipLaunchKernelGGL(adam_kernel<true>, dim3(grid_for(n8)), dim3(256), 0, s, w, wb, g, m, v, n8, lr, b1, b2, eps,
-                       wd, bc1, bc2, gscale);
+                       wd, bc1, bc2, gscale, dbc);
   else
     hipLaunchKernelGGL(adam_kernel<false>, dim3(grid_for(n8)), dim3(256), 0, s, w, wb, g, m, v, n8, lr, b1, b2, eps,
-                       wd, bc1, bc2, gscale);
+                       wd, bc1, bc2, gscale, dbc);
+  return kfa_status();
+}
+
+KFA_API int kfa_adam_bc(int* t, float* bc, float b1, float b2, hipStream_t s) {
+  hipLaunchKernelGGL(adam_bc_kernel, dim3(1), dim3(64), 0, s, t, bc, b1, b2);
   return kfa_status();
 }
 

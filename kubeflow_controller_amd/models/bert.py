@@ -118,6 +118,12 @@ class BertForPreTraining(nn.Module):
         self._step = 0
         self._pos_cache = {}
 
+    @property
+    def graph_capturable(self) -> bool:
+        """Dropout masks come from per-step host seeds: a replayed HIP graph would
+        repeat one step's masks (``Engine.graph_ok``)."""
+        return not (self.training and (self.cfg.hidden_dropout > 0 or self.cfg.attn_dropout > 0))
+
     # ------------------------------------------------------------------ helpers
     def _pos_ids(self, B, S, device):
         key = (B, S, str(device))

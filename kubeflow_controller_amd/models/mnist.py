@@ -58,10 +58,17 @@ class SyntheticMNIST:
         x = (self.protos[y] + self.noise * torch.randn(n, 784, generator=g)).clamp_(0, 1)
         return x, y
 
+    def to(self, device) -> "SyntheticMNIST":
+        """Keep the splits resident on ``device`` (no host copy per step)."""
+        self.train = tuple(t.to(device) for t in self.train)
+        self.validation = tuple(t.to(device) for t in self.validation)
+        self.test = tuple(t.to(device) for t in self.test)
+        return self
+
     def next_batch(self, batch_size: int):
         x, y = self.train
         if self._pos + batch_size > x.shape[0]:
-            perm = torch.randperm(x.shape[0], generator=self._g)
+            perm = torch.randperm(x.shape[0], generator=self._g).to(x.device)
             self.train = (x[perm], y[perm])
             x, y = self.train
             self._pos = 0

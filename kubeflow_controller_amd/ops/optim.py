@@ -20,7 +20,8 @@ from ..parallel.flat import FlatGroup
 
 P, L, I, F = _lib.P, _lib.L, _lib.I, _lib.F
 _lib.register("kfa_sgd_step", [P, P, P, I, P, L, F, F, F, F, I, F, I, P])
-_lib.register("kfa_adam_step", [P, P, P, I, P, P, L, F, F, F, F, F, F, F, F, P])
+_lib.register("kfa_adam_step", [P, P, P, I, P, P, L, F, F, F, F, F, F, F, F, P, P])
+_lib.register("kfa_adam_bc", [P, P, F, F, P])
 _lib.register("kfa_f32_to_bf16", [P, P, L, P])
 _lib.register("kfa_sumsq", [P, I, L, P, P])
 
@@ -136,10 +137,19 @@ class FusedAdam(_FusedBase):
         self.eps = eps
         self.m = [torch.zeros(s.numel, dtype=torch.float32, device=s.device) for s in self.spaces]
         self.v = [torch.zeros(s.numel, dtype=torch.float32, device=s.device) for s in self.spaces]
+        # GPU: the step count t and (1 - b1^t, 1 - b2^t) live on the device, advanced
+        # by kfa_adam_bc inside the step, so the step replays from a HIP graph
+        dev = self.spaces[0].device if self.spaces else torch.device("cpu")
+        self._t = torch.zeros(1, dtype=torch.int32, device=dev) if dev.type == "cuda" else None
+        self._bc = torch.ones(2, dtype=torch.float32, device=dev) if dev.type == "cuda" else None
 
     @torch.no_grad()
     def step(self, grad_scale: float = 1.0, lr: Optional[float] = None) -> None:
         lr = self.lr if lr is None else lr
+        if self._t is not None:
+            if not torch.cuda.is_current_stream_capturing():
+                self._t.fill_(self.step_count)  # eager steps (and resumes) re-seed the device count
+            _lib.call("kfa_adam_bc", _lib.ptr(self._t), _lib.ptr(self._bc), self.b1, self.b2, _lib.stream())
         self.step_count += 1
         t = self.step_count
         bc1 = 1.0 - self.b1 ** t
@@ -162,4 +172,4 @@ class FusedAdam(_FusedBase):
                 continue
             _lib.call("kfa_adam_step", _lib.ptr(w), _lib.ptr(wb), _lib.ptr(gr), int(gr.dtype == torch.bfloat16),
                       _lib.ptr(m), _lib.ptr(v), n, lr, self.b1, self.b2, self.eps, wd, bc1, bc2, grad_scale,
-                      _lib.stream())
+                      _lib.ptr(self._bc), _lib.stream())

@@ -234,7 +234,7 @@ class DeviceAsyncPSServer:
         bc1, bc2 = 1.0 - b1 ** self.t, 1.0 - b2 ** self.t
         # TF AdamOptimizer form (eps outside the bias-corrected sqrt) with the fused HIP kernel
         _lib.call("kfa_adam_step", _lib.ptr(self.w), None, _lib.ptr(g), 0, _lib.ptr(self.m), _lib.ptr(self.v), n,
-                  self.lr, b1, b2, self.eps / math.sqrt(bc2), 0.0, bc1, bc2, 1.0, _lib.stream())
+                  self.lr, b1, b2, self.eps / math.sqrt(bc2), 0.0, bc1, bc2, 1.0, None, _lib.stream())
 
     def serve(self, log=None) -> int:
         active = self.W

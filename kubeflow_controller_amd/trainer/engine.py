@@ -122,24 +122,25 @@ class Engine:
         """None if the whole step can be one HIP graph, else why not.
 
         Every kernel argument is frozen at capture, so what changes per step
-        must live in device memory or not change at all: SGD's lr / momentum
-        / decay are constants, Adam's bias corrections are not (host scalars
-        per step).  Collectives stay eager (world > 1): RCCL work issued from
-        backward hooks is not replayed through this path.  The conv tuner and
-        every lazily-created workspace are settled by the eager warm-up steps
-        before capture."""
-        from ..ops.optim import FusedSGD
+        must live in device memory or not change at all: lr / momentum /
+        decay are constants, Adam's step count and bias corrections are
+        advanced on the device (``kfa_adam_bc``).  A model whose forward takes
+        per-step host values (dropout seeds) says so with
+        ``graph_capturable = False``.  Collectives stay eager (world > 1): RCCL
+        work issued from backward hooks is not replayed through this path.
+        The conv tuner and every lazily-created workspace are settled by the
+        eager warm-up steps before capture."""
         if self.info.device.type != "cuda":
             return "not on a GPU"
         if self.info.world > 1:
             return "world > 1 (bucket collectives stay eager)"
-        if not isinstance(self.opt, FusedSGD):
-            return "optimizer has per-step host scalars (Adam bias correction)"
+        if not getattr(self.model, "graph_capturable", True):
+            return "the model's forward takes per-step host values (e.g. dropout seeds)"
         if self.opt.step_count == 0:
             return "capture needs one eager step first (momentum init, lazy workspaces)"
         return None
 
-    def capture(self, *batch) -> None:
+    def capture(self, *batch) -> torch.Tensor:
         """Record one whole training step — zero-grad, forward, loss, backward,
         fused optimizer — as a HIP graph (``torch.cuda.CUDAGraph`` is
         hipGraph on ROCm).  ``train_step`` then copies its batch into the
@@ -151,11 +152,12 @@ class Engine:
             raise RuntimeError(f"Engine.capture: {why}")
         static = tuple(batch)
         # warm-up on a side stream first (torch's capture recipe): autograd /
-        # allocator state of the capture stream settles before recording
+        # allocator state of the capture stream settles before recording.  It is
+        # a real training step on `batch`; its loss is returned.
         side = torch.cuda.Stream(self.info.device)
         side.wait_stream(torch.cuda.current_stream(self.info.device))
         with torch.cuda.stream(side):
-            self._eager_step(*static)
+            warm_loss = self._eager_step(*static)
         torch.cuda.current_stream(self.info.device).wait_stream(side)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
@@ -163,6 +165,7 @@ class Engine:
         self.steps -= 1  # recorded, not executed: each replay counts its step
         self.opt.step_count -= 1
         self._graph = (g, static, loss)
+        return warm_loss
 
     def _replay(self, batch) -> torch.Tensor:
         g, static, loss = self._graph

@@ -349,13 +349,23 @@ def run_worker(spec: ClusterSpec, args) -> int:
         if spec.is_chief:
             checkpoint.write_manifest(args.model_dir, global_step, world)
 
+    # HIP graph replay of the whole step (Engine.capture) for single-replica GPU
+    # jobs: the reference's MNIST steps are a few tiny kernels each, so launch
+    # overhead is the step time; the batch is copied into the captured inputs.
+    use_graph = args.graph == "on" or (args.graph == "auto" and world == 1)
+    if data is not None and device.type == "cuda" and hasattr(data, "to"):
+        data.to(device)  # dataset resident in HBM: no host copy per step
     for local_step in range(steps_per_worker):
         if data is not None:
             xb, yb = data.next_batch(args.batch_size)
             batch = (xb.to(device), yb.to(device))
         else:
             batch = fixed
-        loss = engine.train_step(*batch)
+        if use_graph and local_step == 1 and engine.graph_ok() is None:
+            loss = engine.capture(*(b.clone() for b in batch))  # its warm-up step trains on this batch
+            _log(f"Worker {rank}: step captured as a HIP graph; replaying it from step 2 on")
+        else:
+            loss = engine.train_step(*batch)
         global_step += inc
         if store is not None and spec.is_chief:
             store.add(STEP_KEY, inc)
@@ -437,6 +447,8 @@ def build_parser() -> argparse.ArgumentParser:
                     help="Wide&Deep table rows: interleaved over all workers, or only the PS-co-located ranks")
     ap.add_argument("--grad_reduce", default="fp32", choices=["fp32", "bf16"],
                     help="dtype of the cross-rank gradient sum")
+    ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
+                    help="replay the training step as one HIP graph after step 1 (auto: single-replica GPU jobs)")
     ap.add_argument("--log_every", type=int, default=1)
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--ps_connect_timeout", type=float, default=300.0)
