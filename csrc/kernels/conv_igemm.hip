@@ -26,6 +26,8 @@
 // per k-tile) and XOR-swizzled (chunk ^= (row>>1)&7) so the 16-lane groups of
 // each ds_read_b128 hit 16 distinct 16-B slots.  Operand roles are chosen so
 // each lane's 4 accumulator rows are 4 CONSECUTIVE output channels (8-B stores).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -644,7 +646,17 @@ KFA_API int kfa_conv_igemm(const bf16_t* T, const bf16_t* B, bf16_t* D, const bf
     }
     cus = cached;
   }
-  const int slots = 2 * cus;  // 2 resident blocks per CU (64 KB LDS, <=256 VGPR/2 waves)
+  // persistent grid: 2 resident blocks per CU (64 KB LDS, <=256 VGPR/2 waves).
+  // KFA_CONV_OVERSUB=k caps the grid at k x that (0: one block per tile), so the
+  // dispatcher, not the tile ranges, balances the work when other kernels (RCCL)
+  // hold part of the CUs.
+  static int oversub = -1;
+  if (oversub < 0) {
+    const char* e = getenv("KFA_CONV_OVERSUB");
+    oversub = e ? atoi(e) : 1;
+    if (oversub < 0) oversub = 1;
+  }
+  const long slots = oversub == 0 ? (1L << 30) : 2L * cus * oversub;
   auto pgrid = [&](long tiles) { return (int)(tiles < slots ? tiles : slots); };
   const unsigned epi = (E ? kEpiE : 0u) | (stats ? kEpiStats : 0u) | (bn_x ? kEpiBnBwd : 0u) |
                        ((E && add_mb) ? kEpiEmb : 0u) | ((bn_x && bn_y && bn_relu) ? kEpiYMask : 0u);

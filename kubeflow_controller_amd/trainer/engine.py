@@ -39,6 +39,12 @@ def init_distributed(backend: Optional[str] = None, prefer_gpu: bool = True) -> 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        # RCCL's collectives run concurrently with backward and hold part of the CUs:
+        # conv grids of 2x the resident slots let the dispatcher balance around them
+        # (a persistent grid waits on its slowest CU).  Costs 0.15 % on one GPU
+        # (11,345 -> 11,336 img/s, same box); KFA_CONV_OVERSUB=1 restores persistent.
+        os.environ.setdefault("KFA_CONV_OVERSUB", "2")
     use_gpu = prefer_gpu and torch.cuda.is_available()
     if use_gpu:
         torch.cuda.set_device(local % torch.cuda.device_count())

@@ -79,3 +79,43 @@ for (Cin, H, Cout, k, s, p, cnt) in SH:
         row += f" | dgrad+bnstats 128x128 {g0:.3f} ({flops / g0 / 1e9:.0f} TF) 256x256 {g2:.3f} ({flops / g2 / 1e9:.0f} TF)"
     print(row, flush=True)
 print("TOTAL (x count, best-of per shape) ms:", {k: round(v, 3) for k, v in tot.items()})
+
+# N <= 64 launches: 128x64 (4 waves of 32x64, 3 blocks/CU) vs 256x64 (4 waves of 64x64, 2 blocks/CU)
+def with_narrow(v, fn):
+    orig = conv.NARROW
+    conv.NARROW = v
+    try:
+        return t(fn)
+    finally:
+        conv.NARROW = orig
+
+
+nt = {"n1": 0.0, "n3": 0.0, "best": 0.0}
+for (Cin, H, Cout, k, s, p, cnt) in SH:
+    x = torch.randn(B, Cin, H, H, device=d, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(Cout, Cin, k, k, device=d) * 0.05).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y = conv.conv_fwd(x, w, s, p)
+    dy = torch.randn_like(y)
+    row = f"Cin{Cin:5d} H{H:3d} Cout{Cout:5d} k{k} s{s} x{cnt}:"
+    if Cout <= 64:
+        st = bn_slot_workspace(Cout, d)
+        a = with_narrow(1, lambda: conv.conv_fwd(x, w, s, p, st))
+        b = with_narrow(3, lambda: conv.conv_fwd(x, w, s, p, st))
+        st.zero_()
+        nt["n1"] += a * cnt
+        nt["n3"] += b * cnt
+        nt["best"] += min(a, b) * cnt
+        row += f" fwd+stats K={Cin * k * k}: 128x64 {a:.3f} 256x64 {b:.3f}"
+    if Cin <= 64:
+        link = Link(x, Cin)
+        st = bn_slot_workspace(Cin, d)
+        a = with_narrow(1, lambda: conv.conv_dgrad(dy, w, x.shape, s, p, bn=link))
+        b = with_narrow(3, lambda: conv.conv_dgrad(dy, w, x.shape, s, p, bn=link))
+        st.zero_()
+        nt["n1"] += a * cnt
+        nt["n3"] += b * cnt
+        nt["best"] += min(a, b) * cnt
+        row += f" | dgrad+bnstats K={Cout * k * k}: 128x64 {a:.3f} 256x64 {b:.3f}"
+    if Cout <= 64 or Cin <= 64:
+        print(row, flush=True)
+print("NARROW TOTAL (x count) ms:", {k: round(v, 3) for k, v in nt.items()})
