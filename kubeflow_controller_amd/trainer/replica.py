@@ -303,6 +303,8 @@ def run_worker(spec: ClusterSpec, args) -> int:
     rank = 0 if spec.is_local else spec.task_index
     store = None
     if not spec.is_local:
+        if world > 1:
+            os.environ.setdefault("KFA_CONV_OVERSUB", "2")  # see engine.init_distributed
         store = _store(spec, spec.is_chief)
         backend = os.environ.get("KFA_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
         dist.init_process_group(backend, store=store, rank=rank, world_size=world,
