@@ -42,6 +42,18 @@ Geom geom(long M, int C, int max_blocks) {
 }
 
 __device__ __forceinline__ uint4 ld16(const bf16_t* p) { return *reinterpret_cast<const uint4*>(p); }
+#ifndef KFA_BN_NT
+#define KFA_BN_NT 0
+#endif
+// activation-sized outputs (y, dx, dres)
+__device__ __forceinline__ void st16(bf16_t* p, uint4 v) {
+#if KFA_BN_NT
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  __builtin_nontemporal_store(*reinterpret_cast<u32x4*>(&v), reinterpret_cast<u32x4*>(p));
+#else
+  *reinterpret_cast<uint4*>(p) = v;
+#endif
+}
 
 // ------------------------------------------------------------------ forward stats
 // block sums -> slot accumulators [kSlots][2][C] (shifted sum, shifted sum of squares)
@@ -243,7 +255,7 @@ __global__ __launch_bounds__(NT) void bn_apply(const bf16_t* __restrict__ x, con
         f[j] = RELU ? fmaxf(z, 0.f) : z;
       }
       const uint4 out = pack8(f);
-      *reinterpret_cast<uint4*>(y + o) = out;
+      st16(y + o, out);
       if (MB) mb[o >> 3] = (uint8_t)pos_bits(out);
     };
     long r = rb + r0;
@@ -450,8 +462,8 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply(const bf16_t* __restrict__ dy
       masked_dy<MASK>(dv, yv, xf, sc, sf, bits, dz);
 #pragma unroll
       for (int j = 0; j < 8; j++) out[j] = fmaf(ca[j], dz[j], fmaf(cb[j], xf[j], ck[j]));
-      *reinterpret_cast<uint4*>(dx + o) = pack8(out);
-      if (DRES) *reinterpret_cast<uint4*>(dres + o) = pack8(dz);
+      st16(dx + o, pack8(out));
+      if (DRES) st16(dres + o, pack8(dz));
     }
   }
 }
@@ -505,7 +517,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_rstats(const bf16_t* __restri
           s1[j] += dz[j];
           s2[j] += dz[j] * (rf[j] - mu[j]);
         }
-        *reinterpret_cast<uint4*>(dx + o) = pack8(out);
+        st16(dx + o, pack8(out));
       }
     }
     if (active) {

@@ -32,6 +32,10 @@
 
 namespace {
 
+#ifndef KFA_CONV_STORE_AUX
+#define KFA_CONV_STORE_AUX 2  // output stores non-temporal (streamed; +1.7 % ResNet-50 vs 0, docs/kernels.md)
+#endif
+
 constexpr int BK = 64;
 constexpr int kBnSlots = 64;  // must match batchnorm.hip kSlots (fused statistics land in its slots)
 
@@ -79,6 +83,14 @@ __device__ __forceinline__ uint4 bload16(__amdgpu_buffer_rsrc_t r, unsigned off)
 // kernels' launch stubs.
 __device__ __forceinline__ void buf_dma16(__amdgpu_buffer_rsrc_t r, bf16_t* lds, int voff, int soff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
+}
+#ifndef KFA_CONV_LOAD_AUX
+#define KFA_CONV_LOAD_AUX 0
+#endif
+// the gathered activation operand (each element used by one tile column only)
+__device__ __forceinline__ void buf_dma16_act(__amdgpu_buffer_rsrc_t r, bf16_t* lds, int voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0,
+                                           KFA_CONV_LOAD_AUX);
 }
 
 // x / d for 0 <= x < 2^24 via an fp32 reciprocal + one correction step
@@ -223,14 +235,14 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
     if (lin_a) {  // the whole offset but the slice's is fixed per tile (a_vo, setup)
 #pragma unroll
       for (int i = 0; i < AR; i++)
-        buf_dma16(rT, As + buf * BM * BK + (i * RPP + wave * 8) * BK, a_vo[i], k0 * 2);
+        buf_dma16_act(rT, As + buf * BM * BK + (i * RPP + wave * 8) * BK, a_vo[i], k0 * 2);
     } else {
 #pragma unroll
       for (int i = 0; i < AR; i++) {
         const int ih = a_hb[i] + dh, iw = a_wb[i] + dw;
         const bool ok = (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
         const int vo = ok ? a_vo[i] + (ih * g.W + iw) * g.C * 2 : (int)kOOB;
-        buf_dma16(rT, As + buf * BM * BK + (i * RPP + wave * 8) * BK, vo, c0 * 2);
+        buf_dma16_act(rT, As + buf * BM * BK + (i * RPP + wave * 8) * BK, vo, c0 * 2);
       }
     }
 #pragma unroll
@@ -403,7 +415,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
           }
           o = pack8(f);
         }
-        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<decltype(__builtin_amdgcn_raw_buffer_load_b128(rD, 0, 0, 0))*>(&o), rD, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<decltype(__builtin_amdgcn_raw_buffer_load_b128(rD, 0, 0, 0))*>(&o), rD, off, 0, KFA_CONV_STORE_AUX);
         if (kST && stats && off != kOOB) {  // wave-uniform pointer test; per-lane row mask
           float f[8];
           unpack8(o, f);  // the bf16-rounded values the BatchNorm will see
