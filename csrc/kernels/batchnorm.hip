@@ -41,7 +41,22 @@ Geom geom(long M, int C, int max_blocks) {
   return g;
 }
 
-__device__ __forceinline__ uint4 ld16(const bf16_t* p) { return *reinterpret_cast<const uint4*>(p); }
+// Activation-sized inputs are read once per pass: non-temporal loads keep them from
+// displacing the tensors the next kernels re-read from L2 / the Infinity Cache
+// (ResNet-50 +1.9 %, docs/kernels.md).  Outputs stay write-back (the next conv
+// reads them right away: non-temporal stores there measured -1..-2.5 %).
+#ifndef KFA_BN_LD_NT
+#define KFA_BN_LD_NT 1
+#endif
+__device__ __forceinline__ uint4 ld16(const bf16_t* p) {
+#if KFA_BN_LD_NT
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+  return make_uint4(v[0], v[1], v[2], v[3]);
+#else
+  return *reinterpret_cast<const uint4*>(p);
+#endif
+}
 #ifndef KFA_BN_NT
 #define KFA_BN_NT 0
 #endif

@@ -72,8 +72,11 @@ constexpr unsigned kOOB = 0x80000000u;
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
 }
+#ifndef KFA_CONV_EPI_LOAD_AUX
+#define KFA_CONV_EPI_LOAD_AUX 2  // epilogue addend / BN-input loads non-temporal (read once; +0.2 %)
+#endif
 __device__ __forceinline__ uint4 bload16(__amdgpu_buffer_rsrc_t r, unsigned off) {
-  auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+  auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, KFA_CONV_EPI_LOAD_AUX);
   return *reinterpret_cast<uint4*>(&v);
 }
 
