@@ -51,8 +51,15 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t wrsrc(const void* p, unsigned 
 }
 // 16 B per lane buffer -> LDS DMA; a plain device function (the builtin inside the
 // templated kernel's lambda stops clang's host pass from emitting launch stubs)
+#ifndef KFA_WG_DY_AUX
+#define KFA_WG_DY_AUX 0
+#endif
+#ifndef KFA_WG_X_AUX
+#define KFA_WG_X_AUX 0
+#endif
+template <int AUX = 0>
 __device__ __forceinline__ void buf_dma16(__amdgpu_buffer_rsrc_t r, bf16_t* lds, int voff, int soff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, AUX);
 }
 
 typedef short v4i16 __attribute__((ext_vector_type(4)));
@@ -189,10 +196,10 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_kernel(const bf16_t* __
   auto issue = [&](int step, int buf) {
     const int k0 = kb + step * BKW;
 #pragma unroll
-    for (int i = 0; i < A_IPW; i++) buf_dma16(rA, As + buf * BKW * BM + a_lds[i], a_vo[i], k0 * g.Co * 2);
+    for (int i = 0; i < A_IPW; i++) buf_dma16<KFA_WG_DY_AUX>(rA, As + buf * BKW * BM + a_lds[i], a_vo[i], k0 * g.Co * 2);
     if (lin_b) {
 #pragma unroll
-      for (int i = 0; i < B_IPW; i++) buf_dma16(rX, Bs + buf * BKW * BN + b_lds[i], b_vo[i], k0 * g.Ci * 2);
+      for (int i = 0; i < B_IPW; i++) buf_dma16<KFA_WG_X_AUX>(rX, Bs + buf * BKW * BN + b_lds[i], b_vo[i], k0 * g.Ci * 2);
       return;
     }
 #pragma unroll
@@ -215,7 +222,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_kernel(const bf16_t* __
         if ((unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W)
           vo = ((((img * g.H + h) * g.W) + w) * g.Ci + b_ci[i]) * 2;
       }
-      buf_dma16(rX, Bs + buf * BKW * BN + b_lds[i], vo, 0);
+      buf_dma16<KFA_WG_X_AUX>(rX, Bs + buf * BKW * BN + b_lds[i], vo, 0);
       if constexpr (INC) {  // advance this row's pixel by BKW (issue() runs once per step, in order)
         int q = b_q[i] + dq, p = b_p[i] + dp, img = b_img[i] + dimg;
         if (q >= g.Q) { q -= g.Q; p++; }
@@ -300,6 +307,17 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_kernel(const bf16_t* __
 // x 4 split-lanes; each thread keeps 8 independent loads in flight (the split
 // count reaches hundreds for the early, pixel-heavy layers), then an LDS
 // reduce over the split-lanes.
+#ifndef KFA_WG_PART_NT
+#define KFA_WG_PART_NT 1  // +0.15 % ResNet-50 (docs/kernels.md)
+#endif
+__device__ __forceinline__ floatx4 ldpart(const float* p) {  // split-K partials: read exactly once
+#if KFA_WG_PART_NT
+  return __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(p));
+#else
+  return *reinterpret_cast<const floatx4*>(p);
+#endif
+}
+
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int splits, long total,
                                                            void* __restrict__ grad, int grad_f32, int accumulate) {
   __shared__ floatx4 red[4][64];
@@ -311,11 +329,11 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
     for (; k + 28 < splits; k += 32) {
       floatx4 v[8];
 #pragma unroll
-      for (int u = 0; u < 8; u++) v[u] = *reinterpret_cast<const floatx4*>(part + (long)(k + 4 * u) * total + i * 4);
+      for (int u = 0; u < 8; u++) v[u] = ldpart(part + (long)(k + 4 * u) * total + i * 4);
 #pragma unroll
       for (int u = 0; u < 8; u++) s += v[u];
     }
-    for (; k < splits; k += 4) s += *reinterpret_cast<const floatx4*>(part + (long)k * total + i * 4);
+    for (; k < splits; k += 4) s += ldpart(part + (long)k * total + i * 4);
   }
   red[sl][el] = s;
   __syncthreads();
