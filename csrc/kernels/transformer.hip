@@ -41,7 +41,19 @@ __device__ __forceinline__ bool keep(uint64_t seed, uint64_t i, uint32_t thresh)
   return drop_hash(seed, i) >= thresh;
 }
 
-__device__ __forceinline__ void load8(const bf16_t* p, float f[8]) { unpack8(*reinterpret_cast<const uint4*>(p), f); }
+#ifndef KFA_TF_LD_NT
+#define KFA_TF_LD_NT 1  // BERT-base +0.8 % (docs/kernels.md)
+#endif
+__device__ __forceinline__ uint4 ld16(const bf16_t* p) {  // activation-sized inputs, read once per pass
+#if KFA_TF_LD_NT
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+  return make_uint4(v[0], v[1], v[2], v[3]);
+#else
+  return *reinterpret_cast<const uint4*>(p);
+#endif
+}
+__device__ __forceinline__ void load8(const bf16_t* p, float f[8]) { unpack8(ld16(p), f); }
 __device__ __forceinline__ void store8(bf16_t* p, const float f[8]) { *reinterpret_cast<uint4*>(p) = pack8(f); }
 __device__ __forceinline__ void load8f(const float* p, float f[8]) {
   const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
@@ -150,8 +162,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
     for (int j = 0; j < NV; j++) {
       const int c = (j * 64 + lane) * 8;
       if (c < H && row < r1) {
-        nd[j] = *reinterpret_cast<const uint4*>(dy + row * (long)H + c);
-        nx[j] = *reinterpret_cast<const uint4*>(xs + row * (long)H + c);
+        nd[j] = ld16(dy + row * (long)H + c);
+        nx[j] = ld16(xs + row * (long)H + c);
       }
     }
   };
