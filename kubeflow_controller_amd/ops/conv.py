@@ -139,15 +139,16 @@ NARROW = int(os.environ.get("KFA_CONV_NARROW", "1"))  # tile variant for N <= 64
 # streaming a 256-wide output tile keeps more of the epilogue's stores in flight
 # (0.176 -> 0.163 ms, 0.283 -> 0.236 ms); every compute-bound shape loses there.
 BIG_AUTO = os.environ.get("KFA_CONV_BIG_AUTO", "1") != "0"
+BIG_AUTO_E = os.environ.get("KFA_CONV_BIG_AUTO_E", "1") != "0"  # also for launches with an addend
 
 
-def _variant(M: int, N: int, K: int = 0) -> int:
+def _variant(M: int, N: int, K: int = 0, addend: bool = False) -> int:
     """Tile shape of one implicit-GEMM launch: M output pixels x N channels, reduction K."""
     if N <= 64:
         return NARROW
     if BIG and N % 256 == 0 and K >= BIG_MIN_K:
         return 2
-    if BIG_AUTO and N % 256 == 0 and 0 < K <= 128 and M >= 200704:
+    if BIG_AUTO and (BIG_AUTO_E or not addend) and N % 256 == 0 and 0 < K <= 128 and M >= 200704:
         return 2
     return 0
 
@@ -268,7 +269,7 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride: int, pad: int
     if stride == 1:
         wt = _transposed_weight(w, 0, 1, R, 0, 1, S)
         _lib.call("kfa_conv_igemm", _lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), _lib.ptr(E), Nb, Po, Qo, Co, H, W, R, S,
-                  1, -1, pad, pad, Ci, H, W, 1, 0, 0, Ci, _variant(Nb * H * W, Ci, R * S * Co), *bn_args,
+                  1, -1, pad, pad, Ci, H, W, 1, 0, 0, Ci, _variant(Nb * H * W, Ci, R * S * Co, E is not None), *bn_args,
                   _lib.ptr(EM), st)
         return dx
     # stride s: output parity classes.  For class (ph, pw) the rows h = s*i + ph
@@ -289,7 +290,8 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride: int, pad: int
             oa_h = (ph + pad - r0) // stride
             oa_w = (pw + pad - s0) // stride
             _lib.call("kfa_conv_igemm", _lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), _lib.ptr(E), Nb, Po, Qo, Co, Hc, Wc,
-                      Rs, Ss, 1, -1, oa_h, oa_w, Ci, H, W, stride, ph, pw, Ci, _variant(Nb * Hc * Wc, Ci, Rs * Ss * Co),
+                      Rs, Ss, 1, -1, oa_h, oa_w, Ci, H, W, stride, ph, pw, Ci,
+                      _variant(Nb * Hc * Wc, Ci, Rs * Ss * Co, E is not None),
                       *bn_args, _lib.ptr(EM), st)
     return dx
 
