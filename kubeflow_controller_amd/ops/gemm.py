@@ -34,15 +34,43 @@ _lib.register("kfa_gemm_pick_bn", [I, I])
 
 ACTS = {None: 0, "none": 0, "gelu": 1, "tanh": 2, "relu": 3}
 # Which dense-layer GEMMs run on this kernel (KFA_GEMM):
-#   "1"      every projection (forward and dgrad);
+#   "auto"   (default) the Linear layers (``DenseFn``: ResNet FC, MLP heads, W&D
+#            MLP) pick own-vs-library per shape, timed once at first use
+#            (:func:`prefer_own`); the BERT encoder projections stay on the library;
+#   "1"      every projection (forward and dgrad), encoder layers included;
 #   "fused"  only the ones whose epilogue replaces a separate pass: the FFN-up
 #            forward (bias + GELU + pre-activation) and its dgrad (GELU' +
 #            bias-gradient column sums);
 #   "0"      none (hipBLASLt via torch.mm / addmm for all of them).
 # Measured on MI355X (tools/bench_gemm.py, tools/gpu_bert_gemm.sh; docs/kernels.md).
-_ROUTE = os.environ.get("KFA_GEMM", "0")
+_ROUTE = os.environ.get("KFA_GEMM", "auto")
 ROUTE_LAYERS = _ROUTE == "1"
 ROUTE_FUSED = _ROUTE in ("1", "fused")
+ROUTE_AUTO = _ROUTE == "auto"
+TUNE_LOG = os.environ.get("KFA_GEMM_TUNE_LOG", "0") == "1"
+_choice: dict = {}
+
+
+def prefer_own(kind: str, key: tuple, device, run_own, run_lib) -> bool:
+    """Per-shape own-kernel vs library choice (``KFA_GEMM=auto``): both forms timed
+    once at first use, outside any graph capture, and rank 0's decision applied on
+    every rank (data-parallel ranks must run the same kernels).  ``run_own`` /
+    ``run_lib`` must be free of side effects (they run a few times)."""
+    k = (kind,) + tuple(key)
+    hit = _choice.get(k)
+    if hit is not None:
+        return hit
+    if torch.cuda.is_current_stream_capturing():
+        return False
+    from .conv import _agree, _time_ms
+    with torch.no_grad():
+        t_own, t_lib = _time_ms(run_own), _time_ms(run_lib)
+    hit = _choice[k] = _agree(t_own < 0.97 * t_lib, device)
+    if TUNE_LOG:
+        import sys
+        print(f"[kfa gemm tune] {kind} {key}: own {t_own:.4f} ms, library {t_lib:.4f} ms -> "
+              f"{'own' if hit else 'library'}", file=sys.stderr, flush=True)
+    return hit
 
 
 def gemm_ok(a: torch.Tensor, b: torch.Tensor) -> bool:

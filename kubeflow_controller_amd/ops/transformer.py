@@ -213,8 +213,16 @@ class DenseFn(torch.autograd.Function):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
         has_act = act not in (None, "none")
-        fused = p == 0 and (_gemm.ROUTE_LAYERS or (_gemm.ROUTE_FUSED and has_act)) and _gemm.gemm_ok(x2, weight) and (
+        fusable = p == 0 and _gemm.gemm_ok(x2, weight) and (
             bias is None or (bias.dtype == torch.float32 and bias.is_contiguous() and bias.data_ptr() % 16 == 0))
+        fused = fusable and (_gemm.ROUTE_LAYERS or (_gemm.ROUTE_FUSED and has_act))
+        if fusable and _gemm.ROUTE_AUTO:
+            def _lib_fwd():
+                zz = torch.mm(x2, weight.t())
+                return bias_act_fwd(zz, bias, act) if (bias is not None or has_act) else zz
+            fused = _gemm.prefer_own("dense_fwd", (x2.shape[0], weight.shape[0], x2.shape[1], act, bias is not None),
+                                     x2.device, lambda: _gemm.gemm_nt(x2, weight, bias=bias, act=act, want_z=has_act),
+                                     _lib_fwd)
         if fused:
             y, z = _gemm.gemm_nt(x2, weight, bias=bias, act=act, want_z=has_act)  # z includes the bias
         else:
@@ -243,7 +251,13 @@ class DenseFn(torch.autograd.Function):
             dz = dy2
         dx = None
         if ctx.needs_input_grad[0]:
-            wt = _gemm.transpose(weight) if (fused and _gemm.ROUTE_LAYERS and weight.shape[1] % 8 == 0) else None
+            own_dx = fused and _gemm.ROUTE_LAYERS and weight.shape[1] % 8 == 0
+            if (_gemm.ROUTE_AUTO and weight.shape[0] % 8 == 0 and weight.shape[1] % 8 == 0 and dz.is_cuda
+                    and dz.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16 and dz.is_contiguous()):
+                own_dx = _gemm.prefer_own("dense_dgrad", (dz.shape[0], weight.shape[1], weight.shape[0]), dz.device,
+                                          lambda: _gemm.gemm_nt(dz, _gemm.transpose(weight)),
+                                          lambda: torch.mm(dz, weight))
+            wt = _gemm.transpose(weight) if own_dx else None
             if wt is not None and _gemm.gemm_ok(dz, wt):
                 dx = _gemm.gemm_nt(dz, wt)[0].view(shp)
             else:

@@ -164,3 +164,30 @@ def test_linear_module_runs_hip_dense_and_matches_fp32(route, monkeypatch, _pers
     _close(x.grad, xr.grad, 3e-2, "dx")
     _close(lin.weight.grad, wr.grad, 3e-2, "dw")
     _close(lin.bias.grad, br.grad, 3e-2, "db")
+
+
+def test_dense_auto_route_matches_fp32(monkeypatch):
+    """KFA_GEMM=auto: a Linear layer times own-GEMM vs library once per shape (forward
+    and dgrad), records the choice, and its outputs / gradients match fp32 either way."""
+    from kubeflow_controller_amd.ops import gemm as G
+    from kubeflow_controller_amd.ops.linear import Linear
+    monkeypatch.setattr(G, "ROUTE_AUTO", True)
+    monkeypatch.setattr(G, "ROUTE_LAYERS", False)
+    monkeypatch.setattr(G, "ROUTE_FUSED", False)
+    monkeypatch.setattr(G, "_choice", {})
+    torch.manual_seed(0)
+    d = torch.device("cuda")
+    lin = Linear(512, 1000).to(d)
+    x = torch.randn(256, 512, device=d).to(torch.bfloat16).requires_grad_()
+    y = lin(x)
+    y.float().pow(2).mean().backward()
+    kinds = {k[0] for k in G._choice}
+    assert kinds == {"dense_fwd", "dense_dgrad"}, G._choice
+    xr = x.detach().float().requires_grad_()
+    wr = lin.weight.detach().to(torch.bfloat16).float().requires_grad_()
+    br = lin.bias.detach().float().requires_grad_()
+    yr = xr @ wr.t() + br
+    yr.pow(2).mean().backward()
+    torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=2e-2)
+    err = (x.grad.float() - xr.grad).abs().max().item() / xr.grad.abs().max().item()
+    assert err < 3e-2, err
