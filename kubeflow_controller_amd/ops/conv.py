@@ -89,12 +89,23 @@ def _time_ms(fn, reps: int = 5) -> float:
     return s.elapsed_time(e) / reps
 
 
+_LOCKSTEP = False  # set by a data-parallel Engine: every rank of the default group runs the same step
+
+
+def set_lockstep(on: bool) -> None:
+    global _LOCKSTEP
+    _LOCKSTEP = bool(on)
+
+
 def _agree(hit: bool, device) -> bool:
     """Data-parallel ranks must run the same kernels: rank 0's tuning decision wins
     (every rank reaches each layer's first use in the same order, so this
-    one-element broadcast is matched)."""
+    one-element broadcast is matched).  Only in lockstep jobs (``set_lockstep``,
+    the collective Engine): async-PS workers share their default group with PS
+    tasks that never run the model, so a broadcast there would never complete —
+    each async worker keeps its own decision."""
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not _LOCKSTEP or not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return hit
     dev = device if dist.get_backend() == "nccl" else torch.device("cpu")
     t = torch.tensor([1 if hit else 0], dtype=torch.int32, device=dev)

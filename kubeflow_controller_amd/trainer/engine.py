@@ -78,6 +78,9 @@ class Engine:
         from ..parallel.ddp import GradSync, broadcast_params
 
         self.info = dist_info or DistInfo()
+        if self.info.world > 1:  # per-shape tuner decisions are broadcast from rank 0 (ops/conv._agree)
+            from ..ops import conv as _conv
+            _conv.set_lockstep(True)
         self.model = model.to(self.info.device)
         if channels_last:
             self.model = self.model.to(memory_format=torch.channels_last)

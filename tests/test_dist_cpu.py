@@ -131,12 +131,18 @@ def _reduce_worker(rank, world, port, out):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     model = _model()
     groups = split_params(model, torch.bfloat16, pad_to=8 * world)
-    sync = GradSync(groups, bucket_mb=0.0005)
     x, y = _data(world, rank)
+    # this rank's own gradient first, with no sync attached: under overlap the fp32
+    # group's buckets are all-reduced IN PLACE while backward is still running, so a
+    # clone taken after backward may already hold partial sums
     for g in groups:
         g.zero_grad()
     _loss(model, x, y).backward()
     local = [g.grad.clone() for g in groups]
+    sync = GradSync(groups, bucket_mb=0.0005)
+    for g in groups:
+        g.zero_grad()
+    _loss(model, x, y).backward()
     scale = sync.finish()
     torch.save({"local": local, "reduced": [g.opt_grad.clone() for g in groups], "scale": scale,
                 "dtypes": [str(g.opt_grad.dtype) for g in groups]}, f"{out}.{rank}")
@@ -176,3 +182,27 @@ def test_bench_rejects_world_mismatch():
                         "--device", "cpu"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert p.returncode != 0
     assert "WORLD_SIZE" in p.stderr
+
+
+def _agree_worker(rank, world, port, lockstep, out):
+    import torch.distributed as dist
+    from kubeflow_controller_amd.ops import conv
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    conv.set_lockstep(lockstep)
+    # rank 1 would pick differently; only a lockstep job takes rank 0's decision
+    got = conv._agree(rank == 0, torch.device("cpu"))
+    out[rank] = bool(got)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("lockstep", [True, False])
+def test_tuner_decision_broadcast_only_in_lockstep_jobs(lockstep):
+    """Per-shape tuner choices (conv / dense GEMM) follow rank 0 in a data-parallel
+    Engine job; outside one (async-PS workers share their group with PS tasks that
+    never run the model) no collective is issued and each rank keeps its own."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_agree_worker, args=(2, _free_port(), lockstep, out), nprocs=2, join=True)
+    assert dict(out) == ({0: True, 1: True} if lockstep else {0: True, 1: False})
