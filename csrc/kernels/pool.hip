@@ -3,6 +3,8 @@
 // as uint8; backward is a GATHER over the <= ceil(k/s)^2 windows that cover an
 // input pixel, so it needs no atomics and no zero-fill pass.
 // Each thread handles 8 channels (16-B vectors).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -156,6 +158,85 @@ __global__ __launch_bounds__(256) void maxpool3s2_fwd(const bf16_t* __restrict__
   }
 }
 
+// Same op, two horizontally adjacent outputs (ow, ow + 1) per thread: their
+// windows share a column, so 15 loads (each BN-mapped once) serve 2 outputs
+// instead of 18 — and each thread keeps 15 loads in flight (the one-output form
+// is latency-bound: 9 loads, then wait).  Wo odd: the last pair's second output is masked.
+template <bool BN>
+__global__ __launch_bounds__(256) void maxpool3s2_fwd2(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                       uint8_t* __restrict__ idx, int N, int H, int W, int C, int Ho,
+                                                       int Wo, int p, const float* __restrict__ ss) {
+  const unsigned cv = C / 8;
+  const unsigned wp = (unsigned)(Wo + 1) / 2;
+  const unsigned total = (unsigned)N * Ho * wp * cv;
+  const unsigned v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= total) return;
+  const int cg = (int)(v % cv);
+  unsigned t = v / cv;
+  const int ow0 = (int)(t % wp) * 2;
+  t /= wp;
+  const int oh = (int)(t % (unsigned)Ho);
+  const int n = (int)(t / (unsigned)Ho);
+  const bf16_t* xb = x + (long)n * H * W * C + cg * 8;
+  uint4 in[15];
+  bool ok[15];
+#pragma unroll
+  for (int kh = 0; kh < 3; kh++)
+#pragma unroll
+    for (int kw = 0; kw < 5; kw++) {
+      const int ih = oh * 2 - p + kh, iw = ow0 * 2 - p + kw;
+      ok[kh * 5 + kw] = ih >= 0 && ih < H && iw >= 0 && iw < W;
+      const int ch = min(max(ih, 0), H - 1), cw = min(max(iw, 0), W - 1);
+      in[kh * 5 + kw] = *reinterpret_cast<const uint4*>(xb + ((long)ch * W + cw) * C);
+    }
+  float sc[8], sf[8], best0[8], best1[8];
+  int bi0[8], bi1[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    sc[j] = BN ? ss[cg * 8 + j] : 1.f;
+    sf[j] = BN ? ss[C + cg * 8 + j] : 0.f;
+    best0[j] = best1[j] = -INFINITY;
+    bi0[j] = bi1[j] = 0;
+  }
+#pragma unroll
+  for (int kh = 0; kh < 3; kh++)
+#pragma unroll
+    for (int kw = 0; kw < 5; kw++) {
+      const int q = kh * 5 + kw;
+      if (!ok[q]) continue;
+      float f[8];
+      unpack8(in[q], f);
+      if (BN) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) f[j] = bf2f(f2bf(fmaxf(fmaf(f[j], sc[j], sf[j]), 0.f)));
+      }
+      if (kw < 3) {  // output ow0: window columns 0..2, tap index kh * 3 + kw
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+          if (f[j] > best0[j] || (f[j] != f[j] && best0[j] == best0[j])) { best0[j] = f[j]; bi0[j] = kh * 3 + kw; }
+      }
+      if (kw >= 2) {  // output ow0 + 1: window columns 2..4
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+          if (f[j] > best1[j] || (f[j] != f[j] && best1[j] == best1[j])) { best1[j] = f[j]; bi1[j] = kh * 3 + kw - 2; }
+      }
+    }
+  const long o0 = ((((long)n * Ho + oh) * Wo) + ow0) * C + cg * 8;
+  *reinterpret_cast<uint4*>(y + o0) = pack8(best0);
+  if (idx) {
+    *reinterpret_cast<uint2*>(idx + o0) = make_uint2(bi0[0] | (bi0[1] << 8) | (bi0[2] << 16) | (bi0[3] << 24),
+                                                     bi0[4] | (bi0[5] << 8) | (bi0[6] << 16) | (bi0[7] << 24));
+  }
+  if (ow0 + 1 < Wo) {
+    const long o1 = o0 + C;
+    *reinterpret_cast<uint4*>(y + o1) = pack8(best1);
+    if (idx) {
+      *reinterpret_cast<uint2*>(idx + o1) = make_uint2(bi1[0] | (bi1[1] << 8) | (bi1[2] << 16) | (bi1[3] << 24),
+                                                       bi1[4] | (bi1[5] << 8) | (bi1[6] << 16) | (bi1[7] << 24));
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void maxpool3s2_bwd(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ idx,
                                                       bf16_t* __restrict__ dx, int N, int H, int W, int C, int Ho,
                                                       int Wo, int p) {
@@ -207,13 +288,26 @@ int grid_for(long work) {
   return (int)(b < (1L << 20) ? (b < 1 ? 1 : b) : (1L << 20));
 }
 
+// two outputs per thread (maxpool3s2_fwd2); KFA_POOL_PAIRS=0 keeps one
+bool pool_pairs() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("KFA_POOL_PAIRS");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+
 }  // namespace
 
 KFA_API int kfa_maxpool_fwd(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H, int W, int C, int Ho, int Wo,
                             int k, int s, int p, hipStream_t st) {
   if (C % 8 || k > 15) return -1;
   const long work = (long)N * Ho * Wo * (C / 8);
-  if (k == 3 && s == 2 && p <= 1 && work < (1L << 31) && (long)N * H * W * C < (1L << 40))
+  if (k == 3 && s == 2 && p <= 1 && work < (1L << 31) && (long)N * H * W * C < (1L << 40) && pool_pairs())
+    hipLaunchKernelGGL(maxpool3s2_fwd2<false>, dim3((unsigned)(((long)N * Ho * ((Wo + 1) / 2) * (C / 8) + 255) / 256)),
+                       dim3(256), 0, st, x, y, idx, N, H, W, C, Ho, Wo, p, nullptr);
+  else if (k == 3 && s == 2 && p <= 1 && work < (1L << 31) && (long)N * H * W * C < (1L << 40))
     hipLaunchKernelGGL(maxpool3s2_fwd<false>, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, st, x, y, idx, N, H,
                        W, C, Ho, Wo, p, nullptr);
   else if (work < (1L << 31))
@@ -247,8 +341,14 @@ KFA_API int kfa_maxpool_fwd_bn(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, 
                                int k, int s, int p, const float* ss, hipStream_t st) {
   const long work = (long)N * Ho * Wo * (C / 8);
   if (C % 8 || k != 3 || s != 2 || p > 1 || !ss || work >= (1L << 31) || (long)N * H * W * C >= (1L << 40)) return -1;
-  hipLaunchKernelGGL(maxpool3s2_fwd<true>, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, st, x, y, idx, N, H, W,
-                     C, Ho, Wo, p, ss);
+  if (pool_pairs()) {
+    const long w2 = (long)N * Ho * ((Wo + 1) / 2) * (C / 8);
+    hipLaunchKernelGGL(maxpool3s2_fwd2<true>, dim3((unsigned)((w2 + 255) / 256)), dim3(256), 0, st, x, y, idx, N, H,
+                       W, C, Ho, Wo, p, ss);
+  } else {
+    hipLaunchKernelGGL(maxpool3s2_fwd<true>, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, st, x, y, idx, N, H,
+                       W, C, Ho, Wo, p, ss);
+  }
   return kfa_status();
 }
 
