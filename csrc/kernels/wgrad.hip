@@ -51,6 +51,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t wrsrc(const void* p, unsigned 
 }
 // 16 B per lane buffer -> LDS DMA; a plain device function (the builtin inside the
 // templated kernel's lambda stops clang's host pass from emitting launch stubs)
+#ifndef KFA_WG_PART_ST_NT
+#define KFA_WG_PART_ST_NT 0  // A/B: split-K partial stores non-temporal
+#endif
 #ifndef KFA_WG_DY_AUX
 #define KFA_WG_DY_AUX 0
 #endif
@@ -287,7 +290,11 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_kernel(const bf16_t* __
       floatx4 v = acc[ni][mi];
       const long e = (long)m * g.N + n;
       if (part) {
+#if KFA_WG_PART_ST_NT
+        __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(part + (long)split * g.Co * g.N + e));
+#else
         *reinterpret_cast<floatx4*>(part + (long)split * g.Co * g.N + e) = v;
+#endif
       } else if (grad_f32) {
         floatx4* gp = reinterpret_cast<floatx4*>(reinterpret_cast<float*>(grad) + e);
         *gp = accumulate ? *gp + v : v;
