@@ -15,6 +15,7 @@
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 from typing import Optional, Tuple
 
@@ -22,9 +23,40 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops import _lib
 from ..ops import transformer as T
 from ..parallel.embedding import ShardedEmbedding
 
+_lib.register("kfa_wd_input_fwd", [_lib.P, _lib.P, _lib.P, _lib.P, _lib.I, _lib.I, _lib.I, _lib.I, _lib.P])
+_lib.register("kfa_wd_input_bwd", [_lib.P, _lib.P, _lib.P, _lib.I, _lib.I, _lib.I, _lib.I, _lib.P])
+
+
+class _WDInputFn(torch.autograd.Function):
+    """(rows [B*F, E+8] bf16, dense_pad [B, Dp] fp32) -> (x [B, Dp+F*E] bf16, wide [B] fp32) in
+    one HIP pass each way (``csrc/kernels/widedeep.hip``) — the slice / reshape / pad /
+    cat / cast chain and its autograd mirror were 16 % of the step."""
+
+    @staticmethod
+    def forward(ctx, rows, dense_pad, B, F, E):
+        Dp = dense_pad.shape[1]
+        x = torch.empty(B, Dp + F * E, dtype=torch.bfloat16, device=rows.device)
+        wide = torch.empty(B, dtype=torch.float32, device=rows.device)
+        _lib.call("kfa_wd_input_fwd", _lib.ptr(rows), _lib.ptr(dense_pad), _lib.ptr(x), _lib.ptr(wide), B, F, E, Dp,
+                  _lib.stream())
+        ctx.dims = (B, F, E, Dp)
+        return x, wide
+
+    @staticmethod
+    def backward(ctx, dx, dwide):
+        B, F, E, Dp = ctx.dims
+        dx = (dx if dx is not None else torch.zeros(B, Dp + F * E, dtype=torch.bfloat16,
+                                                    device=dwide.device)).to(torch.bfloat16).contiguous()
+        dwide = (dwide if dwide is not None else torch.zeros(B, device=dx.device)).float().contiguous()
+        drows = torch.empty(B * F, E + 8, dtype=torch.bfloat16, device=dx.device)
+        _lib.call("kfa_wd_input_bwd", _lib.ptr(dx), _lib.ptr(dwide), _lib.ptr(drows), B, F, E, Dp, _lib.stream())
+        return drows, None, None, None, None
+
+FUSED_INPUT = os.environ.get("KFA_WD_FUSED_INPUT", "1") != "0"  # csrc/kernels/widedeep.hip
 CRITEO_LIKE = (4_000_000,) * 4 + (1_000_000,) * 6 + (100_000,) * 8 + (10_000,) * 8
 
 
@@ -81,12 +113,17 @@ class WideDeep(nn.Module):
         cfg = self.cfg
         B, nf = ids.shape
         gids = (ids + self.offsets.view(1, nf)).reshape(-1)
-        rows = self.tables(gids, getattr(ids, "_kfa_plan", None)).view(B, nf, cfg.row_width)  # [B, nf, E+8]
-        deep_emb = rows[:, :, :cfg.embed_dim].reshape(B, nf * cfg.embed_dim)
-        wide = rows[:, :, cfg.embed_dim].float().sum(1)
+        flat_rows = self.tables(gids, getattr(ids, "_kfa_plan", None))  # [B*nf, E+8]
         cdt = self.weights[0].dtype
         dpad = F.pad(dense, (0, cfg.dense_pad - cfg.num_dense))
-        x = torch.cat([dpad.to(rows.dtype), deep_emb], 1)
+        if (FUSED_INPUT and flat_rows.is_cuda and flat_rows.dtype == torch.bfloat16 and cdt == torch.bfloat16
+                and cfg.embed_dim % 8 == 0 and flat_rows.is_contiguous()):
+            x, wide = _WDInputFn.apply(flat_rows, dpad.float().contiguous(), B, nf, cfg.embed_dim)
+        else:
+            rows = flat_rows.view(B, nf, cfg.row_width)  # [B, nf, E+8]
+            deep_emb = rows[:, :, :cfg.embed_dim].reshape(B, nf * cfg.embed_dim)
+            wide = rows[:, :, cfg.embed_dim].float().sum(1)
+            x = torch.cat([dpad.to(rows.dtype), deep_emb], 1)
         if x.is_cuda:
             x = x.to(cdt)
             for w, b in zip(self.weights, self.biases):

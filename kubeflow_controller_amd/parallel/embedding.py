@@ -98,6 +98,7 @@ class _LookupFn(torch.autograd.Function):
 
 
 class ShardedEmbedding(nn.Module):
+    kfa_sparse_module = True  # split_params leaves the table out of the dense flat groups
     def __init__(self, num_rows: int, dim: int, owners: Optional[int] = None, process_group=None,
                  optimizer: str = "adam", lr: float = 1e-3, betas: Tuple[float, float] = (0.9, 0.999),
                  eps: float = 1e-8, weight_decay: float = 0.0, init_std: float = 0.01, seed: int = 0,

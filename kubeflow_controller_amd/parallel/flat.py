@@ -115,8 +115,12 @@ def split_params(model: torch.nn.Module, compute_dtype=torch.bfloat16, pad_to: i
     Group names: ``"weights"`` (weight decay applies) and ``"norms_biases"``
     (no decay — the usual large-batch recipe)."""
     big, small = [], []
+    # row-sharded tables: marked on the tensor and by their module's class (a
+    # tensor attribute does not survive copy.deepcopy of the model)
+    sparse = {id(p) for m in model.modules() if getattr(type(m), "kfa_sparse_module", False)
+              for p in m.parameters(recurse=False)}
     for p in model.parameters():
-        if not p.requires_grad or getattr(p, "_kfa_sparse", False):
+        if not p.requires_grad or getattr(p, "_kfa_sparse", False) or id(p) in sparse:
             continue  # frozen, or a row-sharded table updated by its owner (parallel/embedding.py)
         if p.dim() >= 2 and compute_dtype is not None and p.dtype != compute_dtype:
             p.data = p.data.to(compute_dtype)

@@ -259,3 +259,17 @@ def test_apply_bit_mask_matches_channels_last_bit_order():
     out = apply_bit_mask(t, bits)
     want = t * keep.permute(0, 3, 1, 2)
     assert torch.equal(out, want)
+
+
+def test_sharded_table_stays_out_of_flat_groups_after_deepcopy():
+    """A deep-copied Wide&Deep (tensor attributes do not survive copy.deepcopy) must
+    still keep its row-sharded table out of the dense flat groups: cast to the bf16
+    compute dtype there, the table's fp32 sparse kernels would write past it."""
+    import copy
+    from kubeflow_controller_amd.models.wide_deep import WideDeep, WideDeepConfig
+    from kubeflow_controller_amd.parallel.flat import split_params
+    m = copy.deepcopy(WideDeep(WideDeepConfig.tiny(), device="cpu"))
+    groups = split_params(m, torch.bfloat16)
+    flat = {id(p) for g in groups for p in g.params}
+    assert id(m.tables.weight) not in flat
+    assert m.tables.weight.dtype == torch.float32
