@@ -143,10 +143,21 @@ class ShardedEmbedding(nn.Module):
                 f"optimizer={self.optimizer}")
 
     # ---------------------------------------------------------------- owner-side kernels
+    def _check_table(self) -> None:
+        """The HIP gather / sparse-optimizer kernels index fp32 [local_rows, dim] rows:
+        refuse anything else (e.g. a table some other code cast to bf16) instead of
+        letting them address past it."""
+        for name, t in (("weight", self.weight), ("exp_avg", self.exp_avg), ("exp_avg_sq", self.exp_avg_sq)):
+            if t is not None and (t.dtype != torch.float32 or not t.is_contiguous()
+                                  or tuple(t.shape) != (self.local_rows, self.dim)):
+                raise RuntimeError(f"ShardedEmbedding.{name}: expected contiguous fp32 [{self.local_rows}, "
+                                   f"{self.dim}], got {t.dtype} {tuple(t.shape)}")
+
     def gather(self, local: torch.Tensor) -> torch.Tensor:
         n = local.numel()
         if not self.weight.is_cuda:
             return self.weight.detach().index_select(0, local)
+        self._check_table()
         out = torch.empty(n, self.dim, dtype=torch.bfloat16, device=local.device)
         if n:
             _lib.call("kfa_embed_fwd", _lib.ptr(local), _lib.ptr(self.weight), None, None, None, None, 1,
@@ -162,6 +173,7 @@ class ShardedEmbedding(nn.Module):
         if not self.weight.is_cuda:
             self._apply_cpu(local, g.float(), b1, b2)
             return
+        self._check_table()
         scratch = _lib.workspace(self.local_rows * self.dim * 4, self.weight.device,
                                  f"sparse_scratch{id(self)}").view(torch.float32)
         st = _lib.stream()
