@@ -12,6 +12,8 @@
 // a fixed group of 8 channels so per-channel coefficients live in registers.
 // Row sums use a per-channel pivot (x[0][c]) to avoid E[x^2]-E[x]^2
 // cancellation; cross-block partials are combined in fp64.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -289,9 +291,32 @@ __global__ __launch_bounds__(NT) void bn_apply(const bf16_t* __restrict__ x, con
   }
 }
 
+// The apply passes keep no per-block partials, so their grid need not follow the
+// statistics passes' (max_row_blocks caps C >= 1024 at 512-1024 blocks: 2-4 per
+// CU, too few loads in flight to stream at HBM rate).  KFA_BN_APPLY_BLOCKS=0
+// restores the shared geometry.
+static Geom apply_geom(long M, int C) {
+  static int cap = -1;
+  if (cap < 0) {
+    const char* e = getenv("KFA_BN_APPLY_BLOCKS");
+    cap = e ? atoi(e) : 4096;
+    if (cap < 0) cap = 4096;
+  }
+  int shared = (1 << 20) / C;  // == max_row_blocks(C)
+  shared = shared > 2048 ? 2048 : (shared < 64 ? 64 : shared);
+  return geom(M, C, cap > 0 ? cap : shared);
+}
+
 static void launch_apply(int relu, const bf16_t* res, uint8_t* mb, dim3 grid, hipStream_t s, const bf16_t* x,
                          bf16_t* y, const float* scale, const float* shift, long M, int C, long chunk, int tpr,
                          int rpi, const float* rss = nullptr) {
+  {
+    const Geom ga = apply_geom(M, C);
+    grid = dim3(ga.gx);
+    chunk = ga.chunk;
+    tpr = ga.tpr;
+    rpi = ga.rpi;
+  }
   if (rss && relu && res && mb)
     hipLaunchKernelGGL((bn_apply<true, true, true, true>), grid, dim3(NT), 0, s, x, res, y, mb, scale, shift, M, C,
                        chunk, tpr, rpi, rss);
@@ -629,9 +654,10 @@ KFA_API int kfa_bn_fwd_eval(const bf16_t* x, const bf16_t* res, bf16_t* y, const
 }
 
 template <int MASK>
-static void launch_bwd_apply(const Geom& g, const bf16_t* dy, const bf16_t* x, const bf16_t* y, const uint8_t* mb,
+static void launch_bwd_apply(const Geom&, const bf16_t* dy, const bf16_t* x, const bf16_t* y, const uint8_t* mb,
                              const float* ss, const float* coef, bf16_t* dx, bf16_t* dres, long M, int C,
                              hipStream_t s) {
+  const Geom g = apply_geom(M, C);
   if (dres)
     hipLaunchKernelGGL((bn_bwd_apply<MASK, true>), dim3(g.gx), dim3(NT), 0, s, dy, x, y, mb, ss, coef, dx, dres, M, C,
                        g.chunk, g.tpr, g.rpi);
