@@ -3,19 +3,31 @@
 variables round-robin on PS tasks via ``replica_device_setter`` :137-141, every
 worker's ``sess.run(train_step)`` pulls the variables, computes gradients
 against that (possibly stale) copy and pushes them to the PS, which applies
-Adam immediately :184,:256; the global step advances once per push).
+Adam immediately :184,:256; the global step advances once per push) — and its
+``--sync_replicas --replicas_to_aggregate N`` form (``SyncReplicasOptimizer``
+:172-195) on the same service loop.
 
 Transport (SURVEY §5.8 "Async PS = send/recv to the owner rank", H5): a
 process group over workers AND PS tasks (ranks ``0..W-1`` workers, ``W..W+P-1``
 PS tasks).  Each PS runs a single-threaded service loop that receives request
-headers from ANY worker (``recv(src=None)``), so workers progress
-independently — no collective, no lock-step:
+headers ``[op, step_tag]`` from ANY worker (``recv(src=None)``), so workers
+progress independently — no collective, no lock-step:
 
 * ``PULL``  → PS sends its shard (all owned tensors, flattened fp32);
-* ``PUSH``  → PS receives the gradient for its shard, applies Adam to it in
-  place (owner-side apply, optimizer state lives only on the PS) and replies
-  with the new global step (PS 0 owns the global step counter);
+* ``PUSH``  → PS receives the gradient for its shard and applies Adam/SGD to it
+  in place (owner-side apply: optimizer state lives only on the PS); the reply
+  is ``[global_step, applied]`` (PS 0's counter is the job's global step);
+* ``PUSH_DEV`` → the same with the gradient already in the worker's device
+  mailbox (device transport, below);
 * ``DONE``  → a worker finished; the PS exits when every worker has.
+
+Aggregation (``aggregate = N``, the ``SyncReplicasOptimizer`` semantics): a
+push tagged with a step older than the PS's current step is DROPPED (stale;
+reply ``applied = 0`` at once); fresh pushes are summed, and the N-th one
+applies their MEAN, advances the step and releases every waiting pusher (the
+token queue).  When every still-active worker is waiting (fewer than N left,
+e.g. at the end of training) the partial sum is applied so no one blocks
+forever.  ``aggregate = 0``: every push applies at once (async).
 
 Headers and payloads use distinct tags, and every request from one worker is
 sequential, so a PS never interleaves two workers' payloads.  Two transports:
@@ -24,31 +36,37 @@ sequential, so a PS never interleaves two workers' payloads.  Two transports:
   tensors over gloo — TF's gRPC PS in spirit, for CPU replicas;
 * **device** (:class:`DeviceAsyncPSServer` / :class:`DeviceAsyncPSClient`): the
   PS task keeps its variables, Adam slots and one gradient mailbox per worker
-  in GPU memory on the GPU it is co-located with, and exports them to the
-  workers by HIP IPC (dmabuf handles published in the job's TCPStore).  A pull
-  is a device-to-device copy straight out of the PS's fp32 variables (over
-  xGMI when the PS sits on another GPU of the node; no PS involvement, and —
-  like TF's ``use_locking=False`` Adam — it may overlap an update); a push is a
-  device-to-device write into the worker's mailbox followed by a PUSH header;
-  the PS applies the fused HIP Adam kernel to the mailbox and replies with the
-  global step.  Only headers and step numbers cross the host.
+  in the HBM of the GPU it is co-located with and exports them by HIP IPC
+  (dmabuf handles published in the job's TCPStore as JSON — nothing is
+  unpickled).  The worker holds its weights and gradients in per-PS flat
+  buffers laid out exactly like the PS's, so a pull is ONE device copy (+cast)
+  per PS and dtype run straight out of the PS's fp32 variables and a push is
+  one copy into the mailbox followed by a ``PUSH_DEV`` header.  Before using a
+  PS's memory the client verifies the mapping against a canary pattern the PS
+  published (value + nonce); if the import fails or reads wrong data (e.g. the
+  PS's GPU is not visible to this replica) that PS is served over the host
+  transport instead, with a loud log line — the server speaks both.
 
-The synchronous modes (``--sync_replicas``, or no PS) use RCCL reduce /
-reduce-scatter / all-gather on the GPUs instead (``parallel/ps.py``,
-``parallel/ddp.py``).
+The synchronous collective modes (``--sync_replicas`` with N = W, or no PS) use
+RCCL reduce / reduce-scatter / all-gather on the GPUs instead
+(``parallel/ps.py``, ``parallel/ddp.py``).
 """
 from __future__ import annotations
 
+import base64
+import json
 import math
-from typing import Dict, List, Sequence, Tuple
+import os
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
 
 from .ps import ps_assignment
 
-PULL, PUSH, DONE = 1, 2, 3
+PULL, PUSH, DONE, PUSH_DEV = 1, 2, 3, 4
 TAG_HDR, TAG_DATA, TAG_REPLY = 11, 12, 13
+ALIGN = 8  # = parallel/flat.py ALIGN: device-layout offsets match the worker's FlatGroups
 
 
 def _layout(shapes: Sequence[Tuple[str, torch.Size]], assignment: Dict[str, int], ps: int):
@@ -58,11 +76,127 @@ def _layout(shapes: Sequence[Tuple[str, torch.Size]], assignment: Dict[str, int]
     return names, sum(sizes[n] for n in names)
 
 
-class AsyncPSServer:
-    """Service loop of PS task ``ps_index`` (rank ``num_workers + ps_index``)."""
+def _round_up(n: int, m: int) -> int:
+    return (n + m - 1) // m * m
+
+
+def device_layout(shapes: Sequence[Tuple[str, torch.Size]], assignment: Dict[str, int], ps: int):
+    """Layout of PS ``ps``'s variables in the device transport: the matrices
+    (dim >= 2, bf16 on the worker) first, then the vectors, each run laid out as
+    ``parallel.flat.FlatGroup`` lays it (offsets rounded up to ``ALIGN``, run
+    length padded to ``ALIGN``).  Returns ``[(names, offsets, run_start,
+    run_len)]`` for the two runs (empty runs omitted) and the total length."""
+    names, _ = _layout(shapes, assignment, ps)
+    dims = {n: len(s) for n, s in shapes}
+    sizes = {n: int(torch.Size(s).numel()) for n, s in shapes}
+    runs, start = [], 0
+    for sel in ([n for n in names if dims[n] >= 2], [n for n in names if dims[n] < 2]):
+        if not sel:
+            continue
+        offs, off = [], 0
+        for n in sel:
+            offs.append(off)
+            off = _round_up(off + sizes[n], ALIGN)
+        length = _round_up(max(off, 1), ALIGN)
+        runs.append((sel, offs, start, length))
+        start += length
+    return runs, start
+
+
+def _flat_order(t: torch.Tensor, channels_last: bool) -> torch.Tensor:
+    """``t`` flattened in the worker's memory order (NHWC for channels-last convs)."""
+    if channels_last and t.dim() == 4:
+        return t.permute(0, 2, 3, 1).reshape(-1)
+    return t.reshape(-1)
+
+
+class _Service:
+    """The PS service loop shared by both transports (see module docstring)."""
+
+    W: int
+    idx: int
+    aggregate: int
+
+    def _init_service(self, aggregate: int) -> None:
+        if aggregate < 0 or aggregate > self.W:
+            raise ValueError(f"replicas_to_aggregate must be in 1..{self.W} (num workers), got {aggregate}")
+        self.aggregate = aggregate
+        self.global_step = 0
+        self.t = 0
+        self.dropped = 0
+        self.applied_pushes = 0
+        self.update_sizes: List[int] = []  # gradients averaged into each aggregated update
+
+    # transport hooks
+    def _send_vars(self, src: int) -> None: ...
+    def _recv_grad(self, src: int, op: int) -> torch.Tensor: ...
+    def _apply(self, g: torch.Tensor, scale: float) -> None: ...
+    def _acc_reset(self) -> None: ...
+    def _acc_add(self, g: torch.Tensor) -> None: ...
+    def _acc(self) -> torch.Tensor: ...
+    def _reply(self, dst: int, applied: int) -> None:
+        dist.send(torch.tensor([self.global_step, applied], dtype=torch.int64), dst, group=self.group,
+                  tag=TAG_REPLY)
+
+    def serve(self, log: Optional[Callable[[str], None]] = None) -> int:
+        """Run until every worker sent DONE; returns the number of pushes applied."""
+        active = self.W
+        hdr = torch.zeros(2, dtype=torch.int64)
+        waiting: List[int] = []
+        count = 0
+        if self.aggregate:
+            self._acc_reset()
+
+        def flush():
+            nonlocal count
+            self._apply(self._acc(), 1.0 / count)
+            self.update_sizes.append(count)
+            self.global_step += 1
+            for w in waiting:
+                self._reply(w, 1)
+            waiting.clear()
+            count = 0
+            self._acc_reset()
+
+        while active > 0:
+            src = dist.recv(hdr, src=None, group=self.group, tag=TAG_HDR)
+            op, tag = int(hdr[0]), int(hdr[1])
+            if op == PULL:
+                self._send_vars(src)
+            elif op in (PUSH, PUSH_DEV):
+                g = self._recv_grad(src, op)
+                if not self.aggregate:
+                    self._apply(g, 1.0)
+                    self.applied_pushes += 1
+                    self.global_step += 1
+                    self._reply(src, 1)
+                elif tag < self.global_step:  # computed on variables older than the current step
+                    self.dropped += 1
+                    self._reply(src, 0)
+                else:
+                    self._acc_add(g)
+                    self.applied_pushes += 1
+                    count += 1
+                    waiting.append(src)
+                    if count >= self.aggregate:
+                        flush()
+                if log and self.global_step and self.global_step % 50 == 0 and not waiting:
+                    log(f"PS {self.idx}: applied {self.global_step} updates")
+            elif op == DONE:
+                active -= 1
+            else:
+                raise RuntimeError(f"PS {self.idx}: bad request {op} from rank {src}")
+            if self.aggregate and waiting and len(waiting) >= active:
+                flush()  # nobody left who could complete the aggregate
+        return self.applied_pushes
+
+
+class AsyncPSServer(_Service):
+    """Service loop of PS task ``ps_index`` (rank ``num_workers + ps_index``), host memory."""
 
     def __init__(self, init_params: Sequence[Tuple[str, torch.Tensor]], num_workers: int, num_ps: int, ps_index: int,
-                 lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, optimizer: str = "adam", group=None):
+                 lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, optimizer: str = "adam", group=None,
+                 aggregate: int = 0):
         self.W, self.P, self.idx = num_workers, num_ps, ps_index
         shapes = [(n, p.shape) for n, p in init_params]
         self.assignment = ps_assignment(list(init_params), num_ps)
@@ -72,13 +206,15 @@ class AsyncPSServer:
             else torch.zeros(0)
         self.m = torch.zeros_like(self.w)
         self.v = torch.zeros_like(self.w)
+        self.grad = torch.empty_like(self.w)
         self.lr, self.betas, self.eps, self.opt = lr, betas, eps, optimizer
-        self.t = 0
-        self.global_step = 0
         self.group = group
+        self._init_service(aggregate)
 
-    def _apply(self, g: torch.Tensor) -> None:
+    def _apply(self, g: torch.Tensor, scale: float = 1.0) -> None:
         self.t += 1
+        if scale != 1.0:
+            g = g * scale
         if self.opt == "sgd":
             self.w.add_(g, alpha=-self.lr)
             return
@@ -88,35 +224,49 @@ class AsyncPSServer:
         step = self.lr * math.sqrt(1 - b2 ** self.t) / (1 - b1 ** self.t)  # TF AdamOptimizer form
         self.w.addcdiv_(self.m, self.v.sqrt().add_(self.eps), value=-step)
 
-    def serve(self, log=None) -> int:
-        """Run until every worker sent DONE; returns the number of pushes applied."""
-        active = self.W
-        hdr = torch.zeros(2, dtype=torch.int64)
-        grad = torch.empty_like(self.w)
-        pushes = 0
-        while active > 0:
-            src = dist.recv(hdr, src=None, group=self.group, tag=TAG_HDR)
-            op = int(hdr[0])
-            if op == PULL:
-                dist.send(self.w, src, group=self.group, tag=TAG_DATA)
-            elif op == PUSH:
-                dist.recv(grad, src, group=self.group, tag=TAG_DATA)
-                self._apply(grad)
-                pushes += 1
-                self.global_step += 1
-                dist.send(torch.tensor([self.global_step], dtype=torch.int64), src, group=self.group,
-                          tag=TAG_REPLY)
-                if log and self.global_step % 50 == 0:
-                    log(f"PS {self.idx}: applied {self.global_step} updates")
-            elif op == DONE:
-                active -= 1
-            else:
-                raise RuntimeError(f"PS {self.idx}: bad request {op} from rank {src}")
-        return pushes
+    def _send_vars(self, src: int) -> None:
+        dist.send(self.w, src, group=self.group, tag=TAG_DATA)
+
+    def _recv_grad(self, src: int, op: int) -> torch.Tensor:
+        if op != PUSH:
+            raise RuntimeError(f"PS {self.idx}: host server got a device push from rank {src}")
+        dist.recv(self.grad, src, group=self.group, tag=TAG_DATA)
+        return self.grad
+
+    def _acc_reset(self) -> None:
+        self.acc = torch.zeros_like(self.w)
+
+    def _acc_add(self, g: torch.Tensor) -> None:
+        self.acc.add_(g)
+
+    def _acc(self) -> torch.Tensor:
+        return self.acc
 
 
-class AsyncPSClient:
-    """Worker side: pull variables from / push gradients to every PS task."""
+class _ClientSteps:
+    """Per-PS step tags: the PS's step as last reported to this worker."""
+
+    def _init_steps(self, num_ps: int) -> None:
+        self.tags = [0] * num_ps
+        self.pushes_dropped = 0
+        self._hdr = torch.zeros(2, dtype=torch.int64)
+        self._reply = torch.zeros(2, dtype=torch.int64)
+
+    def _header(self, rank: int, op: int, tag: int = 0) -> None:
+        self._hdr[0], self._hdr[1] = op, tag
+        dist.send(self._hdr, rank, group=self.group, tag=TAG_HDR)
+
+    def _await_reply(self, k: int, rank: int) -> int:
+        dist.recv(self._reply, rank, group=self.group, tag=TAG_REPLY)
+        step, applied = int(self._reply[0]), int(self._reply[1])
+        self.tags[k] = step
+        if not applied:
+            self.pushes_dropped += 1
+        return step
+
+
+class AsyncPSClient(_ClientSteps):
+    """Worker side: pull variables from / push gradients to every PS task (host transport)."""
 
     def __init__(self, params: Sequence[Tuple[str, torch.nn.Parameter]], num_workers: int, num_ps: int, group=None):
         self.W, self.P, self.group = num_workers, num_ps, group
@@ -128,14 +278,13 @@ class AsyncPSClient:
         for k in range(num_ps):
             names, n = _layout(shapes, self.assignment, k)
             self.plan.append((num_workers + k, [by_name[x] for x in names], torch.zeros(n)))
-        self._hdr = torch.zeros(2, dtype=torch.int64)
+        self._init_steps(num_ps)
 
     def pull(self) -> None:
         for rank, ps, buf in self.plan:
             if not ps:
                 continue
-            self._hdr[0] = PULL
-            dist.send(self._hdr, rank, group=self.group, tag=TAG_HDR)
+            self._header(rank, PULL)
             dist.recv(buf, rank, group=self.group, tag=TAG_DATA)
             off = 0
             with torch.no_grad():
@@ -147,7 +296,6 @@ class AsyncPSClient:
     def push(self) -> int:
         """Send every PS its gradient shard; returns the global step reported by PS 0."""
         step = -1
-        reply = torch.zeros(1, dtype=torch.int64)
         for k, (rank, ps, buf) in enumerate(self.plan):
             if not ps:
                 continue
@@ -159,18 +307,16 @@ class AsyncPSClient:
                 else:
                     buf[off:off + n].copy_(p.grad.reshape(-1))
                 off += n
-            self._hdr[0] = PUSH
-            dist.send(self._hdr, rank, group=self.group, tag=TAG_HDR)
+            self._header(rank, PUSH, self.tags[k])
             dist.send(buf, rank, group=self.group, tag=TAG_DATA)
-            dist.recv(reply, rank, group=self.group, tag=TAG_REPLY)
+            s = self._await_reply(k, rank)
             if k == 0:
-                step = int(reply[0])
+                step = s
         return step
 
     def done(self) -> None:
-        self._hdr[0] = DONE
         for rank, _, _ in self.plan:
-            dist.send(self._hdr, rank, group=self.group, tag=TAG_HDR)
+            self._header(rank, DONE)
 
 
 # ---------------------------------------------------------------------------
@@ -179,102 +325,179 @@ def _ipc_key(ps: int, what: str) -> str:
     return f"kfa/async_ps/{ps}/{what}"
 
 
+_TENSOR_CLS = {"Tensor": torch.Tensor, "Parameter": torch.nn.Parameter}
+_STORAGE_CLS = {"UntypedStorage": torch.UntypedStorage, "TypedStorage": torch.storage.TypedStorage}
+
+
+def _enc(v):
+    if isinstance(v, (bytes, bytearray)):
+        return {"b64": base64.b64encode(bytes(v)).decode()}
+    if isinstance(v, torch.Size):
+        return list(v)
+    if isinstance(v, tuple):
+        return list(v)
+    return v
+
+
+def _dec(v):
+    if isinstance(v, dict) and set(v) == {"b64"}:
+        return base64.b64decode(v["b64"])
+    return v
+
+
 def _export(store, key: str, t: torch.Tensor) -> None:
-    """Publish a CUDA tensor to other processes of the job (HIP IPC handle)."""
-    import pickle
+    """Publish a CUDA tensor to the other processes of the job (HIP IPC handle)
+    as JSON: plain ints / strings and base64 handle bytes, no pickled objects."""
     from torch.multiprocessing.reductions import reduce_tensor
-    _, args = reduce_tensor(t)
-    store.set(key, pickle.dumps(args))
+    _, a = reduce_tensor(t)
+    (tensor_cls, size, stride, offset, storage_cls, dtype, device, handle, size_bytes, offset_bytes, req_grad,
+     ref_handle, ref_offset, ev_handle, ev_sync) = a
+    rec = {"tensor_cls": tensor_cls.__name__, "size": list(size), "stride": list(stride), "offset": int(offset),
+           "storage_cls": storage_cls.__name__, "dtype": str(dtype).replace("torch.", ""), "device": int(device),
+           "handle": _enc(handle), "size_bytes": int(size_bytes), "offset_bytes": int(offset_bytes),
+           "requires_grad": bool(req_grad), "ref_handle": _enc(ref_handle), "ref_offset": int(ref_offset),
+           "event_handle": _enc(ev_handle), "event_sync": bool(ev_sync)}
+    store.set(key, json.dumps(rec))
 
 
 def _import(store, key: str) -> torch.Tensor:
-    import pickle
+    """Map a tensor another process of this job exported with :func:`_export`."""
     from torch.multiprocessing.reductions import rebuild_cuda_tensor
-    return rebuild_cuda_tensor(*pickle.loads(store.get(key)))  # bytes this job's own PS wrote
+    r = json.loads(store.get(key).decode())
+    dtype = getattr(torch, r["dtype"])
+    if not isinstance(dtype, torch.dtype):
+        raise ValueError(f"bad dtype {r['dtype']!r} in {key}")
+    return rebuild_cuda_tensor(_TENSOR_CLS[r["tensor_cls"]], torch.Size(r["size"]), tuple(r["stride"]),
+                               int(r["offset"]), _STORAGE_CLS[r["storage_cls"]], dtype, int(r["device"]),
+                               _dec(r["handle"]), int(r["size_bytes"]), int(r["offset_bytes"]),
+                               bool(r["requires_grad"]), _dec(r["ref_handle"]), int(r["ref_offset"]),
+                               _dec(r["event_handle"]), bool(r["event_sync"]))
 
 
-class DeviceAsyncPSServer:
+CANARY_N = 64
+
+
+def _canary_values(nonce: int) -> torch.Tensor:
+    return torch.arange(CANARY_N, dtype=torch.float32) * 0.5 + float(nonce % 1000003)
+
+
+class DeviceAsyncPSServer(_Service):
     """PS task ``ps_index`` with its variables in GPU memory (see module docstring)."""
 
     def __init__(self, init_params: Sequence[Tuple[str, torch.Tensor]], num_workers: int, num_ps: int, ps_index: int,
                  store, device, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, optimizer: str = "adam",
-                 group=None):
+                 group=None, aggregate: int = 0, channels_last: bool = False):
         self.W, self.P, self.idx = num_workers, num_ps, ps_index
         shapes = [(n, p.shape) for n, p in init_params]
         self.assignment = ps_assignment(list(init_params), num_ps)
-        self.names, n = _layout(shapes, self.assignment, ps_index)
+        self.runs, n = device_layout(shapes, self.assignment, ps_index)
+        self._shapes = shapes
+        self.names = [x for run in self.runs for x in run[0]]
         src = dict(init_params)
         self.device = device
-        npad = (n + 7) // 8 * 8  # the fused Adam kernel moves 8 values per thread; the tail stays 0
+        npad = max(_round_up(n, ALIGN), ALIGN)  # the fused Adam kernel moves 8 values per thread
         self.w = torch.zeros(npad, dtype=torch.float32, device=device)
-        if self.names:
-            self.w[:n].copy_(torch.cat([src[k].detach().float().reshape(-1) for k in self.names]))
+        for names, offs, start, _ in self.runs:
+            for name, o in zip(names, offs):
+                t = _flat_order(src[name].detach().float(), channels_last)
+                self.w[start + o:start + o + t.numel()].copy_(t)
         self.m = torch.zeros_like(self.w)
         self.v = torch.zeros_like(self.w)
-        self.mail = torch.zeros(num_workers, max(npad, 8), dtype=torch.float32, device=device)
+        self.mail = torch.zeros(num_workers, npad, dtype=torch.float32, device=device)
+        self.stage = torch.empty(npad, dtype=torch.float32)  # host-transport payloads
         self.lr, self.betas, self.eps, self.opt = lr, betas, eps, optimizer
-        self.t = 0
-        self.global_step = 0
         self.group = group
+        self._init_service(aggregate)
+        nonce = int.from_bytes(os.urandom(4), "little")
+        self.canary = _canary_values(nonce).to(device)
         torch.cuda.synchronize(device)
         _export(store, _ipc_key(ps_index, "w"), self.w)
         _export(store, _ipc_key(ps_index, "mail"), self.mail)
+        _export(store, _ipc_key(ps_index, "canary"), self.canary)
+        store.set(_ipc_key(ps_index, "nonce"), str(nonce))
         store.set(_ipc_key(ps_index, "ready"), "1")
 
-    def _apply(self, g: torch.Tensor) -> None:
+    def _apply(self, g: torch.Tensor, scale: float = 1.0) -> None:
         from ..ops import _lib, optim  # noqa: F401  (optim registers kfa_adam_step)
         self.t += 1
         n = self.w.numel()
-        if n == 0:
-            return
         if self.opt == "sgd":
-            self.w.add_(g, alpha=-self.lr)
-            return
-        b1, b2 = self.betas
-        bc1, bc2 = 1.0 - b1 ** self.t, 1.0 - b2 ** self.t
-        # TF AdamOptimizer form (eps outside the bias-corrected sqrt) with the fused HIP kernel
-        _lib.call("kfa_adam_step", _lib.ptr(self.w), None, _lib.ptr(g), 0, _lib.ptr(self.m), _lib.ptr(self.v), n,
-                  self.lr, b1, b2, self.eps / math.sqrt(bc2), 0.0, bc1, bc2, 1.0, None, _lib.stream())
+            self.w.add_(g, alpha=-self.lr * scale)
+        else:
+            b1, b2 = self.betas
+            bc1, bc2 = 1.0 - b1 ** self.t, 1.0 - b2 ** self.t
+            # TF AdamOptimizer form (eps outside the bias-corrected sqrt) with the fused HIP kernel
+            _lib.call("kfa_adam_step", _lib.ptr(self.w), None, _lib.ptr(g), 0, _lib.ptr(self.m), _lib.ptr(self.v), n,
+                      self.lr, b1, b2, self.eps / math.sqrt(bc2), 0.0, bc1, bc2, scale, None, _lib.stream())
+        # the reply below tells the pusher its mailbox may be rewritten: the update must have read it
+        torch.cuda.current_stream(self.device).synchronize()
 
-    def serve(self, log=None) -> int:
-        active = self.W
-        hdr = torch.zeros(2, dtype=torch.int64)
-        pushes = 0
-        n = self.w.numel()  # padded length (the mailbox tail beyond the variables is never written: 0)
-        while active > 0:
-            src = dist.recv(hdr, src=None, group=self.group, tag=TAG_HDR)
-            op = int(hdr[0])
-            if op == PUSH:
-                self._apply(self.mail[src, :n])
-                torch.cuda.current_stream(self.device).synchronize()  # mailbox consumed, update visible
-                pushes += 1
-                self.global_step += 1
-                dist.send(torch.tensor([self.global_step], dtype=torch.int64), src, group=self.group,
-                          tag=TAG_REPLY)
-                if log and self.global_step % 50 == 0:
-                    log(f"PS {self.idx}: applied {self.global_step} updates")
-            elif op == DONE:
-                active -= 1
-            else:
-                raise RuntimeError(f"PS {self.idx}: bad request {op} from rank {src}")
-        return pushes
+    def _send_vars(self, src: int) -> None:  # a host-transport client (IPC mapping failed on its side)
+        self.stage.copy_(self.w)
+        dist.send(self.stage, src, group=self.group, tag=TAG_DATA)
+
+    def _recv_grad(self, src: int, op: int) -> torch.Tensor:
+        if op == PUSH_DEV:
+            return self.mail[src]
+        dist.recv(self.stage, src, group=self.group, tag=TAG_DATA)
+        self.mail[src].copy_(self.stage, non_blocking=False)
+        return self.mail[src]
+
+    def variables(self) -> Dict[str, torch.Tensor]:
+        """name -> view of this PS's fp32 variable (worker memory order, flattened)."""
+        out = {}
+        shapes = dict(self._shapes)
+        for names, offs, start, _ in self.runs:
+            for name, o in zip(names, offs):
+                n = int(torch.Size(shapes[name]).numel())
+                out[name] = self.w[start + o:start + o + n]
+        return out
+
+    def _acc_reset(self) -> None:
+        if not hasattr(self, "acc"):
+            self.acc = torch.zeros_like(self.w)
+        else:
+            self.acc.zero_()
+
+    def _acc_add(self, g: torch.Tensor) -> None:
+        self.acc.add_(g)
+        torch.cuda.current_stream(self.device).synchronize()  # the mailbox may be reused after the reply
+
+    def _acc(self) -> torch.Tensor:
+        return self.acc
 
 
-class DeviceAsyncPSClient:
-    """Worker side of the device transport: pulls and pushes are D2D copies."""
+class DeviceAsyncPSClient(_ClientSteps):
+    """Worker side of the device transport.
+
+    The worker's parameters are re-homed into per-PS flat buffers
+    (``parallel.flat.FlatGroup``: one for the bf16 matrices, one for the fp32
+    vectors, laid out like :func:`device_layout`), their gradients too, so each
+    pull / push is one device copy per PS and run.  Each PS's mapping is
+    checked against its canary first; a PS whose memory cannot be mapped is
+    served over the host transport (``transports[k] == "host"``)."""
 
     def __init__(self, params: Sequence[Tuple[str, torch.nn.Parameter]], num_workers: int, num_ps: int, rank: int,
-                 store, group=None, timeout: float = 300.0):
+                 store, group=None, timeout: float = 300.0, log: Optional[Callable[[str], None]] = None):
         import time
+
+        from .flat import FlatGroup
         self.W, self.P, self.rank, self.group = num_workers, num_ps, rank, group
         self.params = list(params)
         self.assignment = ps_assignment(self.params, num_ps)
         shapes = [(n, p.shape) for n, p in self.params]
         by_name = dict(self.params)
         self.plan = []
+        self.transports: List[str] = []
+        log = log or (lambda s: print(s, flush=True))
         t0 = time.time()
         for k in range(num_ps):
-            names, n = _layout(shapes, self.assignment, k)
+            runs, total = device_layout(shapes, self.assignment, k)
+            groups = []
+            for names, _, start, length in runs:
+                g = FlatGroup([by_name[x] for x in names], pad_to=ALIGN, master=False, name=f"ps{k}")
+                assert g.numel == length, (g.numel, length)
+                groups.append((g, start))
             while True:  # the PS publishes its buffers once its variables are on the GPU
                 try:
                     if store.check([_ipc_key(k, "ready")]):
@@ -284,44 +507,67 @@ class DeviceAsyncPSClient:
                 if time.time() - t0 > timeout:
                     raise TimeoutError(f"PS {k} did not publish its device buffers")
                 time.sleep(0.05)
-            w = _import(store, _ipc_key(k, "w"))
-            mail = _import(store, _ipc_key(k, "mail"))
-            self.plan.append((num_workers + k, [by_name[x] for x in names], w, mail[rank], n))
-        self._hdr = torch.zeros(2, dtype=torch.int64)
+            w = mail = None
+            try:
+                nonce = int(store.get(_ipc_key(k, "nonce")).decode())
+                canary = _import(store, _ipc_key(k, "canary"))
+                got = canary.cpu()
+                if not torch.equal(got, _canary_values(nonce)):
+                    raise RuntimeError(f"canary mismatch (read {got[:4].tolist()}...)")
+                w = _import(store, _ipc_key(k, "w"))
+                mail = _import(store, _ipc_key(k, "mail"))[rank]
+                if w.numel() < total:
+                    raise RuntimeError(f"PS buffer has {w.numel()} values, layout needs {total}")
+                self.transports.append("device")
+            except Exception as e:  # noqa: BLE001 — any mapping failure: fall back, loudly
+                log(f"Worker {rank}: WARNING: HIP IPC mapping of PS {k}'s device buffers failed ({e}); "
+                    f"using the HOST transport for PS {k} (gloo, slower)")
+                self.transports.append("host")
+                w = mail = None
+            stage = torch.empty(max(_round_up(total, ALIGN), ALIGN), dtype=torch.float32) \
+                if self.transports[-1] == "host" else None
+            self.plan.append((num_workers + k, groups, w, mail, stage))
+        self._init_steps(num_ps)
+
+    def zero_grad(self) -> None:
+        for _, groups, *_ in self.plan:
+            for g, _ in groups:
+                g.zero_grad()
 
     @torch.no_grad()
     def pull(self) -> None:
-        for _, ps, w, _, n in self.plan:
-            off = 0
-            for p in ps:
-                k = p.numel()
-                p.copy_(w[off:off + k].view_as(p))   # device-to-device (peer) copy + cast
-                off += k
+        for rank, groups, w, _, stage in self.plan:
+            if not groups:
+                continue
+            if stage is not None:
+                self._header(rank, PULL)
+                dist.recv(stage, rank, group=self.group, tag=TAG_DATA)
+                src = stage
+            else:
+                src = w
+            for g, start in groups:
+                g.data.copy_(src[start:start + g.numel])  # D2D (peer) copy + cast, or H2D
 
     @torch.no_grad()
     def push(self) -> int:
         step = -1
-        reply = torch.zeros(1, dtype=torch.int64)
-        for k, (rank, ps, _, mail, n) in enumerate(self.plan):
-            if not ps:
+        for k, (rank, groups, _, mail, stage) in enumerate(self.plan):
+            if not groups:
                 continue
-            off = 0
-            for p in ps:
-                c = p.numel()
-                if p.grad is None:
-                    mail[off:off + c].zero_()
-                else:
-                    mail[off:off + c].copy_(p.grad.reshape(-1))
-                off += c
-            torch.cuda.current_stream(mail.device).synchronize()  # the mailbox is written before the header
-            self._hdr[0] = PUSH
-            dist.send(self._hdr, rank, group=self.group, tag=TAG_HDR)
-            dist.recv(reply, rank, group=self.group, tag=TAG_REPLY)
+            dst = stage if stage is not None else mail
+            for g, start in groups:
+                dst[start:start + g.numel].copy_(g.grad)
+            if stage is None:
+                torch.cuda.current_stream(mail.device).synchronize()  # mailbox written before the header
+                self._header(rank, PUSH_DEV, self.tags[k])
+            else:
+                self._header(rank, PUSH, self.tags[k])
+                dist.send(stage, rank, group=self.group, tag=TAG_DATA)
+            s = self._await_reply(k, rank)
             if k == 0:
-                step = int(reply[0])
+                step = s
         return step
 
     def done(self) -> None:
-        self._hdr[0] = DONE
         for rank, *_ in self.plan:
-            dist.send(self._hdr, rank, group=self.group, tag=TAG_HDR)
+            self._header(rank, DONE)

@@ -30,12 +30,17 @@ class DistInfo:
         return self.rank == 0
 
 
-def init_distributed(backend: Optional[str] = None, prefer_gpu: bool = True) -> DistInfo:
+def init_distributed(backend: Optional[str] = None, prefer_gpu: bool = True,
+                     timeout_s: Optional[float] = None) -> DistInfo:
     """Initialise from torchrun-style env (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR/PORT).
 
     ``KFA_DIST_BACKEND=gloo`` forces gloo even on GPUs: a rehearsal of the
     multi-rank path with several ranks sharing one GPU (RCCL refuses two ranks
-    on one device in a communicator)."""
+    on one device in a communicator).
+
+    ``timeout_s`` (default ``KFA_DIST_INIT_TIMEOUT`` or 300 s) bounds the
+    rendezvous and every collective: a rank that never arrives fails the job
+    with an error instead of hanging it (RCCL: async error handling on)."""
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -54,7 +59,11 @@ def init_distributed(backend: Optional[str] = None, prefer_gpu: bool = True) -> 
     if world > 1 and not dist.is_initialized():
         be = backend or os.environ.get("KFA_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
         kw = {"device_id": dev} if (be == "nccl" and use_gpu) else {}
-        dist.init_process_group(be, rank=rank, world_size=world, **kw)
+        if be == "nccl":
+            os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        import datetime
+        t = float(timeout_s if timeout_s is not None else os.environ.get("KFA_DIST_INIT_TIMEOUT", "300"))
+        dist.init_process_group(be, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=t), **kw)
     return DistInfo(rank, world, local, dev)
 
 

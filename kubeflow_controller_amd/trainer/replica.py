@@ -117,11 +117,37 @@ def synthetic_batch(args, model, device, rank: int):
     raise ValueError(args.model)
 
 
+def _aggregate(spec: ClusterSpec, args) -> int:
+    """Gradients per update on the PS service loop: 0 = async (the reference's
+    default); ``--sync_replicas`` aggregates ``--replicas_to_aggregate``
+    (default: every worker), ``mnist_replica.py:172-182``."""
+    if not args.sync_replicas:
+        return 0
+    n = args.replicas_to_aggregate if args.replicas_to_aggregate is not None else spec.num_workers
+    if not 1 <= n <= spec.num_workers:
+        raise SystemExit(f"--replicas_to_aggregate {n}: must be in 1..{spec.num_workers} (the number of workers)")
+    return n
+
+
 def _async_mode(spec: ClusterSpec, args) -> bool:
+    """True: the PS service loop (``parallel/async_ps.py``) — async pushes, or
+    ``--sync_replicas`` aggregation of N < W gradients with stale ones dropped.
+    False: the collective path (RCCL reduce-scatter / all-gather or all-reduce),
+    which always aggregates every worker's gradient, so it refuses N != W."""
+    n = args.replicas_to_aggregate
+    partial = args.sync_replicas and n is not None and n != spec.num_workers
     if spec.is_local or not spec.ps:
+        if partial and not spec.is_local:
+            raise SystemExit(f"--replicas_to_aggregate {n} with {spec.num_workers} workers needs PS tasks: the "
+                             "all-reduce path sums every worker's gradient (no PS to drop stale ones)")
         return False
     if args.ps_mode == "auto":  # the reference's default update mode is async (no --sync_replicas)
+        if partial:
+            return True
         return not args.sync_replicas and (args.model.startswith("mnist") or args.ps_transport == "device")
+    if args.ps_mode == "collective" and partial:
+        raise SystemExit(f"--replicas_to_aggregate {n} != {spec.num_workers} workers is not supported by "
+                         "--ps_mode collective (reduce-scatter aggregates every worker); use --ps_mode async")
     return args.ps_mode == "async"
 
 
@@ -161,17 +187,22 @@ def run_ps_async(spec: ClusterSpec, args) -> int:
     if spec.task_index == 0:
         store.set(TRANSPORT_KEY, transport)
     model, _, _ = build(args, torch.device("cpu"))
+    agg = _aggregate(spec, args)
     if transport == "device":
         torch.cuda.set_device(0)
         server = DeviceAsyncPSServer(list(model.named_parameters()), W, P, spec.task_index, store,
-                                     torch.device("cuda", 0), lr=args.learning_rate, optimizer=args.optimizer)
+                                     torch.device("cuda", 0), lr=args.learning_rate, optimizer=args.optimizer,
+                                     aggregate=agg, channels_last=model.__class__.__name__ == "ResNet")
     else:
         server = AsyncPSServer(list(model.named_parameters()), W, P, spec.task_index, lr=args.learning_rate,
-                               optimizer=args.optimizer)
+                               optimizer=args.optimizer, aggregate=agg)
     _log(f"PS {spec.task_index}: serving {len(server.names)} variables ({server.w.numel()} values), "
-         f"{transport}-resident ({'GPU HBM, HIP IPC pull/push' if transport == 'device' else 'host memory, gloo'})")
+         f"{transport}-resident ({'GPU HBM, HIP IPC pull/push' if transport == 'device' else 'host memory, gloo'}), "
+         + (f"sync replicas: mean of {agg} of {W} workers' gradients per update, stale ones dropped" if agg
+            else "async updates"))
     pushes = server.serve(log=_log)
-    _log(f"PS {spec.task_index}: all {W} workers done after {pushes} updates; exiting")
+    _log(f"PS {spec.task_index}: all {W} workers done; {pushes} gradients applied in {server.global_step} updates, "
+         f"{server.dropped} stale dropped; exiting")
     dist.destroy_process_group()
     return 0
 
@@ -203,11 +234,17 @@ def run_worker_async(spec: ClusterSpec, args) -> int:
     if transport == "device" and not use_gpu:
         raise SystemExit("device-resident async PS needs GPU workers")
     if transport == "device":
-        client = DeviceAsyncPSClient(list(model.named_parameters()), W, P, spec.task_index, store)
+        client = DeviceAsyncPSClient(list(model.named_parameters()), W, P, spec.task_index, store, log=_log)
+        zero_grad = client.zero_grad
+        transport = "+".join(sorted(set(client.transports)))
     else:
         client = AsyncPSClient(list(model.named_parameters()), W, P)
+        zero_grad = lambda: model.zero_grad(set_to_none=False)  # noqa: E731
+    agg = _aggregate(spec, args)
     _log(f"Worker {spec.task_index}: {W} workers, {P} ps, device {device}, model {args.model}, "
-         f"{sum(p.numel() for p in model.parameters())} params, async parameter server ({transport} transport)")
+         f"{sum(p.numel() for p in model.parameters())} params, "
+         f"{'sync replicas (%d of %d aggregated)' % (agg, W) if agg else 'async'} parameter server "
+         f"({transport} transport)")
     fixed = None if data is not None else synthetic_batch(args, model, device, spec.task_index)
     t_begin = time.time()
     _log(f"Training begins @ {t_begin:f}")
@@ -219,7 +256,7 @@ def run_worker_async(spec: ClusterSpec, args) -> int:
         else:
             batch = fixed
         client.pull()
-        model.zero_grad(set_to_none=False)
+        zero_grad()
         loss = loss_fn(model, *batch)
         loss.backward()
         global_step = client.push()
@@ -235,6 +272,8 @@ def run_worker_async(spec: ClusterSpec, args) -> int:
     if t_first is not None and local_step > 1:
         sps = (local_step - 1) / max(t_end - t_first, 1e-9)
         _log(f"Steady-state: {sps:.1f} steps/s/worker, {sps * args.batch_size:.1f} examples/s (this worker)")
+    if agg:
+        _log(f"Worker {spec.task_index}: {local_step} pushes, {client.pushes_dropped} dropped as stale")
     client.pull()  # evaluate the PS's current variables, as the reference's session does
     client.done()
     if data is not None:
@@ -301,6 +340,9 @@ def run_worker(spec: ClusterSpec, args) -> int:
         torch.cuda.set_device(0)
     world = 1 if spec.is_local else spec.num_workers
     rank = 0 if spec.is_local else spec.task_index
+    if args.replicas_to_aggregate is not None and not spec.is_local and args.replicas_to_aggregate != world:
+        raise SystemExit(f"--replicas_to_aggregate {args.replicas_to_aggregate} != {world} workers: the collective "
+                         "path aggregates every worker's gradient; use --ps_mode async with PS tasks")
     store = None
     if not spec.is_local:
         if world > 1:
@@ -411,6 +453,17 @@ def run_worker(spec: ClusterSpec, args) -> int:
     return 0
 
 
+def _flag(v) -> bool:
+    """TF-style boolean flag value: ``--x``, ``--x=true``, ``--x false``."""
+    if isinstance(v, bool):
+        return v
+    if str(v).lower() in ("1", "true", "yes", "t", "y"):
+        return True
+    if str(v).lower() in ("0", "false", "no", "f", "n"):
+        return False
+    raise argparse.ArgumentTypeError(f"expected a boolean, got {v!r}")
+
+
 def build_parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     add_cluster_flags(ap)
@@ -433,7 +486,14 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--ps_transport", default="auto", choices=["auto", "host", "device"],
                     help="async PS payloads: device = variables in the co-located GPU's HBM, pulled / pushed by "
                          "HIP IPC device copies; host = CPU tensors over gloo; auto = device when the PS has a GPU")
-    ap.add_argument("--replicas_to_aggregate", type=int, default=None, help="accepted; = #workers")
+    ap.add_argument("--replicas_to_aggregate", type=int, default=None,
+                    help="with --sync_replicas: gradients averaged per update (default: number of workers); "
+                         "N < workers runs the PS service loop, which drops stale gradients")
+    ap.add_argument("--existing_servers", type=_flag, nargs="?", const=True, default=False,
+                    help="accepted for compatibility (no in-process gRPC server exists here; the job's "
+                         "rendezvous store plays that part)")
+    ap.add_argument("--download_only", type=_flag, nargs="?", const=True, default=False,
+                    help="prepare the data set and exit 0 (synthetic data: nothing to download)")
     ap.add_argument("--num_gpus", type=int, default=1, help="accepted (one GPU per replica)")
     ap.add_argument("--data_dir", default="", help="accepted (synthetic data; no network)")
     ap.add_argument("--model_dir", default=os.environ.get("KFA_MODEL_DIR", ""),
@@ -459,7 +519,17 @@ def build_parser() -> argparse.ArgumentParser:
 
 def main(argv: Optional[list] = None) -> int:
     args = build_parser().parse_args(argv)
+    if args.download_only:  # mnist_replica.py:94-96: read the data set, then exit before any cluster work
+        if args.model.startswith("mnist"):
+            from ..models import mnist
+            d = mnist.SyntheticMNIST(seed=args.seed)
+            _log(f"data ready: synthetic MNIST, {len(d.train[0])} training examples (--download_only)")
+        else:
+            _log(f"data ready: synthetic {args.model} batches are generated in-process (--download_only)")
+        return 0
     spec = parse_cluster(args)
+    if not spec.is_local:
+        _aggregate(spec, args)  # validates --replicas_to_aggregate before any connection is made
     if _async_mode(spec, args):
         return run_ps_async(spec, args) if spec.is_ps else run_worker_async(spec, args)
     if spec.is_ps:

@@ -23,7 +23,7 @@ def _free_port():
     return p
 
 
-def _proc(rank, W, P, port, out):
+def _proc(rank, W, P, port, out, opt, agg):
     sys.path.insert(0, ROOT)
     import datetime
 
@@ -37,42 +37,64 @@ def _proc(rank, W, P, port, out):
         torch.nn.init.constant_(p, 0.5)
     if rank >= W:
         s = DeviceAsyncPSServer(list(m.named_parameters()), W, P, rank - W, store, torch.device("cuda", 0), lr=0.25,
-                                optimizer="sgd")
+                                optimizer=opt, aggregate=agg)
         pushes = s.serve()
-        torch.save({"w": s.w.cpu(), "names": s.names, "pushes": pushes}, f"{out}.ps{rank - W}")
+        torch.save({"vars": {k: v.cpu() for k, v in s.variables().items()}, "names": s.names, "pushes": pushes,
+                    "step": s.global_step}, f"{out}.ps{rank - W}")
     else:
         m = m.cuda()
         c = DeviceAsyncPSClient(list(m.named_parameters()), W, P, rank, store)
         steps = []
         for _ in range(5):
             c.pull()
-            for p in m.parameters():
-                p.grad = torch.full_like(p, float(rank + 1))
+            c.zero_grad()
+            for p in m.parameters():   # the grads are views of the client's flat buffers
+                p.grad.fill_(1.0 if opt == "adam" else float(rank + 1))
             steps.append(c.push())
         c.pull()
         final = {n: p.detach().cpu().clone() for n, p in m.named_parameters()}
         c.done()
-        torch.save({"steps": steps, "final": final}, f"{out}.w{rank}")
+        torch.save({"steps": steps, "final": final, "transports": c.transports}, f"{out}.w{rank}")
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_device_async_ps_applies_every_push_once(tmp_path):
+@pytest.mark.parametrize("opt,agg", [("sgd", 0), ("adam", 0), ("adam", 2)])
+def test_device_async_ps_matches_host_server(tmp_path, opt, agg):
+    """Every push applied once (async) or every 2 averaged (sync replicas), the
+    variables equal the host PS's TF-form update on the same gradients (Adam:
+    fused HIP kernel vs AsyncPSServer._apply in fp32), and every client mapped
+    the PS memory (canary check passed: device transport, no host fallback)."""
+    from kubeflow_controller_amd.parallel.async_ps import AsyncPSServer
     W, P = 2, 2
     out = str(tmp_path / "dps")
-    mp.start_processes(_proc, args=(W, P, _free_port(), out), nprocs=W + P, join=True, start_method="spawn")
-    total = 0.25 * 5 * sum(range(1, W + 1))
+    mp.start_processes(_proc, args=(W, P, _free_port(), out, opt, agg), nprocs=W + P, join=True,
+                       start_method="spawn")
     names = ["0.weight", "0.bias", "1.weight", "1.bias"]
+    updates = 5 if agg else 5 * W
     for k in range(P):
         ps = torch.load(f"{out}.ps{k}", weights_only=True)
-        assert ps["names"] == names[k::P] and ps["pushes"] == 5 * W
-        torch.testing.assert_close(ps["w"], torch.full_like(ps["w"], 0.5 - total))
+        assert sorted(ps["names"]) == sorted(names[k::P]) and ps["pushes"] == 5 * W and ps["step"] == updates
+        for n, v in ps["vars"].items():
+            if opt == "sgd":
+                want = torch.full_like(v, 0.5 - 0.25 * 5 * sum(range(1, W + 1)))
+            else:  # constant gradient 1: the same update sequence whatever the arrival order
+                ref = AsyncPSServer([(n, torch.full((v.numel(),), 0.5))], 1, 1, 0, lr=0.25, optimizer="adam")
+                for _ in range(updates):
+                    ref._apply(torch.ones(v.numel()))
+                want = ref.w
+            torch.testing.assert_close(v, want, rtol=1e-5, atol=1e-5)
     for w in range(W):
         got = torch.load(f"{out}.w{w}", weights_only=True)
-        for n, t in got["final"].items():   # the last pull (after every push) sees the final PS values
-            assert t.min().item() >= 0.5 - total - 1e-5
+        assert got["transports"] == ["device"] * P
+        if opt == "sgd":
+            for n, t in got["final"].items():   # the last pull (after every push) sees the final PS values
+                assert t.min().item() >= 0.5 - 0.25 * 5 * sum(range(1, W + 1)) - 1e-5
     steps = sorted(s for w in range(W) for s in torch.load(f"{out}.w{w}", weights_only=True)["steps"])
-    assert steps == list(range(1, 5 * W + 1))
+    if agg:
+        assert steps == sorted(list(range(1, 6)) * W)
+    else:
+        assert steps == list(range(1, 5 * W + 1))
 
 
 def test_replica_async_bert_tiny_device_transport(tmp_path):

@@ -176,6 +176,39 @@ def test_bench_launches_ranks_itself():
     assert res["value"] > 0
 
 
+def test_bench_ps_layout_reports_workers_and_ps():
+    """``bench.py --gpus 2 --ps 1``: the '2 workers + 1 PS' BASELINE layout
+    (reference examples/tfjob/dist.yml) through the reduce-scatter / owner-apply /
+    all-gather path, reported as parallelism "2w1ps"."""
+    env = dict(os.environ, KFA_DIST_BACKEND="gloo", OMP_NUM_THREADS="2")
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--ps", "1", "--steps", "2",
+                        "--warmup", "1", "--batch", "4", "--image", "32", "--model", "resnet_tiny", "--device",
+                        "cpu"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    res = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][0])
+    assert res["n_gpus"] == 2 and res["config"]["parallelism"] == "2w1ps"
+    assert res["value"] > 0 and res["config"]["loss"] == res["config"]["loss"]
+
+
+def test_bench_watchdog_kills_a_hung_rank_and_names_it():
+    """One rank stuck before the timed region (the others wait in the barrier):
+    the per-rank watchdog dumps every rank's stack and the job exits non-zero
+    well inside the watchdog + backstop, with the stuck rank's frame shown."""
+    import time
+    env = dict(os.environ, KFA_DIST_BACKEND="gloo", OMP_NUM_THREADS="2", KFA_BENCH_HANG_RANK="1")
+    env.pop("WORLD_SIZE", None)
+    t0 = time.monotonic()
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2",
+                        "--warmup", "1", "--batch", "4", "--image", "32", "--model", "resnet_tiny", "--device",
+                        "cpu", "--watchdog", "25"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    dt = time.monotonic() - t0
+    assert p.returncode != 0
+    assert dt < 25 + 60 + 30, dt
+    assert "[rank 1]" in p.stderr and "_test_hang" in p.stderr, p.stderr[-4000:]
+    assert "---- rank 1 ----" in p.stderr
+
+
 def test_bench_rejects_world_mismatch():
     env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--model", "resnet_tiny",

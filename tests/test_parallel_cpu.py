@@ -247,6 +247,82 @@ def test_async_ps_applies_every_push_exactly_once(tmp_path):
     assert steps == list(range(1, 7 * W + 1))                  # every push advanced the global step once
 
 
+def _agg_worker(rank, W, P, N, port, target, out):
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    from kubeflow_controller_amd.parallel.async_ps import AsyncPSClient, AsyncPSServer
+    torch.set_num_threads(1)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=W + P)
+    m = torch.nn.Sequential(torch.nn.Linear(64, 8), torch.nn.Linear(8, 4))
+    for p in m.parameters():
+        torch.nn.init.constant_(p, 0.5)
+    if rank >= W:
+        s = AsyncPSServer(list(m.named_parameters()), W, P, rank - W, lr=0.25, optimizer="sgd", aggregate=N)
+        s.serve()
+        torch.save({"w": s.w, "step": s.global_step, "applied": s.applied_pushes, "dropped": s.dropped,
+                    "sizes": s.update_sizes}, f"{out}.ps{rank - W}")
+    else:
+        import time
+        c = AsyncPSClient(list(m.named_parameters()), W, P)
+        step, pushes = 0, 0
+        while step < target:
+            c.pull()
+            for p in m.parameters():
+                p.grad = torch.ones_like(p)
+            if rank == 0:
+                time.sleep(0.01)  # an uneven pace makes some pushes stale
+            step = c.push()
+            pushes += 1
+        c.done()
+        torch.save({"pushes": pushes, "dropped": c.pushes_dropped}, f"{out}.w{rank}")
+    dist.destroy_process_group()
+
+
+def test_sync_replicas_aggregates_n_of_w_and_drops_stale(tmp_path):
+    """--sync_replicas --replicas_to_aggregate 2 with 3 workers (mnist_replica.py:172-182):
+    each update is the MEAN of 2 fresh gradients, pushes computed on an older step
+    are dropped, the global step counts updates, and no worker is left waiting."""
+    W, P, N, target = 3, 2, 2, 12
+    out = str(tmp_path / "agg")
+    mp.start_processes(_agg_worker, args=(W, P, N, _free_port(), target, out), nprocs=W + P, join=True,
+                       start_method="spawn")
+    ws = [torch.load(f"{out}.w{r}", weights_only=True) for r in range(W)]
+    total_pushes = sum(w["pushes"] for w in ws)
+    for k in range(P):
+        ps = torch.load(f"{out}.ps{k}", weights_only=True)
+        assert ps["step"] >= target and ps["step"] == len(ps["sizes"])
+        assert ps["applied"] + ps["dropped"] == total_pushes          # every push accepted or dropped once
+        assert sum(ps["sizes"]) == ps["applied"]
+        assert all(1 <= n <= N for n in ps["sizes"]) and ps["sizes"].count(N) >= target - 2
+        # all gradients are 1: every update applies a mean of 1 -> w = 0.5 - lr * updates
+        torch.testing.assert_close(ps["w"], torch.full_like(ps["w"], 0.5 - 0.25 * ps["step"]))
+    ps0 = torch.load(f"{out}.ps0", weights_only=True)
+    assert sum(w["dropped"] for w in ws) >= ps0["dropped"] > 0
+
+
+def test_replicas_to_aggregate_rejected_where_it_cannot_hold():
+    """The collective path sums every worker's gradient: N != W is an error, not ignored."""
+    from kubeflow_controller_amd.trainer import replica
+    base = ["--model", "mnist_mlp", "--sync_replicas", "--replicas_to_aggregate", "1",
+            "--worker_hosts=127.0.0.1:1,127.0.0.1:2", "--job_name=worker", "--task_index=0"]
+    with pytest.raises(SystemExit, match="collective"):
+        replica.main(base + ["--ps_hosts=127.0.0.1:3", "--ps_mode", "collective"])
+    with pytest.raises(SystemExit, match="needs PS tasks"):
+        replica.main(base + ["--ps_hosts="])
+    with pytest.raises(SystemExit, match="1..2"):
+        replica.main(base[:4] + ["3"] + base[5:] + ["--ps_hosts=127.0.0.1:3"])
+
+
+def test_reference_replica_flags_accepted():
+    """--existing_servers and --download_only (mnist_replica.py:51-53,76-80) parse;
+    --download_only exits 0 once the data set is ready."""
+    from kubeflow_controller_amd.trainer import replica
+    args = replica.build_parser().parse_args(["--existing_servers", "--download_only=false"])
+    assert args.existing_servers is True and args.download_only is False
+    assert replica.main(["--download_only", "--model", "mnist_softmax"]) == 0
+
+
 def test_apply_bit_mask_matches_channels_last_bit_order():
     """ReLU bit masks cover a tensor's channels-last elements, 8 per byte, LSB first."""
     import torch
