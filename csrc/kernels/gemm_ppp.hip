@@ -1,0 +1,376 @@
+// Persistent ping-pong GEMM with the C write overlapped with the next tile's
+// main loop — SURVEY §2.6 K1 (dense GEMM + epilogue), the BERT / W&D / ResNet-FC
+// projections, forward and dgrad:
+//
+//   C[m][n] = epilogue( Σ_k A[m][k] · B[n][k] )      A [M][lda], B [N][ldb]: K-contiguous
+//
+// Main loop = gemm_pp_kernel's (gemm.hip): 256 x 256 tiles, 512 threads as two
+// wave groups one s_barrier apart (on every SIMD one wave's 16 MFMAs run under
+// the other wave's LDS reads + LDS-DMA issue), 64-deep k-tiles in four 16 KB
+// pieces, `buffer_load ... lds` with 32-bit row offsets, 8 DMAs per lane in
+// flight across the barriers, XOR-swizzled 128-B LDS rows.
+//
+// What is new is the ORDER of work around the tile boundary.  The kernel is
+// persistent (one 512-thread block per CU, XCD-aware tile ranges) and the
+// k-tile sequence of ALL of a block's tiles is one continuous pipeline: the
+// pieces of tile i+1's first k-tiles are issued while tile i's last MFMAs run.
+// Tile i's epilogue is not a separate stage: its 128 x 64 wave tile is four
+// 64 x 32 quadrants, and the ping-pong k-tile visits them in a fixed order
+// (s0: (0,0), s1: (0,1), s2: (1,1), s3: (1,0)).  In the FIRST k-tile of tile
+// i+1, phase s writes quadrant s of tile i (bf16, straight from the
+// accumulator registers) and zeroes it just before the phase's MFMAs start
+// accumulating tile i+1 into those registers.  So the 128 KB C write of a tile
+// is spread over four phases and issued while the partner wave group
+// multiplies — no LDS staging (which would need vmcnt(0) with LDS-DMA in
+// flight: hipcc drains every outstanding DMA before a C++ LDS store), no extra
+// registers, no idle MFMA pipe while C drains.
+//
+// Stores: per 16-row block a lane holds 4 consecutive columns of two 16-column
+// halves; one v_permlane16_swap per dword pair gives every lane 8 consecutive
+// columns (lanes of row fq hold columns {0, 16, 8, 24}[fq] .. +7 of the
+// quadrant), so each store is 16 B per lane, 64 contiguous bytes per row.
+//
+// vmcnt: stores and LDS-DMA share the in-order counter.  The wait of phase P
+// retires the piece issued 4 phases earlier, so it leaves in flight the pieces
+// of phases P-3..P (2 DMAs each) AND the stores of those phases:
+//   vmcnt(2 * pieces + S * store-phases among P-3..P)
+// — a store has ~1 k-tile of MFMA work (four phases) to drain before any wait
+// depends on it.  Steady k-tiles away from a tile boundary use the fixed
+// vmcnt(8); the boundary k-tiles and the pipeline tail take the runtime count.
+#include "common.h"
+
+#include <utility>
+
+namespace {
+
+constexpr int BK = 64;
+constexpr int PIECE = 128 * BK * 2;  // bytes per LDS piece (128 rows x 64 k)
+constexpr unsigned kOOB = 0x80000000u;
+
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+typedef __attribute__((ext_vector_type(2))) float floatx2_t;
+
+// two floats -> packed bf16x2 (v_cvt_pk_bf16_f32: round to nearest even, NaN kept)
+__device__ __forceinline__ unsigned cvt2(float lo, float hi) {
+  const floatx2_t f = {lo, hi};
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(f, bf16x2_t));
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, int voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
+}
+
+__device__ __forceinline__ void store16(__amdgpu_buffer_rsrc_t r, unsigned off, uint4 v) {
+  using V = decltype(__builtin_amdgcn_raw_buffer_load_b128(r, 0, 0, 0));
+  __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<V*>(&v), r, off, 0, 0);
+}
+
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (even, 0..62)
+__device__ __forceinline__ void vm_wait_rt(int n) {
+  switch (n) {
+#define KFA_VMW(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+    KFA_VMW(0) KFA_VMW(2) KFA_VMW(4) KFA_VMW(6) KFA_VMW(8) KFA_VMW(10) KFA_VMW(12) KFA_VMW(14)
+    KFA_VMW(16) KFA_VMW(18) KFA_VMW(20) KFA_VMW(22) KFA_VMW(24) KFA_VMW(26) KFA_VMW(28) KFA_VMW(30)
+    KFA_VMW(32) KFA_VMW(34) KFA_VMW(36) KFA_VMW(38) KFA_VMW(40) KFA_VMW(42) KFA_VMW(44) KFA_VMW(46)
+    KFA_VMW(48) KFA_VMW(50) KFA_VMW(52) KFA_VMW(54) KFA_VMW(56) KFA_VMW(58) KFA_VMW(60) KFA_VMW(62)
+#undef KFA_VMW
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+struct PppArgs {
+  const bf16_t* A;
+  const bf16_t* B;
+  bf16_t* C;
+  int M, N, K, lda, ldb, ldc;
+  unsigned c_bytes;
+};
+
+constexpr int kStoresPerPhase = 4;  // one 16-B store per 16-row block of a 64 x 32 quadrant
+
+__global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
+  constexpr int TM = 8, TN = 4;
+  __shared__ __attribute__((aligned(16))) char smem[2 * 4 * PIECE];  // 128 KB: two k-tiles of four pieces
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  // T1: blocks that share an XCD (blockIdx % 8) get consecutive logical indices,
+  // so the tiles an XCD runs at one time are neighbours in the grouped raster
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q8 = nwg >> 3, r8 = nwg & 7, x8 = bid & 7;
+  const int lc = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + (bid >> 3);
+  const int ntn = (g.N + 255) / 256, ntm = (g.M + 255) / 256, ntiles = ntm * ntn;
+  const int my_tiles = lc < ntiles ? (ntiles - 1 - lc) / nwg + 1 : 0;
+  const int nk = g.K / BK;
+  const int J = my_tiles * nk;  // k-tiles this block runs, all tiles back to back
+  if (J == 0) return;
+  constexpr int GM = 4;
+  auto tile_mn = [&](int i, int& m0, int& n0) __attribute__((always_inline)) {
+    const int wg = lc + i * nwg;
+    const int grp = wg / (GM * ntn), gm0 = grp * GM, gmn = min(GM, ntm - gm0), rem = wg - grp * GM * ntn;
+    m0 = (gm0 + rem % gmn) * 256;
+    n0 = (rem / gmn) * 256;
+  };
+
+  const __amdgpu_buffer_rsrc_t rA = rsrc(g.A, (unsigned)(((long)(g.M - 1) * g.lda + g.K) * 2));
+  const __amdgpu_buffer_rsrc_t rB = rsrc(g.B, (unsigned)(((long)(g.N - 1) * g.ldb + g.K) * 2));
+  const __amdgpu_buffer_rsrc_t rC = rsrc(g.C, g.c_bytes);
+  // DMA plan: instruction j of wave w fills piece rows j*64 + w*8 + lane/8,
+  // physical chunk lane&7 <- logical chunk (lane&7) ^ ((row >> 1) & 7)
+  const int prow = wave * 8 + (lane >> 3);
+  const int lcx = (lane & 7) ^ ((prow >> 1) & 7);
+  int voff[4][2];
+  // piece p of tile (m0, n0): A pieces 0 (rows h=0) / 3 (h=1), B pieces 1 (h=0) / 2 (h=1)
+  auto set_voff = [&](int p, int m0, int n0) __attribute__((always_inline)) {
+    const int h = (p == 2 || p == 3) ? 1 : 0;
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      if (p == 0 || p == 3) {
+        const int m = m0 + j * 128 + h * 64 + prow;
+        voff[p][j] = m < g.M ? (m * g.lda + lcx * 8) * 2 : (int)kOOB;
+      } else {
+        const int n = n0 + (2 * j + (prow >> 5)) * 64 + h * 32 + (prow & 31);
+        voff[p][j] = n < g.N ? (n * g.ldb + lcx * 8) * 2 : (int)kOOB;
+      }
+    }
+  };
+  // issue cursors: X feeds pieces 2, 3 (k-tile u+1 in k-tile u), Y pieces 0, 1 (k-tile u+2)
+  int xg = 0, xkt = 0, xti = 0, yg = 0, ykt = 0, yti = 0;
+  {
+    int m0, n0;
+    tile_mn(0, m0, n0);
+#pragma unroll
+    for (int p = 0; p < 4; p++) set_voff(p, m0, n0);
+  }
+  auto issue = [&](auto pc) __attribute__((always_inline)) {
+    constexpr int p = decltype(pc)::value;
+    constexpr bool X = (p == 2 || p == 3);
+    int& cg = X ? xg : yg;
+    int& ckt = X ? xkt : ykt;
+    int& cti = X ? xti : yti;
+    if (cg < J) {
+      char* dst = smem + (cg & 1) * (4 * PIECE) + p * PIECE + wave * 8 * 128;
+      const __amdgpu_buffer_rsrc_t r = (p == 0 || p == 3) ? rA : rB;
+      dma16(r, dst, voff[p][0], ckt * BK * 2);
+      dma16(r, dst + 64 * 128, voff[p][1], ckt * BK * 2);
+    }
+    if (p == 1 || p == 3) {  // the cursor's second piece: advance to its next k-tile
+      cg++;
+      if (++ckt == nk) {
+        ckt = 0;
+        if (++cti < my_tiles) {
+          int m0, n0;
+          tile_mn(cti, m0, n0);
+          set_voff(X ? 2 : 0, m0, n0);
+          set_voff(X ? 3 : 1, m0, n0);
+        }
+      }
+    }
+  };
+
+  const int fr = lane & 15, fq = lane >> 4;
+  const int ro0 = fr * 128 + ((fq ^ (fr >> 1)) << 4), ro1 = fr * 128 + (((4 + fq) ^ (fr >> 1)) << 4);
+  floatx4 acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; i++)
+#pragma unroll
+    for (int j = 0; j < TM; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  short8 a[4][2], b0[2][2], b1[2][2];
+
+  // quadrant (mh, nh) of this wave's tile at (m0, n0) -> bf16 C, then zeroed for the next tile
+  const int cb = ((fq & 1) << 4) | ((fq >> 1) << 3);
+  auto store_q = [&](int mh, int nh, int m0, int n0) __attribute__((always_inline)) {
+    const int n = n0 + wc * 64 + nh * 32 + cb;
+    const bool nok = n < g.N;
+#pragma unroll
+    for (int mi = 0; mi < 4; mi++) {
+      floatx4& x = acc[nh * 2][mh * 4 + mi];
+      floatx4& y = acc[nh * 2 + 1][mh * 4 + mi];
+      unsigned x0 = cvt2(x[0], x[1]), x1 = cvt2(x[2], x[3]);
+      unsigned y0 = cvt2(y[0], y[1]), y1 = cvt2(y[2], y[3]);
+      const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+      const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+      const int m = m0 + wr * 128 + mh * 64 + mi * 16 + fr;
+      const unsigned off = (m < g.M && nok) ? ((unsigned)m * (unsigned)g.ldc + (unsigned)n) * 2u : kOOB;
+      store16(rC, off, make_uint4(s0[0], s1[0], s0[1], s1[1]));
+      x = floatx4{0.f, 0.f, 0.f, 0.f};
+      y = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+
+  auto mfma_q = [&](short8 (&bb)[2][2], int mh, int nh) __attribute__((always_inline)) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ks++)
+#pragma unroll
+      for (int ni = 0; ni < 2; ni++)
+#pragma unroll
+        for (int mi = 0; mi < 4; mi++)
+          acc[nh * 2 + ni][mh * 4 + mi] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[ni][ks], a[mi][ks], acc[nh * 2 + ni][mh * 4 + mi], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto rd = [&](const char* p) -> short8 { return *reinterpret_cast<const short8*>(p); };
+
+  // prologue: pieces of phases -6..-1 (A0 B0 B1 A1 of k-tile 0, A0 B0 of k-tile 1)
+  issue(std::integral_constant<int, 0>{});
+  issue(std::integral_constant<int, 1>{});
+  issue(std::integral_constant<int, 2>{});
+  issue(std::integral_constant<int, 3>{});
+  issue(std::integral_constant<int, 0>{});
+  issue(std::integral_constant<int, 1>{});
+  const int plast = 4 * J - 7;  // last phase that issues a piece
+  {
+    const int younger = min(-1, plast) - (-1 - 3) + 1;
+    vm_wait_rt(2 * (younger < 0 ? 0 : younger));
+  }
+  asm volatile("s_barrier" ::: "memory");
+  if (wr) asm volatile("s_barrier" ::: "memory");  // group 1 runs one barrier behind
+
+  int cm0, cn0, pm0 = 0, pn0 = 0;  // compute-side tile and the previous one (whose C is being written)
+  tile_mn(0, cm0, cn0);
+  int ckt = 0;  // k-tile index within the compute-side tile
+
+  // one k-tile = four phases.  FAST: steady state away from a tile boundary
+  // (every phase issues a piece, no stores among the last four phases): vmcnt(8).
+  // Otherwise the counts are computed: `epi` = this k-tile writes the previous
+  // tile's C, `pepi` = the previous k-tile did.
+  auto ktile = [&](int u, auto fast) __attribute__((always_inline)) {
+    constexpr bool FAST = decltype(fast)::value;
+    const char* buf = smem + (u & 1) * (4 * PIECE);
+    const bool epi = !FAST && ckt == 0 && u > 0;
+    const bool pepi = !FAST && u > 1 && (nk == 1 || ckt == 1);
+    auto retire = [&](int s) __attribute__((always_inline)) {
+      if constexpr (FAST) {
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      } else {
+        const int P = 4 * u + s;
+        int younger = min(P, plast) - (P - 3) + 1;
+        younger = younger < 0 ? 0 : younger;
+        const int st = kStoresPerPhase * ((epi ? s + 1 : 0) + (pepi ? 3 - s : 0));
+        vm_wait_rt(2 * younger + st);
+      }
+    };
+    // s0: A0 + B0 -> quadrant (0, 0)
+    {
+      const char* pa = buf + wr * 64 * 128;
+      const char* pb = buf + PIECE + wc * 32 * 128;
+#pragma unroll
+      for (int ni = 0; ni < 2; ni++) {
+        b0[ni][0] = rd(pb + ni * 16 * 128 + ro0);
+        b0[ni][1] = rd(pb + ni * 16 * 128 + ro1);
+      }
+#pragma unroll
+      for (int mi = 0; mi < 4; mi++) {
+        a[mi][0] = rd(pa + mi * 16 * 128 + ro0);
+        a[mi][1] = rd(pa + mi * 16 * 128 + ro1);
+      }
+      if (epi) store_q(0, 0, pm0, pn0);
+      issue(std::integral_constant<int, 2>{});
+      retire(0);
+      asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      mfma_q(b0, 0, 0);
+      asm volatile("s_barrier" ::: "memory");
+    }
+    // s1: B1 -> quadrant (0, 1)
+    {
+      const char* pb = buf + 2 * PIECE + wc * 32 * 128;
+#pragma unroll
+      for (int ni = 0; ni < 2; ni++) {
+        b1[ni][0] = rd(pb + ni * 16 * 128 + ro0);
+        b1[ni][1] = rd(pb + ni * 16 * 128 + ro1);
+      }
+      if (epi) store_q(0, 1, pm0, pn0);
+      issue(std::integral_constant<int, 3>{});
+      retire(1);
+      asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      mfma_q(b1, 0, 1);
+      asm volatile("s_barrier" ::: "memory");
+    }
+    // s2: A1 -> quadrant (1, 1)
+    {
+      const char* pa = buf + 3 * PIECE + wr * 64 * 128;
+#pragma unroll
+      for (int mi = 0; mi < 4; mi++) {
+        a[mi][0] = rd(pa + mi * 16 * 128 + ro0);
+        a[mi][1] = rd(pa + mi * 16 * 128 + ro1);
+      }
+      if (epi) store_q(1, 1, pm0, pn0);
+      issue(std::integral_constant<int, 0>{});
+      retire(2);
+      asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      mfma_q(b1, 1, 1);
+      asm volatile("s_barrier" ::: "memory");
+    }
+    // s3: registers only -> quadrant (1, 0)
+    {
+      if (epi) store_q(1, 0, pm0, pn0);
+      issue(std::integral_constant<int, 1>{});
+      retire(3);
+      asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      mfma_q(b0, 1, 0);
+      asm volatile("s_barrier" ::: "memory");
+    }
+  };
+
+  int u = 0;
+  while (u < J) {
+    // boundary k-tiles (the first two of every tile after the first) and the pipeline tail
+    do {
+      if (ckt == 0 && u > 0) {  // a new tile starts: its first k-tile writes the previous tile
+        pm0 = cm0;
+        pn0 = cn0;
+        tile_mn(u / nk, cm0, cn0);
+      }
+      ktile(u, std::false_type{});
+      u++;
+      if (++ckt == nk) ckt = 0;
+    } while (u < J && !(ckt >= 2 && u + 2 < J));
+    // steady k-tiles
+    while (ckt != 0 && u + 2 < J) {
+      ktile(u, std::true_type{});
+      u++;
+      if (++ckt == nk) ckt = 0;
+    }
+  }
+  if (!wr) asm volatile("s_barrier" ::: "memory");  // both groups at the same barrier count
+  // the last tile's C
+  store_q(0, 0, cm0, cn0);
+  store_q(0, 1, cm0, cn0);
+  store_q(1, 1, cm0, cn0);
+  store_q(1, 0, cm0, cn0);
+}
+
+int ppp_cus() {
+  static int c = 0;
+  if (!c) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+    if (c <= 0) c = 256;
+  }
+  return c;
+}
+
+}  // namespace
+
+// C = A · Bᵀ (bf16 out) on the persistent ping-pong kernel.  K % 64 == 0,
+// N % 8 == 0, every extent within 31-bit buffer offsets; grid = min(tiles, CUs)
+// (or `blocks` if > 0).  Returns 0, -1 on unsupported operands.
+KFA_API int kfa_gemm_ppp(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int K, int lda, int ldb, int ldc,
+                         int blocks, hipStream_t st) {
+  if (M <= 0 || N <= 0) return 0;
+  if (K <= 0 || K % BK || N % 8 || lda % 8 || ldb % 8 || ldc % 8 || lda < K || ldb < K || ldc < N) return -1;
+  const long cb = (long)M * ldc * 2;
+  if (cb >= (long)kOOB || (long)M * lda * 2 >= (long)kOOB || (long)N * ldb * 2 >= (long)kOOB) return -2;
+  const long tiles = (long)((M + 255) / 256) * ((N + 255) / 256);
+  const long cus = blocks > 0 ? blocks : ppp_cus();
+  const int grid = (int)(tiles < cus ? tiles : cus);
+  const PppArgs g{A, B, C, M, N, K, lda, ldb, ldc, (unsigned)cb};
+  hipLaunchKernelGGL(gemm_ppp_kernel, dim3(grid), dim3(512), 0, st, g);
+  return kfa_status();
+}

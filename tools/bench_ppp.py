@@ -1,0 +1,52 @@
+"""Dense GEMM shapes of BERT-base / W&D / ResNet-FC on 1x MI355X: hipBLASLt
+(``torch.mm``) vs the ping-pong kernel (per-tile launch) vs the persistent
+ping-pong kernel with the C write overlapped (``gemm_ppp``).  Random bf16
+operands, CUDA-event timing, A/B interleaved in one process (rule 24)."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from kubeflow_controller_amd.ops import gemm as G  # noqa: E402
+
+SHAPES = [(32768, 2304, 768), (32768, 768, 768), (32768, 3072, 768), (32768, 768, 3072), (32768, 768, 2304),
+          (8192, 8192, 8192)]
+
+
+def timeit(fn, iters=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def main():
+    d = torch.device("cuda")
+    shapes = SHAPES
+    if len(sys.argv) > 1:
+        shapes = [tuple(int(v) for v in s.split("x")) for s in sys.argv[1:]]
+    for M, N, K in shapes:
+        x = torch.randn(M, K, device=d).to(torch.bfloat16)
+        w = torch.randn(N, K, device=d).to(torch.bfloat16)
+        fl = 2.0 * M * N * K
+        res = {}
+        for rnd in range(3):
+            for name, fn in (("hipblaslt", lambda: torch.mm(x, w.t())),
+                             ("pp", lambda: G.gemm_nt(x, w, persistent=6)),
+                             ("ppp", lambda: G.gemm_ppp(x, w))):
+                res.setdefault(name, []).append(timeit(fn))
+        ref = torch.mm(x, w.t()).float()
+        err = (G.gemm_ppp(x, w).float() - ref).abs().max().item()
+        line = " | ".join(f"{k} {min(v) * 1e3:7.1f} us {fl / min(v) / 1e9:6.0f} TF/s" for k, v in res.items())
+        print(f"{M:6d} {N:5d} {K:5d} | {line} | ppp max|err| {err:.3g}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
