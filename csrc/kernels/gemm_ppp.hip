@@ -69,6 +69,12 @@ __device__ __forceinline__ void store16(__amdgpu_buffer_rsrc_t r, unsigned off, 
   __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<V*>(&v), r, off, 0, 0);
 }
 
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 // s_waitcnt vmcnt(n) for a wave-uniform runtime n (even, 0..62)
 __device__ __forceinline__ void vm_wait_rt(int n) {
   switch (n) {
@@ -92,6 +98,8 @@ struct PppArgs {
 
 constexpr int kStoresPerPhase = 4;  // one 16-B store per 16-row block of a 64 x 32 quadrant
 
+// NOST: timing probe — every C store dropped (the values kept live)
+template <bool NOST = false>
 __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
   constexpr int TM = 8, TN = 4;
   __shared__ __attribute__((aligned(16))) char smem[2 * 4 * PIECE];  // 128 KB: two k-tiles of four pieces
@@ -138,38 +146,42 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
       }
     }
   };
-  // issue cursors: X feeds pieces 2, 3 (k-tile u+1 in k-tile u), Y pieces 0, 1 (k-tile u+2)
-  int xg = 0, xkt = 0, xti = 0, yg = 0, ykt = 0, yti = 0;
+  // Issue side, advanced ONCE per k-tile outside the phases (the phases only
+  // issue): pieces 2, 3 of k-tile u fetch k-tile u+1 ("X"), pieces 0, 1 fetch
+  // u+2 ("Y"); each side keeps its k index, its local tile and that tile's
+  // offsets (voff[2..3] / voff[0..1]).
+  int xkt = 0, xti = 0, ykt = 0, yti = 0;
   {
     int m0, n0;
     tile_mn(0, m0, n0);
 #pragma unroll
     for (int p = 0; p < 4; p++) set_voff(p, m0, n0);
   }
-  auto issue = [&](auto pc) __attribute__((always_inline)) {
-    constexpr int p = decltype(pc)::value;
-    constexpr bool X = (p == 2 || p == 3);
-    int& cg = X ? xg : yg;
-    int& ckt = X ? xkt : ykt;
-    int& cti = X ? xti : yti;
-    if (cg < J) {
-      char* dst = smem + (cg & 1) * (4 * PIECE) + p * PIECE + wave * 8 * 128;
-      const __amdgpu_buffer_rsrc_t r = (p == 0 || p == 3) ? rA : rB;
-      dma16(r, dst, voff[p][0], ckt * BK * 2);
-      dma16(r, dst + 64 * 128, voff[p][1], ckt * BK * 2);
-    }
-    if (p == 1 || p == 3) {  // the cursor's second piece: advance to its next k-tile
-      cg++;
-      if (++ckt == nk) {
-        ckt = 0;
-        if (++cti < my_tiles) {
-          int m0, n0;
-          tile_mn(cti, m0, n0);
-          set_voff(X ? 2 : 0, m0, n0);
-          set_voff(X ? 3 : 1, m0, n0);
-        }
+  auto advance = [&](bool X) __attribute__((always_inline)) {  // next k-tile of side X / Y
+    int& kt = X ? xkt : ykt;
+    int& ti = X ? xti : yti;
+    if (++kt == nk) {
+      kt = 0;
+      if (++ti < my_tiles) {
+        int m0, n0;
+        tile_mn(ti, m0, n0);
+        set_voff(X ? 2 : 0, m0, n0);
+        set_voff(X ? 3 : 1, m0, n0);
       }
     }
+  };
+  // Every phase issues exactly two DMAs: past the block's last k-tile the row
+  // offsets are out of range (the buffer range check reads zeros, no memory
+  // traffic), so the vmcnt counts never change shape at the pipeline tail.
+  auto issue = [&](auto pc, int gk) __attribute__((always_inline)) {  // gk: k-tile fetched
+    constexpr int p = decltype(pc)::value;
+    constexpr bool X = (p == 2 || p == 3);
+    char* dst = smem + (gk & 1) * (4 * PIECE) + p * PIECE + wave * 8 * 128;
+    const __amdgpu_buffer_rsrc_t r = (p == 0 || p == 3) ? rA : rB;
+    const int soff = (X ? xkt : ykt) * BK * 2;
+    const bool live = gk < J;
+    dma16(r, dst, live ? voff[p][0] : (int)kOOB, soff);
+    dma16(r, dst + 64 * 128, live ? voff[p][1] : (int)kOOB, soff);
   };
 
   const int fr = lane & 15, fq = lane >> 4;
@@ -196,7 +208,8 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
       const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
       const int m = m0 + wr * 128 + mh * 64 + mi * 16 + fr;
       const unsigned off = (m < g.M && nok) ? ((unsigned)m * (unsigned)g.ldc + (unsigned)n) * 2u : kOOB;
-      store16(rC, off, make_uint4(s0[0], s1[0], s0[1], s1[1]));
+      if constexpr (NOST) asm volatile("" :: "v"(s0[0]), "v"(s1[0]), "v"(s0[1]), "v"(s1[1]), "v"(off));
+      else store16(rC, off, make_uint4(s0[0], s1[0], s0[1], s1[1]));
       x = floatx4{0.f, 0.f, 0.f, 0.f};
       y = floatx4{0.f, 0.f, 0.f, 0.f};
     }
@@ -217,17 +230,16 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
   auto rd = [&](const char* p) -> short8 { return *reinterpret_cast<const short8*>(p); };
 
   // prologue: pieces of phases -6..-1 (A0 B0 B1 A1 of k-tile 0, A0 B0 of k-tile 1)
-  issue(std::integral_constant<int, 0>{});
-  issue(std::integral_constant<int, 1>{});
-  issue(std::integral_constant<int, 2>{});
-  issue(std::integral_constant<int, 3>{});
-  issue(std::integral_constant<int, 0>{});
-  issue(std::integral_constant<int, 1>{});
-  const int plast = 4 * J - 7;  // last phase that issues a piece
-  {
-    const int younger = min(-1, plast) - (-1 - 3) + 1;
-    vm_wait_rt(2 * (younger < 0 ? 0 : younger));
-  }
+  issue(std::integral_constant<int, 0>{}, 0);
+  issue(std::integral_constant<int, 1>{}, 0);
+  advance(false);
+  issue(std::integral_constant<int, 2>{}, 0);
+  issue(std::integral_constant<int, 3>{}, 0);
+  advance(true);
+  issue(std::integral_constant<int, 0>{}, 1);
+  issue(std::integral_constant<int, 1>{}, 1);
+  advance(false);
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   asm volatile("s_barrier" ::: "memory");
   if (wr) asm volatile("s_barrier" ::: "memory");  // group 1 runs one barrier behind
 
@@ -235,25 +247,18 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
   tile_mn(0, cm0, cn0);
   int ckt = 0;  // k-tile index within the compute-side tile
 
-  // one k-tile = four phases.  FAST: steady state away from a tile boundary
-  // (every phase issues a piece, no stores among the last four phases): vmcnt(8).
-  // Otherwise the counts are computed: `epi` = this k-tile writes the previous
-  // tile's C, `pepi` = the previous k-tile did.
-  auto ktile = [&](int u, auto fast) __attribute__((always_inline)) {
-    constexpr bool FAST = decltype(fast)::value;
+  // One k-tile = four phases, branch-free: MODE bit 0 = this k-tile writes the
+  // previous tile's C (4 stores per phase), bit 1 = the previous k-tile did.
+  // Phase s retires the piece of four phases ago, leaving in flight 2 DMAs per
+  // later phase plus the stores issued among those phases (compile-time counts).
+  auto ktile = [&](int u, auto mode) __attribute__((always_inline)) {
+    constexpr int MODE = decltype(mode)::value;
+    constexpr bool EPI = MODE & 1, PEPI = MODE & 2;
     const char* buf = smem + (u & 1) * (4 * PIECE);
-    const bool epi = !FAST && ckt == 0 && u > 0;
-    const bool pepi = !FAST && u > 1 && (nk == 1 || ckt == 1);
-    auto retire = [&](int s) __attribute__((always_inline)) {
-      if constexpr (FAST) {
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      } else {
-        const int P = 4 * u + s;
-        int younger = min(P, plast) - (P - 3) + 1;
-        younger = younger < 0 ? 0 : younger;
-        const int st = kStoresPerPhase * ((epi ? s + 1 : 0) + (pepi ? 3 - s : 0));
-        vm_wait_rt(2 * younger + st);
-      }
+    auto retire = [&](auto sc) __attribute__((always_inline)) {
+      constexpr int s = decltype(sc)::value;
+      constexpr int n = 8 + kStoresPerPhase * ((EPI ? s + 1 : 0) + (PEPI ? 3 - s : 0));
+      vm_wait<n>();
     };
     // s0: A0 + B0 -> quadrant (0, 0)
     {
@@ -269,9 +274,9 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
         a[mi][0] = rd(pa + mi * 16 * 128 + ro0);
         a[mi][1] = rd(pa + mi * 16 * 128 + ro1);
       }
-      if (epi) store_q(0, 0, pm0, pn0);
-      issue(std::integral_constant<int, 2>{});
-      retire(0);
+      if constexpr (EPI) store_q(0, 0, pm0, pn0);
+      issue(std::integral_constant<int, 2>{}, u + 1);
+      retire(std::integral_constant<int, 0>{});
       asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
       mfma_q(b0, 0, 0);
       asm volatile("s_barrier" ::: "memory");
@@ -284,9 +289,9 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
         b1[ni][0] = rd(pb + ni * 16 * 128 + ro0);
         b1[ni][1] = rd(pb + ni * 16 * 128 + ro1);
       }
-      if (epi) store_q(0, 1, pm0, pn0);
-      issue(std::integral_constant<int, 3>{});
-      retire(1);
+      if constexpr (EPI) store_q(0, 1, pm0, pn0);
+      issue(std::integral_constant<int, 3>{}, u + 1);
+      retire(std::integral_constant<int, 1>{});
       asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
       mfma_q(b1, 0, 1);
       asm volatile("s_barrier" ::: "memory");
@@ -299,43 +304,40 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
         a[mi][0] = rd(pa + mi * 16 * 128 + ro0);
         a[mi][1] = rd(pa + mi * 16 * 128 + ro1);
       }
-      if (epi) store_q(1, 1, pm0, pn0);
-      issue(std::integral_constant<int, 0>{});
-      retire(2);
+      if constexpr (EPI) store_q(1, 1, pm0, pn0);
+      issue(std::integral_constant<int, 0>{}, u + 2);
+      retire(std::integral_constant<int, 2>{});
       asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
       mfma_q(b1, 1, 1);
       asm volatile("s_barrier" ::: "memory");
     }
     // s3: registers only -> quadrant (1, 0)
     {
-      if (epi) store_q(1, 0, pm0, pn0);
-      issue(std::integral_constant<int, 1>{});
-      retire(3);
+      if constexpr (EPI) store_q(1, 0, pm0, pn0);
+      issue(std::integral_constant<int, 1>{}, u + 2);
+      retire(std::integral_constant<int, 3>{});
       asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
       mfma_q(b0, 1, 0);
       asm volatile("s_barrier" ::: "memory");
     }
+    advance(true);
+    advance(false);
   };
 
+  // tile by tile: the first k-tile of every tile after the first writes the
+  // previous tile's C, the second still has those stores in its count window
   int u = 0;
-  while (u < J) {
-    // boundary k-tiles (the first two of every tile after the first) and the pipeline tail
-    do {
-      if (ckt == 0 && u > 0) {  // a new tile starts: its first k-tile writes the previous tile
-        pm0 = cm0;
-        pn0 = cn0;
-        tile_mn(u / nk, cm0, cn0);
-      }
-      ktile(u, std::false_type{});
-      u++;
-      if (++ckt == nk) ckt = 0;
-    } while (u < J && !(ckt >= 2 && u + 2 < J));
-    // steady k-tiles
-    while (ckt != 0 && u + 2 < J) {
-      ktile(u, std::true_type{});
-      u++;
-      if (++ckt == nk) ckt = 0;
+  for (int t = 0; t < my_tiles; t++) {
+    int k = 0;
+    if (t > 0) {
+      pm0 = cm0;
+      pn0 = cn0;
+      tile_mn(t, cm0, cn0);
+      ktile(u++, std::integral_constant<int, 1>{});
+      ktile(u++, std::integral_constant<int, 2>{});
+      k = 2;
     }
+    for (; k < nk; k++) ktile(u++, std::integral_constant<int, 0>{});
   }
   if (!wr) asm volatile("s_barrier" ::: "memory");  // both groups at the same barrier count
   // the last tile's C
@@ -343,6 +345,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
   store_q(0, 1, cm0, cn0);
   store_q(1, 1, cm0, cn0);
   store_q(1, 0, cm0, cn0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail's zero-fill DMAs land before the LDS is released
 }
 
 int ppp_cus() {
@@ -362,15 +365,20 @@ int ppp_cus() {
 // N % 8 == 0, every extent within 31-bit buffer offsets; grid = min(tiles, CUs)
 // (or `blocks` if > 0).  Returns 0, -1 on unsupported operands.
 KFA_API int kfa_gemm_ppp(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int K, int lda, int ldb, int ldc,
-                         int blocks, hipStream_t st) {
+                         int blocks, int probe, hipStream_t st) {
   if (M <= 0 || N <= 0) return 0;
-  if (K <= 0 || K % BK || N % 8 || lda % 8 || ldb % 8 || ldc % 8 || lda < K || ldb < K || ldc < N) return -1;
+  // K >= 128: two k-tiles per tile at least (a tile's first two k-tiles carry its predecessor's stores)
+  if (K < 2 * BK || K % BK || N % 8 || lda % 8 || ldb % 8 || ldc % 8 || lda < K || ldb < K || ldc < N) return -1;
   const long cb = (long)M * ldc * 2;
   if (cb >= (long)kOOB || (long)M * lda * 2 >= (long)kOOB || (long)N * ldb * 2 >= (long)kOOB) return -2;
   const long tiles = (long)((M + 255) / 256) * ((N + 255) / 256);
   const long cus = blocks > 0 ? blocks : ppp_cus();
   const int grid = (int)(tiles < cus ? tiles : cus);
   const PppArgs g{A, B, C, M, N, K, lda, ldb, ldc, (unsigned)cb};
-  hipLaunchKernelGGL(gemm_ppp_kernel, dim3(grid), dim3(512), 0, st, g);
+  if (probe == 1)  // timing probe: no C stores
+    hipLaunchKernelGGL(gemm_ppp_kernel<true>, dim3(grid), dim3(512), 0, st, g);
+
+  else
+    hipLaunchKernelGGL(gemm_ppp_kernel<false>, dim3(grid), dim3(512), 0, st, g);
   return kfa_status();
 }

@@ -31,7 +31,7 @@ P, I = _lib.P, _lib.I
 _lib.register("kfa_gemm_nt", [P] * 9 + [I] * 10 + [P])
 _lib.register("kfa_gemm_dpart_floats", [I, I, I, I], restype=_lib.L)
 _lib.register("kfa_gemm_pick_bn", [I, I])
-_lib.register("kfa_gemm_ppp", [P, P, P] + [I] * 7 + [P])
+_lib.register("kfa_gemm_ppp", [P, P, P] + [I] * 8 + [P])
 
 ACTS = {None: 0, "none": 0, "gelu": 1, "tanh": 2, "relu": 3}
 # Which dense-layer GEMMs run on this kernel (KFA_GEMM):
@@ -147,20 +147,21 @@ def gemm_nt(a, b, *, bias=None, act=None, addend=None, want_z=False, zin=None, d
     return c, z
 
 
-def gemm_ppp(a, b, *, out=None, blocks: int = 0):
+def gemm_ppp(a, b, *, out=None, blocks: int = 0, probe: int = 0):
     """``a @ b.T`` (bf16) on the persistent ping-pong kernel (``csrc/kernels/gemm_ppp.hip``):
     one block per CU sweeps its tiles as one continuous k-tile pipeline, each tile's
-    C written from the accumulators during the next tile's first k-tile.  K % 64 == 0.
-    ``blocks`` > 0 caps the persistent grid (tests: many tiles per block).  Opt-in:
+    C written from the accumulators during the next tile's first k-tile.  K % 64 == 0, K >= 128.
+    ``blocks`` > 0 caps the persistent grid (tests: many tiles per block).  ``probe=1``:
+    timing probe with every C store dropped (C is left unwritten).  Opt-in:
     measured below hipBLASLt on the BERT shapes (``profiles/r3_gemm_ppp.txt``)."""
-    if not gemm_ok(a, b) or a.shape[1] % 64:
+    if not gemm_ok(a, b) or a.shape[1] % 64 or a.shape[1] < 128:
         raise ValueError(f"gemm_ppp: unsupported operands {tuple(a.shape)} x {tuple(b.shape)}")
     M, K = a.shape
     N = b.shape[0]
     c = out if out is not None else torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
     _check_mn(c, M, N, "out")
     _lib.call("kfa_gemm_ppp", _lib.ptr(a), _lib.ptr(b), _lib.ptr(c), M, N, K, a.stride(0), b.stride(0), N,
-              int(blocks), _lib.stream())
+              int(blocks), int(probe), _lib.stream())
     return c
 
 

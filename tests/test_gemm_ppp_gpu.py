@@ -22,7 +22,7 @@ def _bf(*shape, s=1.0):
 
 
 @pytest.mark.parametrize("M,N,K,blocks", [
-    (256, 256, 64, 0),        # one tile, one k-tile
+    (256, 256, 128, 0),       # one tile, two k-tiles
     (512, 512, 128, 1),       # 4 tiles on one block, two k-tiles each (every k-tile a boundary one)
     (1000, 776, 192, 3),      # edge tiles in M and N, uneven tile counts per block
     (4096, 4096, 768, 0),     # one tile per CU
@@ -31,7 +31,8 @@ def _bf(*shape, s=1.0):
     (32768, 3072, 768, 0),    # BERT FFN-up: 6 tiles per CU
     (2048, 768, 3072, 5),     # long k-loop, many tiles per block
     (1024, 1024, 4096, 64),   # grid capped at the 16 tiles, 64 k-tiles each
-    (300, 8, 64, 0),          # N = 8
+    (300, 8, 128, 0),         # N = 8
+    (512, 512, 128, 2),       # two k-tiles per tile: every other k-tile a boundary one
 ])
 def test_gemm_ppp_matches_fp32(M, N, K, blocks):
     from kubeflow_controller_amd.ops import gemm as G

@@ -40,7 +40,9 @@ def main():
         for rnd in range(3):
             for name, fn in (("hipblaslt", lambda: torch.mm(x, w.t())),
                              ("pp", lambda: G.gemm_nt(x, w, persistent=6)),
-                             ("ppp", lambda: G.gemm_ppp(x, w))):
+                             ("ppp", lambda: G.gemm_ppp(x, w)),
+                             ("ppp-nostore", lambda: G.gemm_ppp(x, w, probe=1)),
+                             ("pp-noepi", lambda: G.gemm_nt(x, w, persistent=7))):
                 res.setdefault(name, []).append(timeit(fn))
         ref = torch.mm(x, w.t()).float()
         err = (G.gemm_ppp(x, w).float() - ref).abs().max().item()

@@ -15,6 +15,8 @@ def main(paths):
     for path in paths:
         for r in csv.DictReader(open(path)):
             k = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0][:60]
+            if r.get("Grid_Size"):
+                k += f" [grid {r['Grid_Size']}]"
             d = (path, r["Dispatch_Id"])
             vals[k][r["Counter_Name"]][d] += float(r["Counter_Value"])
             ns[k][d] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
