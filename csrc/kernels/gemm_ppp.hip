@@ -98,8 +98,10 @@ struct PppArgs {
 
 constexpr int kStoresPerPhase = 4;  // one 16-B store per 16-row block of a 64 x 32 quadrant
 
-// NOST: timing probe — every C store dropped (the values kept live)
-template <bool NOST = false>
+// NOST: timing probe — every C store dropped (the values kept live).
+// SMODE: bit 0 = non-temporal C stores; bit 1 = row pairs (quadrants (0,0)+(0,1)
+// in phase 0, (1,1)+(1,0) in phase 2: each 128-B row segment written in one phase)
+template <bool NOST = false, int SMODE = 0>
 __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
   constexpr int TM = 8, TN = 4;
   __shared__ __attribute__((aligned(16))) char smem[2 * 4 * PIECE];  // 128 KB: two k-tiles of four pieces
@@ -209,7 +211,11 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
       const int m = m0 + wr * 128 + mh * 64 + mi * 16 + fr;
       const unsigned off = (m < g.M && nok) ? ((unsigned)m * (unsigned)g.ldc + (unsigned)n) * 2u : kOOB;
       if constexpr (NOST) asm volatile("" :: "v"(s0[0]), "v"(s1[0]), "v"(s0[1]), "v"(s1[1]), "v"(off));
-      else store16(rC, off, make_uint4(s0[0], s1[0], s0[1], s1[1]));
+      else if constexpr (SMODE & 1) {
+        using V = decltype(__builtin_amdgcn_raw_buffer_load_b128(rC, 0, 0, 0));
+        uint4 v = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<V*>(&v), rC, off, 0, 2);
+      } else store16(rC, off, make_uint4(s0[0], s1[0], s0[1], s1[1]));
       x = floatx4{0.f, 0.f, 0.f, 0.f};
       y = floatx4{0.f, 0.f, 0.f, 0.f};
     }
@@ -257,7 +263,11 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
     const char* buf = smem + (u & 1) * (4 * PIECE);
     auto retire = [&](auto sc) __attribute__((always_inline)) {
       constexpr int s = decltype(sc)::value;
-      constexpr int n = 8 + kStoresPerPhase * ((EPI ? s + 1 : 0) + (PEPI ? 3 - s : 0));
+      // stores per phase: 4 each (quadrant per phase) or 8, 0, 8, 0 (row pairs)
+      constexpr int RP = (SMODE & 2) ? 1 : 0;
+      constexpr int upto = RP ? 8 * (s / 2 + 1) : 4 * (s + 1);          // phases 0..s
+      constexpr int after = RP ? 8 * ((3 - s + (s % 2 == 0 ? 0 : 1)) / 2) : 4 * (3 - s);  // phases s+1..3
+      constexpr int n = 8 + (EPI ? upto : 0) + (PEPI ? after : 0);
       vm_wait<n>();
     };
     // s0: A0 + B0 -> quadrant (0, 0)
@@ -274,7 +284,10 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
         a[mi][0] = rd(pa + mi * 16 * 128 + ro0);
         a[mi][1] = rd(pa + mi * 16 * 128 + ro1);
       }
-      if constexpr (EPI) store_q(0, 0, pm0, pn0);
+      if constexpr (EPI) {
+        store_q(0, 0, pm0, pn0);
+        if constexpr (SMODE & 2) store_q(0, 1, pm0, pn0);
+      }
       issue(std::integral_constant<int, 2>{}, u + 1);
       retire(std::integral_constant<int, 0>{});
       asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
@@ -289,7 +302,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
         b1[ni][0] = rd(pb + ni * 16 * 128 + ro0);
         b1[ni][1] = rd(pb + ni * 16 * 128 + ro1);
       }
-      if constexpr (EPI) store_q(0, 1, pm0, pn0);
+      if constexpr (EPI && !(SMODE & 2)) store_q(0, 1, pm0, pn0);
       issue(std::integral_constant<int, 3>{}, u + 1);
       retire(std::integral_constant<int, 1>{});
       asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
@@ -304,7 +317,10 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
         a[mi][0] = rd(pa + mi * 16 * 128 + ro0);
         a[mi][1] = rd(pa + mi * 16 * 128 + ro1);
       }
-      if constexpr (EPI) store_q(1, 1, pm0, pn0);
+      if constexpr (EPI) {
+        store_q(1, 1, pm0, pn0);
+        if constexpr (SMODE & 2) store_q(1, 0, pm0, pn0);
+      }
       issue(std::integral_constant<int, 0>{}, u + 2);
       retire(std::integral_constant<int, 2>{});
       asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
@@ -313,7 +329,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
     }
     // s3: registers only -> quadrant (1, 0)
     {
-      if constexpr (EPI) store_q(1, 0, pm0, pn0);
+      if constexpr (EPI && !(SMODE & 2)) store_q(1, 0, pm0, pn0);
       issue(std::integral_constant<int, 1>{}, u + 2);
       retire(std::integral_constant<int, 3>{});
       asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
@@ -377,6 +393,12 @@ KFA_API int kfa_gemm_ppp(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int
   const PppArgs g{A, B, C, M, N, K, lda, ldb, ldc, (unsigned)cb};
   if (probe == 1)  // timing probe: no C stores
     hipLaunchKernelGGL(gemm_ppp_kernel<true>, dim3(grid), dim3(512), 0, st, g);
+  else if (probe == 2)  // store-policy experiments: nt / row pairs / both
+    hipLaunchKernelGGL((gemm_ppp_kernel<false, 1>), dim3(grid), dim3(512), 0, st, g);
+  else if (probe == 3)
+    hipLaunchKernelGGL((gemm_ppp_kernel<false, 2>), dim3(grid), dim3(512), 0, st, g);
+  else if (probe == 4)
+    hipLaunchKernelGGL((gemm_ppp_kernel<false, 3>), dim3(grid), dim3(512), 0, st, g);
 
   else
     hipLaunchKernelGGL(gemm_ppp_kernel<false>, dim3(grid), dim3(512), 0, st, g);

@@ -165,6 +165,39 @@ def gemm_ppp(a, b, *, out=None, blocks: int = 0, probe: int = 0):
     return c
 
 
+def ppp_ok(a, b) -> bool:
+    """Operands :func:`gemm_ppp` takes (plain ``a @ b.T``, bf16 out)."""
+    return gemm_ok(a, b) and a.shape[1] % 64 == 0 and a.shape[1] >= 128
+
+
+def mm_auto(a, w, kind: str = "proj"):
+    """``a @ w.T`` (bf16): the persistent MFMA GEMM where it measured faster than
+    hipBLASLt for this shape (timed once at first use, rank 0's choice applied
+    everywhere — :func:`prefer_own`), else the library.  ``KFA_GEMM=0`` forces
+    the library."""
+    if ROUTE_AUTO and ppp_ok(a, w):
+        if prefer_own(kind, (a.shape[0], w.shape[0], a.shape[1]), a.device, lambda: gemm_ppp(a, w),
+                      lambda: torch.mm(a, w.t())):
+            return gemm_ppp(a, w)
+    return torch.mm(a, w.t())
+
+
+def dgrad_auto(dz, w, kind: str = "proj_dgrad"):
+    """``dz @ w`` (the data gradient of ``y = x @ w.T``): the persistent MFMA GEMM on
+    the transposed weight (transpose included in its timing) where it measured
+    faster than hipBLASLt for this shape, else the library."""
+    M, K = dz.shape if dz.dim() == 2 else (0, 0)
+    N = w.shape[1] if w.dim() == 2 else 0
+    if (ROUTE_AUTO and dz.is_cuda and dz.dim() == 2 and w.dim() == 2 and dz.dtype == torch.bfloat16
+            and w.dtype == torch.bfloat16 and dz.is_contiguous() and dz.data_ptr() % 16 == 0 and K == w.shape[0]
+            and K % 64 == 0 and K >= 128 and N % 8 == 0 and M > 0
+            and max(M * N, M * K, N * K) * 2 < (1 << 31)):
+        if prefer_own(kind, (dz.shape[0], w.shape[1], w.shape[0]), dz.device, lambda: gemm_ppp(dz, transpose(w)),
+                      lambda: torch.mm(dz, w)):
+            return gemm_ppp(dz, transpose(w))
+    return torch.mm(dz, w)
+
+
 def transpose(w: torch.Tensor) -> torch.Tensor:
     """Contiguous ``w.T`` of a bf16 ``[R, C]`` matrix on the LDS-tiled HIP transpose
     (the dgrad B operand: ``dx = dy · W`` is ``gemm_nt(dy, transpose(W))``)."""

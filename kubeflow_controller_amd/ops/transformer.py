@@ -431,7 +431,9 @@ class EncoderLayerFn(torch.autograd.Function):
         s_attn, s_h1, s_h2 = mix_seed(seed, 1), mix_seed(seed, 2), mix_seed(seed, 3)
         use_g = _gemm.ROUTE_LAYERS and _gemm.gemm_ok(x, wqkv) and _gemm.gemm_ok(x, w1) and w2.shape[0] % 8 == 0 and w2.shape[1] % 8 == 0
         use_f = use_g or (_gemm.ROUTE_FUSED and _gemm.gemm_ok(x, w1) and w2.shape[0] % 8 == 0 and w2.shape[1] % 8 == 0)
-        mm = (lambda a, w: _gemm.gemm_nt(a, w)[0]) if use_g else (lambda a, w: torch.mm(a, w.t()))  # noqa: E731
+        # plain projections: the fused-epilogue MFMA GEMM (KFA_GEMM=1), else per shape the
+        # persistent MFMA GEMM or hipBLASLt, whichever measured faster (ops/gemm.mm_auto)
+        mm = (lambda a, w: _gemm.gemm_nt(a, w)[0]) if use_g else _gemm.mm_auto  # noqa: E731
         fused = fused_attention_ok(S, d)
         # attention
         qkv = mm(x, wqkv)                                                 # [T, 3H]
@@ -461,7 +463,7 @@ class EncoderLayerFn(torch.autograd.Function):
         if use_f:
             f1a, f1 = _gemm.gemm_nt(h1, w1, bias=b1, act="gelu", want_z=True)
         else:
-            f1 = torch.mm(h1, w1.t())                                      # [T, I]
+            f1 = _gemm.mm_auto(h1, w1)                                     # [T, I]
             f1a = bias_act_fwd(f1, b1, "gelu")
         f2 = mm(f1a, w2)
         h2, h2s, m2, r2 = ln_fwd(f2, g2, be2, res=h1, bias=b2, eps=eps, p=ph, seed=s_h2)
@@ -489,7 +491,7 @@ class EncoderLayerFn(torch.autograd.Function):
         if use_f:   # df1 = (df2 · W2) * gelu'(z1), db1 += colsum(df1): one GEMM launch
             df1 = _gemm.gemm_nt(df2, _gemm.transpose(w2), zin=f1, dact="gelu", dbias=G(b1))[0]
         else:
-            df1 = bias_act_bwd(torch.mm(df2, w2), f1, b1, "gelu", G(b1))
+            df1 = bias_act_bwd(_gemm.dgrad_auto(df2, w2), f1, b1, "gelu", G(b1))
         del df2
         _wgrad_side_(G(w1), df1, h1)
         if use_g:   # residual-gradient join as the GEMM addend
@@ -501,7 +503,7 @@ class EncoderLayerFn(torch.autograd.Function):
         dx_res, dao = ln_bwd(dh1, h1s, m1, r1, g1, G(g1), G(be1), G(bo), p=ph, seed=s_h1, want_branch=True)
         del dh1
         _wgrad_side_(G(wo), dao, ctxr)
-        dctxr = _gemm.gemm_nt(dao, _gemm.transpose(wo))[0] if use_g else torch.mm(dao, wo)
+        dctxr = _gemm.gemm_nt(dao, _gemm.transpose(wo))[0] if use_g else _gemm.dgrad_auto(dao, wo)
         del dao
         if fused:
             qkv, lse = att

@@ -53,3 +53,13 @@ def test_gemm_ppp_strided_a_and_repeatable():
     c2 = G.gemm_ppp(a, b, blocks=7)
     assert torch.equal(c1, c2)
     _close(c1, a.float() @ b.float().t(), 1e-2, "strided")
+
+
+@pytest.mark.parametrize("probe", [2, 3, 4], ids=["writeback_stores", "row_pairs", "row_pairs_nt"])
+def test_gemm_ppp_store_policies(probe):
+    """The store-policy builds (non-temporal C stores, whole-row store phases) write the same C."""
+    from kubeflow_controller_amd.ops import gemm as G
+    torch.manual_seed(probe)
+    a, b = _bf(1000, 640), _bf(776, 640, s=0.05)
+    c = G.gemm_ppp(a, b, blocks=3, probe=probe)
+    _close(c, a.float() @ b.float().t(), 1e-2, f"probe {probe}")

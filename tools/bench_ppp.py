@@ -42,6 +42,9 @@ def main():
                              ("pp", lambda: G.gemm_nt(x, w, persistent=6)),
                              ("ppp", lambda: G.gemm_ppp(x, w)),
                              ("ppp-nostore", lambda: G.gemm_ppp(x, w, probe=1)),
+                             ("ppp-wb", lambda: G.gemm_ppp(x, w, probe=2)),
+                             ("ppp-rows", lambda: G.gemm_ppp(x, w, probe=3)),
+                             ("ppp-rows-nt", lambda: G.gemm_ppp(x, w, probe=4)),
                              ("pp-noepi", lambda: G.gemm_nt(x, w, persistent=7))):
                 res.setdefault(name, []).append(timeit(fn))
         ref = torch.mm(x, w.t()).float()
