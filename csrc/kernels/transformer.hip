@@ -281,23 +281,28 @@ __global__ __launch_bounds__(256) void bias_act_fwd_kernel(const bf16_t* __restr
   }
 }
 
-// dx = dy * act'(x + b), dbias partials.  Block = 64 column-lanes x 4 row-lanes
-// covering 512 columns; grid = (ceil(N/512), row chunks).
+// dx = dy * act'(x + b), dbias partials.  Block = CL column-lanes (8 columns
+// each) x 256/CL row-lanes; grid = (ceil(N / (8 CL)), row chunks).  CL = 16 for
+// wide N keeps >= 2048 blocks in flight (memory-bound: 8 waves/CU are not enough
+// outstanding loads) while each row still reads 256 contiguous bytes.
+template <int CL>
 __global__ __launch_bounds__(256) void bias_act_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                            const float* __restrict__ b, bf16_t* __restrict__ dx,
                                                            float* __restrict__ dbias, long rows, int N, int act,
                                                            long rows_per_block, uint32_t thresh, float dscale,
                                                            uint64_t seed) {
-  __shared__ float red[4][512];
-  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
-  const int c = blockIdx.x * 512 + cl * 8;
+  constexpr int RL = 256 / CL, W = CL * 8;
+  __shared__ float red[RL][W];
+  const int cl = threadIdx.x % CL, rl = threadIdx.x / CL;
+  const int c = blockIdx.x * W + cl * 8;
   const long r0 = (long)blockIdx.y * rows_per_block;
   const long r1 = min(rows, r0 + rows_per_block);
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (c < N) {
     float bb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (b) load8f(b + c, bb);
-    for (long r = r0 + rl; r < r1; r += 4) {
+#pragma unroll 2
+    for (long r = r0 + rl; r < r1; r += RL) {
       float d[8], z[8];
       load8(dy + r * N + c, d);
       if (thresh)
@@ -317,9 +322,12 @@ __global__ __launch_bounds__(256) void bias_act_bwd_kernel(const bf16_t* __restr
   for (int e = 0; e < 8; e++) red[rl][cl * 8 + e] = acc[e];
   __syncthreads();
   if (dbias)
-    for (int k = threadIdx.x; k < 512; k += 256) {
-      const int cc = blockIdx.x * 512 + k;
-      if (cc < N) atomicAdd(dbias + cc, red[0][k] + red[1][k] + red[2][k] + red[3][k]);
+    for (int k = threadIdx.x; k < W; k += 256) {
+      const int cc = blockIdx.x * W + k;
+      float sum = 0.f;
+#pragma unroll
+      for (int j = 0; j < RL; ++j) sum += red[j][k];
+      if (cc < N) atomicAdd(dbias + cc, sum);
     }
 }
 
@@ -696,7 +704,18 @@ KFA_API int kfa_bias_act_bwd(const void* dy, const void* x, const float* b, void
   const uint32_t th = drop_thresh(p);
   const float ds = p > 0.f ? 1.f / (1.f - p) : 1.f;
   zero_if(dbias, N, accumulate, s);
-  hipLaunchKernelGGL(bias_act_bwd_kernel, dim3((N + 511) / 512, (unsigned)chunks), dim3(256), 0, s,
+  if (N >= 128) {
+    // >= 2048 blocks, >= 4 rows per thread; the dbias atomics stay at <= max(chunks, 256) per column
+    const long bx = (N + 127) / 128;
+    const long want = std::max(chunks, (2048 + bx - 1) / bx);
+    const long ch = std::max(1L, std::min(want, (rows + 63) / 64));
+    const long rp = (rows + ch - 1) / ch;
+    hipLaunchKernelGGL(bias_act_bwd_kernel<16>, dim3((unsigned)bx, (unsigned)ch), dim3(256), 0, s,
+                       (const bf16_t*)dy, (const bf16_t*)x, b, (bf16_t*)dx, dbias, rows, N, act, rp, th, ds,
+                       (uint64_t)seed);
+    return kfa_status();
+  }
+  hipLaunchKernelGGL(bias_act_bwd_kernel<64>, dim3((N + 511) / 512, (unsigned)chunks), dim3(256), 0, s,
                      (const bf16_t*)dy, (const bf16_t*)x, b, (bf16_t*)dx, dbias, rows, N, act, rpb, th, ds,
                      (uint64_t)seed);
   return kfa_status();

@@ -83,6 +83,10 @@ class WideDeepConfig:
 
 
 class WideDeep(nn.Module):
+    # the tables' lazy Adam takes its bias corrections from a host step count, so
+    # the step must run eagerly (Engine.graph_ok), not replay a captured graph
+    graph_capturable = False
+
     def __init__(self, cfg: WideDeepConfig, device=None):
         super().__init__()
         self.cfg = cfg

@@ -11,9 +11,12 @@ the PS applies the optimizer (``:184, :256``).  MI355X design:
   (SURVEY §7.3 H1 option a), otherwise every rank owns a slice;
 * **pull** = ``all_to_all`` of the requested ids to their owners, a HIP gather
   of the fp32 master rows straight to bf16, and an ``all_to_all`` back;
-* **push** = ``all_to_all`` of the row gradients to the owners, a HIP
-  scatter-add into a self-cleaning fp32 scratch and a fused sparse Adam/SGD
-  that updates only the looked-up rows (``csrc/kernels/sparse.hip``) — applied
+* **push** = ``all_to_all`` of the row gradients to the owners, then a
+  segment-reduce sparse Adam/SGD (``csrc/kernels/segsparse.hip``): the ids are
+  radix-sorted, each row's gradients are summed in fp32 by one workgroup and
+  the optimizer is applied once per unique row — no table-sized scratch and
+  no per-element atomics (the older scatter-add + atomic-exchange kernels of
+  ``csrc/kernels/sparse.hip`` stay behind ``KFA_SPARSE_ATOMIC=1``).  Applied
   during backward, so no dense gradient or optimizer state is ever touched
   for rows outside the batch;
 * with one rank (or CPU) the same code runs without collectives;
@@ -27,6 +30,7 @@ part of the dense flat groups / all-reduce).
 from __future__ import annotations
 
 import math
+import os
 from typing import List, Optional, Tuple
 
 import torch
@@ -40,6 +44,26 @@ _lib.register("kfa_scatter_add_rows", [_P, _P, _P, _L, _I, _P])
 _lib.register("kfa_sparse_adam", [_P, _P, _P, _P, _P, _L, _I, _F, _F, _F, _F, _F, _F, _F, _F, _P])
 _lib.register("kfa_sparse_sgd", [_P, _P, _P, _L, _I, _F, _F, _P])
 _lib.register("kfa_embed_fwd", [_P, _P, _P, _P, _P, _P, _I, _P, _L, _I, _L, _P])
+_lib.register("kfa_seg_slot_floats", [_L, _I], restype=_L)
+_lib.register("kfa_seg_ws_bytes", [_L, _I], restype=_L)
+_lib.register("kfa_seg_sparse_apply", [_P, _P, _L, _I, _I, _P, _L, _P, _P, _P, _P, _I] + [_F] * 8 + [_P])
+_lib.register("kfa_seg_prepare", [_P, _L, _I, _P, _L, _P])
+_lib.register("kfa_seg_apply", [_P, _L, _I, _I, _P, _L, _P, _P, _P, _P, _I] + [_F] * 8 + [_P])
+
+_SIDE = {}
+
+
+def _side_stream(device) -> "torch.cuda.Stream":
+    key = str(device)
+    if key not in _SIDE:
+        _SIDE[key] = torch.cuda.Stream(device=device)
+    return _SIDE[key]
+
+
+def _segment_path(n: int, dim: int) -> bool:
+    """Sorted segment-reduce update (default) vs the scatter-add + atomic-exchange
+    kernels: the segment kernels take 16-byte row vectors (dim % 8 == 0, dim <= 248)."""
+    return os.environ.get("KFA_SPARSE_ATOMIC", "0") != "1" and dim % 8 == 0 and dim <= 248 and n < 2 ** 31
 
 
 def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits: List[int], in_splits: List[int], pg) -> None:
@@ -68,6 +92,8 @@ class _LookupFn(torch.autograd.Function):
         else:
             order, send_l, recv_l, req = None, None, None, ids
         local = torch.div(req, emb.owners, rounding_mode="floor") if emb.owners > 1 else req
+        # the id sort of the sparse update needs no gradient: start it now, beside the dense layers
+        ctx.prep = emb.prepare_sparse(local) if ctx.needs_input_grad[1] else None
         rows = emb.gather(local)
         if comm:
             out_sorted = torch.empty(n, D, dtype=rows.dtype, device=rows.device)
@@ -93,7 +119,8 @@ class _LookupFn(torch.autograd.Function):
             _a2a(g, d_sorted, recv_l, send_l, emb.pg)
         else:
             g = dout
-        emb.apply_sparse(local, g)
+        emb.apply_sparse(local, g, prep=ctx.prep)
+        ctx.prep = None
         return None, None, None, None
 
 
@@ -164,8 +191,34 @@ class ShardedEmbedding(nn.Module):
                       _lib.ptr(out), n, self.dim, self.dim, _lib.stream())
         return out
 
+    def _nbits(self) -> int:
+        return max(1, (self.local_rows - 1).bit_length())
+
     @torch.no_grad()
-    def apply_sparse(self, local: torch.Tensor, g: torch.Tensor) -> None:
+    def prepare_sparse(self, local: torch.Tensor):
+        """Gradient-independent half of the segment update (radix sort of the ids,
+        segment heads) launched on a side stream right after the forward lookup,
+        so it runs under the dense layers instead of inside backward.  Returns the
+        handle :meth:`apply_sparse` consumes, or None (CPU, atomic path,
+        ``KFA_SPARSE_OVERLAP=0``)."""
+        n = local.numel()
+        if (not self.weight.is_cuda or n == 0 or not _segment_path(n, self.dim)
+                or os.environ.get("KFA_SPARSE_OVERLAP", "1") == "0"):
+            return None
+        nbits = self._nbits()
+        ws = torch.empty(_lib.lib().kfa_seg_ws_bytes(n, nbits), dtype=torch.uint8, device=local.device)
+        main = torch.cuda.current_stream(local.device)
+        side = _side_stream(local.device)
+        side.wait_stream(main)
+        _lib.call("kfa_seg_prepare", _lib.ptr(local), n, nbits, _lib.ptr(ws), ws.numel(), side.cuda_stream)
+        done = torch.cuda.Event()
+        done.record(side)
+        ws.record_stream(side)
+        local.record_stream(side)
+        return ws, nbits, done
+
+    @torch.no_grad()
+    def apply_sparse(self, local: torch.Tensor, g: torch.Tensor, prep=None) -> None:
         self.t += 1
         if local.numel() == 0:
             return
@@ -174,20 +227,41 @@ class ShardedEmbedding(nn.Module):
             self._apply_cpu(local, g.float(), b1, b2)
             return
         self._check_table()
-        scratch = _lib.workspace(self.local_rows * self.dim * 4, self.weight.device,
-                                 f"sparse_scratch{id(self)}").view(torch.float32)
+        n, D = local.numel(), self.dim
         st = _lib.stream()
-        _lib.call("kfa_scatter_add_rows", _lib.ptr(local), _lib.ptr(g.to(torch.bfloat16)), _lib.ptr(scratch),
-                  local.numel(), self.dim, st)
-        if self.optimizer == "adam":
-            c1 = 1.0 / (1.0 - b1 ** self.t)
-            c2 = 1.0 / (1.0 - b2 ** self.t)
+        g16 = g.to(torch.bfloat16).contiguous()
+        adam = self.optimizer == "adam"
+        c1 = 1.0 / (1.0 - b1 ** self.t) if adam else 1.0
+        c2 = 1.0 / (1.0 - b2 ** self.t) if adam else 1.0
+        if prep is not None and _segment_path(n, D):
+            ws, nbits, done = prep
+            torch.cuda.current_stream().wait_event(done)
+            slots = _lib.workspace(_lib.lib().kfa_seg_slot_floats(n, D) * 4, self.weight.device,
+                                   f"seg_sparse_slots{id(self)}").view(torch.float32)
+            _lib.call("kfa_seg_apply", _lib.ptr(g16), n, D, nbits, _lib.ptr(ws), ws.numel(), _lib.ptr(slots),
+                      _lib.ptr(self.weight), _lib.ptr(self.exp_avg), _lib.ptr(self.exp_avg_sq), 0 if adam else 1,
+                      self.lr, b1, b2, self.eps, self.wd, c1, c2, self.grad_scale, st)
+            return
+        if _segment_path(n, D):
+            nbits = self._nbits()
+            ws = _lib.workspace(_lib.lib().kfa_seg_ws_bytes(n, nbits), self.weight.device, "seg_sparse_ws")
+            slots = _lib.workspace(_lib.lib().kfa_seg_slot_floats(n, D) * 4, self.weight.device,
+                                   f"seg_sparse_slots{id(self)}").view(torch.float32)
+            _lib.call("kfa_seg_sparse_apply", _lib.ptr(local), _lib.ptr(g16), n, D, nbits, _lib.ptr(ws),
+                      ws.numel(), _lib.ptr(slots), _lib.ptr(self.weight), _lib.ptr(self.exp_avg),
+                      _lib.ptr(self.exp_avg_sq), 0 if adam else 1, self.lr, b1, b2, self.eps, self.wd, c1, c2,
+                      self.grad_scale, st)
+            return
+        scratch = _lib.workspace(self.local_rows * D * 4, self.weight.device,
+                                 f"sparse_scratch{id(self)}").view(torch.float32)
+        _lib.call("kfa_scatter_add_rows", _lib.ptr(local), _lib.ptr(g16), _lib.ptr(scratch), n, D, st)
+        if adam:
             _lib.call("kfa_sparse_adam", _lib.ptr(local), _lib.ptr(scratch), _lib.ptr(self.weight),
-                      _lib.ptr(self.exp_avg), _lib.ptr(self.exp_avg_sq), local.numel(), self.dim, self.lr, b1, b2,
+                      _lib.ptr(self.exp_avg), _lib.ptr(self.exp_avg_sq), n, D, self.lr, b1, b2,
                       self.eps, self.wd, c1, c2, self.grad_scale, st)
         else:
-            _lib.call("kfa_sparse_sgd", _lib.ptr(local), _lib.ptr(scratch), _lib.ptr(self.weight), local.numel(),
-                      self.dim, self.lr, self.grad_scale, st)
+            _lib.call("kfa_sparse_sgd", _lib.ptr(local), _lib.ptr(scratch), _lib.ptr(self.weight), n, D, self.lr,
+                      self.grad_scale, st)
 
     def _apply_cpu(self, local, g, b1, b2) -> None:
         """Plain-PyTorch reference of the same lazy row update."""
