@@ -94,16 +94,35 @@ struct PppArgs {
   bf16_t* C;
   int M, N, K, lda, ldb, ldc;
   unsigned c_bytes;
+  // split remainder (split > 1): the tiles past the last full round of the grid
+  // are cut into `split` k-ranges run by `split` blocks; parts 1.. leave fp32
+  // partial accumulators in `ws` and count themselves in `flags[unit]`, part 0
+  // adds them and writes C (flags self-cleaning: part 0 resets its counter)
+  float* ws;
+  int* flags;
+  int split;
 };
 
 constexpr int kStoresPerPhase = 4;  // one 16-B store per 16-row block of a 64 x 32 quadrant
 
+// BN: tile width in N, 256 or 192.  A wave's 128 x WN tile (WN = BN / 4) is a
+// 32-column half (nh = 0: two 16-column MFMA blocks) and a NB1-block half
+// (nh = 1: two blocks at BN = 256, one at BN = 192).  BN = 192 serves N = 768
+// (BERT-base's hidden size): 4 tiles per 256-row band, so M = 32768 is 512
+// tiles = exactly two per CU where 256-wide tiles leave 1.5 (384 tiles, half
+// the CUs idle for the second round).  Piece 2 (the nh = 1 B rows) is then 64
+// rows = one DMA per lane, so a k-tile issues D = 6 + NB1 DMAs.
 // NOST: timing probe — every C store dropped (the values kept live).
 // SMODE: bit 0 = non-temporal C stores; bit 1 = row pairs (quadrants (0,0)+(0,1)
 // in phase 0, (1,1)+(1,0) in phase 2: each 128-B row segment written in one phase)
-template <bool NOST = false, int SMODE = 0>
+template <int BN = 256, bool NOST = false, int SMODE = 0>
 __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
-  constexpr int TM = 8, TN = 4;
+  static_assert(BN == 256 || BN == 192, "tile width");
+  static_assert(BN == 256 || !(SMODE & 2), "row pairs need two-block halves");
+  constexpr int NB1 = BN == 256 ? 2 : 1;  // 16-column MFMA blocks in a wave's nh = 1 half
+  constexpr int WN = BN / 4;              // wave tile width
+  constexpr int TM = 8, TN = 2 + NB1;
+  constexpr int D = 6 + NB1;              // DMAs per k-tile
   __shared__ __attribute__((aligned(16))) char smem[2 * 4 * PIECE];  // 128 KB: two k-tiles of four pieces
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -113,17 +132,23 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int q8 = nwg >> 3, r8 = nwg & 7, x8 = bid & 7;
   const int lc = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + (bid >> 3);
-  const int ntn = (g.N + 255) / 256, ntm = (g.M + 255) / 256, ntiles = ntm * ntn;
-  const int my_tiles = lc < ntiles ? (ntiles - 1 - lc) / nwg + 1 : 0;
+  const int ntn = (g.N + BN - 1) / BN, ntm = (g.M + 255) / 256, ntiles = ntm * ntn;
   const int nk = g.K / BK;
-  const int J = my_tiles * nk;  // k-tiles this block runs, all tiles back to back
+  // data-parallel tiles of this block (lc, lc + nwg, ...), then at most one split unit
+  const int ns = g.split;
+  const int ndp = ns > 1 ? ntiles / nwg : (lc < ntiles ? (ntiles - 1 - lc) / nwg + 1 : 0);
+  const int unit = lc / ns, part = lc - unit * ns;
+  const bool has_split = ns > 1 && lc < (ntiles - ndp * nwg) * ns;
+  const int my_tiles = ndp + (has_split ? 1 : 0);
+  const int skb = part * nk / ns, skl = (part + 1) * nk / ns - skb;  // the split unit's k-range
+  const int J = ndp * nk + (has_split ? skl : 0);  // k-tiles this block runs, all tiles back to back
   if (J == 0) return;
   constexpr int GM = 4;
   auto tile_mn = [&](int i, int& m0, int& n0) __attribute__((always_inline)) {
-    const int wg = lc + i * nwg;
+    const int wg = i < ndp ? lc + i * nwg : ndp * nwg + unit;
     const int grp = wg / (GM * ntn), gm0 = grp * GM, gmn = min(GM, ntm - gm0), rem = wg - grp * GM * ntn;
     m0 = (gm0 + rem % gmn) * 256;
-    n0 = (rem / gmn) * 256;
+    n0 = (rem / gmn) * BN;
   };
 
   const __amdgpu_buffer_rsrc_t rA = rsrc(g.A, (unsigned)(((long)(g.M - 1) * g.lda + g.K) * 2));
@@ -142,9 +167,13 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
       if (p == 0 || p == 3) {
         const int m = m0 + j * 128 + h * 64 + prow;
         voff[p][j] = m < g.M ? (m * g.lda + lcx * 8) * 2 : (int)kOOB;
-      } else {
-        const int n = n0 + (2 * j + (prow >> 5)) * 64 + h * 32 + (prow & 31);
+      } else if (p == 1 || j < NB1) {
+        // piece row r -> wave column group r / rows-per-group, column h * 32 + r % rows-per-group
+        const int r = j * 64 + prow, rg = h ? 16 * NB1 : 32;
+        const int n = n0 + (r / rg) * WN + h * 32 + (r % rg);
         voff[p][j] = n < g.N ? (n * g.ldb + lcx * 8) * 2 : (int)kOOB;
+      } else {
+        voff[p][j] = (int)kOOB;
       }
     }
   };
@@ -152,7 +181,10 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
   // issue): pieces 2, 3 of k-tile u fetch k-tile u+1 ("X"), pieces 0, 1 fetch
   // u+2 ("Y"); each side keeps its k index, its local tile and that tile's
   // offsets (voff[2..3] / voff[0..1]).
+  // Each side also keeps its tile's k-range (base, length): the whole K for a
+  // data-parallel tile, [skb, skb + skl) for the split unit.
   int xkt = 0, xti = 0, ykt = 0, yti = 0;
+  int xkb = ndp > 0 ? 0 : skb, xkl = ndp > 0 ? nk : skl, ykb = xkb, ykl = xkl;
   {
     int m0, n0;
     tile_mn(0, m0, n0);
@@ -162,13 +194,15 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
   auto advance = [&](bool X) __attribute__((always_inline)) {  // next k-tile of side X / Y
     int& kt = X ? xkt : ykt;
     int& ti = X ? xti : yti;
-    if (++kt == nk) {
+    if (++kt == (X ? xkl : ykl)) {
       kt = 0;
       if (++ti < my_tiles) {
         int m0, n0;
         tile_mn(ti, m0, n0);
         set_voff(X ? 2 : 0, m0, n0);
         set_voff(X ? 3 : 1, m0, n0);
+        (X ? xkb : ykb) = ti < ndp ? 0 : skb;
+        (X ? xkl : ykl) = ti < ndp ? nk : skl;
       }
     }
   };
@@ -180,10 +214,10 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
     constexpr bool X = (p == 2 || p == 3);
     char* dst = smem + (gk & 1) * (4 * PIECE) + p * PIECE + wave * 8 * 128;
     const __amdgpu_buffer_rsrc_t r = (p == 0 || p == 3) ? rA : rB;
-    const int soff = (X ? xkt : ykt) * BK * 2;
+    const int soff = (X ? xkt + xkb : ykt + ykb) * BK * 2;
     const bool live = gk < J;
     dma16(r, dst, live ? voff[p][0] : (int)kOOB, soff);
-    dma16(r, dst + 64 * 128, live ? voff[p][1] : (int)kOOB, soff);
+    if constexpr (p != 2 || NB1 == 2) dma16(r, dst + 64 * 128, live ? voff[p][1] : (int)kOOB, soff);
   };
 
   const int fr = lane & 15, fq = lane >> 4;
@@ -193,12 +227,31 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
   for (int i = 0; i < TN; i++)
 #pragma unroll
     for (int j = 0; j < TM; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-  short8 a[4][2], b0[2][2], b1[2][2];
+  short8 a[4][2], b0[2][2], b1[NB1][2];
 
   // quadrant (mh, nh) of this wave's tile at (m0, n0) -> bf16 C, then zeroed for the next tile
   const int cb = ((fq & 1) << 4) | ((fq >> 1) << 3);
   auto store_q = [&](int mh, int nh, int m0, int n0) __attribute__((always_inline)) {
-    const int n = n0 + wc * 64 + nh * 32 + cb;
+    if (NB1 == 1 && nh == 1) {  // one 16-column block: 4 consecutive columns (8 B) per lane
+      const int n = n0 + wc * WN + 32 + fq * 4;
+      const bool nok = n < g.N;
+#pragma unroll
+      for (int mi = 0; mi < 4; mi++) {
+        floatx4& x = acc[2][mh * 4 + mi];
+        const unsigned x0 = cvt2(x[0], x[1]), x1 = cvt2(x[2], x[3]);
+        const int m = m0 + wr * 128 + mh * 64 + mi * 16 + fr;
+        const unsigned off = (m < g.M && nok) ? ((unsigned)m * (unsigned)g.ldc + (unsigned)n) * 2u : kOOB;
+        if constexpr (NOST) asm volatile("" :: "v"(x0), "v"(x1), "v"(off));
+        else {
+          using V2 = decltype(__builtin_amdgcn_raw_buffer_load_b64(rC, 0, 0, 0));
+          uint2 v = make_uint2(x0, x1);
+          __builtin_amdgcn_raw_buffer_store_b64(*reinterpret_cast<V2*>(&v), rC, off, 0, (SMODE & 1) ? 2 : 0);
+        }
+        x = floatx4{0.f, 0.f, 0.f, 0.f};
+      }
+      return;
+    }
+    const int n = n0 + wc * WN + nh * 32 + cb;
     const bool nok = n < g.N;
 #pragma unroll
     for (int mi = 0; mi < 4; mi++) {
@@ -221,12 +274,13 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
     }
   };
 
-  auto mfma_q = [&](short8 (&bb)[2][2], int mh, int nh) __attribute__((always_inline)) {
+  auto mfma_q = [&](auto& bb, int mh, int nh) __attribute__((always_inline)) {
+    constexpr int NI = sizeof(bb) / sizeof(bb[0]);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int ks = 0; ks < 2; ks++)
 #pragma unroll
-      for (int ni = 0; ni < 2; ni++)
+      for (int ni = 0; ni < NI; ni++)
 #pragma unroll
         for (int mi = 0; mi < 4; mi++)
           acc[nh * 2 + ni][mh * 4 + mi] =
@@ -245,7 +299,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
   issue(std::integral_constant<int, 0>{}, 1);
   issue(std::integral_constant<int, 1>{}, 1);
   advance(false);
-  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  vm_wait<D>();
   asm volatile("s_barrier" ::: "memory");
   if (wr) asm volatile("s_barrier" ::: "memory");  // group 1 runs one barrier behind
 
@@ -267,13 +321,13 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
       constexpr int RP = (SMODE & 2) ? 1 : 0;
       constexpr int upto = RP ? 8 * (s / 2 + 1) : 4 * (s + 1);          // phases 0..s
       constexpr int after = RP ? 8 * ((3 - s + (s % 2 == 0 ? 0 : 1)) / 2) : 4 * (3 - s);  // phases s+1..3
-      constexpr int n = 8 + (EPI ? upto : 0) + (PEPI ? after : 0);
+      constexpr int n = D + (EPI ? upto : 0) + (PEPI ? after : 0);
       vm_wait<n>();
     };
     // s0: A0 + B0 -> quadrant (0, 0)
     {
       const char* pa = buf + wr * 64 * 128;
-      const char* pb = buf + PIECE + wc * 32 * 128;
+      const char* pb = buf + PIECE + wc * 32 * 128;  // 32 rows per wave column group
 #pragma unroll
       for (int ni = 0; ni < 2; ni++) {
         b0[ni][0] = rd(pb + ni * 16 * 128 + ro0);
@@ -296,9 +350,9 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
     }
     // s1: B1 -> quadrant (0, 1)
     {
-      const char* pb = buf + 2 * PIECE + wc * 32 * 128;
+      const char* pb = buf + 2 * PIECE + wc * (16 * NB1) * 128;
 #pragma unroll
-      for (int ni = 0; ni < 2; ni++) {
+      for (int ni = 0; ni < NB1; ni++) {
         b1[ni][0] = rd(pb + ni * 16 * 128 + ro0);
         b1[ni][1] = rd(pb + ni * 16 * 128 + ro1);
       }
@@ -345,6 +399,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
   int u = 0;
   for (int t = 0; t < my_tiles; t++) {
     int k = 0;
+    const int kl = t < ndp ? nk : skl;
     if (t > 0) {
       pm0 = cm0;
       pn0 = cn0;
@@ -353,9 +408,42 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
       ktile(u++, std::integral_constant<int, 2>{});
       k = 2;
     }
-    for (; k < nk; k++) ktile(u++, std::integral_constant<int, 0>{});
+    for (; k < kl; k++) ktile(u++, std::integral_constant<int, 0>{});
   }
   if (!wr) asm volatile("s_barrier" ::: "memory");  // both groups at the same barrier count
+  if (has_split) {
+    // partial slot of (unit, part >= 1): [TN * TM floatx4][512 threads], coalesced
+    // 16 B per lane; the reader has the same register layout, so no permutation
+    constexpr int NR = TN * TM;
+    floatx4* slots = reinterpret_cast<floatx4*>(g.ws) + (long)unit * (ns - 1) * NR * 512;
+    int* flag = g.flags + unit;
+    if (part) {
+      floatx4* dst = slots + (long)(part - 1) * NR * 512 + tid;
+#pragma unroll
+      for (int i = 0; i < TN; i++)
+#pragma unroll
+        for (int j = 0; j < TM; j++) __builtin_nontemporal_store(acc[i][j], dst + (i * TM + j) * 512);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) __hip_atomic_fetch_add(flag, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    // spin with relaxed loads (an acquire per iteration would invalidate the
+    // XCD's L2 under every CU still streaming), then ONE acquire fence
+    if (tid == 0) {
+      while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < ns - 1) __builtin_amdgcn_s_sleep(2);
+      __hip_atomic_store(flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    for (int q = 0; q < ns - 1; q++) {
+      const floatx4* src = slots + (long)q * NR * 512 + tid;
+#pragma unroll
+      for (int i = 0; i < TN; i++)
+#pragma unroll
+        for (int j = 0; j < TM; j++) acc[i][j] += __builtin_nontemporal_load(src + (i * TM + j) * 512);
+    }
+  }
   // the last tile's C
   store_q(0, 0, cm0, cn0);
   store_q(0, 1, cm0, cn0);
@@ -379,28 +467,78 @@ int ppp_cus() {
 
 // C = A · Bᵀ (bf16 out) on the persistent ping-pong kernel.  K % 64 == 0,
 // N % 8 == 0, every extent within 31-bit buffer offsets; grid = min(tiles, CUs)
-// (or `blocks` if > 0).  Returns 0, -1 on unsupported operands.
+// (or `blocks` if > 0).  bn: tile width 256 or 192 (0 = pick: 192 when N is a
+// multiple of 192 and 256-wide tiles would leave a partial last round).
+// Returns 0, -1 on unsupported operands.
+KFA_API int kfa_gemm_ppp_pick_bn(int M, int N);
+
+// Split factor for the tiles past the last full round of a `cus`-block grid:
+// r leftover tiles each cut into s = min(cus / r, nk / 2, 8) k-ranges when that
+// is >= 2 (every block then runs the same number of k-tiles, +-1 range); 1 = no split.
+static int ppp_split(long tiles, long cus, int nk) {
+  const long r = tiles % cus;
+  if (r == 0 || 2 * r > cus) return 1;
+  long s = cus / r;
+  if (s > nk / 2) s = nk / 2;
+  if (s > 8) s = 8;
+  return s >= 2 ? (int)s : 1;
+}
+
+// Workspace bytes kfa_gemm_ppp needs for this problem (0: no split): the
+// self-cleaning unit counters (zero-initialised once), then the fp32 partial slots.
+KFA_API long kfa_gemm_ppp_ws_bytes(int M, int N, int K, int bn, int blocks) {
+  if (bn == 0) bn = kfa_gemm_ppp_pick_bn(M, N);
+  const long tiles = (long)((M + 255) / 256) * ((N + bn - 1) / bn);
+  const long cus = blocks > 0 ? blocks : ppp_cus();
+  if (tiles <= 0 || K % BK) return 0;
+  const int s = ppp_split(tiles, cus, K / BK);
+  if (s == 1) return 0;
+  const long r = tiles % cus;
+  return 4096 + r * (s - 1) * 256L * bn * 4;
+}
+
+KFA_API int kfa_gemm_ppp_pick_bn(int M, int N) {
+  const long cus = ppp_cus();
+  if (N % 192) return 256;
+  const long t256 = (long)((M + 255) / 256) * ((N + 255) / 256), t192 = (long)((M + 255) / 256) * (N / 192);
+  // rounds of the persistent grid, in 256-wide tile units of work
+  const double r256 = (double)((t256 + cus - 1) / cus), r192 = 0.75 * (double)((t192 + cus - 1) / cus);
+  return r192 < r256 ? 192 : 256;
+}
+
 KFA_API int kfa_gemm_ppp(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int K, int lda, int ldb, int ldc,
-                         int blocks, int probe, hipStream_t st) {
+                         int blocks, int probe, int bn, void* ws, long ws_bytes, int nosplit, hipStream_t st) {
   if (M <= 0 || N <= 0) return 0;
   // K >= 128: two k-tiles per tile at least (a tile's first two k-tiles carry its predecessor's stores)
   if (K < 2 * BK || K % BK || N % 8 || lda % 8 || ldb % 8 || ldc % 8 || lda < K || ldb < K || ldc < N) return -1;
   const long cb = (long)M * ldc * 2;
   if (cb >= (long)kOOB || (long)M * lda * 2 >= (long)kOOB || (long)N * ldb * 2 >= (long)kOOB) return -2;
-  const long tiles = (long)((M + 255) / 256) * ((N + 255) / 256);
+  if (bn == 0) bn = kfa_gemm_ppp_pick_bn(M, N);
+  if (bn != 256 && bn != 192) return -1;
+  const long tiles = (long)((M + 255) / 256) * ((N + bn - 1) / bn);
   const long cus = blocks > 0 ? blocks : ppp_cus();
-  const int grid = (int)(tiles < cus ? tiles : cus);
-  const PppArgs g{A, B, C, M, N, K, lda, ldb, ldc, (unsigned)cb};
+  int split = nosplit ? 1 : ppp_split(tiles, cus, K / BK);
+  if (split > 1 && (ws == nullptr || ws_bytes < kfa_gemm_ppp_ws_bytes(M, N, K, bn, blocks))) return -3;
+  // a split grid is the whole `cus` blocks (the split units fill the last round)
+  const int grid = split > 1 ? (int)cus : (int)(tiles < cus ? tiles : cus);
+  const PppArgs g{A, B, C, M, N, K, lda, ldb, ldc, (unsigned)cb, ws ? reinterpret_cast<float*>((char*)ws + 4096) : nullptr,
+                  reinterpret_cast<int*>(ws), split};
+  const dim3 gd(grid), bd(512);
+  if (bn == 192) {
+    if (probe == 1) hipLaunchKernelGGL((gemm_ppp_kernel<192, true>), gd, bd, 0, st, g);
+    else if (probe == 2) hipLaunchKernelGGL((gemm_ppp_kernel<192, false, 1>), gd, bd, 0, st, g);
+    else hipLaunchKernelGGL((gemm_ppp_kernel<192, false>), gd, bd, 0, st, g);
+    return kfa_status();
+  }
   if (probe == 1)  // timing probe: no C stores
-    hipLaunchKernelGGL(gemm_ppp_kernel<true>, dim3(grid), dim3(512), 0, st, g);
+    hipLaunchKernelGGL((gemm_ppp_kernel<256, true>), gd, bd, 0, st, g);
   else if (probe == 2)  // store-policy experiments: nt / row pairs / both
-    hipLaunchKernelGGL((gemm_ppp_kernel<false, 1>), dim3(grid), dim3(512), 0, st, g);
+    hipLaunchKernelGGL((gemm_ppp_kernel<256, false, 1>), gd, bd, 0, st, g);
   else if (probe == 3)
-    hipLaunchKernelGGL((gemm_ppp_kernel<false, 2>), dim3(grid), dim3(512), 0, st, g);
+    hipLaunchKernelGGL((gemm_ppp_kernel<256, false, 2>), gd, bd, 0, st, g);
   else if (probe == 4)
-    hipLaunchKernelGGL((gemm_ppp_kernel<false, 3>), dim3(grid), dim3(512), 0, st, g);
-
+    hipLaunchKernelGGL((gemm_ppp_kernel<256, false, 3>), gd, bd, 0, st, g);
   else
-    hipLaunchKernelGGL(gemm_ppp_kernel<false>, dim3(grid), dim3(512), 0, st, g);
+    hipLaunchKernelGGL((gemm_ppp_kernel<256, false>), gd, bd, 0, st, g);
   return kfa_status();
 }

@@ -137,8 +137,11 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ 
 // each block adds its column sums to dgamma / dbeta / dbias (sum of the branch
 // gradient) with one fp32 atomic per column (no partial buffer, no finalize
 // launch).
-template <int NV>
-__global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ xs,
+// dy2 (nullable): a second gradient summed into dy on the fly — a residual join
+// (dres + dbranch·W) whose GEMM then needs no addend epilogue (ops/transformer.py).
+template <int NV, bool TWO>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ dy2,
+                                                     const bf16_t* __restrict__ xs,
                                                      const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
                                                      const float* __restrict__ gamma, bf16_t* __restrict__ dx,
                                                      bf16_t* __restrict__ dbranch, float* __restrict__ o_gamma,
@@ -156,13 +159,14 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
     for (int e = 0; e < 8; e++) ag[j][e] = ab[j][e] = ad[j][e] = 0.f;
 
   // software pipeline: the next row's dy / x are in flight while this row reduces
-  uint4 nd[NV], nx[NV];
+  uint4 nd[NV], nx[NV], ne[NV];
   auto fetch = [&](long row) {
 #pragma unroll
     for (int j = 0; j < NV; j++) {
       const int c = (j * 64 + lane) * 8;
       if (c < H && row < r1) {
         nd[j] = ld16(dy + row * (long)H + c);
+        if constexpr (TWO) ne[j] = ld16(dy2 + row * (long)H + c);
         nx[j] = ld16(xs + row * (long)H + c);
       }
     }
@@ -171,9 +175,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
   for (long row = r0 + w; row < r1; row += kRowsPerBlock) {
     const long base = row * (long)H;
     const float mean = mean_in[row], rstd = rstd_in[row];
-    uint4 cd[NV], cx[NV];
+    uint4 cd[NV], cx[NV], ce[NV];
 #pragma unroll
-    for (int j = 0; j < NV; j++) { cd[j] = nd[j]; cx[j] = nx[j]; }
+    for (int j = 0; j < NV; j++) { cd[j] = nd[j]; cx[j] = nx[j]; ce[j] = ne[j]; }
     fetch(row + kRowsPerBlock);
     float xh[NV][8], g[NV][8];
     float s1 = 0.f, s2 = 0.f;
@@ -183,6 +187,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
       if (c < H) {
         float d[8], xv[8], gm[8];
         unpack8(cd[j], d);
+        if constexpr (TWO) {
+          float d2[8];
+          unpack8(ce[j], d2);
+#pragma unroll
+          for (int e = 0; e < 8; e++) d[e] += d2[e];
+        }
         unpack8(cx[j], xv);
         load8f(gamma + c, gm);
 #pragma unroll
@@ -608,11 +618,17 @@ void launch_ln_fwd(dim3 g, hipStream_t s, const void* x, const void* res, const 
                      (bf16_t*)y, (bf16_t*)xsum, mean, rstd, rows, H, eps, th, ds, seed);
 }
 template <int NV>
-void launch_ln_bwd(dim3 g, size_t lds, hipStream_t s, const void* dy, const void* xs, const float* mean,
-                   const float* rstd, const float* gamma, void* dx, void* dbranch, float* o0, float* o1, float* o2,
-                   long rows, int H, long rpb, uint32_t th, float ds, uint64_t seed) {
-  hipLaunchKernelGGL(ln_bwd_kernel<NV>, g, dim3(256), lds, s, (const bf16_t*)dy, (const bf16_t*)xs, mean, rstd, gamma,
-                     (bf16_t*)dx, (bf16_t*)dbranch, o0, o1, o2, rows, H, rpb, th, ds, seed);
+void launch_ln_bwd(dim3 g, size_t lds, hipStream_t s, const void* dy, const void* dy2, const void* xs,
+                   const float* mean, const float* rstd, const float* gamma, void* dx, void* dbranch, float* o0,
+                   float* o1, float* o2, long rows, int H, long rpb, uint32_t th, float ds, uint64_t seed) {
+  if (dy2)
+    hipLaunchKernelGGL((ln_bwd_kernel<NV, true>), g, dim3(256), lds, s, (const bf16_t*)dy, (const bf16_t*)dy2,
+                       (const bf16_t*)xs, mean, rstd, gamma, (bf16_t*)dx, (bf16_t*)dbranch, o0, o1, o2, rows, H, rpb,
+                       th, ds, seed);
+  else
+    hipLaunchKernelGGL((ln_bwd_kernel<NV, false>), g, dim3(256), lds, s, (const bf16_t*)dy, nullptr,
+                       (const bf16_t*)xs, mean, rstd, gamma, (bf16_t*)dx, (bf16_t*)dbranch, o0, o1, o2, rows, H, rpb,
+                       th, ds, seed);
 }
 template <int G, int NV>
 void launch_sm_fwd(hipStream_t s, void* scores, const float* key_bias, void* pdrop, long rows, int S, int heads,
@@ -650,9 +666,11 @@ static void zero_if(float* p, int n, int accumulate, hipStream_t s) {
 
 // dgamma/dbeta/dbias: fp32, (+)= when accumulate (else overwritten); any may be
 // null.  `part` is unused (kept for ABI stability).
-KFA_API int kfa_ln_bwd(const void* dy, const void* xs, const float* mean, const float* rstd, const float* gamma,
-                       void* dx, void* dbranch, float* part, float* dgamma, float* dbeta, float* dbias, long rows,
-                       int H, float p, unsigned long long seed, int accumulate, hipStream_t s) {
+// dy2 (nullable): second gradient, the kernel's dy is dy + dy2.
+KFA_API int kfa_ln_bwd2(const void* dy, const void* dy2, const void* xs, const float* mean, const float* rstd,
+                        const float* gamma, void* dx, void* dbranch, float* part, float* dgamma, float* dbeta,
+                        float* dbias, long rows, int H, float p, unsigned long long seed, int accumulate,
+                        hipStream_t s) {
   (void)part;
   if (rows <= 0 || H % 8 || H > 4096) return -1;
   const long nblk = ln_bwd_blocks(rows);
@@ -664,14 +682,21 @@ KFA_API int kfa_ln_bwd(const void* dy, const void* xs, const float* mean, const 
   zero_if(dbeta, H, accumulate, s);
   zero_if(dbias, H, accumulate, s);
   dim3 g((unsigned)nblk);
-#define LNB(NV) launch_ln_bwd<NV>(g, lds, s, dy, xs, mean, rstd, gamma, dx, dbranch, dgamma, dbeta, dbias, rows, H, \
-                                  rpb, th, ds, seed)
+#define LNB(NV) launch_ln_bwd<NV>(g, lds, s, dy, dy2, xs, mean, rstd, gamma, dx, dbranch, dgamma, dbeta, dbias, rows, \
+                                  H, rpb, th, ds, seed)
   if (H <= 512) LNB(1);
   else if (H <= 1024) LNB(2);
   else if (H <= 2048) LNB(4);
   else LNB(8);
 #undef LNB
   return kfa_status();
+}
+
+KFA_API int kfa_ln_bwd(const void* dy, const void* xs, const float* mean, const float* rstd, const float* gamma,
+                       void* dx, void* dbranch, float* part, float* dgamma, float* dbeta, float* dbias, long rows,
+                       int H, float p, unsigned long long seed, int accumulate, hipStream_t s) {
+  return kfa_ln_bwd2(dy, nullptr, xs, mean, rstd, gamma, dx, dbranch, part, dgamma, dbeta, dbias, rows, H, p, seed,
+                     accumulate, s);
 }
 
 KFA_API int kfa_bias_act_fwd(const void* x, const float* b, void* y, long rows, int N, int act, float p,

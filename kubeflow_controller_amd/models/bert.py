@@ -159,9 +159,14 @@ class BertForPreTraining(nn.Module):
         if ph > 0:
             h = T.dense_dropout(h, ph, T.mix_seed(step_seed, 999))
         kb = self.key_bias(attention_mask)
+        # layer i+1's QKV-projection dgrad reaches layer i's LN2 backward through a
+        # ResidualJoin (summed on read) instead of a GEMM addend (ops/transformer.py)
+        join_in = None
         for i, layer in enumerate(self.layers):
-            lcfg = (B, S, cfg.heads, ph, pa, T.mix_seed(step_seed, i), cfg.ln_eps)
+            join_out = T.ResidualJoin() if (self.training and i + 1 < len(self.layers)) else None
+            lcfg = (B, S, cfg.heads, ph, pa, T.mix_seed(step_seed, i), cfg.ln_eps, join_in, join_out)
             h = T.EncoderLayerFn.apply(h, kb, lcfg, *layer.params())
+            join_in = join_out
         # MLM on the masked positions only
         hm = h.index_select(0, mlm_positions.reshape(-1))
         t = T.dense(hm, self.mlm_w, self.mlm_b, "gelu")

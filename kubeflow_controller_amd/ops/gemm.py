@@ -31,7 +31,9 @@ P, I = _lib.P, _lib.I
 _lib.register("kfa_gemm_nt", [P] * 9 + [I] * 10 + [P])
 _lib.register("kfa_gemm_dpart_floats", [I, I, I, I], restype=_lib.L)
 _lib.register("kfa_gemm_pick_bn", [I, I])
-_lib.register("kfa_gemm_ppp", [P, P, P] + [I] * 8 + [P])
+_lib.register("kfa_gemm_ppp", [P, P, P] + [I] * 9 + [P, _lib.L, I, P])
+_lib.register("kfa_gemm_ppp_ws_bytes", [I] * 5, restype=_lib.L)
+_lib.register("kfa_gemm_ppp_pick_bn", [I, I])
 
 ACTS = {None: 0, "none": 0, "gelu": 1, "tanh": 2, "relu": 3}
 # Which dense-layer GEMMs run on this kernel (KFA_GEMM):
@@ -147,21 +149,28 @@ def gemm_nt(a, b, *, bias=None, act=None, addend=None, want_z=False, zin=None, d
     return c, z
 
 
-def gemm_ppp(a, b, *, out=None, blocks: int = 0, probe: int = 0):
+def gemm_ppp(a, b, *, out=None, blocks: int = 0, probe: int = 0, bn: int = 0, split: bool = True):
     """``a @ b.T`` (bf16) on the persistent ping-pong kernel (``csrc/kernels/gemm_ppp.hip``):
     one block per CU sweeps its tiles as one continuous k-tile pipeline, each tile's
     C written from the accumulators during the next tile's first k-tile.  K % 64 == 0, K >= 128.
     ``blocks`` > 0 caps the persistent grid (tests: many tiles per block).  ``probe=1``:
-    timing probe with every C store dropped (C is left unwritten).  Opt-in:
-    measured below hipBLASLt on the BERT shapes (``profiles/r3_gemm_ppp.txt``)."""
+    timing probe with every C store dropped (C is left unwritten).  ``bn``: tile
+    width 256 or 192 (0 = the kernel's pick: 192-wide tiles where N % 192 == 0 and
+    256-wide ones would leave a partial last round, e.g. N = 768 at M = 32768).
+    ``split``: the tiles past the grid's last full round are cut into k-ranges
+    run by several blocks (fp32 partials combined in-kernel), so every CU runs
+    about the same number of k-tiles — e.g. 384 tiles on 256 CUs: one full tile
+    plus half a tile each instead of two tiles on half the CUs."""
     if not gemm_ok(a, b) or a.shape[1] % 64 or a.shape[1] < 128:
         raise ValueError(f"gemm_ppp: unsupported operands {tuple(a.shape)} x {tuple(b.shape)}")
     M, K = a.shape
     N = b.shape[0]
     c = out if out is not None else torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
     _check_mn(c, M, N, "out")
+    nb = _lib.lib().kfa_gemm_ppp_ws_bytes(M, N, K, int(bn), int(blocks)) if split else 0
+    ws = _lib.workspace(nb, a.device, f"ppp_ws{_lib.stream() or 0}") if nb > 0 else None
     _lib.call("kfa_gemm_ppp", _lib.ptr(a), _lib.ptr(b), _lib.ptr(c), M, N, K, a.stride(0), b.stride(0), N,
-              int(blocks), int(probe), _lib.stream())
+              int(blocks), int(probe), int(bn), _lib.ptr(ws), nb, int(not split), _lib.stream())
     return c
 
 
@@ -170,31 +179,90 @@ def ppp_ok(a, b) -> bool:
     return gemm_ok(a, b) and a.shape[1] % 64 == 0 and a.shape[1] >= 128
 
 
+def _agree_int(v: int, device) -> int:
+    """Rank 0's choice among several kernels (see ``ops.conv._agree``)."""
+    import torch.distributed as dist
+    from . import conv as _c
+    if not _c._LOCKSTEP or not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return v
+    dev = device if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([int(v)], dtype=torch.int32, device=dev)
+    dist.broadcast(t, 0)
+    return int(t.item())
+
+
+def pick_fastest(kind: str, key: tuple, device, candidates) -> int:
+    """Index of the fastest of ``candidates`` (``[(name, fn), ...]``, index 0 =
+    the library form) for this shape, timed once at first use outside any graph
+    capture; rank 0's choice is applied on every rank.  An own kernel must beat
+    the library by 1 % to be picked (timing noise never flips a tie to it)."""
+    k = (kind,) + tuple(key)
+    hit = _choice.get(k)
+    if hit is not None:
+        return hit
+    if torch.cuda.is_current_stream_capturing():
+        return 0
+    from .conv import _time_ms
+    with torch.no_grad():
+        ts = [_time_ms(fn, reps=10) for _, fn in candidates]
+    best = min(range(1, len(ts)), key=lambda i: ts[i]) if len(ts) > 1 else 0
+    if best and not ts[best] < 0.99 * ts[0]:
+        best = 0
+    hit = _choice[k] = _agree_int(best, device)
+    if TUNE_LOG:
+        import sys
+        desc = ", ".join(f"{n} {t:.4f} ms" for (n, _), t in zip(candidates, ts))
+        print(f"[kfa gemm tune] {kind} {key}: {desc} -> {candidates[hit][0]}", file=sys.stderr, flush=True)
+    return hit
+
+
+def _ppp_candidates(a, b):
+    """Persistent-GEMM variants worth timing for ``a @ b.T``: 256-wide tiles with
+    and without the split remainder, 192-wide tiles where N % 192 == 0."""
+    M, K = a.shape
+    N = b.shape[0]
+    L = _lib.lib()
+    c = [("ppp256", lambda: gemm_ppp(a, b, bn=256, split=False))]
+    if L.kfa_gemm_ppp_ws_bytes(M, N, K, 256, 0) > 0:
+        c.append(("ppp256-split", lambda: gemm_ppp(a, b, bn=256)))
+    if N % 192 == 0:
+        c.append(("ppp192", lambda: gemm_ppp(a, b, bn=192)))
+    return c
+
+
 def mm_auto(a, w, kind: str = "proj"):
-    """``a @ w.T`` (bf16): the persistent MFMA GEMM where it measured faster than
-    hipBLASLt for this shape (timed once at first use, rank 0's choice applied
-    everywhere — :func:`prefer_own`), else the library.  ``KFA_GEMM=0`` forces
-    the library."""
+    """``a @ w.T`` (bf16): the persistent MFMA GEMM variant that measured fastest
+    for this shape when it beats hipBLASLt (timed once at first use, rank 0's
+    choice applied everywhere — :func:`pick_fastest`), else the library.
+    ``KFA_GEMM=0`` forces the library."""
     if ROUTE_AUTO and ppp_ok(a, w):
-        if prefer_own(kind, (a.shape[0], w.shape[0], a.shape[1]), a.device, lambda: gemm_ppp(a, w),
-                      lambda: torch.mm(a, w.t())):
-            return gemm_ppp(a, w)
+        cands = [("hipblaslt", lambda: torch.mm(a, w.t()))] + _ppp_candidates(a, w)
+        i = pick_fastest(kind, (a.shape[0], w.shape[0], a.shape[1]), a.device, cands)
+        if i:
+            return cands[i][1]()
     return torch.mm(a, w.t())
 
 
 def dgrad_auto(dz, w, kind: str = "proj_dgrad"):
-    """``dz @ w`` (the data gradient of ``y = x @ w.T``): the persistent MFMA GEMM on
-    the transposed weight (transpose included in its timing) where it measured
-    faster than hipBLASLt for this shape, else the library."""
+    """``dz @ w`` (the data gradient of ``y = x @ w.T``): the fastest persistent
+    MFMA GEMM variant on the transposed weight (transpose included in its timing)
+    where it beats hipBLASLt for this shape, else the library."""
     M, K = dz.shape if dz.dim() == 2 else (0, 0)
     N = w.shape[1] if w.dim() == 2 else 0
     if (ROUTE_AUTO and dz.is_cuda and dz.dim() == 2 and w.dim() == 2 and dz.dtype == torch.bfloat16
             and w.dtype == torch.bfloat16 and dz.is_contiguous() and dz.data_ptr() % 16 == 0 and K == w.shape[0]
             and K % 64 == 0 and K >= 128 and N % 8 == 0 and M > 0
             and max(M * N, M * K, N * K) * 2 < (1 << 31)):
-        if prefer_own(kind, (dz.shape[0], w.shape[1], w.shape[0]), dz.device, lambda: gemm_ppp(dz, transpose(w)),
-                      lambda: torch.mm(dz, w)):
-            return gemm_ppp(dz, transpose(w))
+        k = (kind, M, N, K)
+        if _choice.get(k) == 0:
+            return torch.mm(dz, w)
+        wt = transpose(w)
+        own = _ppp_candidates(dz, wt)
+        cands = [("hipblaslt", lambda: torch.mm(dz, w))] + [
+            (n, (lambda f: lambda: (transpose(w), f())[1])(f)) for n, f in own]
+        i = pick_fastest(kind, (M, N, K), dz.device, cands)
+        if i:
+            return own[i - 1][1]()
     return torch.mm(dz, w)
 
 

@@ -42,6 +42,7 @@ _lib.register("kfa_ln_part_floats", [L, I], L)
 _lib.register("kfa_colsum_part_floats", [L, I], L)
 _lib.register("kfa_ln_fwd", [P, P, P, P, P, P, P, P, P, L, I, Fl, Fl, U64, P])
 _lib.register("kfa_ln_bwd", [P, P, P, P, P, P, P, P, P, P, P, L, I, Fl, U64, I, P])
+_lib.register("kfa_ln_bwd2", [P, P, P, P, P, P, P, P, P, P, P, P, L, I, Fl, U64, I, P])
 _lib.register("kfa_bias_act_fwd", [P, P, P, L, I, I, Fl, U64, P])
 _lib.register("kfa_bias_act_bwd", [P, P, P, P, P, P, L, I, I, Fl, U64, I, P])
 _lib.register("kfa_qkv_split", [P, P, P, P, P, L, I, I, I, Fl, P])
@@ -106,15 +107,45 @@ def ln_fwd(x, gamma, beta, res=None, bias=None, eps=1e-12, p=0.0, seed=0, save_s
     return y, (xs if xs is not None else x), mean, rstd
 
 
-def ln_bwd(dy, xs, mean, rstd, gamma, dgamma, dbeta, dbias=None, p=0.0, seed=0, want_branch=False):
+def ln_bwd(dy, xs, mean, rstd, gamma, dgamma, dbeta, dbias=None, p=0.0, seed=0, want_branch=False, dy2=None):
+    """LayerNorm backward of the gradient ``dy`` (+ ``dy2``, summed on the fly: a
+    residual join whose projection dgrad then needs no addend)."""
     rows, H = dy.numel() // dy.shape[-1], dy.shape[-1]
+    if dy2 is not None and (dy2.shape != dy.shape or dy2.dtype != dy.dtype or not dy2.is_contiguous()):
+        raise ValueError(f"ln_bwd: dy2 {tuple(dy2.shape)} must match dy {tuple(dy.shape)}")
     dx = torch.empty_like(dy)
     dbr = torch.empty_like(dy) if (want_branch and p > 0) else None
     part = _part(_lib.lib().kfa_ln_part_floats(rows, H), dy.device)
-    _lib.call("kfa_ln_bwd", _lib.ptr(dy), _lib.ptr(xs), _lib.ptr(mean), _lib.ptr(rstd), _lib.ptr(gamma), _lib.ptr(dx),
-              _lib.ptr(dbr), _lib.ptr(part), _lib.ptr(dgamma), _lib.ptr(dbeta), _lib.ptr(dbias), rows, H, float(p), seed,
-              1, _lib.stream())
+    _lib.call("kfa_ln_bwd2", _lib.ptr(dy), _lib.ptr(dy2), _lib.ptr(xs), _lib.ptr(mean), _lib.ptr(rstd), _lib.ptr(gamma),
+              _lib.ptr(dx), _lib.ptr(dbr), _lib.ptr(part), _lib.ptr(dgamma), _lib.ptr(dbeta), _lib.ptr(dbias), rows, H,
+              float(p), seed, 1, _lib.stream())
     return dx, (dbr if dbr is not None else dx)
+
+
+class ResidualJoin:
+    """Gradient hand-off between consecutive encoder layers.  Layer L's input is
+    layer L-1's output h, whose gradient is ``dx_res + dqkv · Wqkv`` (residual
+    path + QKV-projection dgrad).  Layer L's backward deposits the projection
+    term here and returns only ``dx_res``; layer L-1's backward takes it back and
+    its LayerNorm backward sums the two on read (``ln_bwd(dy2=...)``).  So the
+    dgrad is a plain GEMM (no addend epilogue, no beta = 1 read of C) and the sum
+    is never written.  Only valid when h feeds nothing but layer L and the join
+    consumer (``models/bert.py``); autograd's other consumers of h, if any, still
+    add into ``dy`` as usual."""
+
+    __slots__ = ("g",)
+
+    def __init__(self):
+        self.g = None
+
+    def deposit(self, g: torch.Tensor) -> None:
+        if self.g is not None:
+            raise RuntimeError("ResidualJoin: gradient deposited twice (backward through the graph twice?)")
+        self.g = g
+
+    def take(self):
+        g, self.g = self.g, None
+        return g
 
 
 def bias_act_fwd(x, bias, act, p=0.0, seed=0):
@@ -422,7 +453,10 @@ class EncoderLayerFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, key_bias, cfg, wqkv, bqkv, wo, bo, g1, be1, w1, b1, w2, b2, g2, be2):
-        B, S, heads, ph, pa, seed, eps = cfg
+        # cfg[7:9] (optional): ResidualJoin of this layer's input (deposited into by
+        # the backward) and of its output (taken from by the backward)
+        B, S, heads, ph, pa, seed, eps = cfg[:7]
+        ctx.joins = (tuple(cfg[7:9]) + (None, None))[:2]
         T, H = x.shape
         d = H // heads
         qscale = 1.0 / math.sqrt(d)
@@ -483,10 +517,14 @@ class EncoderLayerFn(torch.autograd.Function):
         d = H // heads
         st = _lib.stream()
         dy = dy.contiguous()
+        join_in, join_out = ctx.joins
         tg = {id(p): _grad_target(p) for p in ctx.params}
         G = lambda p: tg[id(p)][0]  # noqa: E731
-        # LN2 (+ FFN2 bias grad, hidden dropout): dres -> h1, dbranch -> f2
-        dh1_res, df2 = ln_bwd(dy, h2s, m2, r2, g2, G(g2), G(be2), G(b2), p=ph, seed=s_h2, want_branch=True)
+        # LN2 (+ FFN2 bias grad, hidden dropout): dres -> h1, dbranch -> f2; the next
+        # layer's QKV dgrad (its ResidualJoin deposit) is summed in on read
+        dy2 = join_out.take() if join_out is not None else None
+        dh1_res, df2 = ln_bwd(dy, h2s, m2, r2, g2, G(g2), G(be2), G(b2), p=ph, seed=s_h2, want_branch=True, dy2=dy2)
+        del dy2
         _wgrad_side_(G(w2), df2, f1a)
         if use_f:   # df1 = (df2 · W2) * gelu'(z1), db1 += colsum(df1): one GEMM launch
             df1 = _gemm.gemm_nt(df2, _gemm.transpose(w2), zin=f1, dact="gelu", dbias=G(b1))[0]
@@ -495,15 +533,16 @@ class EncoderLayerFn(torch.autograd.Function):
         del df2
         _wgrad_side_(G(w1), df1, h1)
         if use_g:   # residual-gradient join as the GEMM addend
-            dh1 = _gemm.gemm_nt(df1, _gemm.transpose(w1), addend=dh1_res)[0]
-        else:
-            dh1 = dh1_res.addmm_(df1, w1)  # in place: addmm(C, ..) would first copy C (a D2D memcpy)
+            dh1, dh1b = _gemm.gemm_nt(df1, _gemm.transpose(w1), addend=dh1_res)[0], None
+        else:       # plain dgrad; LN1's backward sums the residual gradient on read
+            dh1, dh1b = dh1_res, _gemm.dgrad_auto(df1, w1)
         del df1, dh1_res
         # LN1 (+ out-proj bias grad)
-        dx_res, dao = ln_bwd(dh1, h1s, m1, r1, g1, G(g1), G(be1), G(bo), p=ph, seed=s_h1, want_branch=True)
-        del dh1
+        dx_res, dao = ln_bwd(dh1, h1s, m1, r1, g1, G(g1), G(be1), G(bo), p=ph, seed=s_h1, want_branch=True, dy2=dh1b)
+        del dh1, dh1b
         _wgrad_side_(G(wo), dao, ctxr)
         dctxr = _gemm.gemm_nt(dao, _gemm.transpose(wo))[0] if use_g else _gemm.dgrad_auto(dao, wo)
+        res_shared = dao is dx_res  # no hidden dropout: one tensor, also the side stream's wgrad operand
         del dao
         if fused:
             qkv, lse = att
@@ -534,6 +573,11 @@ class EncoderLayerFn(torch.autograd.Function):
         _wgrad_side_(G(wqkv), dqkv, x)
         if use_g:
             dx = _gemm.gemm_nt(dqkv, _gemm.transpose(wqkv), addend=dx_res)[0]
+        elif join_in is not None:  # the previous layer's LN2 backward adds it on read
+            join_in.deposit(_gemm.dgrad_auto(dqkv, wqkv))
+            dx = dx_res
+        elif res_shared:  # never written in place while the side stream may read it
+            dx = torch.addmm(dx_res, dqkv, wqkv)
         else:
             dx = dx_res.addmm_(dqkv, wqkv)
         grads = [_finish(p, tg[id(p)][0], tg[id(p)][2]) for p in ctx.params]
@@ -590,7 +634,7 @@ class DecoderXentFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, t, w, b, labels):
         t = t.contiguous()
-        logits = torch.mm(t, w.t())
+        logits = _gemm.mm_auto(t, w, "decoder")
         n, V = logits.shape
         lab = labels.reshape(-1).to(torch.int64).contiguous()
         row_loss = torch.empty(n, dtype=torch.float32, device=t.device)
@@ -607,7 +651,7 @@ class DecoderXentFn(torch.autograd.Function):
         t, w, dlog = ctx.saved_tensors
         wp, bp = ctx.params
         dlog.mul_(g.to(dlog.dtype))
-        dt = torch.mm(dlog, w)
+        dt = _gemm.dgrad_auto(dlog, w, "decoder_dgrad")
         gw, _, dw = _grad_target(wp)
         _wgrad_(gw, dlog, t)
         gb, _, db = _grad_target(bp)

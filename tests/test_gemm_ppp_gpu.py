@@ -42,6 +42,47 @@ def test_gemm_ppp_matches_fp32(M, N, K, blocks):
     _close(c, a.float() @ b.float().t(), 1e-2, f"C {M}x{N}x{K} blocks={blocks}")
 
 
+@pytest.mark.parametrize("M,N,K,blocks", [
+    (256, 192, 128, 0),       # one 256 x 192 tile, two k-tiles
+    (512, 384, 128, 1),       # 4 tiles on one block: every k-tile a boundary one
+    (1000, 776, 192, 3),      # edge tiles in M and N (N = 776: last tile 8 columns wide), uneven tile counts
+    (32768, 768, 768, 0),     # BERT out-projection: 512 tiles = two per CU
+    (32768, 768, 3072, 0),    # BERT FFN-down
+    (2048, 1536, 2304, 5),    # long k-loop, many tiles per block
+    (300, 200, 128, 0),       # partial nh = 1 half (columns 192..199)
+])
+def test_gemm_ppp_bn192_matches_fp32(M, N, K, blocks):
+    """192-wide tiles (one-block nh = 1 halves, 8-B stores, 7 DMAs per k-tile)."""
+    from kubeflow_controller_amd.ops import gemm as G
+    torch.manual_seed(M + N + K + 1)
+    a, b = _bf(M, K), _bf(N, K, s=0.05)
+    c = G.gemm_ppp(a, b, blocks=blocks, bn=192)
+    _close(c, a.float() @ b.float().t(), 1e-2, f"C {M}x{N}x{K} bn=192 blocks={blocks}")
+
+
+@pytest.mark.parametrize("M,N,K,blocks,bn", [
+    (32768, 768, 768, 0, 256),   # 384 tiles on 256 CUs: 128 leftover tiles in 2 k-ranges each
+    (1024, 1024, 1024, 12, 256), # 16 tiles on 12 blocks: 4 leftover tiles in 3 uneven k-ranges
+    (256, 512, 2048, 0, 256),    # no full round: 2 tiles x 8 k-ranges
+    (256, 1000, 2048, 0, 256),   # ResNet-50 FC shape (partial last tile in N)
+    (300, 200, 4096, 0, 192),    # 192-wide tiles, partial tiles in M and N, 8 k-ranges
+    (5120, 768, 30528 // 64 * 64, 0, 256),  # MLM-decoder dgrad shape: 60 tiles x 4 k-ranges
+])
+def test_gemm_ppp_split_matches_fp32(M, N, K, blocks, bn):
+    """Split remainder: partial accumulators of k-ranges combined in-kernel; run
+    twice so the self-cleaning unit counters are exercised."""
+    from kubeflow_controller_amd.ops import gemm as G
+    torch.manual_seed(M + N + K + 2)
+    a, b = _bf(M, K), _bf(N, K, s=0.05)
+    ref = a.float() @ b.float().t()
+    c1 = G.gemm_ppp(a, b, blocks=blocks, bn=bn)
+    c2 = G.gemm_ppp(a, b, blocks=blocks, bn=bn)
+    _close(c1, ref, 1e-2, f"split C {M}x{N}x{K} bn={bn}")
+    assert torch.equal(c1, c2)
+    c3 = G.gemm_ppp(a, b, blocks=blocks, bn=bn, split=False)
+    _close(c3, ref, 1e-2, f"unsplit C {M}x{N}x{K} bn={bn}")
+
+
 def test_gemm_ppp_strided_a_and_repeatable():
     """Row stride > K on A (a column slice); two launches give identical bits."""
     from kubeflow_controller_amd.ops import gemm as G

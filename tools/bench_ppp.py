@@ -11,7 +11,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from kubeflow_controller_amd.ops import gemm as G  # noqa: E402
 
 SHAPES = [(32768, 2304, 768), (32768, 768, 768), (32768, 3072, 768), (32768, 768, 3072), (32768, 768, 2304),
-          (8192, 8192, 8192)]
+          (5120, 30528, 768), (5120, 768, 30528), (256, 1000, 2048), (8192, 8192, 8192)]
 
 
 def timeit(fn, iters=20):
@@ -39,16 +39,14 @@ def main():
         res = {}
         for rnd in range(3):
             for name, fn in (("hipblaslt", lambda: torch.mm(x, w.t())),
-                             ("pp", lambda: G.gemm_nt(x, w, persistent=6)),
-                             ("ppp", lambda: G.gemm_ppp(x, w)),
-                             ("ppp-nostore", lambda: G.gemm_ppp(x, w, probe=1)),
-                             ("ppp-wb", lambda: G.gemm_ppp(x, w, probe=2)),
-                             ("ppp-rows", lambda: G.gemm_ppp(x, w, probe=3)),
-                             ("ppp-rows-nt", lambda: G.gemm_ppp(x, w, probe=4)),
-                             ("pp-noepi", lambda: G.gemm_nt(x, w, persistent=7))):
+                             ("ppp-nosplit", lambda: G.gemm_ppp(x, w, bn=256, split=False)),
+                             ("ppp", lambda: G.gemm_ppp(x, w, bn=256)),
+                             ("ppp192", lambda: G.gemm_ppp(x, w, bn=192)) if N % 192 == 0 else ("-", lambda: None),
+                             ("ppp-nostore", lambda: G.gemm_ppp(x, w, bn=256, probe=1)),
+                             ("ppp-nostore-nosplit", lambda: G.gemm_ppp(x, w, bn=256, probe=1, split=False))):
                 res.setdefault(name, []).append(timeit(fn))
         ref = torch.mm(x, w.t()).float()
-        err = (G.gemm_ppp(x, w).float() - ref).abs().max().item()
+        err = max((G.gemm_ppp(x, w, bn=b).float() - ref).abs().max().item() for b in ((256, 192) if N % 192 == 0 else (256,)))
         line = " | ".join(f"{k} {min(v) * 1e3:7.1f} us {fl / min(v) / 1e9:6.0f} TF/s" for k, v in res.items())
         print(f"{M:6d} {N:5d} {K:5d} | {line} | ppp max|err| {err:.3g}", flush=True)
 
