@@ -24,6 +24,8 @@
 // Dropout RNG: keep(seed, i) = hash(seed, i) >= p * 2^32 — a stateless
 // counter hash (splitmix64 finaliser), so forward and backward regenerate the
 // same mask from (seed, element index).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -729,7 +731,8 @@ KFA_API int kfa_bias_act_bwd(const void* dy, const void* x, const float* b, void
   const uint32_t th = drop_thresh(p);
   const float ds = p > 0.f ? 1.f / (1.f - p) : 1.f;
   zero_if(dbias, N, accumulate, s);
-  if (N >= 128) {
+  static const int cl16 = [] { const char* e = getenv("KFA_BIAS_ACT_CL16"); return e ? atoi(e) : 1; }();
+  if (N >= 128 && cl16) {
     // >= 2048 blocks, >= 4 rows per thread; the dbias atomics stay at <= max(chunks, 256) per column
     const long bx = (N + 127) / 128;
     const long want = std::max(chunks, (2048 + bx - 1) / bx);
