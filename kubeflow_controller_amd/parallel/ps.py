@@ -31,6 +31,7 @@ two ranks on one GPU, and the PS replicas get no GPU of their own): PS task
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -61,6 +62,15 @@ def ps_assignment(params: Sequence[Tuple[str, torch.Tensor]], num_ps: int, strat
 def ps_owner_ranks(num_workers: int, num_ps: int) -> List[int]:
     """Worker rank hosting each PS task's variables (spread evenly over the node)."""
     return [p * num_workers // num_ps for p in range(max(1, num_ps))]
+
+
+# Pull waits per module (opt-in, env KFA_PS_PULL_PER_MODULE=1): each module's
+# forward pre-hook waits only for the buckets holding its own parameters, so the
+# first layers compute while later buckets still arrive.  That is only correct if
+# no module reads another module's weight before that module's own forward has
+# run (tied or shared weights break it, silently), so the default is one wait for
+# every pull at the start of the forward.
+PER_MODULE_PULL_WAITS = os.environ.get("KFA_PS_PULL_PER_MODULE", "0") == "1"
 
 
 class ShardedGradSync:
@@ -121,7 +131,8 @@ class ShardedGradSync:
                 self._hooks.append(p.register_post_accumulate_grad_hook(hook))
                 set_ready_callback(p, hook)
         self._pull_hooks = []
-        if model is not None and self.world > 1:
+        self._stage: Dict[int, torch.Tensor] = {}  # per-bucket reduce-dtype staging (allocated once)
+        if model is not None and self.world > 1 and PER_MODULE_PULL_WAITS:
             self._install_pull_waits(model)
         self.reset()
 
@@ -164,6 +175,18 @@ class ShardedGradSync:
             b.work = None
             b.tmp = None
 
+    def _staged(self, b: Bucket, view: torch.Tensor, rd: torch.dtype) -> torch.Tensor:
+        """``view`` in the reduce dtype: the view itself, or this bucket's staging
+        buffer (allocated at the first push, reused every step: the previous step's
+        collective on it completed in ``push``)."""
+        if view.dtype == rd:
+            return view
+        buf = self._stage.get(id(b))
+        if buf is None:
+            buf = self._stage[id(b)] = torch.empty(view.numel(), dtype=rd, device=view.device)
+        buf.copy_(view)
+        return buf
+
     def _push(self, b: Bucket) -> None:
         g = self.groups[b.group]
         rd = self.red_dtypes[b.group]
@@ -173,7 +196,7 @@ class ShardedGradSync:
             streams.join(view.device)
         if b.owner == -1:
             c = b.numel // self.world
-            src = view if view.dtype == rd else view.to(rd)
+            src = self._staged(b, view, rd)
             out = self.gshard[b.group][b.shard_off:b.shard_off + c]
             b.tmp = src
             b.work = dist.reduce_scatter_tensor(out, src, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
@@ -182,7 +205,7 @@ class ShardedGradSync:
                 buf = self.gshard[b.group][b.shard_off:b.shard_off + b.numel]
                 buf.copy_(view)
             else:
-                buf = view if view.dtype == rd else view.to(rd)
+                buf = self._staged(b, view, rd)
             b.tmp = buf
             b.work = dist.reduce(buf, b.owner, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
 
