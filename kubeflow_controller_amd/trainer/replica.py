@@ -322,6 +322,9 @@ def run_ps(spec: ClusterSpec, args) -> int:
         time.sleep(0.2)
 
 
+GRAPH_AUTO_MS = float(os.environ.get("KFA_GRAPH_AUTO_MS", "5"))
+
+
 def run_worker(spec: ClusterSpec, args) -> int:
     """Worker / Local replica on the shared training engine (``trainer/engine.py``):
     the same step ``bench.py`` times, plus the reference's logging, global-step
@@ -396,24 +399,39 @@ def run_worker(spec: ClusterSpec, args) -> int:
     # HIP graph replay of the whole step (Engine.capture) for single-replica GPU
     # jobs: the reference's MNIST steps are a few tiny kernels each, so launch
     # overhead is the step time; the batch is copied into the captured inputs.
-    use_graph = args.graph == "on" or (args.graph == "auto" and world == 1)
+    # "auto" captures only launch-bound steps: step 1 is timed (synchronized) and a
+    # step of more than GRAPH_AUTO_MS keeps eager launches (ResNet-50 at batch 256:
+    # 21.8 ms eager, replay measured 0.5 % slower; the reference's MNIST: 0.2 ms).
+    use_graph = args.graph == "on" or (args.graph == "auto" and world == 1 and device.type == "cuda")
+    cap_step = 1 if args.graph == "on" else 2
     if data is not None and device.type == "cuda" and hasattr(data, "to"):
         data.to(device)  # dataset resident in HBM: no host copy per step
+    # steady-state window: from the end of the warm-up steps (step 0 tunes the
+    # per-shape kernels, the capture step records the graph), GPU drained first
+    warm = min(cap_step + 1 if use_graph else 1, max(1, steps_per_worker - 1))
     for local_step in range(steps_per_worker):
         if data is not None:
             xb, yb = data.next_batch(args.batch_size)
             batch = (xb.to(device), yb.to(device))
         else:
             batch = fixed
-        if use_graph and local_step == 1 and engine.graph_ok() is None:
+        if use_graph and local_step == 1 and args.graph == "auto":
+            torch.cuda.synchronize()
+            t1 = time.time()
+            loss = engine.train_step(*batch)
+            torch.cuda.synchronize()
+            use_graph = (time.time() - t1) * 1e3 < GRAPH_AUTO_MS
+        elif use_graph and local_step == cap_step and engine.graph_ok() is None:
             loss = engine.capture(*(b.clone() for b in batch))  # its warm-up step trains on this batch
-            _log(f"Worker {rank}: step captured as a HIP graph; replaying it from step 2 on")
+            _log(f"Worker {rank}: step captured as a HIP graph; replaying it from step {cap_step + 1} on")
         else:
             loss = engine.train_step(*batch)
         global_step += inc
         if store is not None and spec.is_chief:
             store.add(STEP_KEY, inc)
-        if t_first is None:
+        if local_step + 1 == warm:
+            if device.type == "cuda":
+                torch.cuda.synchronize()
             t_first = time.time()
         if args.model_dir and args.checkpoint_every and (local_step + 1) % args.checkpoint_every == 0:
             _save()
@@ -429,8 +447,8 @@ def run_worker(spec: ClusterSpec, args) -> int:
     t_end = time.time()
     _log(f"Training ends @ {t_end:f}")
     _log(f"Training elapsed time: {t_end - t_begin:f} s")
-    if t_first is not None and steps_per_worker > 1:
-        sps = (steps_per_worker - 1) / max(t_end - t_first, 1e-9)
+    if t_first is not None and steps_per_worker > warm:
+        sps = (steps_per_worker - warm) / max(t_end - t_first, 1e-9)
         _log(f"Steady-state: {sps:.1f} steps/s/worker, {sps * args.batch_size * world:.1f} examples/s (job)")
     if data is not None:
         with torch.no_grad():
