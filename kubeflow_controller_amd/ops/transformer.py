@@ -247,17 +247,23 @@ class DenseFn(torch.autograd.Function):
         fusable = p == 0 and _gemm.gemm_ok(x2, weight) and (
             bias is None or (bias.dtype == torch.float32 and bias.is_contiguous() and bias.data_ptr() % 16 == 0))
         fused = fusable and (_gemm.ROUTE_LAYERS or (_gemm.ROUTE_FUSED and has_act))
+        mm = None  # plain GEMM of the unfused path (None: hipBLASLt)
         if fusable and _gemm.ROUTE_AUTO:
-            def _lib_fwd():
-                zz = torch.mm(x2, weight.t())
-                return bias_act_fwd(zz, bias, act) if (bias is not None or has_act) else zz
-            fused = _gemm.prefer_own("dense_fwd", (x2.shape[0], weight.shape[0], x2.shape[1], act, bias is not None),
-                                     x2.device, lambda: _gemm.gemm_nt(x2, weight, bias=bias, act=act, want_z=has_act),
-                                     _lib_fwd)
+            # per shape, the fastest of: hipBLASLt + one bias/act pass, the MFMA GEMM with
+            # the bias/act epilogue fused, the persistent MFMA GEMM + the bias/act pass
+            ba = (lambda zz: bias_act_fwd(zz, bias, act) if (bias is not None or has_act) else zz)  # noqa: E731
+            own_pp = _gemm._ppp_candidates(x2, weight) if _gemm.ppp_ok(x2, weight) else []
+            cands = ([("hipblaslt", lambda: ba(torch.mm(x2, weight.t()))),
+                      ("gemm_nt-fused", lambda: _gemm.gemm_nt(x2, weight, bias=bias, act=act, want_z=has_act))]
+                     + [(n, (lambda f: lambda: ba(f()))(f)) for n, f in own_pp])
+            i = _gemm.pick_fastest("dense_fwd", (x2.shape[0], weight.shape[0], x2.shape[1], act, bias is not None),
+                                   x2.device, cands)
+            fused = i == 1
+            mm = own_pp[i - 2][1] if i >= 2 else None
         if fused:
             y, z = _gemm.gemm_nt(x2, weight, bias=bias, act=act, want_z=has_act)  # z includes the bias
         else:
-            z = torch.mm(x2, weight.t())
+            z = mm() if mm is not None else torch.mm(x2, weight.t())
             y = bias_act_fwd(z, bias, act, p, seed) if (bias is not None or has_act or p > 0) else z
         ctx.save_for_backward(x2, weight, z if has_act else None)
         ctx.bias = bias
@@ -283,16 +289,11 @@ class DenseFn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             own_dx = fused and _gemm.ROUTE_LAYERS and weight.shape[1] % 8 == 0
-            if (_gemm.ROUTE_AUTO and weight.shape[0] % 8 == 0 and weight.shape[1] % 8 == 0 and dz.is_cuda
-                    and dz.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16 and dz.is_contiguous()):
-                own_dx = _gemm.prefer_own("dense_dgrad", (dz.shape[0], weight.shape[1], weight.shape[0]), dz.device,
-                                          lambda: _gemm.gemm_nt(dz, _gemm.transpose(weight)),
-                                          lambda: torch.mm(dz, weight))
             wt = _gemm.transpose(weight) if own_dx else None
             if wt is not None and _gemm.gemm_ok(dz, wt):
                 dx = _gemm.gemm_nt(dz, wt)[0].view(shp)
-            else:
-                dx = torch.mm(dz, weight).view(shp)
+            else:  # per shape: the persistent MFMA GEMM on the transposed weight, or hipBLASLt
+                dx = _gemm.dgrad_auto(dz, weight, "dense_dgrad").view(shp)
         gw, _, dw = _grad_target(weight)
         _wgrad_(gw, dz, x2)
         return dx, _finish(weight, gw, dw), (_finish(bias, gb, db) if bias is not None else None), None, None, None

@@ -167,8 +167,9 @@ def test_linear_module_runs_hip_dense_and_matches_fp32(route, monkeypatch, _pers
 
 
 def test_dense_auto_route_matches_fp32(monkeypatch):
-    """KFA_GEMM=auto: a Linear layer times own-GEMM vs library once per shape (forward
-    and dgrad), records the choice, and its outputs / gradients match fp32 either way."""
+    """KFA_GEMM=auto: a Linear layer times its candidates (hipBLASLt, the fused-epilogue
+    GEMM, the persistent GEMM variants) once per shape, forward and dgrad, records the
+    choice, and its outputs / gradients match fp32 whichever wins."""
     from kubeflow_controller_amd.ops import gemm as G
     from kubeflow_controller_amd.ops.linear import Linear
     monkeypatch.setattr(G, "ROUTE_AUTO", True)
@@ -177,7 +178,7 @@ def test_dense_auto_route_matches_fp32(monkeypatch):
     monkeypatch.setattr(G, "_choice", {})
     torch.manual_seed(0)
     d = torch.device("cuda")
-    lin = Linear(512, 1000).to(d)
+    lin = Linear(512, 1024).to(d)  # dgrad K = 1024: a persistent-GEMM candidate too
     x = torch.randn(256, 512, device=d).to(torch.bfloat16).requires_grad_()
     y = lin(x)
     y.float().pow(2).mean().backward()
@@ -191,3 +192,31 @@ def test_dense_auto_route_matches_fp32(monkeypatch):
     torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=2e-2)
     err = (x.grad.float() - xr.grad).abs().max().item() / xr.grad.abs().max().item()
     assert err < 3e-2, err
+
+
+@pytest.mark.parametrize("pick", [0, 1, 2, 3, 4])
+def test_dense_every_route_matches_fp32(monkeypatch, pick):
+    """Each DenseFn forward candidate (hipBLASLt + bias/act pass, fused-epilogue GEMM,
+    persistent GEMM variants + bias/act pass) and each dgrad candidate, forced."""
+    from kubeflow_controller_amd.ops import gemm as G
+    from kubeflow_controller_amd.ops import transformer as T
+    monkeypatch.setattr(G, "ROUTE_AUTO", True)
+    monkeypatch.setattr(G, "ROUTE_LAYERS", False)
+    monkeypatch.setattr(G, "ROUTE_FUSED", False)
+    monkeypatch.setattr(G, "_choice", {})
+    monkeypatch.setattr(G, "pick_fastest", lambda kind, key, dev, c: min(pick, len(c) - 1))
+    torch.manual_seed(pick)
+    d = torch.device("cuda")
+    x = torch.randn(1000, 768, device=d).to(torch.bfloat16).requires_grad_()
+    w = (torch.randn(1536, 768, device=d) * 0.03).to(torch.bfloat16).requires_grad_()
+    b = torch.randn(1536, device=d).requires_grad_()
+    y = T.dense(x, w, b, "gelu")
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr, wr, br = (t.detach().float().requires_grad_() for t in (x, w, b))
+    yr = torch.nn.functional.gelu(xr @ wr.t() + br)
+    yr.backward(dy.float())
+    _close(y, yr, 2e-2, "y")
+    _close(x.grad, xr.grad, 3e-2, "dx")
+    _close(w.grad, wr.grad, 3e-2, "dw")
+    _close(b.grad, br.grad, 3e-2, "db")

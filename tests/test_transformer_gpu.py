@@ -244,6 +244,7 @@ def test_bert_own_gemm_routes_match_reference(monkeypatch):
     from kubeflow_controller_amd.models.bert import BertConfig, BertForPreTraining, synthetic_mlm_batch
     from kubeflow_controller_amd.ops import gemm as G
     monkeypatch.setattr(G, "prefer_own", lambda *a, **k: True)
+    monkeypatch.setattr(G, "pick_fastest", lambda kind, key, dev, c: len(c) - 1)  # always an own variant
     calls = []
     real = G.gemm_ppp
     monkeypatch.setattr(G, "gemm_ppp", lambda a, b, **k: calls.append((a.shape[0], b.shape[0], a.shape[1])) or real(a, b, **k))
