@@ -225,7 +225,10 @@ def _agree_worker(rank, world, port, lockstep, out):
     conv.set_lockstep(lockstep)
     # rank 1 would pick differently; only a lockstep job takes rank 0's decision
     got = conv._agree(rank == 0, torch.device("cpu"))
-    out[rank] = bool(got)
+    # the GEMM tuner's multi-way choice (index of the fastest candidate) follows the same rule
+    from kubeflow_controller_amd.ops import gemm
+    pick = gemm._agree_int(3 if rank == 0 else 1, torch.device("cpu"))
+    out[rank] = (bool(got), pick)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -238,4 +241,4 @@ def test_tuner_decision_broadcast_only_in_lockstep_jobs(lockstep):
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_agree_worker, args=(2, _free_port(), lockstep, out), nprocs=2, join=True)
-    assert dict(out) == ({0: True, 1: True} if lockstep else {0: True, 1: False})
+    assert dict(out) == ({0: (True, 3), 1: (True, 3)} if lockstep else {0: (True, 3), 1: (False, 1)})

@@ -42,6 +42,8 @@ def main():
                              ("ppp-nosplit", lambda: G.gemm_ppp(x, w, bn=256, split=False)),
                              ("ppp", lambda: G.gemm_ppp(x, w, bn=256)),
                              ("ppp192", lambda: G.gemm_ppp(x, w, bn=192)) if N % 192 == 0 else ("-", lambda: None),
+                             ("ppp-nt", lambda: G.gemm_ppp(x, w, bn=256, split=False, probe=2)),
+                             ("ppp-rows-nt", lambda: G.gemm_ppp(x, w, bn=256, split=False, probe=4)),
                              ("ppp-nostore", lambda: G.gemm_ppp(x, w, bn=256, probe=1)),
                              ("ppp-nostore-nosplit", lambda: G.gemm_ppp(x, w, bn=256, probe=1, split=False))):
                 res.setdefault(name, []).append(timeit(fn))

@@ -9,3 +9,4 @@ for i in 1 2 3; do for v in 0 1; do
   echo "W&D pad64=$v $(echo "$r" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'])")"
 done; done
 KFA_GEMM_TUNE_LOG=1 timeout -k 10 300 python -u tools/bench_model.py --model wide_deep --batch 65536 --steps 5 --warmup 2 2>&1 | grep "gemm tune" | head -20
+timeout -k 10 300 python -u tools/bench_ppp.py 32768x2304x768 32768x3072x768 32768x768x3072 2>&1 | grep -v amdgpu.ids
