@@ -79,16 +79,9 @@ class WideDeepConfig:
 
     @property
     def dense_pad(self) -> int:
-        """Dense features zero-padded so the MLP input width is a multiple of 64
-        (when the embedding part allows it): the first layer's K then fits the
-        64-deep k-tiles of the persistent MFMA GEMM (ops/gemm.py).  The padded
-        features are always zero, so the model is unchanged."""
-        d = (self.num_dense + 7) // 8 * 8
-        emb = len(self.cardinalities) * self.embed_dim
-        if emb % 8 == 0 and os.environ.get("KFA_WD_PAD64", "1") != "0":
-            while (d + emb) % 64:
-                d += 8
-        return d
+        # (padding the MLP input width to a multiple of 64 so the first layer's K fits
+        # the persistent GEMM's k-tiles measured 1 % slower: 25.7 vs 25.9 M ex/s)
+        return (self.num_dense + 7) // 8 * 8
 
 
 class WideDeep(nn.Module):
