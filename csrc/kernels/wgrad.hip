@@ -21,6 +21,7 @@
 // writes an fp32 partial tile; a second kernel sums the partials and adds them
 // (converted) straight into the flat gradient buffer (bf16 or fp32).
 #include <cstdlib>
+#include <utility>
 
 #include "common.h"
 
@@ -310,6 +311,222 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_kernel(const bf16_t* __
   }
 }
 
+// ---------------------------------------------------------------------------
+// Ping-pong 256x256 weight gradient for POINTWISE layers (dense dW = dYᵀ·X, 1x1
+// stride-1 convs: X row k is pixel k).  The main loop of wgrad_kernel<2,4,8,4>
+// runs its 8 waves in lockstep (every wave reads its fragments, then every wave
+// multiplies: the MFMA pipe idles during the reads, ~840 TFLOP/s on the BERT
+// wgrads).  Here the schedule is gemm_pp_kernel's (gemm.hip): two wave groups
+// one s_barrier apart, so on every SIMD one wave's MFMAs run under the other's
+// LDS reads and DMA issue; 64-deep k-tiles in four 16 KB pieces ordered by first
+// use; 8 LDS-DMA per lane in flight across the barriers.  What changes is the
+// operand layout: both operands arrive k-major ([k][channel] rows), so a piece is
+// a [64 k][128 channel] image (256-B rows, the img_swz<128> chunk swizzle applied
+// on the source address) and each MFMA operand is two ds_read_b64_tr_b16.
+//   piece 0 "A0": dY columns m0 + {0-63, 128-191}    (each wave group's first 64 rows)
+//   piece 1 "B0": X columns  n0 + 64c + {0..31}      (each wave's first 32 columns)
+//   piece 2 "B1": X columns  n0 + 64c + {32..63}
+//   piece 3 "A1": dY columns m0 + {64-127, 192-255}
+// One block per (tile, pixel split), as wgrad_kernel; fp32 partials or a direct
+// (accumulating) write into the gradient.
+constexpr int WP_BK = 64;
+constexpr int WP_PIECE = WP_BK * 128 * 2;  // 64 k-rows x 128 channels, bytes
+
+template <int N>
+__device__ __forceinline__ void wp_vmcnt() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+}
+__device__ __forceinline__ void wp_retire(int younger) {  // all but the pieces of the `younger` newest phases
+  if (younger >= 4) wp_vmcnt<8>();
+  else if (younger == 3) wp_vmcnt<6>();
+  else if (younger == 2) wp_vmcnt<4>();
+  else if (younger == 1) wp_vmcnt<2>();
+  else wp_vmcnt<0>();
+}
+
+__global__ __launch_bounds__(512, 1) void wgrad_pp_kernel(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X,
+                                                          float* __restrict__ part, void* __restrict__ grad,
+                                                          int grad_f32, int accumulate, WGeo g) {
+  constexpr int TM = 8, TN = 4;
+  __shared__ __attribute__((aligned(16))) char smem[2 * 4 * WP_PIECE];  // 128 KB
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int ntn = (g.N + 255) / 256;
+  const int nwg = gridDim.x * gridDim.y, bid = blockIdx.x + blockIdx.y * gridDim.x;
+  const int q8 = nwg >> 3, r8 = nwg & 7, x8 = bid & 7;
+  const int ord = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + (bid >> 3);
+  const int tile = ord % gridDim.x, split = ord / gridDim.x;
+  const int m0 = (tile / ntn) * 256, n0 = (tile % ntn) * 256;
+  const int kb = split * g.kchunk;
+  const int ke = min(g.K, kb + g.kchunk);
+  if (kb >= ke) return;
+  const int nk = (ke - kb + WP_BK - 1) / WP_BK;
+
+  const __amdgpu_buffer_rsrc_t rA = wrsrc(dY, (unsigned)g.K * (unsigned)g.Co * 2u);
+  const __amdgpu_buffer_rsrc_t rB = wrsrc(X, (unsigned)g.K * (unsigned)g.Ci * 2u);
+  // DMA plan: instruction j (0, 1) of wave w fills piece rows 4 (2w + j) + lane / 16,
+  // physical chunk lane & 15 <- logical chunk (lane & 15) ^ img_swz<128>(row)
+  int voff[4][2];
+#pragma unroll
+  for (int j = 0; j < 2; j++) {
+    const int row = 4 * (2 * wave + j) + (lane >> 4);
+    const int c = ((lane & 15) ^ img_swz<128>(row)) * 8;  // piece column of this lane's 8 channels
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int m = m0 + h * 64 + (c < 64 ? c : 128 + c - 64);
+      voff[h ? 3 : 0][j] = m < g.Co ? (row * g.Co + m) * 2 : (int)kOOB;
+      const int n = n0 + (c >> 5) * 64 + h * 32 + (c & 31);
+      voff[h ? 2 : 1][j] = n < g.N ? (row * g.Ci + n) * 2 : (int)kOOB;
+    }
+  }
+  const int plast = 4 * nk - 7;  // last phase that issues a piece
+  auto issue = [&](int P, auto pc, auto steady) __attribute__((always_inline)) {
+    constexpr int p = decltype(pc)::value;
+    const int kt = (P + 6) >> 2;
+    if (decltype(steady)::value || kt < nk) {
+      char* dst = smem + (kt & 1) * (4 * WP_PIECE) + p * WP_PIECE + wave * 2 * 1024;
+      const bool isA = p == 0 || p == 3;
+      const int soff = (kb + kt * WP_BK) * (isA ? g.Co : g.Ci) * 2;
+      buf_dma16<0>(isA ? rA : rB, reinterpret_cast<bf16_t*>(dst), voff[p][0], soff);
+      buf_dma16<0>(isA ? rA : rB, reinterpret_cast<bf16_t*>(dst + 1024), voff[p][1], soff);
+    }
+  };
+  auto retire = [&](int P, auto steady) __attribute__((always_inline)) {
+    if constexpr (decltype(steady)::value) {
+      wp_vmcnt<8>();
+    } else {
+      const int younger = min(P, plast) - (P - 3) + 1;
+      wp_retire(younger < 0 ? 0 : younger);
+    }
+  };
+
+  floatx4 acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; i++)
+#pragma unroll
+    for (int j = 0; j < TM; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  short8 a[4][2], b0[2][2], b1[2][2];
+  auto rd = [&](const char* piece, int cb, int ks) -> short8 {
+    return tr_operand<128>(reinterpret_cast<const bf16_t*>(piece), ks * 32, cb, lane);
+  };
+
+  issue(-6, std::integral_constant<int, 0>{}, std::false_type{});
+  issue(-5, std::integral_constant<int, 1>{}, std::false_type{});
+  issue(-4, std::integral_constant<int, 2>{}, std::false_type{});
+  issue(-3, std::integral_constant<int, 3>{}, std::false_type{});
+  issue(-2, std::integral_constant<int, 0>{}, std::false_type{});
+  issue(-1, std::integral_constant<int, 1>{}, std::false_type{});
+  retire(-1, std::false_type{});
+  asm volatile("s_barrier" ::: "memory");
+  if (wr) asm volatile("s_barrier" ::: "memory");  // group 1 runs one barrier behind
+
+  auto mfma_q = [&](short8 (&bb)[2][2], int mh, int nh) __attribute__((always_inline)) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ks++)
+#pragma unroll
+      for (int ni = 0; ni < 2; ni++)
+#pragma unroll
+        for (int mi = 0; mi < 4; mi++)
+          acc[nh * 2 + ni][mh * 4 + mi] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[ni][ks], a[mi][ks], acc[nh * 2 + ni][mh * 4 + mi], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  auto ktile = [&](int u, auto st) __attribute__((always_inline)) {
+    const char* buf = smem + (u & 1) * (4 * WP_PIECE);
+    const int P = 4 * u;
+    {  // s0: A0 + B0
+      const char* pa = buf;
+      const char* pb = buf + WP_PIECE;
+#pragma unroll
+      for (int ni = 0; ni < 2; ni++) {
+        b0[ni][0] = rd(pb, wc * 32 + ni * 16, 0);
+        b0[ni][1] = rd(pb, wc * 32 + ni * 16, 1);
+      }
+#pragma unroll
+      for (int mi = 0; mi < 4; mi++) {
+        a[mi][0] = rd(pa, wr * 64 + mi * 16, 0);
+        a[mi][1] = rd(pa, wr * 64 + mi * 16, 1);
+      }
+      issue(P, std::integral_constant<int, 2>{}, st);
+      retire(P, st);
+      asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      mfma_q(b0, 0, 0);
+      asm volatile("s_barrier" ::: "memory");
+    }
+    {  // s1: B1
+      const char* pb = buf + 2 * WP_PIECE;
+#pragma unroll
+      for (int ni = 0; ni < 2; ni++) {
+        b1[ni][0] = rd(pb, wc * 32 + ni * 16, 0);
+        b1[ni][1] = rd(pb, wc * 32 + ni * 16, 1);
+      }
+      issue(P + 1, std::integral_constant<int, 3>{}, st);
+      retire(P + 1, st);
+      asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      mfma_q(b1, 0, 1);
+      asm volatile("s_barrier" ::: "memory");
+    }
+    {  // s2: A1
+      const char* pa = buf + 3 * WP_PIECE;
+#pragma unroll
+      for (int mi = 0; mi < 4; mi++) {
+        a[mi][0] = rd(pa, wr * 64 + mi * 16, 0);
+        a[mi][1] = rd(pa, wr * 64 + mi * 16, 1);
+      }
+      issue(P + 2, std::integral_constant<int, 0>{}, st);
+      retire(P + 2, st);
+      asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      mfma_q(b1, 1, 1);
+      asm volatile("s_barrier" ::: "memory");
+    }
+    {  // s3: registers only
+      issue(P + 3, std::integral_constant<int, 1>{}, st);
+      retire(P + 3, st);
+      asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      mfma_q(b0, 1, 0);
+      asm volatile("s_barrier" ::: "memory");
+    }
+  };
+  int u = 0;
+  for (; u + 2 < nk; u++) ktile(u, std::true_type{});
+  for (; u < nk; u++) ktile(u, std::false_type{});
+  if (!wr) asm volatile("s_barrier" ::: "memory");  // both groups at the same barrier count
+
+  // acc[ni][mi] = D[m = m0 + 128 wr + 16 mi + fr][n = n0 + 64 wc + 16 ni + 4 fq + r]
+  const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int ni = 0; ni < TN; ni++) {
+    const int n = n0 + wc * 64 + ni * 16 + fq * 4;
+#pragma unroll
+    for (int mi = 0; mi < TM; mi++) {
+      const int m = m0 + wr * 128 + mi * 16 + fr;
+      if (m >= g.Co || n >= g.N) continue;
+      floatx4 v = acc[ni][mi];
+      const long e = (long)m * g.N + n;
+      if (part) {
+        *reinterpret_cast<floatx4*>(part + (long)split * g.Co * g.N + e) = v;
+      } else if (grad_f32) {
+        floatx4* gp = reinterpret_cast<floatx4*>(reinterpret_cast<float*>(grad) + e);
+        *gp = accumulate ? *gp + v : v;
+      } else {
+        uint2* gp = reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(grad) + e);
+        if (accumulate) {
+          const uint2 o = *gp;
+          v[0] += bf2f(o.x & 0xffff); v[1] += bf2f(o.x >> 16); v[2] += bf2f(o.y & 0xffff); v[3] += bf2f(o.y >> 16);
+        }
+        *gp = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+      }
+    }
+  }
+}
+
 // grad[i] (+)= sum_s part[s][i].  Block = 64 element-lanes (4 elements each)
 // x 4 split-lanes; each thread keeps 8 independent loads in flight (the split
 // count reaches hundreds for the early, pixel-heavy layers), then an LDS
@@ -390,6 +607,17 @@ bool wide64() {
   return v == 1;
 }
 
+// KFA_WGRAD_PP=0: pointwise 256x256 weight gradients on the lockstep wgrad_kernel
+// instead of the ping-pong wgrad_pp_kernel
+bool wgrad_pp_on() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("KFA_WGRAD_PP");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+
 struct WPlan {
   int variant;   // 0: 128x128, 1: 64x128 (Co <= 64), 2: 128x64 (N <= 64), 3: 64x64 (both), 4: 256x256 (8 waves),
                  // 5: 64x256 (Co <= 64, N % 256 == 0: 64x64 wave tiles instead of 64x32)
@@ -465,6 +693,11 @@ KFA_API int kfa_conv_wgrad(const bf16_t* dY, const bf16_t* X, void* grad, int gr
     }
     hipLaunchKernelGGL((wgrad_kernel<1, 4, 4, 4>), grid, dim3(256), lds, s, dY, X, pp, grad, grad_f32, accumulate,
                        zero_page(), g);
+  }
+  else if (R == 1 && S == 1 && st == 1 && pad == 0 && K >= 16384 && Co >= 768 && g.N >= 768 && wgrad_pp_on()) {
+    // pointwise, long reduction, big weight: ping-pong 256x256 (BERT-base dW: 2304x768 142 -> 129 us,
+    // 3072x768 176 -> 168; the ResNet 1x1 shapes measured equal or slower: tools/bench_wgrad_pp.py)
+    hipLaunchKernelGGL(wgrad_pp_kernel, grid, dim3(512), 0, s, dY, X, pp, grad, grad_f32, accumulate, g);
   }
   else {
     static bool attr = false;  // 128 KiB of dynamic LDS

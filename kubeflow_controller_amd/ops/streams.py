@@ -18,10 +18,13 @@ Ordering contract:
   side stream (an autograd engine callback), so ``loss.backward()`` returns
   with the main stream ordered after every weight gradient.
 
-env ``KFA_SIDE_STREAM=0`` keeps everything on the current stream.  Measured
-(1x MI355X): BERT-base +1.5 %; ResNet-50 conv wgrads on the side stream gained
-nothing (9223 -> 9200 img/s: the dgrad convs already fill the CUs), so the conv
-path stays on one stream.
+Off by default since round 3 (env ``KFA_SIDE_STREAM=1`` turns it on): with the
+projections on the persistent GEMM (one 128 KB-LDS block per CU, ``gemm_ppp``) a
+co-running wgrad holds CUs the persistent grid expects to own, and one stream
+measured faster — BERT-base 8,444-8,466 vs 8,410-8,442 seq/s (same box, 3
+rounds).  (Round 1, hipBLASLt projections: +1.5 % with the side stream.)
+ResNet-50 conv wgrads never used it (9223 -> 9200 img/s: the dgrad convs
+already fill the CUs).
 """
 from __future__ import annotations
 
@@ -30,7 +33,7 @@ from typing import Callable, Dict, Iterable
 
 import torch
 
-ENABLED = os.environ.get("KFA_SIDE_STREAM", "1") != "0"
+ENABLED = os.environ.get("KFA_SIDE_STREAM", "0") == "1"
 _side: Dict[int, torch.cuda.Stream] = {}
 
 

@@ -118,7 +118,11 @@ def test_resnet_block_grads_igemm_vs_vendor():
 
 @pytest.mark.parametrize("rows,out_f,in_f", [(8192, 2304, 768), (4096, 768, 3072), (1000, 64, 136),
                                              # 64x256 tiles (Co <= 64, N % 256 == 0), split-K, tail rows
-                                             (20000, 64, 256), (3001, 48, 512)])
+                                             (20000, 64, 256), (3001, 48, 512),
+                                             # ping-pong pointwise 256x256 (wgrad_pp_kernel): BERT shapes,
+                                             # a tail k-tile, edge tiles in both dims, a 1x1 conv's pixels
+                                             (32768, 768, 768), (32768, 768, 3072), (12001, 512, 256),
+                                             (9000, 768, 1280), (12544, 1024, 256)])
 def test_wgrad_dense_shapes(rows, out_f, in_f):
     """dW = dYᵀ·X through the wgrad kernel as a 1x1 conv over `rows` pixels."""
     from kubeflow_controller_amd.ops.conv import wgrad_into

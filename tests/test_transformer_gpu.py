@@ -214,8 +214,11 @@ def test_decoder_xent():
     _close(b.grad, br.grad, 3e-2, "db")
 
 
-def test_bert_tiny_gpu_matches_reference():
+@pytest.mark.parametrize("side", [False, True], ids=["one_stream", "wgrad_side_stream"])
+def test_bert_tiny_gpu_matches_reference(monkeypatch, side):
     from kubeflow_controller_amd.models.bert import BertConfig, BertForPreTraining, synthetic_mlm_batch
+    from kubeflow_controller_amd.ops import streams
+    monkeypatch.setattr(streams, "ENABLED", side)
     cfg = BertConfig.tiny()
     cfg.hidden_dropout = cfg.attn_dropout = 0.0
     torch.manual_seed(0)
