@@ -181,16 +181,37 @@ __device__ __forceinline__ void scores_t(const char* Qi, const char* Ki, int qb,
   }
 }
 
-__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restrict__ qkv, const float* __restrict__ bqkv,
+// rows ra..ra+3 and rb..rb+3 (any two 4-row groups) of column cb + (lane & 15):
+// the 16x16x32 operand whose k index runs over a PERMUTED row order.  Used where
+// the other operand comes straight from an MFMA result held in registers (lane
+// = column, 4 consecutive rows per 16-row tile): k order is free in a dot
+// product, so only the two operands have to agree on it.
+template <int W>
+__device__ __forceinline__ short8 rd_tr2(const char* img, int ra, int rb, int cb, int lane) {
+  const int i = lane & 15;
+  const int col = cb + 4 * (i & 3);
+  const v4i16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(img + ioff<W>(ra + (i >> 2), col)));
+  const v4i16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(img + ioff<W>(rb + (i >> 2), col)));
+  return short8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+
+__device__ __forceinline__ short8 pack_pair(floatx4 x, floatx4 y) {
+  const uint2 lo = pack4(x[0], x[1], x[2], x[3]), hi = pack4(y[0], y[1], y[2], y[3]);
+  const uint4 u = make_uint4(lo.x, lo.y, hi.x, hi.y);
+  return *reinterpret_cast<const short8*>(&u);
+}
+
+__global__ __launch_bounds__(256, 3) void attn_fwd_kernel(const bf16_t* __restrict__ qkv, const float* __restrict__ bqkv,
                                                           const float* __restrict__ kbias, bf16_t* __restrict__ out,
                                                           float* __restrict__ lse, int heads, float qscale,
                                                           uint32_t thresh, float dscale, uint64_t seed) {
-  __shared__ __attribute__((aligned(16))) char sm[3 * 16384 + 4 * 8192];  // 80 KiB: 2 workgroups per CU
+  // Q, K, V images only (48 KiB: three workgroups per CU): the probabilities
+  // feed P·V straight from registers and O is staged in the Q image afterwards
+  __shared__ __attribute__((aligned(16))) char sm[3 * 16384];
   char* Qi = sm;
   char* Ki = sm + 16384;
   char* Vi = sm + 32768;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
-  char* Pw = sm + 49152 + wave * 8192;  // this wave's [32 q][128 key] probabilities, later its O stage
   const int bh = blockIdx.x, b = bh / heads, h = bh - b * heads, H = heads * AD;
   const long row0 = (long)b * AS;
   const int qb = wave * 32;
@@ -237,36 +258,37 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restri
     if (fq == 0) lse[(long)bh * AS + q] = mx + __logf(sum);
     const float inv = 1.f / sum;
 #pragma unroll
-    for (int kt = 0; kt < 8; kt++) {
-      float p[4];
+    for (int kt = 0; kt < 8; kt++)
 #pragma unroll
       for (int r = 0; r < 4; r++) {
         float v = s[kt][qt][r] * inv;
         if (thresh)
           v = drop_hash(seed, ((uint64_t)bh * AS + q) * AS + kt * 16 + 4 * fq + r) >= thresh ? v * dscale : 0.f;
-        p[r] = v;
+        s[kt][qt][r] = v;
       }
-      *reinterpret_cast<uint2*>(Pw + off128(qt * 16 + fr, kt * 16 + 4 * fq)) = pack4(p[0], p[1], p[2], p[3]);
-    }
   }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // only this wave reads its P rows
 
-  // Oᵀ[d][q] = Σ_key V[key][d] · Pd[q][key]:  o[dt][qt][r] = O(q = qb + 16qt + fr, d = 16dt + 4fq + r)
+  // Oᵀ[d][q] = Σ_key V[key][d] · Pd[q][key]:  o[dt][qt][r] = O(q = qb + 16qt + fr, d = 16dt + 4fq + r).
+  // The B operand (Pdᵀ, k = key) comes from the registers: tiles 2ks and 2ks+1 give this
+  // lane keys {32ks + 4fq + r, 32ks + 16 + 4fq + r} — a permuted k order, matched by
+  // reading V's rows in the same order (rd_tr2, as the backward's dVᵀ).
   floatx4 o[4][2];
 #pragma unroll
   for (int dt = 0; dt < 4; dt++) o[dt][0] = o[dt][1] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ks = 0; ks < 4; ks++) {
-    const short8 b0 = rd_row<128>(Pw, fr, ks * 32 + fq * 8);
-    const short8 b1 = rd_row<128>(Pw, 16 + fr, ks * 32 + fq * 8);
+    const short8 b0 = pack_pair(s[2 * ks][0], s[2 * ks + 1][0]);
+    const short8 b1 = pack_pair(s[2 * ks][1], s[2 * ks + 1][1]);
+    const int ra = 32 * ks + 4 * fq;
 #pragma unroll
     for (int dt = 0; dt < 4; dt++) {
-      const short8 a = rd_tr<64>(Vi, ks * 32, dt * 16, lane);
+      const short8 a = rd_tr2<64>(Vi, ra, ra + 16, dt * 16, lane);
       o[dt][0] = mma(a, b0, o[dt][0]);
       o[dt][1] = mma(a, b1, o[dt][1]);
     }
   }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();  // every wave is done with the Q image: it becomes the O stage
+  char* Pw = Qi + wave * 4096;  // this wave's [32 q][64] O stage
 #pragma unroll
   for (int dt = 0; dt < 4; dt++)
 #pragma unroll
@@ -280,26 +302,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restri
     *reinterpret_cast<uint4*>(out + (row0 + qb + r) * H + h * AD + c * 8) =
         *reinterpret_cast<const uint4*>(Pw + off64(r, c * 8));
   }
-}
-
-// rows ra..ra+3 and rb..rb+3 (any two 4-row groups) of column cb + (lane & 15):
-// the 16x16x32 operand whose k index runs over a PERMUTED row order.  Used where
-// the other operand comes straight from an MFMA result held in registers (lane
-// = column, 4 consecutive rows per 16-row tile): k order is free in a dot
-// product, so only the two operands have to agree on it.
-template <int W>
-__device__ __forceinline__ short8 rd_tr2(const char* img, int ra, int rb, int cb, int lane) {
-  const int i = lane & 15;
-  const int col = cb + 4 * (i & 3);
-  const v4i16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(img + ioff<W>(ra + (i >> 2), col)));
-  const v4i16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(img + ioff<W>(rb + (i >> 2), col)));
-  return short8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-}
-
-__device__ __forceinline__ short8 pack_pair(floatx4 x, floatx4 y) {
-  const uint2 lo = pack4(x[0], x[1], x[2], x[3]), hi = pack4(y[0], y[1], y[2], y[3]);
-  const uint4 u = make_uint4(lo.x, lo.y, hi.x, hi.y);
-  return *reinterpret_cast<const short8*>(&u);
 }
 
 // Backward, key-owner form (FlashAttention-2 style): wave w owns keys
