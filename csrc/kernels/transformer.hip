@@ -160,9 +160,23 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
 #pragma unroll
     for (int e = 0; e < 8; e++) ag[j][e] = ab[j][e] = ad[j][e] = 0.f;
 
-  // software pipeline: the next row's dy / x are in flight while this row reduces
+  // gamma is per column: in registers for the whole chunk (was re-read every row)
+  float gm[NV][8];
+#pragma unroll
+  for (int j = 0; j < NV; j++) {
+    const int c = (j * 64 + lane) * 8;
+    if (c < H) load8f(gamma + c, gm[j]);
+  }
+  // software pipeline: the next row's dy / x AND its mean / rstd are in flight
+  // while this row reduces (the row statistics were loaded at the top of their
+  // own iteration: one exposed memory latency per row)
   uint4 nd[NV], nx[NV], ne[NV];
+  float nmean = 0.f, nrstd = 0.f;
   auto fetch = [&](long row) {
+    if (row < r1) {
+      nmean = mean_in[row];
+      nrstd = rstd_in[row];
+    }
 #pragma unroll
     for (int j = 0; j < NV; j++) {
       const int c = (j * 64 + lane) * 8;
@@ -176,7 +190,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
   fetch(r0 + w);
   for (long row = r0 + w; row < r1; row += kRowsPerBlock) {
     const long base = row * (long)H;
-    const float mean = mean_in[row], rstd = rstd_in[row];
+    const float mean = nmean, rstd = nrstd;
     uint4 cd[NV], cx[NV], ce[NV];
 #pragma unroll
     for (int j = 0; j < NV; j++) { cd[j] = nd[j]; cx[j] = nx[j]; ce[j] = ne[j]; }
@@ -187,7 +201,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
     for (int j = 0; j < NV; j++) {
       const int c = (j * 64 + lane) * 8;
       if (c < H) {
-        float d[8], xv[8], gm[8];
+        float d[8], xv[8];
         unpack8(cd[j], d);
         if constexpr (TWO) {
           float d2[8];
@@ -196,11 +210,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
           for (int e = 0; e < 8; e++) d[e] += d2[e];
         }
         unpack8(cx[j], xv);
-        load8f(gamma + c, gm);
 #pragma unroll
         for (int e = 0; e < 8; e++) {
           xh[j][e] = (xv[e] - mean) * rstd;
-          g[j][e] = d[e] * gm[e];
+          g[j][e] = d[e] * gm[j][e];
           ag[j][e] += d[e] * xh[j][e];
           ab[j][e] += d[e];
           s1 += g[j][e] * xh[j][e];
