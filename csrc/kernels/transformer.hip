@@ -281,28 +281,42 @@ __device__ __forceinline__ float act_grad(float z, int act) {
   }
 }
 
-// y[r, c] = act(x[r, c] + b[c]); one thread per 8 columns, grid-stride rows.
+// y[r, c] = act(x[r, c] + b[c]); one thread per 8 columns, grid-stride rows,
+// two 8-column groups per iteration with both loads issued before either is
+// used; the activation is a template parameter (no per-element switch).
+template <int ACT>
 __global__ __launch_bounds__(256) void bias_act_fwd_kernel(const bf16_t* __restrict__ x, const float* __restrict__ b,
-                                                           bf16_t* __restrict__ y, long rows, int N, int act,
+                                                           bf16_t* __restrict__ y, long rows, int N,
                                                            uint32_t thresh, float dscale, uint64_t seed) {
-  const long nv = rows * (N / 8);
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < nv; i += (long)gridDim.x * 256) {
-    const long r = i / (N / 8);
-    const int c = (int)(i - r * (N / 8)) * 8;
-    float f[8];
-    load8(x + r * N + c, f);
-    if (b) {
-      float bb[8];
-      load8f(b + c, bb);
+  const long nv = rows * (N / 8), stride = (long)gridDim.x * 256;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < nv; i += 2 * stride) {
+    long idx[2] = {i, i + stride};
+    float f[2][8];
 #pragma unroll
-      for (int e = 0; e < 8; e++) f[e] += bb[e];
+    for (int u = 0; u < 2; u++) {
+      if (idx[u] >= nv) break;
+      const long r = idx[u] / (N / 8);
+      const int c = (int)(idx[u] - r * (N / 8)) * 8;
+      load8(x + r * N + c, f[u]);
+      if (b) {
+        float bb[8];
+        load8f(b + c, bb);
+#pragma unroll
+        for (int e = 0; e < 8; e++) f[u][e] += bb[e];
+      }
     }
 #pragma unroll
-    for (int e = 0; e < 8; e++) f[e] = act_f(f[e], act);
-    if (thresh)
+    for (int u = 0; u < 2; u++) {
+      if (idx[u] >= nv) break;
+      const long r = idx[u] / (N / 8);
+      const int c = (int)(idx[u] - r * (N / 8)) * 8;
 #pragma unroll
-      for (int e = 0; e < 8; e++) f[e] = keep(seed, r * N + c + e, thresh) ? f[e] * dscale : 0.f;
-    store8(y + r * N + c, f);
+      for (int e = 0; e < 8; e++) f[u][e] = act_f(f[u][e], ACT);
+      if (thresh)
+#pragma unroll
+        for (int e = 0; e < 8; e++) f[u][e] = keep(seed, r * N + c + e, thresh) ? f[u][e] * dscale : 0.f;
+      store8(y + r * N + c, f[u]);
+    }
   }
 }
 
@@ -719,8 +733,15 @@ KFA_API int kfa_bias_act_fwd(const void* x, const float* b, void* y, long rows, 
   if (rows <= 0 || N % 8) return -1;
   const uint32_t th = drop_thresh(p);
   const float ds = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  hipLaunchKernelGGL(bias_act_fwd_kernel, dim3(grid_for(rows * (N / 8))), dim3(256), 0, s, (const bf16_t*)x, b,
-                     (bf16_t*)y, rows, N, act, th, ds, (uint64_t)seed);
+  const dim3 g(grid_for((rows * (N / 8) + 1) / 2));  // two 8-column groups per thread per iteration
+#define KFA_BAF(A) \
+  hipLaunchKernelGGL(bias_act_fwd_kernel<A>, g, dim3(256), 0, s, (const bf16_t*)x, b, (bf16_t*)y, rows, N, th, ds, \
+                     (uint64_t)seed)
+  if (act == kGelu) KFA_BAF(kGelu);
+  else if (act == kTanh) KFA_BAF(kTanh);
+  else if (act == kRelu) KFA_BAF(kRelu);
+  else KFA_BAF(kNone);
+#undef KFA_BAF
   return kfa_status();
 }
 
