@@ -624,11 +624,16 @@ struct WPlan {
   int BM, BN, tiles, splits, kchunk, threads, blocks_per_cu;
 };
 
-WPlan plan(long K, int Co, int N) {
+// pointwise weights the ping-pong kernel takes (edge tiles masked, so any Co / N)
+static bool pp_shape(long K, int Co, int N, bool pointwise) {
+  return pointwise && K >= 16384 && Co >= 768 && N >= 768 && wgrad_pp_on();
+}
+
+WPlan plan(long K, int Co, int N, bool pointwise = false) {
   WPlan p;
   // 256x256 (8 waves of 128x64, one block per CU): half the operand bytes per
   // MFMA of the 128x128 tile — for the long reductions of big weights
-  if (Co % 256 == 0 && N % 256 == 0 && K >= 8192) p.variant = 4;
+  if ((Co % 256 == 0 && N % 256 == 0 && K >= 8192) || pp_shape(K, Co, N, pointwise)) p.variant = 4;
   else if (Co <= 64 && N % 256 == 0 && wide64()) p.variant = 5;
   else p.variant = Co <= 64 ? (N <= 64 ? 3 : 1) : (N <= 64 ? 2 : 0);
   p.BM = p.variant == 4 ? 256 : ((p.variant == 1 || p.variant == 3 || p.variant == 5) ? 64 : 128);
@@ -652,7 +657,9 @@ WPlan plan(long K, int Co, int N) {
 }  // namespace
 
 KFA_API long kfa_wgrad_part_floats(int Nb, int P, int Q, int Co, int R, int S, int Ci) {
-  const WPlan p = plan((long)Nb * P * Q, Co, R * S * Ci);
+  // (the pointwise test cannot see stride / pad here: the plan may over-size, never under-size)
+  const WPlan p0 = plan((long)Nb * P * Q, Co, R * S * Ci), p1 = plan((long)Nb * P * Q, Co, R * S * Ci, R == 1 && S == 1);
+  const WPlan& p = p0.splits >= p1.splits ? p0 : p1;
   return p.splits > 1 ? (long)p.splits * Co * R * S * Ci : 0;
 }
 
@@ -666,7 +673,8 @@ KFA_API int kfa_conv_wgrad(const bf16_t* dY, const bf16_t* X, void* grad, int gr
   // 32-bit buffer offsets (dY rows, X pixels; the scalar k offset included)
   if (K * Co * 2 >= (long)kOOB || (long)Nb * H * W * Ci * 2 >= (long)kOOB) return -2;
   WGeo g{H, W, Ci, P, Q, Co, R, S, st, pad, R * S * Ci, (int)K, 0, (unsigned)((long)Nb * H * W * Ci * 2)};
-  const WPlan p = plan(K, Co, g.N);
+  const bool pointwise = R == 1 && S == 1 && st == 1 && pad == 0;
+  const WPlan p = plan(K, Co, g.N, pointwise);
   g.kchunk = p.kchunk;
   const size_t lds = (size_t)2 * BKW * (p.BM + p.BN) * sizeof(bf16_t);
   float* pp = p.splits > 1 ? part : nullptr;
@@ -694,7 +702,7 @@ KFA_API int kfa_conv_wgrad(const bf16_t* dY, const bf16_t* X, void* grad, int gr
     hipLaunchKernelGGL((wgrad_kernel<1, 4, 4, 4>), grid, dim3(256), lds, s, dY, X, pp, grad, grad_f32, accumulate,
                        zero_page(), g);
   }
-  else if (R == 1 && S == 1 && st == 1 && pad == 0 && K >= 16384 && Co >= 768 && g.N >= 768 && wgrad_pp_on()) {
+  else if (pp_shape(K, Co, g.N, pointwise)) {
     // pointwise, long reduction, big weight: ping-pong 256x256 (BERT-base dW: 2304x768 142 -> 129 us,
     // 3072x768 176 -> 168; the ResNet 1x1 shapes measured equal or slower: tools/bench_wgrad_pp.py)
     hipLaunchKernelGGL(wgrad_pp_kernel, grid, dim3(512), 0, s, dY, X, pp, grad, grad_f32, accumulate, g);

@@ -122,7 +122,8 @@ def test_resnet_block_grads_igemm_vs_vendor():
                                              # ping-pong pointwise 256x256 (wgrad_pp_kernel): BERT shapes,
                                              # a tail k-tile, edge tiles in both dims, a 1x1 conv's pixels
                                              (32768, 768, 768), (32768, 768, 3072), (12001, 512, 256),
-                                             (9000, 768, 1280), (12544, 1024, 256)])
+                                             (9000, 768, 1280), (12544, 1024, 256),
+                                             (20000, 1024, 1680), (17000, 776, 1000)])  # edge tiles: N % 256 != 0
 def test_wgrad_dense_shapes(rows, out_f, in_f):
     """dW = dYᵀ·X through the wgrad kernel as a 1x1 conv over `rows` pixels."""
     from kubeflow_controller_amd.ops.conv import wgrad_into
