@@ -609,14 +609,15 @@ bool wide64() {
 
 // KFA_WGRAD_PP=0: pointwise 256x256 weight gradients on the lockstep wgrad_kernel
 // instead of the ping-pong wgrad_pp_kernel
-bool wgrad_pp_on() {
+static int wgrad_pp_mode() {  // 0 off, 1 size rule (default), 2 every pointwise weight (experiments)
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("KFA_WGRAD_PP");
-    v = (e && e[0] == '0') ? 0 : 1;
+    v = e ? atoi(e) : 1;
   }
-  return v == 1;
+  return v;
 }
+bool wgrad_pp_on() { return wgrad_pp_mode() != 0; }
 
 struct WPlan {
   int variant;   // 0: 128x128, 1: 64x128 (Co <= 64), 2: 128x64 (N <= 64), 3: 64x64 (both), 4: 256x256 (8 waves),
@@ -626,7 +627,10 @@ struct WPlan {
 
 // pointwise weights the ping-pong kernel takes (edge tiles masked, so any Co / N)
 static bool pp_shape(long K, int Co, int N, bool pointwise) {
-  return pointwise && K >= 16384 && Co >= 768 && N >= 768 && wgrad_pp_on();
+  if (!pointwise || !wgrad_pp_on()) return false;
+  // per-shape table (tools/bench_wgrad_pp.py, 1x MI355X): wins from 256 x 256 channels up (BERT dW -4..-9 %,
+  // ResNet-50 1x1s at 50176 / 200704 pixels -2..-5 %); the 128-channel ResNet shapes lose 10-24 %
+  return wgrad_pp_mode() == 2 ? (Co >= 128 && N >= 128) : (K >= 8192 && Co >= 256 && N >= 256);
 }
 
 WPlan plan(long K, int Co, int N, bool pointwise = false) {

@@ -9,8 +9,11 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from kubeflow_controller_amd.ops.conv import wgrad_into  # noqa: E402
 
-SHAPES = [(32768, 2304, 768), (32768, 768, 768), (32768, 3072, 768), (32768, 768, 3072),
-          (12544, 1024, 256), (12544, 256, 1024), (3136, 2048, 512), (3136, 512, 2048), (65536, 1024, 1680)]
+SHAPES = [(32768, 2304, 768), (32768, 768, 768), (32768, 3072, 768), (32768, 768, 3072), (65536, 1024, 1680),
+          # ResNet-50 bs 256 pointwise convs (pixels, Cout, Cin)
+          (802816, 256, 64), (802816, 64, 256), (802816, 128, 256), (200704, 512, 128), (200704, 128, 512),
+          (200704, 256, 512), (50176, 1024, 256), (50176, 256, 1024), (50176, 512, 1024), (12544, 2048, 512),
+          (12544, 512, 2048), (200704, 512, 256), (50176, 1024, 512), (12544, 2048, 1024)]
 d = torch.device("cuda")
 for rows, co, ci in SHAPES:
     x = torch.randn(rows, ci, device=d).to(torch.bfloat16)
