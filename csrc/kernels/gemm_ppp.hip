@@ -115,9 +115,19 @@ constexpr int kStoresPerPhase = 4;  // one 16-B store per 16-row block of a 64 x
 // NOST: timing probe — every C store dropped (the values kept live).
 // SMODE: bit 0 = non-temporal C stores; bit 1 = row pairs (quadrants (0,0)+(0,1)
 // in phase 0, (1,1)+(1,0) in phase 2: each 128-B row segment written in one phase)
-template <int BN = 256, bool NOST = false, int SMODE = 0>
+// P3 (BN = 192 only): THREE phases per k-tile of 16 MFMAs each — s0: A0 + B0 ->
+// rows 0-63 x the two 16-column blocks of the wave's first 32 columns; s1: A1 ->
+// rows 64-127 x the same blocks (B0 fragments kept); s2: B1 -> both row halves x
+// the third block (A0 and A1 fragments kept).  The four-phase order gives a
+// 48-column wave tile 16 / 8 / 8 / 16 MFMAs per phase, and the short phases
+// expose the partner group's LDS reads.  Issue: s0 A1(u+1), s1 B1(u+1), s2 A0 and
+// B0 (u+2) — each piece DMA'd 3 phases (one k-tile) before its read phase and
+// only into a buffer whose previous piece was read >= 2 phases earlier; every
+// phase retires the DMAs of three phases ago: steady vmcnt(D = 7).
+template <int BN = 256, bool NOST = false, int SMODE = 0, bool P3 = false>
 __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
   static_assert(BN == 256 || BN == 192, "tile width");
+  static_assert(!P3 || BN == 192, "three-phase k-tiles are the 192-wide schedule");
   static_assert(BN == 256 || !(SMODE & 2), "row pairs need two-block halves");
   constexpr int NB1 = BN == 256 ? 2 : 1;  // 16-column MFMA blocks in a wave's nh = 1 half
   constexpr int WN = BN / 4;              // wave tile width
@@ -228,6 +238,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
 #pragma unroll
     for (int j = 0; j < TM; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
   short8 a[4][2], b0[2][2], b1[NB1][2];
+  short8 a1r[P3 ? 4 : 1][2];  // P3: A1 fragments, live beside A0's for the s2 MFMAs
 
   // quadrant (mh, nh) of this wave's tile at (m0, n0) -> bf16 C, then zeroed for the next tile
   const int cb = ((fq & 1) << 4) | ((fq >> 1) << 3);
@@ -289,12 +300,18 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
   };
   auto rd = [&](const char* p) -> short8 { return *reinterpret_cast<const short8*>(p); };
 
-  // prologue: pieces of phases -6..-1 (A0 B0 B1 A1 of k-tile 0, A0 B0 of k-tile 1)
+  // prologue: pieces of phases -6..-1 (A0 B0 B1 A1 of k-tile 0, A0 B0 of k-tile 1);
+  // P3 needs A1 before B1 (its s1 reads A1, s2 reads B1)
   issue(std::integral_constant<int, 0>{}, 0);
   issue(std::integral_constant<int, 1>{}, 0);
   advance(false);
-  issue(std::integral_constant<int, 2>{}, 0);
-  issue(std::integral_constant<int, 3>{}, 0);
+  if constexpr (P3) {
+    issue(std::integral_constant<int, 3>{}, 0);
+    issue(std::integral_constant<int, 2>{}, 0);
+  } else {
+    issue(std::integral_constant<int, 2>{}, 0);
+    issue(std::integral_constant<int, 3>{}, 0);
+  }
   advance(true);
   issue(std::integral_constant<int, 0>{}, 1);
   issue(std::integral_constant<int, 1>{}, 1);
@@ -394,6 +411,86 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
     advance(false);
   };
 
+  // P3 k-tile (see the kernel comment): stores per phase 4 / 4 / 8 (the two
+  // one-block halves of s2 are 4 8-B stores each)
+  auto ktile3 = [&](int u, auto mode) __attribute__((always_inline)) {
+    constexpr int MODE = decltype(mode)::value;
+    constexpr bool EPI = MODE & 1, PEPI = MODE & 2;
+    const char* buf = smem + (u & 1) * (4 * PIECE);
+    auto retire = [&](auto sc) __attribute__((always_inline)) {
+      constexpr int s = decltype(sc)::value;
+      constexpr int st[3] = {4, 4, 8};
+      constexpr int upto = st[0] + (s >= 1 ? st[1] : 0) + (s >= 2 ? st[2] : 0);
+      constexpr int after = (s < 1 ? st[1] : 0) + (s < 2 ? st[2] : 0);
+      vm_wait<D + (EPI ? upto : 0) + (PEPI ? after : 0)>();
+    };
+    auto mfma_blocks = [&](auto& bb, auto& aa, int mh, int nb0, auto nbc) __attribute__((always_inline)) {
+      constexpr int NBC = decltype(nbc)::value;
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ks++)
+#pragma unroll
+        for (int ni = 0; ni < NBC; ni++)
+#pragma unroll
+          for (int mi = 0; mi < 4; mi++)
+            acc[nb0 + ni][mh * 4 + mi] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[ni][ks], aa[mi][ks], acc[nb0 + ni][mh * 4 + mi], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    };
+    {  // s0: A0 + B0 -> rows 0-63 x blocks 0, 1
+      const char* pa = buf + wr * 64 * 128;
+      const char* pb = buf + PIECE + wc * 32 * 128;
+#pragma unroll
+      for (int ni = 0; ni < 2; ni++) {
+        b0[ni][0] = rd(pb + ni * 16 * 128 + ro0);
+        b0[ni][1] = rd(pb + ni * 16 * 128 + ro1);
+      }
+#pragma unroll
+      for (int mi = 0; mi < 4; mi++) {
+        a[mi][0] = rd(pa + mi * 16 * 128 + ro0);
+        a[mi][1] = rd(pa + mi * 16 * 128 + ro1);
+      }
+      if constexpr (EPI) store_q(0, 0, pm0, pn0);
+      issue(std::integral_constant<int, 3>{}, u + 1);
+      retire(std::integral_constant<int, 0>{});
+      asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      mfma_blocks(b0, a, 0, 0, std::integral_constant<int, 2>{});
+      asm volatile("s_barrier" ::: "memory");
+    }
+    {  // s1: A1 -> rows 64-127 x blocks 0, 1
+      const char* pa = buf + 3 * PIECE + wr * 64 * 128;
+#pragma unroll
+      for (int mi = 0; mi < 4; mi++) {
+        a1r[mi][0] = rd(pa + mi * 16 * 128 + ro0);
+        a1r[mi][1] = rd(pa + mi * 16 * 128 + ro1);
+      }
+      if constexpr (EPI) store_q(1, 0, pm0, pn0);
+      issue(std::integral_constant<int, 2>{}, u + 1);
+      retire(std::integral_constant<int, 1>{});
+      asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      mfma_blocks(b0, a1r, 1, 0, std::integral_constant<int, 2>{});
+      asm volatile("s_barrier" ::: "memory");
+    }
+    {  // s2: B1 -> both row halves x block 2
+      const char* pb = buf + 2 * PIECE + wc * 16 * 128;
+      b1[0][0] = rd(pb + ro0);
+      b1[0][1] = rd(pb + ro1);
+      if constexpr (EPI) {
+        store_q(0, 1, pm0, pn0);
+        store_q(1, 1, pm0, pn0);
+      }
+      issue(std::integral_constant<int, 0>{}, u + 2);
+      issue(std::integral_constant<int, 1>{}, u + 2);
+      retire(std::integral_constant<int, 2>{});
+      asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      mfma_blocks(b1, a, 0, 2, std::integral_constant<int, 1>{});
+      mfma_blocks(b1, a1r, 1, 2, std::integral_constant<int, 1>{});
+      asm volatile("s_barrier" ::: "memory");
+    }
+    advance(true);
+    advance(false);
+  };
+
   // tile by tile: the first k-tile of every tile after the first writes the
   // previous tile's C, the second still has those stores in its count window
   int u = 0;
@@ -404,11 +501,19 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
       pm0 = cm0;
       pn0 = cn0;
       tile_mn(t, cm0, cn0);
-      ktile(u++, std::integral_constant<int, 1>{});
-      ktile(u++, std::integral_constant<int, 2>{});
+      if constexpr (P3) {
+        ktile3(u++, std::integral_constant<int, 1>{});
+        ktile3(u++, std::integral_constant<int, 2>{});
+      } else {
+        ktile(u++, std::integral_constant<int, 1>{});
+        ktile(u++, std::integral_constant<int, 2>{});
+      }
       k = 2;
     }
-    for (; k < kl; k++) ktile(u++, std::integral_constant<int, 0>{});
+    if constexpr (P3)
+      for (; k < kl; k++) ktile3(u++, std::integral_constant<int, 0>{});
+    else
+      for (; k < kl; k++) ktile(u++, std::integral_constant<int, 0>{});
   }
   if (!wr) asm volatile("s_barrier" ::: "memory");  // both groups at the same barrier count
   if (has_split) {
@@ -524,10 +629,12 @@ KFA_API int kfa_gemm_ppp(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int
   const PppArgs g{A, B, C, M, N, K, lda, ldb, ldc, (unsigned)cb, ws ? reinterpret_cast<float*>((char*)ws + 4096) : nullptr,
                   reinterpret_cast<int*>(ws), split};
   const dim3 gd(grid), bd(512);
-  if (bn == 192) {
-    if (probe == 1) hipLaunchKernelGGL((gemm_ppp_kernel<192, true>), gd, bd, 0, st, g);
+  if (bn == 192) {  // three-phase k-tiles (P3); probe 7 / 8: the four-phase schedule (with / without stores)
+    if (probe == 1 || probe == 6) hipLaunchKernelGGL((gemm_ppp_kernel<192, true, 0, true>), gd, bd, 0, st, g);
+    else if (probe == 7) hipLaunchKernelGGL((gemm_ppp_kernel<192, false>), gd, bd, 0, st, g);
+    else if (probe == 8) hipLaunchKernelGGL((gemm_ppp_kernel<192, true>), gd, bd, 0, st, g);
     else if (probe == 2) hipLaunchKernelGGL((gemm_ppp_kernel<192, false, 1>), gd, bd, 0, st, g);
-    else hipLaunchKernelGGL((gemm_ppp_kernel<192, false>), gd, bd, 0, st, g);
+    else hipLaunchKernelGGL((gemm_ppp_kernel<192, false, 0, true>), gd, bd, 0, st, g);
     return kfa_status();
   }
   if (probe == 1)  // timing probe: no C stores

@@ -51,13 +51,15 @@ def test_gemm_ppp_matches_fp32(M, N, K, blocks):
     (2048, 1536, 2304, 5),    # long k-loop, many tiles per block
     (300, 200, 128, 0),       # partial nh = 1 half (columns 192..199)
 ])
-def test_gemm_ppp_bn192_matches_fp32(M, N, K, blocks):
-    """192-wide tiles (one-block nh = 1 halves, 8-B stores, 7 DMAs per k-tile)."""
+@pytest.mark.parametrize("probe", [7, 0], ids=["four_phase", "three_phase"])
+def test_gemm_ppp_bn192_matches_fp32(M, N, K, blocks, probe):
+    """192-wide tiles (one-block nh = 1 halves, 8-B stores, 7 DMAs per k-tile), with the
+    four-phase (probe 7) and the default three-phase k-tile schedules."""
     from kubeflow_controller_amd.ops import gemm as G
     torch.manual_seed(M + N + K + 1)
     a, b = _bf(M, K), _bf(N, K, s=0.05)
-    c = G.gemm_ppp(a, b, blocks=blocks, bn=192)
-    _close(c, a.float() @ b.float().t(), 1e-2, f"C {M}x{N}x{K} bn=192 blocks={blocks}")
+    c = G.gemm_ppp(a, b, blocks=blocks, bn=192, probe=probe)
+    _close(c, a.float() @ b.float().t(), 1e-2, f"C {M}x{N}x{K} bn=192 blocks={blocks} probe={probe}")
 
 
 @pytest.mark.parametrize("M,N,K,blocks,bn", [

@@ -41,9 +41,9 @@ def main():
             for name, fn in (("hipblaslt", lambda: torch.mm(x, w.t())),
                              ("ppp-nosplit", lambda: G.gemm_ppp(x, w, bn=256, split=False)),
                              ("ppp", lambda: G.gemm_ppp(x, w, bn=256)),
+                             ("ppp192-4ph", lambda: G.gemm_ppp(x, w, bn=192, probe=7)) if N % 192 == 0 else ("-", lambda: None),
                              ("ppp192", lambda: G.gemm_ppp(x, w, bn=192)) if N % 192 == 0 else ("-", lambda: None),
-                             ("ppp-nt", lambda: G.gemm_ppp(x, w, bn=256, split=False, probe=2)),
-                             ("ppp-rows-nt", lambda: G.gemm_ppp(x, w, bn=256, split=False, probe=4)),
+                             ("ppp192-nost", lambda: G.gemm_ppp(x, w, bn=192, probe=1)) if N % 192 == 0 else ("-", lambda: None),
                              ("ppp-nostore", lambda: G.gemm_ppp(x, w, bn=256, probe=1)),
                              ("ppp-nostore-nosplit", lambda: G.gemm_ppp(x, w, bn=256, probe=1, split=False))):
                 res.setdefault(name, []).append(timeit(fn))
