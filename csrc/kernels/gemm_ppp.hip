@@ -413,16 +413,22 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
 
   // P3 k-tile (see the kernel comment): stores per phase 4 / 4 / 8 (the two
   // one-block halves of s2 are 4 8-B stores each)
+  // MODE bit 2 (LAST): the block's final k-tile (not a split unit, >= 3 k-tiles in
+  // the tile): rows 0-63 x blocks 0-1 are final after s0 and are written during s1,
+  // rows 64-127 x blocks 0-1 during s2 — only block 2 is left for after the loop
+  // (the last tile's C write was the one nothing overlapped)
   auto ktile3 = [&](int u, auto mode) __attribute__((always_inline)) {
     constexpr int MODE = decltype(mode)::value;
-    constexpr bool EPI = MODE & 1, PEPI = MODE & 2;
+    constexpr bool EPI = MODE & 1, PEPI = MODE & 2, LAST = MODE & 4;
+    static_assert(!(LAST && (EPI || PEPI)), "the last k-tile carries no tile-boundary stores");
     const char* buf = smem + (u & 1) * (4 * PIECE);
     auto retire = [&](auto sc) __attribute__((always_inline)) {
       constexpr int s = decltype(sc)::value;
       constexpr int st[3] = {4, 4, 8};
       constexpr int upto = st[0] + (s >= 1 ? st[1] : 0) + (s >= 2 ? st[2] : 0);
       constexpr int after = (s < 1 ? st[1] : 0) + (s < 2 ? st[2] : 0);
-      vm_wait<D + (EPI ? upto : 0) + (PEPI ? after : 0)>();
+      constexpr int last = s == 0 ? 0 : (s == 1 ? 4 : 8);
+      vm_wait<D + (EPI ? upto : 0) + (PEPI ? after : 0) + (LAST ? last : 0)>();
     };
     auto mfma_blocks = [&](auto& bb, auto& aa, int mh, int nb0, auto nbc) __attribute__((always_inline)) {
       constexpr int NBC = decltype(nbc)::value;
@@ -465,6 +471,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
         a1r[mi][1] = rd(pa + mi * 16 * 128 + ro1);
       }
       if constexpr (EPI) store_q(1, 0, pm0, pn0);
+      if constexpr (LAST) store_q(0, 0, cm0, cn0);  // final since s0
       issue(std::integral_constant<int, 2>{}, u + 1);
       retire(std::integral_constant<int, 1>{});
       asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
@@ -479,6 +486,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
         store_q(0, 1, pm0, pn0);
         store_q(1, 1, pm0, pn0);
       }
+      if constexpr (LAST) store_q(1, 0, cm0, cn0);  // final since s1
       issue(std::integral_constant<int, 0>{}, u + 2);
       issue(std::integral_constant<int, 1>{}, u + 2);
       retire(std::integral_constant<int, 2>{});
@@ -510,9 +518,11 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
       }
       k = 2;
     }
-    if constexpr (P3)
-      for (; k < kl; k++) ktile3(u++, std::integral_constant<int, 0>{});
-    else
+    if constexpr (P3) {
+      const bool last_early = t == my_tiles - 1 && !has_split && kl >= 3;
+      for (; k < kl - (last_early ? 1 : 0); k++) ktile3(u++, std::integral_constant<int, 0>{});
+      if (last_early) ktile3(u++, std::integral_constant<int, 4>{});
+    } else
       for (; k < kl; k++) ktile(u++, std::integral_constant<int, 0>{});
   }
   if (!wr) asm volatile("s_barrier" ::: "memory");  // both groups at the same barrier count
@@ -549,11 +559,12 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
         for (int j = 0; j < TM; j++) acc[i][j] += __builtin_nontemporal_load(src + (i * TM + j) * 512);
     }
   }
-  // the last tile's C
-  store_q(0, 0, cm0, cn0);
+  // the last tile's C (P3 with an early-stored last k-tile: only block 2 is left)
+  const bool stored_early = P3 && !has_split && (my_tiles - 1 < ndp ? nk : skl) >= 3;
+  if (!stored_early) store_q(0, 0, cm0, cn0);
   store_q(0, 1, cm0, cn0);
   store_q(1, 1, cm0, cn0);
-  store_q(1, 0, cm0, cn0);
+  if (!stored_early) store_q(1, 0, cm0, cn0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail's zero-fill DMAs land before the LDS is released
 }
 
