@@ -318,8 +318,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(const bf16_t* __restri
                                                           const float* __restrict__ kbias, const bf16_t* __restrict__ out,
                                                           const float* __restrict__ lse, const bf16_t* __restrict__ dout,
                                                           bf16_t* __restrict__ dqkv, float* __restrict__ dbqkv,
-                                                          int heads, float qscale, uint32_t thresh, float dscale,
-                                                          uint64_t seed) {
+                                                          float* __restrict__ dwork, int heads, float qscale,
+                                                          uint32_t thresh, float dscale, uint64_t seed) {
   __shared__ __attribute__((aligned(16))) char sm[3 * 16384 + 32768];  // 80 KiB
   char* Qi = sm;            // [128 q][64]      q·scale (+ bias)
   char* Ki = sm + 16384;    // [128 key][64]    k (+ bias)
@@ -349,18 +349,20 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(const bf16_t* __restri
     vb[ks][0] = b0.x; vb[ks][1] = b0.y; vb[ks][2] = b0.z; vb[ks][3] = b0.w;
     vb[ks][4] = b1.x; vb[ks][5] = b1.y; vb[ks][6] = b1.z; vb[ks][7] = b1.w;
   }
-  uint4 vraw[2][2], oraw[2][8];
+  // D = rowsum(dO∘O) is formed ONCE per workgroup: wave w takes queries 32w..32w+31,
+  // a lane half a row (32 d), the pair combines with one shuffle and D goes through
+  // a global scratch row of this head (every wave then reads all 128) — each wave
+  // used to load all 128 O rows itself (64 KiB of O per workgroup instead of 16)
+  uint4 vraw[2][2], oraw[4];
 #pragma unroll
   for (int kt = 0; kt < 2; kt++)
 #pragma unroll
     for (int ks = 0; ks < 2; ks++)
       vraw[kt][ks] = *reinterpret_cast<const uint4*>(qkv + (row0 + kw + kt * 16 + fr) * W3 + 2 * H + h * AD +
                                                      ks * 32 + fq * 8);
+  const int dq = wave * 32 + (lane >> 1), dh = (lane & 1) * 32;  // this lane's D row and half
 #pragma unroll
-  for (int u = 0; u < 2; u++)
-#pragma unroll
-    for (int c = 0; c < 8; c++)
-      oraw[u][c] = *reinterpret_cast<const uint4*>(out + (row0 + 2 * lane + u) * H + h * AD + c * 8);
+  for (int c = 0; c < 4; c++) oraw[c] = *reinterpret_cast<const uint4*>(out + (row0 + dq) * H + h * AD + dh + c * 8);
   const float2 lse2 = *reinterpret_cast<const float2*>(lse + (long)bh * AS + 2 * lane);
   float kbv[2];
 #pragma unroll
@@ -380,21 +382,28 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(const bf16_t* __restri
     }
   __syncthreads();
 
-  // D[q] = Σ_d dO[q][d]·O[q][d] for q = 2·lane, 2·lane + 1 (every wave keeps all 128)
-  float dd[2];
-#pragma unroll
-  for (int u = 0; u < 2; u++) {
-    const int q = 2 * lane + u;
+  // D[q] = Σ_d dO[q][d]·O[q][d]: this wave's 32 queries -> the head's scratch row,
+  // then every wave keeps q = 2·lane, 2·lane + 1
+  {
     float acc = 0.f;
 #pragma unroll
-    for (int c = 0; c < 8; c++) {
+    for (int c = 0; c < 4; c++) {
       float g[8], o[8];
-      unpack8(*reinterpret_cast<const uint4*>(Gi + off64(q, c * 8)), g);
-      unpack8(oraw[u][c], o);
+      unpack8(*reinterpret_cast<const uint4*>(Gi + off64(dq, dh + c * 8)), g);
+      unpack8(oraw[c], o);
 #pragma unroll
       for (int e = 0; e < 8; e++) acc += g[e] * o[e];
     }
-    dd[u] = acc;
+    acc += __shfl_xor(acc, 1, 64);
+    if (!(lane & 1)) dwork[(long)bh * AS + dq] = acc;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  float dd[2];
+  {
+    const float2 d2 = *reinterpret_cast<const float2*>(dwork + (long)bh * AS + 2 * lane);
+    dd[0] = d2.x;
+    dd[1] = d2.y;
   }
   short8 kreg[2][2];
 #pragma unroll
@@ -996,7 +1005,7 @@ KFA_API int kfa_attn_fwd(const void* qkv, const float* bqkv, const float* key_bi
 }
 
 // dqkv [B*S, 3H] (overwritten); dbqkv [3H] fp32 (+)= bias gradient (nullable)
-// (out = the forward's ctx: D = rowsum(dO∘O) is formed from it).  work: B*heads*S floats (S > 128 only)
+// (out = the forward's ctx: D = rowsum(dO∘O) is formed from it).  work: B*heads*S floats (D of every query)
 KFA_API int kfa_attn_bwd(const void* qkv, const float* bqkv, const float* key_bias, const void* out, const float* lse,
                          const void* dout, void* dqkv, float* dbqkv, int B, int S, int heads, int d, float qscale,
                          float p, unsigned long long seed, float* work, hipStream_t st) {
@@ -1006,9 +1015,10 @@ KFA_API int kfa_attn_bwd(const void* qkv, const float* bqkv, const float* key_bi
   const uint32_t th = attn_drop_thresh(p);
   const float ds = p > 0.f ? 1.f / (1.f - p) : 1.f;
   if (S == AS && !attn_long_forced()) {
+    if (!work) return -3;
     hipLaunchKernelGGL(attn_bwd_kernel, dim3((unsigned)(B * heads)), dim3(256), 0, st, (const bf16_t*)qkv, bqkv,
-                       key_bias, (const bf16_t*)out, lse, (const bf16_t*)dout, (bf16_t*)dqkv, dbqkv, heads, qscale, th,
-                       ds, (uint64_t)seed);
+                       key_bias, (const bf16_t*)out, lse, (const bf16_t*)dout, (bf16_t*)dqkv, dbqkv, work, heads,
+                       qscale, th, ds, (uint64_t)seed);
     return kfa_status();
   }
   if (!work) return -3;
