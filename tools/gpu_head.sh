@@ -1,5 +1,5 @@
 #!/bin/bash
-# HEAD evidence: GPU tests, ResNet-50 bench + rocprof trace, BERT-base bench + trace, W&D bench.
+# HEAD evidence (gpurun --timeout 1100 -- bash tools/gpu_head.sh): GPU tests, ResNet-50 bench + rocprof trace, BERT-base bench + trace, W&D bench.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R; mkdir -p gpurun_out
