@@ -42,14 +42,6 @@ constexpr int AD = 64;   // head dim
 typedef short v4i16 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
 
-// stateless dropout hash — the same counter hash as csrc/kernels/transformer.hip
-__device__ __forceinline__ uint32_t drop_hash(uint64_t seed, uint64_t i) {
-  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (i + 1);
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return (uint32_t)((z ^ (z >> 31)) >> 32);
-}
-
 // [rows][64] images: chunk c of row r at c ^ m(r), m(r) = 2·((r>>1)&1) + 4·(((r>>2)^(r>>3))&1) + ((r>>3)&1).
 // Conflict-free for the 16x16x32 row reads (ds_read_b128, 16-row groups) AND for
 // both transposed-read row sets (8 consecutive rows; rows R..R+3 with R+8..R+11):

@@ -72,6 +72,24 @@ __device__ __forceinline__ float gelu_grad(float z) {
   return fmaf(z * 0.39894228040143268f, e, cdf);
 }
 
+// Dropout counter hash: keep element i under a (well-mixed, per-launch) 64-bit
+// seed iff drop_hash(seed, i) >= p * 2^32, so forward and backward regenerate
+// the same mask from (seed, index) and no mask is ever stored.  The seed folds
+// into the index with wave-uniform keys and each element costs one 32-bit
+// integer finaliser (lowbias32: two 32-bit multiplies, ~12 VALU) — the
+// splitmix64 finaliser used before took three 64-bit multiplies (~70 VALU
+// slots) and made the dropout hash the largest cost of the attention, LayerNorm
+// and hidden-dropout kernels (BERT-base: 100M+ hashed elements per layer).
+__device__ __forceinline__ uint32_t drop_hash(uint64_t seed, uint64_t i) {
+  uint32_t x = ((uint32_t)i ^ (uint32_t)seed) + (uint32_t)(seed >> 32) + __umul24((uint32_t)(i >> 32), 0x9E3779u);
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+
 static inline int kfa_status() { return (int)hipGetLastError(); }
 
 static inline int kfa_ceil_div(long a, long b) { return (int)((a + b - 1) / b); }

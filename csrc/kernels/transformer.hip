@@ -22,7 +22,7 @@
 //    gradient that touches only the looked-up rows).
 //
 // Dropout RNG: keep(seed, i) = hash(seed, i) >= p * 2^32 — a stateless
-// counter hash (splitmix64 finaliser), so forward and backward regenerate the
+// counter hash (drop_hash, common.h), so forward and backward regenerate the
 // same mask from (seed, element index).
 #include <cstdlib>
 
@@ -31,13 +31,6 @@
 namespace {
 
 constexpr int kRowsPerBlock = 4;  // one wave per row
-
-__device__ __forceinline__ uint32_t drop_hash(uint64_t seed, uint64_t i) {
-  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (i + 1);
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return (uint32_t)((z ^ (z >> 31)) >> 32);
-}
 
 __device__ __forceinline__ bool keep(uint64_t seed, uint64_t i, uint32_t thresh) {
   return drop_hash(seed, i) >= thresh;

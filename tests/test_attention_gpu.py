@@ -1,7 +1,7 @@
 """Fused attention (csrc/kernels/attention.hip) vs a plain PyTorch fp32 reference.
 
-The dropout case rebuilds the kernels' counter-hash keep mask in numpy (uint64
-splitmix finaliser, same constants) so forward AND backward are checked
+The dropout case rebuilds the kernels' counter-hash keep mask in numpy (numpy copy
+of drop_hash in csrc/kernels/common.h) so forward AND backward are checked
 element-wise against the reference with the identical mask."""
 import math
 
@@ -21,13 +21,25 @@ def _close(a, b, tol, what=""):
     assert err <= tol * scale, f"{what}: err {err} scale {scale}"
 
 
-def _keep_mask(seed, B, heads, S, p):
-    i = np.arange(B * heads * S * S, dtype=np.uint64)
+def _drop_hash(seed, i):
+    """numpy copy of drop_hash (csrc/kernels/common.h) over uint64 indices."""
+    s = np.uint64(seed)
+    k0 = np.uint32(int(s) & 0xFFFFFFFF)
+    k1 = np.uint32(int(s) >> 32)
     with np.errstate(over="ignore"):
-        z = np.uint64(seed) + np.uint64(0x9E3779B97F4A7C15) * (i + np.uint64(1))
-        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
-        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
-        h = ((z ^ (z >> np.uint64(31))) >> np.uint64(32)).astype(np.uint32)
+        lo = (i & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+        hi = (i >> np.uint64(32)).astype(np.uint32)
+        x = (lo ^ k0) + k1 + (hi & np.uint32(0xFFFFFF)) * np.uint32(0x9E3779)
+        x ^= x >> np.uint32(16)
+        x *= np.uint32(0x7FEB352D)
+        x ^= x >> np.uint32(15)
+        x *= np.uint32(0x846CA68B)
+        x ^= x >> np.uint32(16)
+    return x
+
+
+def _keep_mask(seed, B, heads, S, p):
+    h = _drop_hash(seed, np.arange(B * heads * S * S, dtype=np.uint64))
     thresh = min(int(p * 4294967296.0), 4294967295)
     return torch.from_numpy((h >= thresh).reshape(B, heads, S, S).astype(np.float32))
 
