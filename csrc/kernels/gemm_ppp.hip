@@ -95,9 +95,9 @@ struct PppArgs {
   int M, N, K, lda, ldb, ldc;
   unsigned c_bytes;
   // split remainder (split > 1): the tiles past the last full round of the grid
-  // are cut into `split` k-ranges run by `split` blocks; parts 1.. leave fp32
-  // partial accumulators in `ws` and count themselves in `flags[unit]`, part 0
-  // adds them and writes C (flags self-cleaning: part 0 resets its counter)
+  // are cut into `split` k-ranges run by `split` blocks; every part leaves its fp32
+  // partial accumulators in `ws` and draws a ticket from `flags[unit]`, the last
+  // arriver adds the others and writes C (flags self-cleaning: it resets the counter)
   float* ws;
   int* flags;
   int split;
@@ -527,31 +527,46 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
   }
   if (!wr) asm volatile("s_barrier" ::: "memory");  // both groups at the same barrier count
   if (has_split) {
-    // partial slot of (unit, part >= 1): [TN * TM floatx4][512 threads], coalesced
-    // 16 B per lane; the reader has the same register layout, so no permutation
+    // Last-arriver combine (no block ever waits for another, so the kernel
+    // finishes whatever share of the CUs it gets — RCCL kernels, a side stream,
+    // another process): every part publishes its fp32 partial slot
+    // [TN * TM floatx4][512 threads] (coalesced 16 B per lane, the reader has the
+    // same register layout), releases it at agent scope and draws a ticket; the
+    // part that draws ns - 1 acquires, adds the other ns - 1 slots and writes C.
     constexpr int NR = TN * TM;
-    floatx4* slots = reinterpret_cast<floatx4*>(g.ws) + (long)unit * (ns - 1) * NR * 512;
+    floatx4* slots = reinterpret_cast<floatx4*>(g.ws) + (long)unit * ns * NR * 512;
     int* flag = g.flags + unit;
-    if (part) {
-      floatx4* dst = slots + (long)(part - 1) * NR * 512 + tid;
+    {
+      floatx4* dst = slots + (long)part * NR * 512 + tid;
 #pragma unroll
       for (int i = 0; i < TN; i++)
 #pragma unroll
-        for (int j = 0; j < TM; j++) __builtin_nontemporal_store(acc[i][j], dst + (i * TM + j) * 512);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) __hip_atomic_fetch_add(flag, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      return;
+        for (int j = 0; j < TM; j++) dst[(i * TM + j) * 512] = acc[i][j];
     }
-    // spin with relaxed loads (an acquire per iteration would invalidate the
-    // XCD's L2 under every CU still streaming), then ONE acquire fence
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's slot stores (and the tail DMAs) done
+    __syncthreads();
+    int* last = reinterpret_cast<int*>(smem);  // the one LDS array: no DMA in flight after the vmcnt(0) above
     if (tid == 0) {
-      while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < ns - 1) __builtin_amdgcn_s_sleep(2);
-      __hip_atomic_store(flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // keep: the fence's own wait can be dropped
+      const int t = __hip_atomic_fetch_add(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int is_last = t == ns - 1;
+      if (is_last) {
+        __hip_atomic_store(flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // self-cleaning
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      *last = is_last;
     }
     __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    for (int q = 0; q < ns - 1; q++) {
+    if (!*last) return;
+    // sum the slots in part order (its own slot re-read too), so C does not depend on
+    // which part arrived last: bit-identical results run to run
+#pragma unroll
+    for (int i = 0; i < TN; i++)
+#pragma unroll
+      for (int j = 0; j < TM; j++) acc[i][j] = __builtin_nontemporal_load(slots + tid + (i * TM + j) * 512);
+    for (int q = 1; q < ns; q++) {
       const floatx4* src = slots + (long)q * NR * 512 + tid;
 #pragma unroll
       for (int i = 0; i < TN; i++)
@@ -610,7 +625,7 @@ KFA_API long kfa_gemm_ppp_ws_bytes(int M, int N, int K, int bn, int blocks) {
   const int s = ppp_split(tiles, cus, K / BK);
   if (s == 1) return 0;
   const long r = tiles % cus;
-  return 4096 + r * (s - 1) * 256L * bn * 4;
+  return 4096 + r * s * 256L * bn * 4;  // every part publishes (the last arriver is not known in advance)
 }
 
 KFA_API int kfa_gemm_ppp_pick_bn(int M, int N) {

@@ -52,6 +52,7 @@ class SyntheticMNIST:
         self.validation = self._make(n_val, g)
         self.test = self._make(n_test, g)
         self._pos = 0
+        self._perm = None  # epoch order after the first pass (indices; the split itself is never re-laid out)
 
     def _make(self, n, g):
         y = torch.randint(0, 10, (n,), generator=g)
@@ -66,12 +67,15 @@ class SyntheticMNIST:
         return self
 
     def next_batch(self, batch_size: int):
+        """Next ``batch_size`` examples; each epoch after the first visits the split in
+        a fresh random order (``input_data``'s shuffle) by gathering the batch's rows."""
         x, y = self.train
         if self._pos + batch_size > x.shape[0]:
-            perm = torch.randperm(x.shape[0], generator=self._g).to(x.device)
-            self.train = (x[perm], y[perm])
-            x, y = self.train
+            self._perm = torch.randperm(x.shape[0], generator=self._g).to(x.device)
             self._pos = 0
         s = slice(self._pos, self._pos + batch_size)
         self._pos += batch_size
-        return x[s], y[s]
+        if self._perm is None:
+            return x[s], y[s]
+        idx = self._perm[s]
+        return x.index_select(0, idx), y.index_select(0, idx)

@@ -7,6 +7,8 @@ the same kernel as the loss so backward launches nothing.
 """
 from __future__ import annotations
 
+import math
+
 import torch
 
 from . import _lib
@@ -45,6 +47,48 @@ def cross_entropy(logits: torch.Tensor, labels: torch.Tensor, label_smoothing: f
     if logits.dtype not in (torch.bfloat16, torch.float32):
         logits = logits.float()
     return _XentFn.apply(logits, labels, label_smoothing)
+
+
+class _ClippedSumXentFn(torch.autograd.Function):
+    """Summed cross-entropy of clipped probabilities, one fused kernel pass: the
+    kernel's per-row loss and ``softmax - onehot`` gradient at scale 1, then the
+    rows whose label probability fell under the clip (loss > -log eps) lose their
+    gradient and are capped — ``tf.clip_by_value`` passes no gradient there."""
+
+    @staticmethod
+    def forward(ctx, logits, labels, eps):
+        z = logits.contiguous()
+        rows, V = z.numel() // z.shape[-1], z.shape[-1]
+        lab = labels.reshape(-1).to(torch.int64).contiguous()
+        if lab.numel() != rows:
+            raise ValueError(f"clipped_sum_cross_entropy: {lab.numel()} labels for {rows} rows")
+        row_loss = torch.empty(rows, dtype=torch.float32, device=z.device)
+        dz = torch.empty_like(z) if logits.requires_grad else None
+        _lib.call("kfa_softmax_xent", _lib.ptr(z), int(z.dtype == torch.bfloat16), _lib.ptr(lab), None,
+                  _lib.ptr(row_loss), _lib.ptr(dz), rows, V, 1.0, 0.0, _lib.stream())
+        cap = -math.log(eps)
+        clipped = row_loss > cap
+        if dz is not None:
+            dz.view(rows, V).masked_fill_(clipped.view(rows, 1), 0)
+        ctx.save_for_backward(dz)
+        return row_loss.clamp(max=cap).sum()
+
+    @staticmethod
+    def backward(ctx, g):
+        (dz,) = ctx.saved_tensors
+        return dz * g.to(dz.dtype), None, None
+
+
+def clipped_sum_cross_entropy(logits: torch.Tensor, labels: torch.Tensor, eps: float = 1e-10) -> torch.Tensor:
+    """``-Σ y · log(clip(softmax(z), eps, 1))`` summed over the batch: the loss the
+    reference's distributed MNIST minimises (``mnist_replica.py:167-168``), where
+    :func:`cross_entropy` is the batch mean of ``mnist_softmax.py:57-58``."""
+    if not logits.is_cuda:
+        p = torch.softmax(logits.float(), -1)
+        return -torch.log(p.gather(-1, labels.reshape(-1, 1).long()).clamp(eps, 1.0)).sum()
+    if logits.dtype not in (torch.bfloat16, torch.float32):
+        logits = logits.float()
+    return _ClippedSumXentFn.apply(logits, labels, float(eps))
 
 
 def argmax(logits: torch.Tensor) -> torch.Tensor:

@@ -73,6 +73,15 @@ def mix_seed(*parts: int) -> int:
     return h
 
 
+def hash_key(seed: int) -> int:
+    """The 64-bit key a kernel's dropout hash is launched with: ``seed`` mixed once
+    per launch on the host.  ``drop_hash`` (``csrc/kernels/common.h``) folds its key
+    into the element index linearly, so raw seeds that differ in a few bits (a
+    step counter) would give index-permuted copies of one mask; mixed keys give
+    unrelated masks.  Forward and backward launchers apply the same mapping."""
+    return mix_seed(int(seed) & _MASK64, 0x5EED)
+
+
 def _part(nfloats: int, device) -> torch.Tensor:
     return _lib.workspace(nfloats * 4, device, "colsum_part").view(torch.float32)
 
@@ -103,7 +112,7 @@ def ln_fwd(x, gamma, beta, res=None, bias=None, eps=1e-12, p=0.0, seed=0, save_s
     mean = torch.empty(rows, dtype=torch.float32, device=x.device)
     rstd = torch.empty_like(mean)
     _lib.call("kfa_ln_fwd", _lib.ptr(x), _lib.ptr(res), _lib.ptr(bias), _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(y),
-              _lib.ptr(xs), _lib.ptr(mean), _lib.ptr(rstd), rows, H, eps, float(p), seed, _lib.stream())
+              _lib.ptr(xs), _lib.ptr(mean), _lib.ptr(rstd), rows, H, eps, float(p), hash_key(seed), _lib.stream())
     return y, (xs if xs is not None else x), mean, rstd
 
 
@@ -118,7 +127,7 @@ def ln_bwd(dy, xs, mean, rstd, gamma, dgamma, dbeta, dbias=None, p=0.0, seed=0, 
     part = _part(_lib.lib().kfa_ln_part_floats(rows, H), dy.device)
     _lib.call("kfa_ln_bwd2", _lib.ptr(dy), _lib.ptr(dy2), _lib.ptr(xs), _lib.ptr(mean), _lib.ptr(rstd), _lib.ptr(gamma),
               _lib.ptr(dx), _lib.ptr(dbr), _lib.ptr(part), _lib.ptr(dgamma), _lib.ptr(dbeta), _lib.ptr(dbias), rows, H,
-              float(p), seed, 1, _lib.stream())
+              float(p), hash_key(seed), 1, _lib.stream())
     return dx, (dbr if dbr is not None else dx)
 
 
@@ -151,7 +160,7 @@ class ResidualJoin:
 def bias_act_fwd(x, bias, act, p=0.0, seed=0):
     rows, N = x.numel() // x.shape[-1], x.shape[-1]
     y = torch.empty_like(x)
-    _lib.call("kfa_bias_act_fwd", _lib.ptr(x), _lib.ptr(bias), _lib.ptr(y), rows, N, ACTS[act], float(p), seed,
+    _lib.call("kfa_bias_act_fwd", _lib.ptr(x), _lib.ptr(bias), _lib.ptr(y), rows, N, ACTS[act], float(p), hash_key(seed),
               _lib.stream())
     return y
 
@@ -161,7 +170,7 @@ def bias_act_bwd(dy, x, bias, act, dbias, p=0.0, seed=0, want_dx=True):
     dx = torch.empty_like(dy) if want_dx else None
     part = _part(_lib.lib().kfa_colsum_part_floats(rows, N), dy.device)
     _lib.call("kfa_bias_act_bwd", _lib.ptr(dy), _lib.ptr(x), _lib.ptr(bias), _lib.ptr(dx), _lib.ptr(part),
-              _lib.ptr(dbias), rows, N, ACTS[act], float(p), seed, 1, _lib.stream())
+              _lib.ptr(dbias), rows, N, ACTS[act], float(p), hash_key(seed), 1, _lib.stream())
     return dx
 
 
@@ -413,7 +422,7 @@ def attn_fwd(qkv, bqkv, key_bias, B, S, heads, p=0.0, seed=0):
     out = torch.empty(T_, H, dtype=qkv.dtype, device=qkv.device)
     lse = torch.empty(B * heads, S, dtype=torch.float32, device=qkv.device)
     _lib.call("kfa_attn_fwd", _lib.ptr(qkv), _lib.ptr(bqkv), _lib.ptr(key_bias), _lib.ptr(out), _lib.ptr(lse), B, S,
-              heads, d, 1.0 / math.sqrt(d), float(p), int(seed) & _MASK64, _lib.stream())
+              heads, d, 1.0 / math.sqrt(d), float(p), hash_key(seed), _lib.stream())
     return out, lse
 
 
@@ -433,7 +442,7 @@ def attn_bwd(qkv, bqkv, key_bias, out, lse, dout, dbqkv, B, S, heads, p=0.0, see
     work = _lib.workspace(B * heads * S * 4, qkv.device, "attn_rowdot")  # D = rowsum(dO∘O) (S > 128)
     _lib.call("kfa_attn_bwd", _lib.ptr(qkv), _lib.ptr(bqkv), _lib.ptr(key_bias), _lib.ptr(out), _lib.ptr(lse),
               _lib.ptr(dout), _lib.ptr(dqkv), _lib.ptr(dbqkv), B, S, heads, d, 1.0 / math.sqrt(d), float(p),
-              int(seed) & _MASK64, _lib.ptr(work), _lib.stream())
+              hash_key(seed), _lib.ptr(work), _lib.stream())
     return dqkv
 
 

@@ -61,6 +61,57 @@ def _use_gpu(args) -> bool:
     return torch.cuda.is_available()
 
 
+_armed_at = [0.0]
+
+
+def _arm_watchdog(args) -> None:
+    """(Re-)arm the replica's hang guard: if the next ``--hang_timeout`` seconds
+    pass without another call (one per training step; the rendezvous and the
+    first, kernel-tuning step get the same budget), every thread's Python stack
+    goes to stderr (the replica log) and the process exits 1, so the supervisor
+    applies the replica's restartPolicy (``dist.yml:45`` OnFailure) instead of
+    the job hanging on a wedged collective or a dead peer."""
+    t = getattr(args, "hang_timeout", 0)
+    now = time.monotonic()
+    # re-arming costs ~0.1 ms (a timer thread restart): at most 8 times per timeout period
+    if t > 0 and now - _armed_at[0] >= t / 8:
+        import faulthandler
+        faulthandler.dump_traceback_later(t, exit=True)
+        _armed_at[0] = now
+
+
+def _disarm_watchdog() -> None:
+    import faulthandler
+    faulthandler.cancel_dump_traceback_later()
+    _armed_at[0] = 0.0
+
+
+def _install_stack_dumps() -> None:
+    """SIGTERM (the supervisor stopping a replica) and SIGUSR1 print all stacks first."""
+    import faulthandler
+    import signal
+    faulthandler.enable()
+    try:
+        faulthandler.register(signal.SIGUSR1, all_threads=True)
+        faulthandler.register(signal.SIGTERM, all_threads=True, chain=True)
+    except (AttributeError, ValueError, RuntimeError):  # not the main thread / platform without it
+        pass
+
+
+def _test_hang(spec: ClusterSpec, step: int) -> None:
+    """Test hook: ``KFA_TEST_HANG=<job_name>:<task_index>:<step>`` stops that replica
+    at that step as a replica stuck in a collective would (tests/test_e2e_cpu.py)."""
+    v = os.environ.get("KFA_TEST_HANG")
+    if v and v == f"{spec.job_name}:{spec.task_index}:{step}":
+        _log(f"{spec.job_name} {spec.task_index}: hanging at step {step} on purpose (KFA_TEST_HANG)")
+        while True:
+            time.sleep(1.0)
+
+
+def _pg_timeout(args) -> datetime.timedelta:
+    return datetime.timedelta(seconds=getattr(args, "dist_timeout", 300.0))
+
+
 def _store(spec: ClusterSpec, is_master: bool, timeout: float = 300.0):
     host, port = spec.rendezvous()
     return dist.TCPStore(host, port, spec.num_workers if is_master else None, is_master,
@@ -70,14 +121,17 @@ def _store(spec: ClusterSpec, is_master: bool, timeout: float = 300.0):
 # ------------------------------------------------------------------ models
 def build(args, device):
     from ..models import mnist
-    from ..ops.loss import cross_entropy
+    from ..ops.loss import clipped_sum_cross_entropy, cross_entropy
     name = args.model
+    # --loss sum_clipped: mnist_replica.py:168's -reduce_sum(y_ * log(clip(y, 1e-10, 1)));
+    # mean: mnist_softmax.py:57-58's mean softmax cross-entropy (every other model)
+    xent = clipped_sum_cross_entropy if getattr(args, "loss", "mean") == "sum_clipped" else cross_entropy
     if name == "mnist_softmax":
         data = mnist.SyntheticMNIST(seed=args.seed)
-        return mnist.MnistSoftmax(), data, lambda m, x, y: cross_entropy(m(x).float(), y)
+        return mnist.MnistSoftmax(), data, lambda m, x, y: xent(m(x).float(), y)
     if name == "mnist_mlp":
         data = mnist.SyntheticMNIST(seed=args.seed)
-        return mnist.MnistMLP(args.hidden_units), data, lambda m, x, y: cross_entropy(m(x).float(), y)
+        return mnist.MnistMLP(args.hidden_units), data, lambda m, x, y: xent(m(x).float(), y)
     if name in ("resnet50", "resnet_tiny"):
         from ..models.resnet import resnet50, resnet_tiny
         model = resnet50() if name == "resnet50" else resnet_tiny(10)
@@ -180,7 +234,7 @@ def run_ps_async(spec: ClusterSpec, args) -> int:
                 _log(f"PS {spec.task_index}: chief unreachable ({e}); exiting")
                 return 1
             time.sleep(0.5)
-    dist.init_process_group("gloo", store=store, rank=rank, world_size=W + P)
+    dist.init_process_group("gloo", store=store, rank=rank, world_size=W + P, timeout=_pg_timeout(args))
     torch.manual_seed(args.seed)  # same initial values as every worker's model
     use_gpu = _use_gpu(args)
     transport = _ps_transport(args, use_gpu)
@@ -219,7 +273,7 @@ def run_worker_async(spec: ClusterSpec, args) -> int:
     if use_gpu:
         torch.cuda.set_device(0)
     store = _store(spec, spec.is_chief)
-    dist.init_process_group("gloo", store=store, rank=spec.task_index, world_size=W + P)
+    dist.init_process_group("gloo", store=store, rank=spec.task_index, world_size=W + P, timeout=_pg_timeout(args))
     torch.manual_seed(args.seed)
     args.num_ps = P
     model, data, loss_fn = build(args, device)
@@ -250,6 +304,8 @@ def run_worker_async(spec: ClusterSpec, args) -> int:
     _log(f"Training begins @ {t_begin:f}")
     local_step, global_step, t_first, loss = 0, 0, None, None
     while global_step < args.train_steps:
+        _arm_watchdog(args)
+        _test_hang(spec, local_step)
         if data is not None:
             xb, yb = data.next_batch(args.batch_size)
             batch = (xb.to(device), yb.to(device))
@@ -343,7 +399,8 @@ def run_worker(spec: ClusterSpec, args) -> int:
         torch.cuda.set_device(0)
     world = 1 if spec.is_local else spec.num_workers
     rank = 0 if spec.is_local else spec.task_index
-    if args.replicas_to_aggregate is not None and not spec.is_local and args.replicas_to_aggregate != world:
+    if (args.sync_replicas and args.replicas_to_aggregate is not None and not spec.is_local
+            and args.replicas_to_aggregate != world):
         raise SystemExit(f"--replicas_to_aggregate {args.replicas_to_aggregate} != {world} workers: the collective "
                          "path aggregates every worker's gradient; use --ps_mode async with PS tasks")
     store = None
@@ -352,7 +409,7 @@ def run_worker(spec: ClusterSpec, args) -> int:
             os.environ.setdefault("KFA_CONV_OVERSUB", "2")  # see engine.init_distributed
         store = _store(spec, spec.is_chief)
         backend = os.environ.get("KFA_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
-        dist.init_process_group(backend, store=store, rank=rank, world_size=world,
+        dist.init_process_group(backend, store=store, rank=rank, world_size=world, timeout=_pg_timeout(args),
                                 **({"device_id": device} if backend == "nccl" else {}))
     torch.manual_seed(args.seed)  # identical init everywhere (+ broadcast in the engine)
     num_ps = 0 if spec.is_local else len(spec.ps)
@@ -410,6 +467,8 @@ def run_worker(spec: ClusterSpec, args) -> int:
     # per-shape kernels, the capture step records the graph), GPU drained first
     warm = min(cap_step + 1 if use_graph else 1, max(1, steps_per_worker - 1))
     for local_step in range(steps_per_worker):
+        _arm_watchdog(args)
+        _test_hang(spec, local_step)
         if data is not None:
             xb, yb = data.next_batch(args.batch_size)
             batch = (xb.to(device), yb.to(device))
@@ -532,6 +591,14 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--log_every", type=int, default=1)
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--ps_connect_timeout", type=float, default=300.0)
+    ap.add_argument("--dist_timeout", type=float, default=float(os.environ.get("KFA_DIST_INIT_TIMEOUT", "300")),
+                    help="torch.distributed init / collective timeout (seconds)")
+    ap.add_argument("--hang_timeout", type=float, default=float(os.environ.get("KFA_REPLICA_HANG_TIMEOUT", "900")),
+                    help="seconds without progress (rendezvous, one training step) before the replica dumps "
+                         "every thread's stack and exits 1 (0 = off)")
+    ap.add_argument("--loss", default="mean", choices=["mean", "sum_clipped"],
+                    help="MNIST loss: mean softmax cross-entropy (mnist_softmax.py) or the summed "
+                         "cross-entropy of clipped probabilities (mnist_replica.py:168)")
     return ap
 
 
@@ -548,11 +615,19 @@ def main(argv: Optional[list] = None) -> int:
     spec = parse_cluster(args)
     if not spec.is_local:
         _aggregate(spec, args)  # validates --replicas_to_aggregate before any connection is made
+    _install_stack_dumps()
     if _async_mode(spec, args):
-        return run_ps_async(spec, args) if spec.is_ps else run_worker_async(spec, args)
-    if spec.is_ps:
+        if spec.is_ps:  # a PS serves for as long as the workers train: no step-level guard
+            return run_ps_async(spec, args)
+        _arm_watchdog(args)
+        rc = run_worker_async(spec, args)
+    elif spec.is_ps:
         return run_ps(spec, args)
-    return run_worker(spec, args)
+    else:
+        _arm_watchdog(args)
+        rc = run_worker(spec, args)
+    _disarm_watchdog()
+    return rc
 
 
 if __name__ == "__main__":

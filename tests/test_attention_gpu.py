@@ -39,7 +39,8 @@ def _drop_hash(seed, i):
 
 
 def _keep_mask(seed, B, heads, S, p):
-    h = _drop_hash(seed, np.arange(B * heads * S * S, dtype=np.uint64))
+    from kubeflow_controller_amd.ops.transformer import hash_key  # the launch key the wrapper passes
+    h = _drop_hash(hash_key(seed), np.arange(B * heads * S * S, dtype=np.uint64))
     thresh = min(int(p * 4294967296.0), 4294967295)
     return torch.from_numpy((h >= thresh).reshape(B, heads, S, S).astype(np.float32))
 

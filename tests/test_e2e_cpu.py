@@ -59,13 +59,14 @@ def test_local_mnist_tfjob_succeeds(node):
     st, n, root = node
     job = serde.load_file(os.path.join(ROOT, "examples", "tfjob", "local.yml"), env=ENV)[0]
     st.create(job)
-    j = wait_for_phase(st, "default", "local-training-job", {"Succeeded", "Failed"}, 120)
+    # the reference's workload: 100,000 GD steps, "step: i" printed for every one
+    j = wait_for_phase(st, "default", "local-training-job", {"Succeeded", "Failed"}, 300)
     assert j.status.phase == "Succeeded"
     assert j.status.tfReplicaStatuses[0].type == "Local"
     assert j.status.tfReplicaStatuses[0].tfReplicasStates == {"Succeeded": 1}
     (p,) = st.list("Pod")
     out = _logs(root, p)
-    assert "Test accuracy:" in out and "step: 0" in out
+    assert "Test accuracy:" in out and "step: 0\n" in out and "step: 99999\n" in out and "step: 50000\n" in out
     acc = float(out.split("Test accuracy:")[1].split()[0])
     assert acc > 0.8
     desc = describe_tfjob(st, "default", "local-training-job")
@@ -310,3 +311,28 @@ def test_multi_worker_tfjob_matches_single_process(node, tmp_path, ps):
     ref = _single_process_bert(3, 2)
     for k, v in ref.items():
         torch.testing.assert_close(state["model"][k], v, atol=1e-4, rtol=1e-4)  # Adam: lr 2e-3
+
+
+def test_hung_replica_dumps_stacks_and_fails_job(node):
+    """A replica wedged mid-training (KFA_TEST_HANG: worker 1 stops at step 2, so
+    worker 0 blocks in the next all-reduce) trips the per-step watchdog
+    (--hang_timeout): both replicas print every thread's stack into their logs and
+    exit 1, and with restartPolicy Never the job ends Failed instead of hanging."""
+    from kubeflow_controller_amd.api.core import EnvVar
+    st, n, root = node
+    cmd = [sys.executable, os.path.join(ROOT, "examples", "workdir", "mnist_replica.py"), "--device", "cpu",
+           "--hang_timeout", "6", "--train_steps", "50", "--log_every", "1"]
+    job = _job("hang", [("Worker", 2, cmd)], restart="Never")
+    job.spec.specs[0].template.spec.containers[0].env = [EnvVar(name="KFA_TEST_HANG", value="worker:1:2")]
+    t0 = time.time()
+    st.create(job)
+    j = wait_for_phase(st, "default", "hang", {"Succeeded", "Failed"}, 120)
+    assert j.status.phase == "Failed", describe_tfjob(st, "default", "hang")
+    assert time.time() - t0 < 100
+    pods = {p.metadata.labels["index"]: p for p in st.list("Pod") if p.metadata.labels.get("tf_job_name") == "hang"}
+    w1 = _logs(root, pods["1"])
+    assert "hanging at step 2 on purpose" in w1
+    for p in pods.values():
+        out = _logs(root, p)
+        assert "Timeout (0:00:06)!" in out and "most recent call first" in out, out[-3000:]
+        assert p.status.containerStatuses[0].terminated.exitCode != 0

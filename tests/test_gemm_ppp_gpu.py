@@ -106,3 +106,40 @@ def test_gemm_ppp_store_policies(probe):
     a, b = _bf(1000, 640), _bf(776, 640, s=0.05)
     c = G.gemm_ppp(a, b, blocks=3, probe=probe)
     _close(c, a.float() @ b.float().t(), 1e-2, f"probe {probe}")
+
+
+def test_gemm_ppp_split_under_cu_hog():
+    """Forward progress without co-residency: a diagnostic kernel holds all but 32
+    CUs for 1 s on another stream while the split-remainder shapes run.  With the
+    last-arriver combine no block waits for another, so the GEMMs finish on the CUs
+    that are left, before the hog ends, bit-identical to the unloaded runs."""
+    from kubeflow_controller_amd.ops import _lib
+    from kubeflow_controller_amd.ops import gemm as G
+    _lib.register("kfa_cu_hog", [_lib.I, _lib.L, _lib.P, _lib.P])
+    shapes = [(32768, 768, 768), (256, 1000, 2048), (1024, 1024, 1024), (5120, 768, 30528 // 64 * 64)]
+    torch.manual_seed(7)
+    ops = [(_bf(M, K), _bf(N, K, s=0.05)) for M, N, K in shapes]
+    for (a, b), (M, N, K) in zip(ops, shapes):
+        assert _lib.lib().kfa_gemm_ppp_ws_bytes(M, N, K, 256, 0) > 0, f"{M}x{N}x{K} should take the split path"
+    ref = [G.gemm_ppp(a, b, bn=256) for a, b in ops]
+    torch.cuda.synchronize()
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    nhog = ncu - 32
+    hog_s, gemm_s = torch.cuda.Stream(), torch.cuda.Stream()
+    flags = torch.zeros(nhog, dtype=torch.int32, device=D)
+    with torch.cuda.stream(hog_s):
+        _lib.call("kfa_cu_hog", nhog, 1_000_000, _lib.ptr(flags), _lib.stream())
+        hog_done = torch.cuda.Event()
+        hog_done.record(hog_s)
+    with torch.cuda.stream(gemm_s):
+        out = [G.gemm_ppp(a, b, bn=256) for a, b in ops]
+        gemm_done = torch.cuda.Event()
+        gemm_done.record(gemm_s)
+    gemm_done.synchronize()
+    finished_under_hog = not hog_done.query()
+    hog_done.synchronize()
+    torch.cuda.synchronize()
+    assert (flags.cpu() == (torch.arange(nhog) * 7 % 64 + 1).int()).all(), "hog kernel did not run to completion"
+    for r, o, s in zip(ref, out, shapes):
+        assert torch.equal(r, o), f"split GEMM {s} under load differs from the unloaded run"
+    assert finished_under_hog, "split GEMMs waited for the hog kernel to release its CUs"

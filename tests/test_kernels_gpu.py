@@ -311,3 +311,27 @@ def test_global_avg_pool_fwd_bwd(N, C, H, W):
     yf.backward(dy.float())
     assert x.grad.is_contiguous(memory_format=torch.channels_last)
     torch.testing.assert_close(x.grad.float(), xf.grad, atol=1e-3, rtol=1e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_clipped_sum_xent_matches_fp32(dtype):
+    """mnist_replica.py:168's summed clipped cross-entropy on the fused xent kernel:
+    loss and gradient vs the float64 TensorFlow-semantics reference (clip_by_value
+    passes no gradient where the label probability is below 1e-10)."""
+    from kubeflow_controller_amd.ops.loss import clipped_sum_cross_entropy
+    torch.manual_seed(3)
+    z = (torch.randn(100, 10, device="cuda") * 3)
+    z[5] = torch.tensor([80.0, -80.0] + [0.0] * 8, device="cuda")
+    y = torch.randint(0, 10, (100,), device="cuda")
+    y[5] = 1
+    zz = z.to(dtype).requires_grad_()
+    loss = clipped_sum_cross_entropy(zz, y)
+    loss.backward()
+    zr = z.to(dtype).double().cpu().requires_grad_()
+    p = torch.softmax(zr, -1)
+    ref = -(torch.nn.functional.one_hot(y.cpu(), 10).double() * torch.log(p.clamp(1e-10, 1.0))).sum()
+    ref.backward()
+    assert abs(float(loss.detach()) - float(ref)) <= 2e-3 * float(ref)
+    torch.testing.assert_close(zz.grad.double().cpu(), zr.grad, atol=2e-2 if dtype == torch.bfloat16 else 1e-5,
+                               rtol=2e-2 if dtype == torch.bfloat16 else 1e-4)
+    assert float(zz.grad[5].float().abs().sum()) == 0.0
