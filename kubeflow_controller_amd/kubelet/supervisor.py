@@ -169,6 +169,44 @@ class Supervisor:
             return None
         return [int(pod.metadata.labels.get("index", "0")) % self.num_gpus]
 
+    def _colocated_ps_gpus(self, pod: Pod) -> List[int]:
+        """Physical GPUs of the job's GPU-co-located PS replicas, by PS index, for a
+        Worker pod of a job whose PS template sets ``KFA_PS_COLOCATE=1``; else [].
+
+        The device-resident async PS keeps its variables and the workers' gradient
+        mailboxes in its GPU's HBM and every worker reads / writes them by HIP IPC
+        peer copies over xGMI (``parallel/async_ps.py``).  A worker must therefore
+        SEE those GPUs: they are appended to its ``HIP_VISIBLE_DEVICES`` after its
+        own (exclusive) GPU, which stays ordinal 0 for its compute.  The PS count
+        and template come from the TFJob spec (or, without a TFJob informer, the
+        worker's ``--ps_hosts`` and the job's PS pods)."""
+        if pod.metadata.labels.get("job_type", "") != v1alpha1.WORKER or self.num_gpus == 0:
+            return []
+        name = pod.metadata.labels.get("tf_job_name")
+        nps, colocate = 0, False
+        job = None
+        if self.tfjobs is not None and name:
+            try:
+                job = self.tfjobs.get(pod.metadata.namespace, name)
+            except errors.NotFound:
+                job = None
+        if job is not None:
+            for spec in job.spec.specs:
+                if spec.tfReplicaType == v1alpha1.PS:
+                    nps = spec.replicas if spec.replicas is not None else 1
+                    cs = spec.template.spec.containers if spec.template and spec.template.spec else []
+                    colocate = bool(cs) and any(e.name == "KFA_PS_COLOCATE" and e.value == "1" for e in cs[0].env)
+        else:
+            for a in pod.spec.containers[0].args:
+                if a.startswith("--ps_hosts="):
+                    nps = len([h for h in a.split("=", 1)[1].split(",") if h])
+            colocate = any(p.metadata.labels.get("tf_job_name") == name and p.metadata.labels.get("job_type") == v1alpha1.PS
+                           and any(e.name == "KFA_PS_COLOCATE" and e.value == "1" for e in p.spec.containers[0].env)
+                           for p in self.pods.list(pod.metadata.namespace))
+        if not colocate:
+            return []
+        return [i % self.num_gpus for i in range(nps)]
+
     def _bind_gpus(self, key: str, n: int) -> Optional[List[int]]:
         if n == 0:
             return []
@@ -228,7 +266,12 @@ class Supervisor:
             env[e.name] = e.value
         pp = env.get("PYTHONPATH", "")
         env["PYTHONPATH"] = REPO_ROOT + (os.pathsep + pp if pp else "")
-        env["HIP_VISIBLE_DEVICES"] = ",".join(str(g) for g in gpus) if gpus else ""
+        visible = list(gpus)
+        ps_gpus = self._colocated_ps_gpus(pod) if gpus else []
+        if ps_gpus:  # the job's PS GPUs after the worker's own: IPC peer copies need them visible
+            visible += [g for g in dict.fromkeys(ps_gpus) if g not in visible]
+            env["KFA_PS_GPUS"] = ",".join(str(g) for g in ps_gpus)
+        env["HIP_VISIBLE_DEVICES"] = ",".join(str(g) for g in visible) if visible else ""
         env.pop("ROCR_VISIBLE_DEVICES", None)
         env.pop("CUDA_VISIBLE_DEVICES", None)
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
@@ -238,7 +281,7 @@ class Supervisor:
         env["KFA_REPLICA_TYPE"] = pod.metadata.labels.get("job_type", "")
         env["KFA_REPLICA_INDEX"] = pod.metadata.labels.get("index", "0")
         env["KFA_TFJOB_NAME"] = pod.metadata.labels.get("tf_job_name", "")
-        env["KFA_GPUS"] = ",".join(str(g) for g in gpus)
+        env["KFA_GPUS"] = ",".join(str(g) for g in visible)  # physical GPU of each local ordinal
         cwd = self._rewrite(c.workingDir, mounts) if c.workingDir else self._pod_dir(pod)
         return argv, env, cwd
 

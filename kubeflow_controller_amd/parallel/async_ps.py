@@ -360,10 +360,14 @@ def _export(store, key: str, t: torch.Tensor) -> None:
     store.set(key, json.dumps(rec))
 
 
-def _import(store, key: str) -> torch.Tensor:
-    """Map a tensor another process of this job exported with :func:`_export`."""
+def _import(store, key: str, device: Optional[int] = None) -> torch.Tensor:
+    """Map a tensor another process of this job exported with :func:`_export`.
+    ``device``: this process's ordinal of the exporter's GPU (the record holds the
+    EXPORTER's ordinal, which differs whenever the two see different GPU lists)."""
     from torch.multiprocessing.reductions import rebuild_cuda_tensor
     r = json.loads(store.get(key).decode())
+    if device is not None:
+        r["device"] = int(device)
     dtype = getattr(torch, r["dtype"])
     if not isinstance(dtype, torch.dtype):
         raise ValueError(f"bad dtype {r['dtype']!r} in {key}")
@@ -375,6 +379,28 @@ def _import(store, key: str) -> torch.Tensor:
 
 
 CANARY_N = 64
+
+
+def physical_gpu() -> str:
+    """Physical index of this process's cuda:0 (the supervisor's ``KFA_GPUS`` /
+    ``HIP_VISIBLE_DEVICES`` list, first entry); "" when not pinned."""
+    vis = os.environ.get("KFA_GPUS") or os.environ.get("HIP_VISIBLE_DEVICES") or ""
+    first = vis.split(",")[0].strip()
+    return first
+
+
+def local_ordinal(phys: str) -> Tuple[Optional[int], str]:
+    """This process's device ordinal of physical GPU ``phys`` (None + the reason
+    when it is not visible here).  ``phys == ""`` (exporter not pinned): ordinal 0."""
+    if phys == "":
+        return 0, "exporter GPU unknown: assuming this process's cuda:0"
+    vis = os.environ.get("KFA_GPUS") or os.environ.get("HIP_VISIBLE_DEVICES")
+    if vis is None or not vis.strip():
+        return int(phys), f"all GPUs visible: cuda:{phys}"
+    lst = [v.strip() for v in vis.split(",") if v.strip()]
+    if phys in lst:
+        return lst.index(phys), f"GPU {phys} = cuda:{lst.index(phys)} (visible {','.join(lst)})"
+    return None, f"its GPU {phys} is not visible to this worker (HIP_VISIBLE_DEVICES={vis})"
 
 
 def _canary_values(nonce: int) -> torch.Tensor:
@@ -415,6 +441,8 @@ class DeviceAsyncPSServer(_Service):
         _export(store, _ipc_key(ps_index, "mail"), self.mail)
         _export(store, _ipc_key(ps_index, "canary"), self.canary)
         store.set(_ipc_key(ps_index, "nonce"), str(nonce))
+        store.set(_ipc_key(ps_index, "gpu"), physical_gpu())
+        self._done = torch.cuda.Event()
         store.set(_ipc_key(ps_index, "ready"), "1")
 
     def _apply(self, g: torch.Tensor, scale: float = 1.0) -> None:
@@ -429,8 +457,10 @@ class DeviceAsyncPSServer(_Service):
             # TF AdamOptimizer form (eps outside the bias-corrected sqrt) with the fused HIP kernel
             _lib.call("kfa_adam_step", _lib.ptr(self.w), None, _lib.ptr(g), 0, _lib.ptr(self.m), _lib.ptr(self.v), n,
                       self.lr, b1, b2, self.eps / math.sqrt(bc2), 0.0, bc1, bc2, scale, None, _lib.stream())
-        # the reply below tells the pusher its mailbox may be rewritten: the update must have read it
-        torch.cuda.current_stream(self.device).synchronize()
+        # the reply below tells the pusher its mailbox may be rewritten and its next pull
+        # sees this update: host wait on THIS update's completion event (not the stream)
+        self._done.record(torch.cuda.current_stream(self.device))
+        self._done.synchronize()
 
     def _send_vars(self, src: int) -> None:  # a host-transport client (IPC mapping failed on its side)
         self.stage.copy_(self.w)
@@ -461,7 +491,9 @@ class DeviceAsyncPSServer(_Service):
 
     def _acc_add(self, g: torch.Tensor) -> None:
         self.acc.add_(g)
-        torch.cuda.current_stream(self.device).synchronize()  # the mailbox may be reused after the reply
+        # the pusher may reuse its mailbox once replied to: wait for the add that read it
+        self._done.record(torch.cuda.current_stream(self.device))
+        self._done.synchronize()
 
     def _acc(self) -> torch.Tensor:
         return self.acc
@@ -489,6 +521,7 @@ class DeviceAsyncPSClient(_ClientSteps):
         by_name = dict(self.params)
         self.plan = []
         self.transports: List[str] = []
+        self.transport_desc: List[str] = []
         log = log or (lambda s: print(s, flush=True))
         t0 = time.time()
         for k in range(num_ps):
@@ -509,24 +542,31 @@ class DeviceAsyncPSClient(_ClientSteps):
                 time.sleep(0.05)
             w = mail = None
             try:
+                phys = store.get(_ipc_key(k, "gpu")).decode() if store.check([_ipc_key(k, "gpu")]) else ""
+                dev, where = local_ordinal(phys)
+                if dev is None:
+                    raise RuntimeError(where)
                 nonce = int(store.get(_ipc_key(k, "nonce")).decode())
-                canary = _import(store, _ipc_key(k, "canary"))
+                canary = _import(store, _ipc_key(k, "canary"), dev)
                 got = canary.cpu()
                 if not torch.equal(got, _canary_values(nonce)):
                     raise RuntimeError(f"canary mismatch (read {got[:4].tolist()}...)")
-                w = _import(store, _ipc_key(k, "w"))
-                mail = _import(store, _ipc_key(k, "mail"))[rank]
+                w = _import(store, _ipc_key(k, "w"), dev)
+                mail = _import(store, _ipc_key(k, "mail"), dev)[rank]
                 if w.numel() < total:
                     raise RuntimeError(f"PS buffer has {w.numel()} values, layout needs {total}")
                 self.transports.append("device")
+                self.transport_desc.append(f"PS {k}: device ({where})")
             except Exception as e:  # noqa: BLE001 — any mapping failure: fall back, loudly
                 log(f"Worker {rank}: WARNING: HIP IPC mapping of PS {k}'s device buffers failed ({e}); "
                     f"using the HOST transport for PS {k} (gloo, slower)")
                 self.transports.append("host")
+                self.transport_desc.append(f"PS {k}: host ({e})")
                 w = mail = None
             stage = torch.empty(max(_round_up(total, ALIGN), ALIGN), dtype=torch.float32) \
                 if self.transports[-1] == "host" else None
             self.plan.append((num_workers + k, groups, w, mail, stage))
+        self._ev: Dict[torch.device, torch.cuda.Event] = {}
         self._init_steps(num_ps)
 
     def zero_grad(self) -> None:
@@ -558,7 +598,11 @@ class DeviceAsyncPSClient(_ClientSteps):
             for g, start in groups:
                 dst[start:start + g.numel].copy_(g.grad)
             if stage is None:
-                torch.cuda.current_stream(mail.device).synchronize()  # mailbox written before the header
+                # the mailbox is written before the header: host wait on the copies' events only
+                for d in {mail.device, groups[0][0].grad.device}:
+                    ev = self._ev.setdefault(d, torch.cuda.Event())
+                    ev.record(torch.cuda.current_stream(d))
+                    ev.synchronize()
                 self._header(rank, PUSH_DEV, self.tags[k])
             else:
                 self._header(rank, PUSH, self.tags[k])

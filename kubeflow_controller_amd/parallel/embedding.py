@@ -9,9 +9,13 @@ the PS applies the optimizer (``:184, :256``).  MI355X design:
 * rows are interleaved over ``owners`` ranks (``owner = row % owners``) — with
   PS replicas present the owners are the ranks co-located with the PS tasks
   (SURVEY §7.3 H1 option a), otherwise every rank owns a slice;
-* **pull** = ``all_to_all`` of the requested ids to their owners, a HIP gather
-  of the fp32 master rows straight to bf16, and an ``all_to_all`` back;
-* **push** = ``all_to_all`` of the row gradients to the owners, then a
+* **pull** = each sender's DISTINCT ids (``torch.unique``: ~30 % of the looked-up
+  ids at the Criteo-like W&D shape) ``all_to_all``-ed to their owners as local
+  row numbers, a HIP gather of the fp32 master rows straight to bf16, an
+  ``all_to_all`` back, and an expansion to every lookup;
+* **push** = the lookups' gradients pre-summed per distinct id (fp32), one
+  ``all_to_all`` of those to the owners (``KFA_EMB_DEDUP=0``: every lookup's id
+  and gradient cross, as before), then a
   segment-reduce sparse Adam/SGD (``csrc/kernels/segsparse.hip``): the ids are
   radix-sorted, each row's gradients are summed in fp32 by one workgroup and
   the optimizer is applied once per unique row — no table-sized scratch and
@@ -76,47 +80,71 @@ class _LookupFn(torch.autograd.Function):
         ids = ids.reshape(-1)
         n, D = ids.numel(), emb.dim
         comm = emb.world > 1
+        inv = order = None
         if comm:
-            owner = ids % emb.owners
-            order = torch.argsort(owner, stable=True)
-            sorted_ids = ids.index_select(0, order)
+            # local row of each id on its owner; key = owner-major (owner, local row)
+            key = (ids % emb.owners) * emb.rows_per_owner + torch.div(ids, emb.owners, rounding_mode="floor")
+            if emb.dedup:   # each distinct id crosses the fabric once per sender, both ways
+                ukey, inv = torch.unique(key, sorted=True, return_inverse=True)
+                send_ids = ukey
+            else:
+                order = torch.argsort(key, stable=True)
+                send_ids = key.index_select(0, order)
+            owner_s = torch.div(send_ids, emb.rows_per_owner, rounding_mode="floor")
+            send_ids = send_ids - owner_s * emb.rows_per_owner
             if plan is not None:   # split sizes known on the host already: no device sync
                 send_l, recv_l = plan
             else:                  # derive them on the device (one D2H sync per lookup)
-                send = torch.bincount(owner, minlength=emb.world)
+                send = torch.bincount(owner_s, minlength=emb.world)
                 recv = torch.empty_like(send)
                 dist.all_to_all_single(recv, send, group=emb.pg)
                 send_l, recv_l = send.tolist(), recv.tolist()
-            req = torch.empty(sum(recv_l), dtype=ids.dtype, device=ids.device)
-            _a2a(req, sorted_ids, recv_l, send_l, emb.pg)
+            if sum(send_l) != send_ids.numel():
+                raise RuntimeError(f"ShardedEmbedding: plan sends {sum(send_l)} ids, lookup has {send_ids.numel()} "
+                                   f"({'unique ' if emb.dedup else ''}ids); plan and dedup setting disagree")
+            local = torch.empty(sum(recv_l), dtype=ids.dtype, device=ids.device)
+            _a2a(local, send_ids, recv_l, send_l, emb.pg)
         else:
-            order, send_l, recv_l, req = None, None, None, ids
-        local = torch.div(req, emb.owners, rounding_mode="floor") if emb.owners > 1 else req
+            send_l, recv_l = None, None
+            local = torch.div(ids, emb.owners, rounding_mode="floor") if emb.owners > 1 else ids
         # the id sort of the sparse update needs no gradient: start it now, beside the dense layers
         ctx.prep = emb.prepare_sparse(local) if ctx.needs_input_grad[1] else None
         rows = emb.gather(local)
         if comm:
-            out_sorted = torch.empty(n, D, dtype=rows.dtype, device=rows.device)
-            _a2a(out_sorted, rows, send_l, recv_l, emb.pg)
-            out = torch.empty_like(out_sorted)
-            out.index_copy_(0, order, out_sorted)
+            back = torch.empty(sum(send_l), D, dtype=rows.dtype, device=rows.device)
+            _a2a(back, rows, send_l, recv_l, emb.pg)
+            if inv is not None:
+                out = back.index_select(0, inv)
+            else:
+                out = torch.empty_like(back)
+                out.index_copy_(0, order, back)
+            isz = ids.element_size()
+            emb.exchange_bytes = {"lookups": n, "sent_ids": sum(send_l), "ids": sum(send_l) * isz,
+                                  "rows": sum(send_l) * D * rows.element_size(),
+                                  "grads": sum(send_l) * D * rows.element_size()}
         else:
             out = rows
         ctx.emb = emb
-        ctx.save_for_backward(local, order if order is not None else torch.empty(0, device=ids.device))
+        e = torch.empty(0, device=ids.device)
+        ctx.save_for_backward(local, order if order is not None else e, inv if inv is not None else e)
         ctx.splits = (send_l, recv_l)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        local, order = ctx.saved_tensors
+        local, order, inv = ctx.saved_tensors
         emb = ctx.emb
         send_l, recv_l = ctx.splits
         dout = dout.contiguous()
         if emb.world > 1:
-            d_sorted = dout.index_select(0, order)
+            if inv.numel():   # one pre-summed (fp32) gradient per distinct id of this sender
+                gu = torch.zeros(sum(send_l), emb.dim, dtype=torch.float32, device=dout.device)
+                gu.index_add_(0, inv, dout.float())
+                d_send = gu.to(dout.dtype)
+            else:
+                d_send = dout.index_select(0, order)
             g = torch.empty(local.numel(), emb.dim, dtype=dout.dtype, device=dout.device)
-            _a2a(g, d_sorted, recv_l, send_l, emb.pg)
+            _a2a(g, d_send, recv_l, send_l, emb.pg)
         else:
             g = dout
         emb.apply_sparse(local, g, prep=ctx.prep)
@@ -138,6 +166,10 @@ class ShardedEmbedding(nn.Module):
         self.owners = max(1, min(owners or self.world, self.world))
         self.num_rows, self.dim = num_rows, dim
         self.local_rows = len(range(self.rank, num_rows, self.owners)) if self.rank < self.owners else 0
+        self.rows_per_owner = -(-num_rows // self.owners)
+        # KFA_EMB_DEDUP=0: every looked-up id (duplicates included) crosses the all-to-alls
+        self.dedup = os.environ.get("KFA_EMB_DEDUP", "1") != "0"
+        self.exchange_bytes = {}  # last lookup's per-direction all-to-all volume (this rank's sends)
         self.optimizer, self.lr, self.betas, self.eps, self.wd = optimizer, lr, betas, eps, weight_decay
         self.grad_scale = 1.0 / self.world  # data-parallel mean, like the dense groups
         self.t = 0
@@ -293,7 +325,11 @@ class ShardedEmbedding(nn.Module):
         if self.world == 1:
             return None
         ids_cpu = ids_cpu.reshape(-1).cpu()
-        send = torch.bincount(ids_cpu % self.owners, minlength=self.world)
+        owner = ids_cpu % self.owners
+        if self.dedup:
+            owner = torch.unique(owner * self.rows_per_owner + torch.div(ids_cpu, self.owners, rounding_mode="floor"))
+            owner = torch.div(owner, self.rows_per_owner, rounding_mode="floor")
+        send = torch.bincount(owner, minlength=self.world)
         recv = torch.empty_like(send)
         dist.all_to_all_single(recv, send, group=self._meta_group())
         return send.tolist(), recv.tolist()

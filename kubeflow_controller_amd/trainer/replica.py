@@ -290,7 +290,7 @@ def run_worker_async(spec: ClusterSpec, args) -> int:
     if transport == "device":
         client = DeviceAsyncPSClient(list(model.named_parameters()), W, P, spec.task_index, store, log=_log)
         zero_grad = client.zero_grad
-        transport = "+".join(sorted(set(client.transports)))
+        transport = "; ".join(client.transport_desc)
     else:
         client = AsyncPSClient(list(model.named_parameters()), W, P)
         zero_grad = lambda: model.zero_grad(set_to_none=False)  # noqa: E731

@@ -336,3 +336,47 @@ def test_hung_replica_dumps_stacks_and_fails_job(node):
         out = _logs(root, p)
         assert "Timeout (0:00:06)!" in out and "most recent call first" in out, out[-3000:]
         assert p.status.containerStatuses[0].terminated.exitCode != 0
+
+
+def test_async_ps_workers_see_ps_gpus(tmp_path):
+    """The 4 workers + 2 PS device-resident async layout (bert-base-async-4w2ps.yml):
+    each worker's HIP_VISIBLE_DEVICES lists its own GPU first (its compute device,
+    cuda:0) and then the PS replicas' GPUs, so the PS buffers it maps by HIP IPC are
+    on GPUs it can see; KFA_GPUS names the physical GPU of every local ordinal."""
+    st = ObjectStore()
+    n = Node(st, kubelet=True, root_dir=str(tmp_path), num_gpus=8, resync=30).start()
+    try:
+        job = serde.load_file(os.path.join(ROOT, "examples", "tfjob", "bert-base-async-4w2ps.yml"), env=ENV)[0]
+        cmd = [sys.executable, "-c", "import os; print('HIP=' + os.environ['HIP_VISIBLE_DEVICES'] + ' KG=' + "
+               "os.environ['KFA_GPUS'] + ' PSG=' + os.environ.get('KFA_PS_GPUS', '-'))"]
+        for spec in job.spec.specs:
+            spec.template.spec.containers[0].command = cmd
+            spec.template.spec.containers[0].args = []
+        st.create(job)
+        wait_for_phase(st, "default", "bert-base-async-4w2ps", {"Succeeded"}, 60)
+        pods = st.list("Pod")
+        ps = {p.metadata.labels["index"]: p.status.gpus for p in pods if p.metadata.labels["job_type"] == "PS"}
+        assert ps == {"0": [0], "1": [1]}, ps
+        workers = [p for p in pods if p.metadata.labels["job_type"] == "Worker"]
+        assert len(workers) == 4
+        for p in workers:
+            own = p.status.gpus[0]
+            vis = [own] + [g for g in (0, 1) if g != own]
+            want = ",".join(map(str, vis))
+            out = _logs(str(tmp_path), p)
+            assert f"HIP={want} KG={want} PSG=0,1" in out, out
+    finally:
+        n.shutdown()
+
+
+def test_local_ordinal_of_ps_gpu(monkeypatch):
+    from kubeflow_controller_amd.parallel.async_ps import local_ordinal, physical_gpu
+    monkeypatch.setenv("KFA_GPUS", "5,0,1")
+    assert physical_gpu() == "5"
+    assert local_ordinal("1")[0] == 2 and local_ordinal("5")[0] == 0
+    dev, why = local_ordinal("3")
+    assert dev is None and "not visible" in why
+    assert local_ordinal("")[0] == 0
+    monkeypatch.delenv("KFA_GPUS")
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES", raising=False)
+    assert local_ordinal("4")[0] == 4

@@ -135,8 +135,9 @@ def test_ps_assignment():
     assert max(load) == 100 and min(load) == 75
 
 
-def _wd_worker(rank, world, port, owners, out):
+def _wd_worker(rank, world, port, owners, out, dedup="1"):
     sys.path.insert(0, ROOT)
+    os.environ["KFA_EMB_DEDUP"] = dedup
     import torch.distributed as dist
     from kubeflow_controller_amd.models.wide_deep import WideDeep, WideDeepConfig, synthetic_batch, wide_deep_loss
     from kubeflow_controller_amd.trainer.engine import DistInfo, Engine
@@ -161,20 +162,29 @@ def _wd_worker(rank, world, port, owners, out):
     if rank == 0:
         sd = {k: v.clone() for k, v in m.state_dict().items() if not k.startswith("tables.")}
         sd["table"] = table
+        sd["xbytes"] = torch.tensor([m.tables.exchange_bytes["lookups"], m.tables.exchange_bytes["sent_ids"],
+                                     m.tables.exchange_bytes["rows"]])
         torch.save(sd, out)
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("owners", [1, 2])
-def test_sharded_embedding_ps_matches_single_process(tmp_path, owners):
+@pytest.mark.parametrize("owners,dedup", [(1, "1"), (2, "1"), (2, "0")])
+def test_sharded_embedding_ps_matches_single_process(tmp_path, owners, dedup):
     """Wide&Deep with row-sharded tables (all-to-all pull/push, owner-side sparse
-    Adam) on 2 ranks == one process on the whole batch."""
+    Adam) on 2 ranks == one process on the whole batch — with the deduplicated
+    exchange (each sender's distinct ids and pre-summed gradients) and without."""
     from kubeflow_controller_amd.models.wide_deep import WideDeep, WideDeepConfig, synthetic_batch, wide_deep_loss
     from kubeflow_controller_amd.trainer.engine import Engine
     out = str(tmp_path / "wd.pt")
-    mp.start_processes(_wd_worker, args=(2, _free_port(), owners, out), nprocs=2, join=True, start_method="spawn")
+    mp.start_processes(_wd_worker, args=(2, _free_port(), owners, out, dedup), nprocs=2, join=True,
+                       start_method="spawn")
     got = torch.load(out, weights_only=True)
+    lookups, sent, row_bytes = got.pop("xbytes").tolist()
+    if dedup == "1":
+        assert sent < lookups, (sent, lookups)   # duplicates never cross the fabric
+    else:
+        assert sent == lookups
     cfg = WideDeepConfig.tiny()
     torch.manual_seed(0)
     m = WideDeep(cfg, device="cpu")
