@@ -9,10 +9,10 @@
 // to each other and one workgroup can sum them without atomics:
 //
 //   1. ids -> u32 keys + positions, radix-sorted on the low ``nbits`` bits
-//      (hipCUB; the table's row count bounds the key width);
+//      (radix_sort.h: own LSD passes; the table's row count bounds the key width);
 //   2. per 64-entry chunk of the sorted list: the last segment head in the chunk;
-//   3. exclusive max-scan over the chunks (hipCUB) -> start of the segment that
-//      spans each chunk's first entry;
+//   3. exclusive max-scan over the chunks (radix_sort.h) -> start of the segment
+//      that spans each chunk's first entry;
 //   4. per chunk: gather its 64 gradient rows (bf16, by position) into LDS, sum
 //      each segment in fp32 (segmented wave scan) and apply Adam / SGD to that row of the master table
 //      and its moments.  A segment that crosses a chunk edge (hot rows span many
@@ -25,7 +25,7 @@
 // same as the atomic path and ShardedEmbedding._apply_cpu).
 #include "common.h"
 
-#include <hipcub/hipcub.hpp>
+#include "radix_sort.h"
 
 namespace {
 
@@ -208,17 +208,6 @@ __global__ __launch_bounds__(256) void seg_fixup_kernel(const unsigned* __restri
 
 inline long align256(long x) { return (x + 255) & ~255L; }
 
-// hipCUB temp storage: the radix sort and the chunk max-scan run one after the other
-long temp_bytes(int n, int nbits) {
-  size_t sort = 0, scan = 0;
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sort, (const unsigned*)nullptr, (unsigned*)nullptr,
-                                           (const int*)nullptr, (int*)nullptr, n, 0, nbits, (hipStream_t)0);
-  const int nch = (n + CH - 1) / CH;
-  (void)hipcub::DeviceScan::ExclusiveScan(nullptr, scan, (const int*)nullptr, (int*)nullptr, hipcub::Max(), -1, nch,
-                                          (hipStream_t)0);
-  return (long)(sort > scan ? sort : scan);
-}
-
 }  // namespace
 
 KFA_API long kfa_seg_slot_floats(long n, int D) { return ((n + CH - 1) / CH) * (long)D; }
@@ -226,15 +215,14 @@ KFA_API long kfa_seg_slot_floats(long n, int D) { return ((n + CH - 1) / CH) * (
 // scratch bytes for kfa_seg_sparse_apply (the slot buffer is separate: it must stay zeroed)
 KFA_API long kfa_seg_ws_bytes(long n, int nbits) {
   const long nch = (n + CH - 1) / CH;
-  return 4 * align256(n * 4) + 2 * align256(nch * 4) + align256(temp_bytes((int)n, nbits));
+  (void)nbits;
+  return 4 * align256(n * 4) + 2 * align256(nch * 4) + kfa_radix::hist_bytes(n);
 }
 
 namespace {
 struct WsLayout {
   unsigned *keys_in, *keys;
-  int *pos_in, *pos, *lh, *segbeg;
-  void* temp;
-  size_t temp_bytes;
+  int *pos_in, *pos, *lh, *segbeg, *hist;
 };
 
 WsLayout layout(void* ws, long n, int nbits) {
@@ -247,8 +235,8 @@ WsLayout layout(void* ws, long n, int nbits) {
   L.pos = (int*)p;          p += align256(n * 4);
   L.lh = (int*)p;           p += align256(nch * 4);
   L.segbeg = (int*)p;       p += align256(nch * 4);
-  L.temp = p;
-  L.temp_bytes = (size_t)temp_bytes((int)n, nbits);
+  L.hist = (int*)p;
+  (void)nbits;
   return L;
 }
 
@@ -268,16 +256,16 @@ KFA_API int kfa_seg_prepare(const long* ids, long n, int nbits, void* ws, long w
   WsLayout L = layout(ws, n, nbits);
   const int gp = min(16384, (ni + 255) / 256);
   hipLaunchKernelGGL(seg_prep_kernel, dim3(gp), dim3(256), 0, s, ids, L.keys_in, L.pos_in, ni);
-  size_t tb = L.temp_bytes;
-  hipError_t e = hipcub::DeviceRadixSort::SortPairs(L.temp, tb, L.keys_in, L.keys, L.pos_in, L.pos, ni, 0, nbits, s);
-  if (e != hipSuccess) return (int)e;
+  int e = kfa_radix::sort_pairs(L.keys_in, L.pos_in, L.keys, L.pos, ni, nbits, L.hist, s);
+  if (e) return e;
   const int gh = min(16384, (nch + 3) / 4);
   hipLaunchKernelGGL(seg_heads_kernel, dim3(gh), dim3(256), 0, s, L.keys, L.lh, ni, nch);
   // segbeg[c] = last segment head before entry c*CH = start of the segment holding that
   // entry whenever it is not a head itself (the only case seg_apply_kernel reads it)
-  tb = L.temp_bytes;
-  e = hipcub::DeviceScan::ExclusiveScan(L.temp, tb, L.lh, L.segbeg, hipcub::Max(), -1, nch, s);
-  if (e != hipSuccess) return (int)e;
+  e = (int)hipMemcpyAsync(L.segbeg, L.lh, (size_t)nch * 4, hipMemcpyDeviceToDevice, s);
+  if (e) return e;
+  e = kfa_radix::scan_max_excl(L.segbeg, nch, -1, s);
+  if (e) return e;
   return kfa_status();
 }
 
@@ -315,4 +303,28 @@ KFA_API int kfa_seg_sparse_apply(const long* ids, const void* g, long n, int D, 
   const int rc = kfa_seg_prepare(ids, n, nbits, ws, ws_bytes, s);
   if (rc) return rc;
   return kfa_seg_apply(g, n, D, nbits, ws, ws_bytes, slots, w, m, v, opt, lr, b1, b2, eps, wd, c1, c2, gscale, s);
+}
+
+// Test / bench entry of the pair sort alone: sorts (keys, vals) of n entries on the
+// low nbits bits in place (stable); ws: kfa_radix_ws_bytes(n).
+KFA_API long kfa_radix_ws_bytes(long n) { return 2 * kfa_radix::align256(n * 4) + kfa_radix::hist_bytes(n); }
+
+KFA_API int kfa_radix_sort_pairs(unsigned* keys, int* vals, long n, int nbits, void* ws, long ws_bytes,
+                                 hipStream_t s) {
+  if (n <= 0) return 0;
+  if (n > 0x7fffffffL || nbits < 1 || nbits > 32 || ws_bytes < kfa_radix_ws_bytes(n)) return (int)hipErrorInvalidValue;
+  char* p = (char*)ws;
+  unsigned* k1 = (unsigned*)p;
+  int* v1 = (int*)(p + kfa_radix::align256(n * 4));
+  int* hist = (int*)(p + 2 * kfa_radix::align256(n * 4));
+  int e = kfa_radix::sort_pairs(keys, vals, k1, v1, (int)n, nbits, hist, s);
+  if (e) return e;
+  e = (int)hipMemcpyAsync(keys, k1, (size_t)n * 4, hipMemcpyDeviceToDevice, s);
+  if (!e) e = (int)hipMemcpyAsync(vals, v1, (size_t)n * 4, hipMemcpyDeviceToDevice, s);
+  return e;
+}
+
+// exclusive prefix max of a[0..n) in place from init (test entry of the chunk-head scan)
+KFA_API int kfa_scan_max_excl(int* a, long n, int init, hipStream_t s) {
+  return kfa_radix::scan_max_excl(a, (int)n, init, s);
 }

@@ -47,6 +47,9 @@ _lib.register("kfa_stem_wgrad_fold", [P, P, I, I, I, I, I, I, P])
 # Runtime switches (tests compare against the vendor path); env KFA_CONV_IGEMM=0 / KFA_WGRAD=0 disable.
 ENABLED = os.environ.get("KFA_CONV_IGEMM", "1") != "0"
 WGRAD_ENABLED = os.environ.get("KFA_WGRAD", "1") != "0"
+# KFA_CONV_WGRAD_SIDE=1: conv weight gradients on the side stream (ops/streams.py),
+# concurrent with the data-gradient chain (dgrad convs, BatchNorm backward passes)
+WGRAD_SIDE = os.environ.get("KFA_CONV_WGRAD_SIDE", "0") == "1"
 
 
 def igemm_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
@@ -485,7 +488,14 @@ class _ConvFn(torch.autograd.Function):
                 if addend is not None:
                     dx = dx + addend
         if ctx.needs_input_grad[1]:
-            dw = conv_wgrad(x, dy, w, ctx.stride, ctx.pad, ctx.wparam)
+            if WGRAD_SIDE and x.is_cuda:
+                from . import streams as _streams
+                dw = _streams.run_on_side(lambda: conv_wgrad(x, dy, w, ctx.stride, ctx.pad, ctx.wparam), x.device,
+                                          (x, dy, w))
+                if dw is not None:  # a returned gradient is consumed on the main stream
+                    torch.cuda.current_stream(x.device).wait_stream(_streams.side_stream(x.device))
+            else:
+                dw = conv_wgrad(x, dy, w, ctx.stride, ctx.pad, ctx.wparam)
         return dx, dw, None, None, None, None, None
 
 

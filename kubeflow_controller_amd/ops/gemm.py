@@ -34,6 +34,8 @@ _lib.register("kfa_gemm_pick_bn", [I, I])
 _lib.register("kfa_gemm_ppp", [P, P, P] + [I] * 9 + [P, _lib.L, I, P])
 _lib.register("kfa_gemm_ppp_ws_bytes", [I] * 5, restype=_lib.L)
 _lib.register("kfa_gemm_ppp_pick_bn", [I, I])
+_lib.register("kfa_gemm_skinny", [P, P, P, P] + [I] * 7 + [P, _lib.L, P])
+_lib.register("kfa_gemm_skinny_ws_bytes", [I] * 4, restype=_lib.L)
 
 ACTS = {None: 0, "none": 0, "gelu": 1, "tanh": 2, "relu": 3}
 # Which dense-layer GEMMs run on this kernel (KFA_GEMM):
@@ -174,6 +176,34 @@ def gemm_ppp(a, b, *, out=None, blocks: int = 0, probe: int = 0, bn: int = 0, sp
     return c
 
 
+def skinny_ok(a, b) -> bool:
+    """Operands :func:`gemm_skinny` takes: M <= 256, N % 4 == 0 (bf16, K-contiguous)."""
+    return (a.is_cuda and b.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16
+            and a.dim() == 2 and b.dim() == 2 and a.shape[1] == b.shape[1] and 0 < a.shape[0] <= 256
+            and a.shape[1] % 8 == 0 and b.shape[0] % 4 == 0 and a.stride(1) == 1 and b.stride(1) == 1
+            and a.stride(0) % 8 == 0 and b.stride(0) % 8 == 0 and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0
+            and b.shape[0] * b.stride(0) * 2 < (1 << 31))
+
+
+def gemm_skinny(a, b, bias=None, *, splits: int = 0, out=None):
+    """``a @ b.T (+ bias)`` (bf16 out, fp32 bias) for M <= 256 on the split-K skinny
+    kernel (``csrc/kernels/gemm_skinny.hip``): 256 x 64 output tiles, the reduction
+    cut into slices run by separate blocks, partials summed in slice order by the
+    last-arriving slice of each tile.  ``splits`` 0 = about one block per CU."""
+    if not skinny_ok(a, b):
+        raise ValueError(f"gemm_skinny: unsupported operands {tuple(a.shape)} x {tuple(b.shape)}")
+    M, K = a.shape
+    N = b.shape[0]
+    _check_vec(bias, N, "bias")
+    c = out if out is not None else torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
+    _check_mn(c, M, N, "out")
+    nb = _lib.lib().kfa_gemm_skinny_ws_bytes(M, N, K, int(splits))
+    ws = _lib.workspace(nb, a.device, f"skinny_ws{_lib.stream() or 0}") if nb > 0 else None
+    _lib.call("kfa_gemm_skinny", _lib.ptr(a), _lib.ptr(b), _lib.ptr(c), _lib.ptr(bias), M, N, K, a.stride(0),
+              b.stride(0), N, int(splits), _lib.ptr(ws), nb, _lib.stream())
+    return c
+
+
 def ppp_ok(a, b) -> bool:
     """Operands :func:`gemm_ppp` takes (plain ``a @ b.T``, bf16 out)."""
     return gemm_ok(a, b) and a.shape[1] % 64 == 0 and a.shape[1] >= 128
@@ -244,26 +274,50 @@ def mm_auto(a, w, kind: str = "proj"):
 
 
 def dgrad_auto(dz, w, kind: str = "proj_dgrad"):
-    """``dz @ w`` (the data gradient of ``y = x @ w.T``): the fastest persistent
-    MFMA GEMM variant on the transposed weight (transpose included in its timing)
-    where it beats hipBLASLt for this shape, else the library."""
+    """``dz @ w`` (the data gradient of ``y = x @ w.T``): the fastest own MFMA GEMM
+    on the transposed weight (the persistent kernel's variants; the split-K skinny
+    kernel for M <= 256) where it beats hipBLASLt for this shape, else the library.
+    Flat-buffer weights take their transpose from the step's batched transpose
+    cache (one launch per backward for every such weight, ``ops/conv.py``)."""
     M, K = dz.shape if dz.dim() == 2 else (0, 0)
     N = w.shape[1] if w.dim() == 2 else 0
     if (ROUTE_AUTO and dz.is_cuda and dz.dim() == 2 and w.dim() == 2 and dz.dtype == torch.bfloat16
             and w.dtype == torch.bfloat16 and dz.is_contiguous() and dz.data_ptr() % 16 == 0 and K == w.shape[0]
-            and K % 64 == 0 and K >= 128 and N % 8 == 0 and M > 0
+            and K % 8 == 0 and N % 8 == 0 and M > 0
             and max(M * N, M * K, N * K) * 2 < (1 << 31)):
         k = (kind, M, N, K)
         if _choice.get(k) == 0:
             return torch.mm(dz, w)
-        wt = transpose(w)
-        own = _ppp_candidates(dz, wt)
-        cands = [("hipblaslt", lambda: torch.mm(dz, w))] + [
-            (n, (lambda f: lambda: (transpose(w), f())[1])(f)) for n, f in own]
-        i = pick_fastest(kind, (M, N, K), dz.device, cands)
-        if i:
-            return own[i - 1][1]()
+        wt = transpose_cached(w)
+        own = []
+        if K % 64 == 0 and K >= 128:
+            own += _ppp_candidates(dz, wt)
+        if skinny_ok(dz, wt):
+            own.append(("skinny", lambda: gemm_skinny(dz, wt)))
+        if own:
+            cands = [("hipblaslt", lambda: torch.mm(dz, w))] + own
+            i = pick_fastest(kind, (M, N, K), dz.device, cands)
+            if i:
+                return own[i - 1][1]()
     return torch.mm(dz, w)
+
+
+def transpose_cached(w: torch.Tensor) -> torch.Tensor:
+    """``w.T`` contiguous: from the per-step batched transpose cache for a flat-buffer
+    (optimizer-updated) weight, else a fresh :func:`transpose`."""
+    if getattr(w, "_kfa_flat", False) and w.is_contiguous():
+        from .conv import _tcache, BATCHED_TRANSPOSE
+        if BATCHED_TRANSPOSE:
+            R, C = w.shape
+            return _tcache.get(w.view(R, C, 1, 1), 0, 1, 1, 0, 1, 1).view(C, R)
+    return transpose(w)
+
+
+def mark_weights_stale() -> None:
+    """The weights may have changed since the last backward (a forward is running):
+    the cached transposes are refreshed at the next backward's first dgrad."""
+    from .conv import _tcache
+    _tcache.mark_stale()
 
 
 def transpose(w: torch.Tensor) -> torch.Tensor:

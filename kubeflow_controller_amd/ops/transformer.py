@@ -256,34 +256,44 @@ class DenseFn(torch.autograd.Function):
         fusable = p == 0 and _gemm.gemm_ok(x2, weight) and (
             bias is None or (bias.dtype == torch.float32 and bias.is_contiguous() and bias.data_ptr() % 16 == 0))
         fused = fusable and (_gemm.ROUTE_LAYERS or (_gemm.ROUTE_FUSED and has_act))
+        _gemm.mark_weights_stale()  # the dgrad's cached weight transposes refresh at the next backward
         mm = None  # plain GEMM of the unfused path (None: hipBLASLt)
+        skinny = False  # the split-K skinny GEMM with the bias fused (M <= 256, e.g. the ResNet FC)
         if fusable and _gemm.ROUTE_AUTO:
             # per shape, the fastest of: hipBLASLt + one bias/act pass, the MFMA GEMM with
-            # the bias/act epilogue fused, the persistent MFMA GEMM + the bias/act pass
+            # the bias/act epilogue fused, the persistent MFMA GEMM + the bias/act pass,
+            # the skinny split-K GEMM with the bias fused (+ the act pass)
             ba = (lambda zz: bias_act_fwd(zz, bias, act) if (bias is not None or has_act) else zz)  # noqa: E731
+            act_only = (lambda zz: bias_act_fwd(zz, None, act) if has_act else zz)  # noqa: E731
             own_pp = _gemm._ppp_candidates(x2, weight) if _gemm.ppp_ok(x2, weight) else []
             cands = ([("hipblaslt", lambda: ba(torch.mm(x2, weight.t()))),
                       ("gemm_nt-fused", lambda: _gemm.gemm_nt(x2, weight, bias=bias, act=act, want_z=has_act))]
                      + [(n, (lambda f: lambda: ba(f()))(f)) for n, f in own_pp])
+            if _gemm.skinny_ok(x2, weight):
+                cands.append(("skinny-bias", lambda: act_only(_gemm.gemm_skinny(x2, weight, bias))))
             i = _gemm.pick_fastest("dense_fwd", (x2.shape[0], weight.shape[0], x2.shape[1], act, bias is not None),
                                    x2.device, cands)
             fused = i == 1
-            mm = own_pp[i - 2][1] if i >= 2 else None
+            skinny = cands[i][0] == "skinny-bias"
+            mm = own_pp[i - 2][1] if 2 <= i < 2 + len(own_pp) else None
         if fused:
             y, z = _gemm.gemm_nt(x2, weight, bias=bias, act=act, want_z=has_act)  # z includes the bias
+        elif skinny:
+            z = _gemm.gemm_skinny(x2, weight, bias)  # z includes the bias
+            y = bias_act_fwd(z, None, act, p, seed) if (has_act or p > 0) else z
         else:
             z = mm() if mm is not None else torch.mm(x2, weight.t())
             y = bias_act_fwd(z, bias, act, p, seed) if (bias is not None or has_act or p > 0) else z
         ctx.save_for_backward(x2, weight, z if has_act else None)
         ctx.bias = bias
-        ctx.cfg = (act, p, seed, shp, fused)
+        ctx.cfg = (act, p, seed, shp, fused, fused or skinny)
         return y.view(*shp[:-1], weight.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
         x2, weight, z = ctx.saved_tensors
         bias = ctx.bias
-        act, p, seed, shp, fused = ctx.cfg
+        act, p, seed, shp, fused, z_has_bias = ctx.cfg
         has_act = act not in (None, "none")
         dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
         gb = db = None
@@ -291,7 +301,7 @@ class DenseFn(torch.autograd.Function):
             gb, _, db = _grad_target(bias)
         if has_act or p > 0 or bias is not None:
             # fused forward: z already holds the bias, so act' is evaluated at z itself
-            dz = bias_act_bwd(dy2, z, None if fused else bias, act, gb, p, seed, want_dx=(has_act or p > 0))
+            dz = bias_act_bwd(dy2, z, None if z_has_bias else bias, act, gb, p, seed, want_dx=(has_act or p > 0))
             dz = dy2 if dz is None else dz
         else:
             dz = dy2
@@ -467,6 +477,7 @@ class EncoderLayerFn(torch.autograd.Function):
         # the backward) and of its output (taken from by the backward)
         B, S, heads, ph, pa, seed, eps = cfg[:7]
         ctx.joins = (tuple(cfg[7:9]) + (None, None))[:2]
+        _gemm.mark_weights_stale()  # the dgrad's cached weight transposes refresh at the next backward
         T, H = x.shape
         d = H // heads
         qscale = 1.0 / math.sqrt(d)

@@ -76,7 +76,10 @@ def _arm_watchdog(args) -> None:
     # re-arming costs ~0.1 ms (a timer thread restart): at most 8 times per timeout period
     if t > 0 and now - _armed_at[0] >= t / 8:
         import faulthandler
-        faulthandler.dump_traceback_later(t, exit=True)
+        try:
+            faulthandler.dump_traceback_later(t, exit=True)
+        except (ValueError, OSError, RuntimeError, AttributeError):  # stderr without a file descriptor (in-process)
+            return
         _armed_at[0] = now
 
 
@@ -90,11 +93,11 @@ def _install_stack_dumps() -> None:
     """SIGTERM (the supervisor stopping a replica) and SIGUSR1 print all stacks first."""
     import faulthandler
     import signal
-    faulthandler.enable()
     try:
+        faulthandler.enable()
         faulthandler.register(signal.SIGUSR1, all_threads=True)
         faulthandler.register(signal.SIGTERM, all_threads=True, chain=True)
-    except (AttributeError, ValueError, RuntimeError):  # not the main thread / platform without it
+    except (AttributeError, ValueError, RuntimeError, OSError):  # in-process caller without a real stderr fd
         pass
 
 
@@ -290,7 +293,7 @@ def run_worker_async(spec: ClusterSpec, args) -> int:
     if transport == "device":
         client = DeviceAsyncPSClient(list(model.named_parameters()), W, P, spec.task_index, store, log=_log)
         zero_grad = client.zero_grad
-        transport = "; ".join(client.transport_desc)
+        transport = "+".join(sorted(set(client.transports))) + " transport; " + "; ".join(client.transport_desc)
     else:
         client = AsyncPSClient(list(model.named_parameters()), W, P)
         zero_grad = lambda: model.zero_grad(set_to_none=False)  # noqa: E731
@@ -298,7 +301,7 @@ def run_worker_async(spec: ClusterSpec, args) -> int:
     _log(f"Worker {spec.task_index}: {W} workers, {P} ps, device {device}, model {args.model}, "
          f"{sum(p.numel() for p in model.parameters())} params, "
          f"{'sync replicas (%d of %d aggregated)' % (agg, W) if agg else 'async'} parameter server "
-         f"({transport} transport)")
+         f"({transport if transport.endswith(')') else transport + ' transport'})")
     fixed = None if data is not None else synthetic_batch(args, model, device, spec.task_index)
     t_begin = time.time()
     _log(f"Training begins @ {t_begin:f}")

@@ -143,3 +143,47 @@ def test_gemm_ppp_split_under_cu_hog():
     for r, o, s in zip(ref, out, shapes):
         assert torch.equal(r, o), f"split GEMM {s} under load differs from the unloaded run"
     assert finished_under_hog, "split GEMMs waited for the hog kernel to release its CUs"
+
+
+@pytest.mark.parametrize("M,N,K,splits,bias", [
+    (256, 1000, 2048, 0, True),    # ResNet-50 FC forward (bias fused)
+    (256, 2048, 1000, 0, False),   # its data gradient: K = 1000, a partial last k-step
+    (256, 1000, 2048, 1, True),    # one slice: no partial exchange
+    (100, 64, 520, 3, False),      # M < 256, uneven slices, k tail
+    (256, 4, 8, 0, True),          # tiny
+    (200, 1024, 4096, 16, False),  # many slices
+])
+def test_gemm_skinny_matches_fp32(M, N, K, splits, bias):
+    """Split-K skinny GEMM (csrc/kernels/gemm_skinny.hip): partials of K slices summed by
+    the last-arriving slice in slice order (bit-identical run to run), bias fused."""
+    from kubeflow_controller_amd.ops import gemm as G
+    torch.manual_seed(M + N + K)
+    a, b = _bf(M, K), _bf(N, K, s=0.05)
+    bv = torch.randn(N, device=D) if bias else None
+    ref = a.float() @ b.float().t() + (bv if bias else 0)
+    c1 = G.gemm_skinny(a, b, bv, splits=splits)
+    c2 = G.gemm_skinny(a, b, bv, splits=splits)
+    _close(c1, ref, 1e-2, f"skinny {M}x{N}x{K} s={splits}")
+    assert torch.equal(c1, c2)
+
+
+def test_dense_layer_small_batch_routes_own():
+    """The ResNet-50 FC shape through Linear: the per-shape tuner times the skinny
+    kernel against hipBLASLt; forward and both gradients match fp32 either way."""
+    from kubeflow_controller_amd.ops.linear import Linear
+    torch.manual_seed(0)
+    lin = Linear(2048, 1000).cuda()
+    x = torch.randn(256, 2048, device=D).to(torch.bfloat16).requires_grad_()
+    w = lin.weight.detach().to(torch.bfloat16)
+    lin.weight.data = w
+    y = lin(x)
+    g = torch.randn_like(y)
+    y.backward(g)
+    xr = x.detach().float().requires_grad_()
+    wr = w.float().requires_grad_()
+    br = lin.bias.detach().float().requires_grad_()
+    yr = xr @ wr.t() + br
+    yr.backward(g.float())
+    _close(y, yr, 2e-2, "fc fwd")
+    _close(x.grad, xr.grad, 2e-2, "fc dgrad")
+    _close(lin.bias.grad, br.grad, 2e-2, "fc dbias")

@@ -62,3 +62,42 @@ def test_segment_slots_are_left_zero():
     torch.cuda.synchronize()
     slots = _lib.workspace(0, emb.weight.device, f"seg_sparse_slots{id(emb)}")
     assert int(torch.count_nonzero(slots)) == 0
+
+
+@pytest.mark.parametrize("n,nbits", [(1, 5), (1000, 3), (8192, 9), (8193, 17), (100003, 25), (1_700_000, 25),
+                                     (300000, 32)])
+def test_own_radix_sort_pairs_matches_stable_sort(n, nbits):
+    """csrc/kernels/radix_sort.h (the id sort of the segment-reduce update, replacing
+    hipCUB): keys and carried values equal a stable sort on the low nbits bits."""
+    from kubeflow_controller_amd.ops import _lib
+    _lib.register("kfa_radix_ws_bytes", [_lib.L], restype=_lib.L)
+    _lib.register("kfa_radix_sort_pairs", [_lib.P, _lib.P, _lib.L, _lib.I, _lib.P, _lib.L, _lib.P])
+    g = torch.Generator().manual_seed(n + nbits)
+    hi = 1 << min(nbits, 31)
+    keys = torch.randint(0, hi, (n,), generator=g, dtype=torch.int64)
+    keys[: n // 3] = keys[: n // 3] % 97   # many duplicates: stability matters
+    if nbits == 32:
+        keys = keys * 2 + 1                 # use the top bit too
+    k32 = keys.to(torch.int64).bitwise_and(0xFFFFFFFF)
+    ref_k, ref_i = torch.sort(k32, stable=True)
+    kd = k32.to(torch.int32).cuda()  # bit pattern of the u32 keys
+    vd = torch.arange(n, dtype=torch.int32, device="cuda")
+    ws = torch.empty(_lib.lib().kfa_radix_ws_bytes(n), dtype=torch.uint8, device="cuda")
+    _lib.call("kfa_radix_sort_pairs", kd.data_ptr(), vd.data_ptr(), n, nbits, ws.data_ptr(), ws.numel(),
+              _lib.stream())
+    got_k = kd.cpu().to(torch.int64).bitwise_and(0xFFFFFFFF)
+    assert torch.equal(got_k, ref_k)
+    assert torch.equal(vd.cpu().to(torch.int64), ref_i)
+
+
+@pytest.mark.parametrize("n", [1, 63, 1024, 1025, 26561, 300000])
+def test_scan_max_exclusive(n):
+    from kubeflow_controller_amd.ops import _lib
+    _lib.register("kfa_scan_max_excl", [_lib.P, _lib.L, _lib.I, _lib.P])
+    g = torch.Generator().manual_seed(n)
+    a = torch.randint(-1, 1 << 20, (n,), generator=g, dtype=torch.int32)
+    a[torch.rand(n, generator=g) < 0.5] = -1
+    ref = torch.cummax(torch.cat([torch.tensor([-1], dtype=torch.int32), a[:-1]]), 0).values
+    d = a.cuda()
+    _lib.call("kfa_scan_max_excl", d.data_ptr(), n, -1, _lib.stream())
+    assert torch.equal(d.cpu(), ref)

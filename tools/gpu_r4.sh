@@ -1,0 +1,40 @@
+#!/bin/bash
+# Round-4 GPU session: GPU tests, the headline bench, BERT-base / Wide&Deep benches
+# (per-shape GEMM tuner log), a Wide&Deep kernel trace, an env A/B, PMC passes.
+# Each GPU step has its own time limit; the chain stops at the first failure.
+#   gpurun --timeout 1200 -- bash tools/gpu_r4.sh [steps...]   (default: all)
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R"; mkdir -p gpurun_out
+steps=${*:-"tests bench bert wd ab pmc"}
+log() { echo "== $(date +%T) $*" | tee -a gpurun_out/r4_session.log; }
+for s in $steps; do
+  case $s in
+    tests)
+      log "pytest -m gpu"
+      timeout -k 10 420 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+        > gpurun_out/gpu_tests.log 2>&1 || { tail -40 gpurun_out/gpu_tests.log; exit 1; }
+      tail -3 gpurun_out/gpu_tests.log ;;
+    bench)
+      log "bench 1 GPU"
+      timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > gpurun_out/bench1.log 2> gpurun_out/bench1.err \
+        || { tail -30 gpurun_out/bench1.err; exit 1; }
+      tail -1 gpurun_out/bench1.log ;;
+    bert)
+      log "BERT-base 256x128"
+      KFA_GEMM_TUNE_LOG=1 timeout -k 10 300 python -u tools/bench_model.py --model bert_base --batch 256 --seq 128 \
+        --steps 20 --warmup 5 > gpurun_out/bert.log 2> gpurun_out/bert.err || { tail -30 gpurun_out/bert.err; exit 1; }
+      tail -1 gpurun_out/bert.log; grep "kfa gemm tune" gpurun_out/bert.err | head -20 ;;
+    wd)
+      log "Wide&Deep kernel trace"
+      KFA_GEMM_TUNE_LOG=1 bash tools/gpu_prof_wd.sh 2> gpurun_out/wd_tune.err || exit 1 ;;
+    ab)
+      log "A/B conv wgrad side stream"
+      bash tools/gpu_ab_env.sh "KFA_CONV_WGRAD_SIDE=0" "KFA_CONV_WGRAD_SIDE=1 KFA_CONV_OVERSUB=2" || exit 1 ;;
+    pmc)
+      log "PMC round-3 kernels"
+      bash tools/gpu_pmc_r4.sh > gpurun_out/pmc_r4.log 2>&1 || { tail -20 gpurun_out/pmc_r4.log; exit 1; }
+      head -60 gpurun_out/pmc_r4/table.txt ;;
+  esac
+done
+log done
