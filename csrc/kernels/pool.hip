@@ -283,6 +283,128 @@ __global__ __launch_bounds__(256) void maxpool3s2_bwd(const bf16_t* __restrict__
   *reinterpret_cast<uint4*>(dx + (long)v * 8) = pack8(acc);
 }
 
+// Same gradient, one thread per 2 x 2 block of input pixels x 8 channels: input rows
+// 2t-p, 2t-p+1 are covered by exactly the windows t-1, t (columns likewise), so the
+// block's four outputs share ONE set of 4 window loads (dy + argmax bytes) instead
+// of 4 each — a quarter of the gathers and index math of maxpool3s2_bwd.
+// STATS (C == 64 only): the pool gradient feeds a BatchNorm + ReLU backward (the
+// ResNet stem): also accumulate that BN's backward statistics sum(dz) and
+// sum(dz * (x - mean)), dz = the written (bf16) gradient where relu(fma(x, scale,
+// shift)) > 0, into the BN slots ([64 slots][2][C], slot = block % 64) — the
+// statistics pass over the 4x-pooled-size gradient and x is then skipped
+// (kfa_bn_bwd_prestats).  Lanes with the same 8-channel group (lane % 8) reduce
+// by butterfly; lane L then adds channel 8 (L % 8) + L / 8: one 64-lane atomic
+// per statistic per wave.
+struct PoolBnStats {
+  const bf16_t* x;
+  const float* ss;    // the BN forward's [scale | shift]
+  const float* mean;
+  float* slots;
+};
+
+template <bool STATS>
+__global__ __launch_bounds__(256) void maxpool3s2_bwd4(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ idx,
+                                                       bf16_t* __restrict__ dx, int N, int H, int W, int C, int Ho,
+                                                       int Wo, int p, int T, int U, PoolBnStats bs) {
+  const unsigned cv = C / 8;
+  const unsigned total = (unsigned)N * T * U * cv;
+  const unsigned v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (!STATS && v >= total) return;
+  const bool live = v < total;  // STATS: every lane takes part in the butterfly
+  float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float mu[8], sc[8], sf[8];
+  const int cg = (int)(v % cv);
+  if (STATS)
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      mu[j] = bs.mean[cg * 8 + j];
+      sc[j] = bs.ss[cg * 8 + j];
+      sf[j] = bs.ss[C + cg * 8 + j];
+    }
+  unsigned q = v / cv;
+  const int u = (int)(q % (unsigned)U);
+  q /= (unsigned)U;
+  const int t = (int)(q % (unsigned)T);
+  const int n = (int)(q / (unsigned)T);
+  uint4 g[4];
+  uint2 pk[4];
+  bool ok[4];
+#pragma unroll
+  for (int b = 0; b < 2; b++)    // window row t - 1 + b
+#pragma unroll
+    for (int e = 0; e < 2; e++) {  // window column u - 1 + e
+      const int oh = t - 1 + b, ow = u - 1 + e, w = b * 2 + e;
+      ok[w] = live && oh >= 0 && oh < Ho && ow >= 0 && ow < Wo;
+      const long o = (((long)n * Ho + min(max(oh, 0), Ho - 1)) * Wo + min(max(ow, 0), Wo - 1)) * C + cg * 8;
+      g[w] = *reinterpret_cast<const uint4*>(dy + o);
+      pk[w] = *reinterpret_cast<const uint2*>(idx + o);
+    }
+#pragma unroll
+  for (int a = 0; a < 2; a++)      // input row 2t - p + a
+#pragma unroll
+    for (int c = 0; c < 2; c++) {  // input column 2u - p + c
+      const int ih = 2 * t - p + a, iw = 2 * u - p + c;
+      if (!live || ih < 0 || ih >= H || iw < 0 || iw >= W) continue;
+      float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+      for (int b = 0; b < 2; b++)
+#pragma unroll
+        for (int e = 0; e < 2; e++) {
+          const int kh = a + 2 - 2 * b, kw = c + 2 - 2 * e;  // tap of (ih, iw) in window (t-1+b, u-1+e)
+          const int w = b * 2 + e;
+          if (kh > 2 || kw > 2 || !ok[w]) continue;
+          const int pos = kh * 3 + kw;
+          float f[8];
+          unpack8(g[w], f);
+          const uint32_t qq[2] = {pk[w].x, pk[w].y};
+#pragma unroll
+          for (int j = 0; j < 8; j++)
+            if ((int)((qq[j >> 2] >> ((j & 3) * 8)) & 0xff) == pos) acc[j] += f[j];
+        }
+      const long o = (((long)n * H + ih) * W + iw) * C + cg * 8;
+      const uint4 packed = pack8(acc);
+      *reinterpret_cast<uint4*>(dx + o) = packed;
+      if (STATS) {
+        float dz[8], xf[8];
+        unpack8(packed, dz);  // the bf16 values the BN backward apply will read
+        unpack8(*reinterpret_cast<const uint4*>(bs.x + o), xf);
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+          const float d = fmaf(xf[j], sc[j], sf[j]) > 0.f ? dz[j] : 0.f;
+          s1[j] += d;
+          s2[j] += d * (xf[j] - mu[j]);
+        }
+      }
+    }
+  if (STATS) {
+#pragma unroll
+    for (int o = 8; o < 64; o <<= 1)
+#pragma unroll
+      for (int j = 0; j < 8; j++) { s1[j] += __shfl_xor(s1[j], o, 64); s2[j] += __shfl_xor(s2[j], o, 64); }
+    const int lane = threadIdx.x & 63, jj = lane >> 3;
+    float a1 = s1[0], a2 = s2[0];
+#pragma unroll
+    for (int j = 1; j < 8; j++) {
+      a1 = jj == j ? s1[j] : a1;
+      a2 = jj == j ? s2[j] : a2;
+    }
+    const int ch = (lane & 7) * 8 + jj;
+    float* slot = bs.slots + (long)(blockIdx.x % 64) * 2 * C;
+    __hip_atomic_fetch_add(slot + ch, a1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(slot + C + ch, a2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// KFA_POOL_BWD4=0: one thread per input pixel (maxpool3s2_bwd) instead of per 2 x 2 block
+bool pool_bwd4() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("KFA_POOL_BWD4");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+
 int grid_for(long work) {
   long b = (work + 255) / 256;
   return (int)(b < (1L << 20) ? (b < 1 ? 1 : b) : (1L << 20));
@@ -323,7 +445,12 @@ KFA_API int kfa_maxpool_bwd(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, in
                             int Wo, int k, int s, int p, hipStream_t st) {
   if (C % 8 || k > 15) return -1;
   const long work = (long)N * H * W * (C / 8);
-  if (k == 3 && s == 2 && p <= 1 && work < (1L << 31))
+  const int T = (H + p + 1) / 2, U = (W + p + 1) / 2;
+  const long work4 = (long)N * T * U * (C / 8);
+  if (k == 3 && s == 2 && p <= 1 && pool_bwd4() && work4 < (1L << 31))
+    hipLaunchKernelGGL(maxpool3s2_bwd4<false>, dim3((unsigned)((work4 + 255) / 256)), dim3(256), 0, st, dy, idx, dx, N,
+                       H, W, C, Ho, Wo, p, T, U, PoolBnStats{nullptr, nullptr, nullptr, nullptr});
+  else if (k == 3 && s == 2 && p <= 1 && work < (1L << 31))
     hipLaunchKernelGGL(maxpool3s2_bwd, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, st, dy, idx, dx, N, H, W, C,
                        Ho, Wo, p);
   else if (work < (1L << 31))
@@ -332,6 +459,20 @@ KFA_API int kfa_maxpool_bwd(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, in
   else
     hipLaunchKernelGGL(maxpool_bwd<long>, dim3(grid_for(work)), dim3(256), 0, st, dy, idx, dx, N, H, W, C, Ho, Wo, k,
                        s, p);
+  return kfa_status();
+}
+
+// 3x3/s2 max-pool gradient of maxpool(relu(bn(x))) with that BN's backward
+// statistics accumulated into `slots` (see maxpool3s2_bwd4<true>); C == 64.
+// Then kfa_bn_bwd_prestats finishes the BN backward.
+KFA_API int kfa_maxpool_bwd_bnstats(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, int H, int W, int C,
+                                    int Ho, int Wo, int p, const bf16_t* x, const float* ss, const float* mean,
+                                    float* slots, hipStream_t st) {
+  const int T = (H + p + 1) / 2, U = (W + p + 1) / 2;
+  const long work4 = (long)N * T * U * (C / 8);
+  if (C != 64 || p > 1 || work4 >= (1L << 31) || !x || !ss || !mean || !slots) return -1;
+  hipLaunchKernelGGL(maxpool3s2_bwd4<true>, dim3((unsigned)((work4 + 255) / 256)), dim3(256), 0, st, dy, idx, dx, N, H,
+                     W, C, Ho, Wo, p, T, U, PoolBnStats{x, ss, mean, slots});
   return kfa_status();
 }
 

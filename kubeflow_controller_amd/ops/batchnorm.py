@@ -309,6 +309,10 @@ def bn_act_dual(bn: "BatchNorm2dAct", x: torch.Tensor, bn_r: "BatchNorm2dAct", r
 
 _lib.register("kfa_maxpool_fwd_bn", [_lib.P, _lib.P, _lib.P] + [_lib.I] * 9 + [_lib.P, _lib.P])
 _lib.register("kfa_maxpool_bwd", [_lib.P, _lib.P, _lib.P] + [_lib.I] * 9 + [_lib.P])
+_lib.register("kfa_maxpool_bwd_bnstats", [_lib.P, _lib.P, _lib.P] + [_lib.I] * 7 + [_lib.P] * 5)
+# KFA_POOL_BN_STATS=0: the stem BN's backward statistics in their own pass instead of
+# accumulated by the pool-gradient kernel (64-channel stems)
+POOL_BN_STATS = os.environ.get("KFA_POOL_BN_STATS", "1") != "0"
 
 
 class _BNReluPoolFn(torch.autograd.Function):
@@ -350,14 +354,22 @@ class _BNReluPoolFn(torch.autograd.Function):
         st = _lib.stream()
         dy = dy.contiguous(memory_format=torch.channels_last)
         dbn = torch.empty_like(x)
-        _lib.call("kfa_maxpool_bwd", _lib.ptr(dy), _lib.ptr(idx), _lib.ptr(dbn), N, H, W, C, Ho, Wo, k, s, p, st)
         w, b = ctx.params
         dg, db, direct = _param_grads(w, b, C, dev)
         slots, coef = _workspaces(C, dev)
         dx = torch.empty_like(x)
-        _lib.call("kfa_bn_bwd", _lib.ptr(dbn), _lib.ptr(x), None, _lib.ptr(weight), _lib.ptr(mean), _lib.ptr(invstd),
-                  _lib.ptr(dx), None, _lib.ptr(dg), _lib.ptr(db), _lib.ptr(slots), _lib.ptr(coef), N * H * W, C, 1,
-                  int(direct), _lib.ptr(ss), None, st)
+        if POOL_BN_STATS and C == 64 and k == 3 and s == 2:
+            # pool gradient + the BN's backward statistics in one pass, then finalize + apply
+            _lib.call("kfa_maxpool_bwd_bnstats", _lib.ptr(dy), _lib.ptr(idx), _lib.ptr(dbn), N, H, W, C, Ho, Wo, p,
+                      _lib.ptr(x), _lib.ptr(ss), _lib.ptr(mean), _lib.ptr(slots), st)
+            _lib.call("kfa_bn_bwd_prestats", _lib.ptr(dbn), _lib.ptr(x), None, _lib.ptr(weight), _lib.ptr(mean),
+                      _lib.ptr(invstd), _lib.ptr(dx), None, _lib.ptr(dg), _lib.ptr(db), _lib.ptr(slots),
+                      _lib.ptr(coef), N * H * W, C, 1, int(direct), _lib.ptr(ss), None, st)
+        else:
+            _lib.call("kfa_maxpool_bwd", _lib.ptr(dy), _lib.ptr(idx), _lib.ptr(dbn), N, H, W, C, Ho, Wo, k, s, p, st)
+            _lib.call("kfa_bn_bwd", _lib.ptr(dbn), _lib.ptr(x), None, _lib.ptr(weight), _lib.ptr(mean),
+                      _lib.ptr(invstd), _lib.ptr(dx), None, _lib.ptr(dg), _lib.ptr(db), _lib.ptr(slots),
+                      _lib.ptr(coef), N * H * W, C, 1, int(direct), _lib.ptr(ss), None, st)
         if direct:
             notify_grad_ready(w)
             notify_grad_ready(b)

@@ -145,6 +145,8 @@ def _use_vendor_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, sta
 
 
 NARROW = int(os.environ.get("KFA_CONV_NARROW", "1"))  # tile variant for N <= 64: 1 = 128x64, 3 = 256x64
+# ... for N <= 64 with a long reduction (K >= 512: the 3x3 64-channel convs, fwd and dgrad)
+NARROW_LONGK = int(os.environ.get("KFA_CONV_NARROW_LONGK", str(NARROW)))
 
 
 # 256x256 tiles where they win per shape (tools/bench_conv_tiles.py, bs 256): the
@@ -159,7 +161,7 @@ BIG_AUTO_E = os.environ.get("KFA_CONV_BIG_AUTO_E", "1") != "0"  # also for launc
 def _variant(M: int, N: int, K: int = 0, addend: bool = False) -> int:
     """Tile shape of one implicit-GEMM launch: M output pixels x N channels, reduction K."""
     if N <= 64:
-        return NARROW
+        return NARROW_LONGK if K >= 512 else NARROW
     if BIG and N % 256 == 0 and K >= BIG_MIN_K:
         return 2
     if BIG_AUTO and (BIG_AUTO_E or not addend) and N % 256 == 0 and 0 < K <= 128 and M >= 200704:
