@@ -583,6 +583,300 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail's zero-fill DMAs land before the LDS is released
 }
 
+// ---------------------------------------------------------------------------
+// gemm_ppw_kernel: the same persistent ping-pong pipeline (256 x 256 tiles, four
+// phases per 64-deep k-tile, the previous tile's C written during the next tile's
+// first k-tile) with the roles of the two wave groups SPECIALISED so that no C
+// store ever sits in the in-order vmcnt window of an LDS-DMA retire:
+//
+// * group 0 (waves 0-3) issues EVERY LDS-DMA piece (4 DMAs per 16 KB piece per
+//   wave) and waits only on those (fixed vmcnt(16): the pieces of the last four
+//   phases).  At a tile boundary it hands its C quadrant to group 1 through a
+//   32 KB LDS hand-off area (two 16 KB halves by phase parity; inline-asm
+//   ds_write_b128, so hipcc adds no vmcnt(0) for the DMAs in flight) instead of
+//   storing it;
+// * group 1 (waves 4-7) issues no DMA and never waits on vmcnt: at a boundary
+//   phase it stores its own quadrant from its accumulators AND its partner's
+//   from the hand-off area (inline-asm ds_read_b128 + counted lgkmcnt).
+//
+// gemm_ppp_kernel's stores share the counter with the DMAs, so when all CUs cross
+// a tile boundary together (equal work per CU) the 32 MB C burst stalls every
+// DMA retire behind it (profiles/r3_gemm_ppp.txt); here the burst drains from
+// group 1's counter while group 0's pipeline keeps running.  LDS: 128 KB ring +
+// 32 KB hand-off = the CU's whole 160 KB.  No split remainder (data-parallel tiles).
+constexpr int HANDOFF = 16384;  // bytes per hand-off half: 4 waves x 64 rows x 32 cols x bf16
+
+template <bool NT>
+__global__ __launch_bounds__(512, 1) void gemm_ppw_kernel(PppArgs g) {
+  constexpr int BN = 256, WN = 64, TM = 8, TN = 4, NB1 = 2;
+  constexpr int DW = 4;  // DMAs per piece per group-0 wave
+  __shared__ __attribute__((aligned(16))) char smem[2 * 4 * PIECE + 2 * HANDOFF];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const bool loader = wr == 0;  // group 0: DMA; group 1: stores
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q8 = nwg >> 3, r8 = nwg & 7, x8 = bid & 7;
+  const int lc = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + (bid >> 3);
+  const int ntn = (g.N + BN - 1) / BN, ntm = (g.M + 255) / 256, ntiles = ntm * ntn;
+  const int nk = g.K / BK;
+  const int my_tiles = lc < ntiles ? (ntiles - 1 - lc) / nwg + 1 : 0;
+  const int J = my_tiles * nk;
+  if (J == 0) return;
+  constexpr int GM = 4;
+  auto tile_mn = [&](int i, int& m0, int& n0) __attribute__((always_inline)) {
+    const int wg = lc + i * nwg;
+    const int grp = wg / (GM * ntn), gm0 = grp * GM, gmn = min(GM, ntm - gm0), rem = wg - grp * GM * ntn;
+    m0 = (gm0 + rem % gmn) * 256;
+    n0 = (rem / gmn) * BN;
+  };
+  const __amdgpu_buffer_rsrc_t rA = rsrc(g.A, (unsigned)(((long)(g.M - 1) * g.lda + g.K) * 2));
+  const __amdgpu_buffer_rsrc_t rB = rsrc(g.B, (unsigned)(((long)(g.N - 1) * g.ldb + g.K) * 2));
+  const __amdgpu_buffer_rsrc_t rC = rsrc(g.C, g.c_bytes);
+  // DMA plan (group 0): instruction j of wave w fills piece rows j*32 + w*8 + lane/8
+  const int prow = wc * 8 + (lane >> 3);
+  const int lcx = (lane & 7) ^ ((prow >> 1) & 7);
+  int voff[4][DW];
+  auto set_voff = [&](int p, int m0, int n0) __attribute__((always_inline)) {
+    const int h = (p == 2 || p == 3) ? 1 : 0;
+#pragma unroll
+    for (int j = 0; j < DW; j++) {
+      const int r = j * 32 + prow;  // piece row
+      if (p == 0 || p == 3) {
+        const int m = m0 + (r >> 6) * 128 + h * 64 + (r & 63);
+        voff[p][j] = m < g.M ? (m * g.lda + lcx * 8) * 2 : (int)kOOB;
+      } else {
+        const int n = n0 + (r >> 5) * WN + h * 32 + (r & 31);
+        voff[p][j] = n < g.N ? (n * g.ldb + lcx * 8) * 2 : (int)kOOB;
+      }
+    }
+  };
+  int xkt = 0, xti = 0, ykt = 0, yti = 0;
+  {
+    int m0, n0;
+    tile_mn(0, m0, n0);
+#pragma unroll
+    for (int p = 0; p < 4; p++) set_voff(p, m0, n0);
+  }
+  auto advance = [&](bool X) __attribute__((always_inline)) {
+    int& kt = X ? xkt : ykt;
+    int& ti = X ? xti : yti;
+    if (++kt == nk) {
+      kt = 0;
+      if (++ti < my_tiles) {
+        int m0, n0;
+        tile_mn(ti, m0, n0);
+        set_voff(X ? 2 : 0, m0, n0);
+        set_voff(X ? 3 : 1, m0, n0);
+      }
+    }
+  };
+  auto issue = [&](auto pc, int gk) __attribute__((always_inline)) {
+    constexpr int p = decltype(pc)::value;
+    constexpr bool X = (p == 2 || p == 3);
+    if (!loader) return;
+    char* dst = smem + (gk & 1) * (4 * PIECE) + p * PIECE + wc * 8 * 128;
+    const __amdgpu_buffer_rsrc_t r = (p == 0 || p == 3) ? rA : rB;
+    const int soff = (X ? xkt : ykt) * BK * 2;
+    const bool live = gk < J;
+#pragma unroll
+    for (int j = 0; j < DW; j++) dma16(r, dst + j * 32 * 128, live ? voff[p][j] : (int)kOOB, soff);
+  };
+  const int fr = lane & 15, fq = lane >> 4;
+  const int ro0 = fr * 128 + ((fq ^ (fr >> 1)) << 4), ro1 = fr * 128 + (((4 + fq) ^ (fr >> 1)) << 4);
+  floatx4 acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; i++)
+#pragma unroll
+    for (int j = 0; j < TM; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  short8 a[4][2], b0[2][2], b1[NB1][2];
+  const int cb = ((fq & 1) << 4) | ((fq >> 1) << 3);
+  // C of quadrant (mh, nh) of this wave's tile at (m0, n0) as 4 x 16 B per lane (one per 16-row block)
+  auto pack_q = [&](int mh, int nh, uint4 (&v)[4]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int mi = 0; mi < 4; mi++) {
+      floatx4& x = acc[nh * 2][mh * 4 + mi];
+      floatx4& y = acc[nh * 2 + 1][mh * 4 + mi];
+      const unsigned x0 = cvt2(x[0], x[1]), x1 = cvt2(x[2], x[3]);
+      const unsigned y0 = cvt2(y[0], y[1]), y1 = cvt2(y[2], y[3]);
+      const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+      const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+      v[mi] = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+      x = floatx4{0.f, 0.f, 0.f, 0.f};
+      y = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  // quadrant stores of wave-row group `grp` (a group-1 wave stores its partner's with grp = 0)
+  auto store_v = [&](int grp, int mh, int nh, int m0, int n0, const uint4 (&v)[4]) __attribute__((always_inline)) {
+    const int n = n0 + wc * WN + nh * 32 + cb;
+    const bool nok = n < g.N;
+#pragma unroll
+    for (int mi = 0; mi < 4; mi++) {
+      const int m = m0 + grp * 128 + mh * 64 + mi * 16 + fr;
+      const unsigned off = (m < g.M && nok) ? ((unsigned)m * (unsigned)g.ldc + (unsigned)n) * 2u : kOOB;
+      using V = decltype(__builtin_amdgcn_raw_buffer_load_b128(rC, 0, 0, 0));
+      uint4 w = v[mi];
+      __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<V*>(&w), rC, off, 0, NT ? 2 : 0);
+    }
+  };
+  // hand-off area of phase parity `hp`: [wave column wc][mi][lane] 16-B slots (each wave its own 4 KB)
+  auto ho_addr = [&](int hp, int mi) __attribute__((always_inline)) {
+    return (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)(smem + 2 * 4 * PIECE + hp * HANDOFF) +
+           (unsigned)((wc * 4 + mi) * 1024 + lane * 16);
+  };
+  // boundary phase s of the next tile's first k-tile: quadrant q of the previous tile (pm0, pn0)
+  auto epi = [&](int mh, int nh, int hp, int pm0, int pn0) __attribute__((always_inline)) {
+    uint4 v[4];
+    pack_q(mh, nh, v);
+    typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+    if (loader) {
+#pragma unroll
+      for (int mi = 0; mi < 4; mi++) {
+        const u32x4 w = {v[mi].x, v[mi].y, v[mi].z, v[mi].w};
+        asm volatile("ds_write_b128 %0, %1" ::"v"(ho_addr(hp, mi)), "v"(w) : "memory");
+      }
+    } else {
+      u32x4 pw[4];
+#pragma unroll
+      for (int mi = 0; mi < 4; mi++) asm volatile("ds_read_b128 %0, %1" : "=v"(pw[mi]) : "v"(ho_addr(hp, mi)) : "memory");
+      store_v(1, mh, nh, pm0, pn0, v);  // own quadrant first: its registers are ready
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(pw[0]), "+v"(pw[1]), "+v"(pw[2]), "+v"(pw[3]) :: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      uint4 pv[4];
+#pragma unroll
+      for (int mi = 0; mi < 4; mi++) pv[mi] = make_uint4(pw[mi][0], pw[mi][1], pw[mi][2], pw[mi][3]);
+      store_v(0, mh, nh, pm0, pn0, pv);
+    }
+  };
+  auto mfma_q = [&](auto& bb, int mh, int nh) __attribute__((always_inline)) {
+    constexpr int NI = sizeof(bb) / sizeof(bb[0]);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ks++)
+#pragma unroll
+      for (int ni = 0; ni < NI; ni++)
+#pragma unroll
+        for (int mi = 0; mi < 4; mi++)
+          acc[nh * 2 + ni][mh * 4 + mi] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[ni][ks], a[mi][ks], acc[nh * 2 + ni][mh * 4 + mi], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto rd = [&](const char* p) -> short8 { return *reinterpret_cast<const short8*>(p); };
+
+  issue(std::integral_constant<int, 0>{}, 0);
+  issue(std::integral_constant<int, 1>{}, 0);
+  advance(false);
+  issue(std::integral_constant<int, 2>{}, 0);
+  issue(std::integral_constant<int, 3>{}, 0);
+  advance(true);
+  issue(std::integral_constant<int, 0>{}, 1);
+  issue(std::integral_constant<int, 1>{}, 1);
+  advance(false);
+  if (loader) vm_wait<4 * DW>();
+  asm volatile("s_barrier" ::: "memory");
+  if (wr) asm volatile("s_barrier" ::: "memory");
+
+  int cm0, cn0, pm0 = 0, pn0 = 0;
+  tile_mn(0, cm0, cn0);
+  // retire: group 0 leaves the pieces of the last four phases in flight; with a
+  // hand-off written this phase it also drains its LDS writes before the barrier
+  auto retire = [&](bool ho) __attribute__((always_inline)) {
+    if (loader) {
+      vm_wait<4 * DW>();
+      if (ho) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+  };
+  auto ktile = [&](int u, auto mode) __attribute__((always_inline)) {
+    constexpr bool EPI = decltype(mode)::value;
+    const char* buf = smem + (u & 1) * (4 * PIECE);
+    {  // s0: A0 + B0 -> quadrant (0, 0)
+      const char* pa = buf + wr * 64 * 128;
+      const char* pb = buf + PIECE + wc * 32 * 128;
+#pragma unroll
+      for (int ni = 0; ni < 2; ni++) {
+        b0[ni][0] = rd(pb + ni * 16 * 128 + ro0);
+        b0[ni][1] = rd(pb + ni * 16 * 128 + ro1);
+      }
+#pragma unroll
+      for (int mi = 0; mi < 4; mi++) {
+        a[mi][0] = rd(pa + mi * 16 * 128 + ro0);
+        a[mi][1] = rd(pa + mi * 16 * 128 + ro1);
+      }
+      if constexpr (EPI) epi(0, 0, 0, pm0, pn0);
+      issue(std::integral_constant<int, 2>{}, u + 1);
+      retire(EPI);
+      asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      mfma_q(b0, 0, 0);
+      asm volatile("s_barrier" ::: "memory");
+    }
+    {  // s1: B1 -> quadrant (0, 1)
+      const char* pb = buf + 2 * PIECE + wc * 32 * 128;
+#pragma unroll
+      for (int ni = 0; ni < NB1; ni++) {
+        b1[ni][0] = rd(pb + ni * 16 * 128 + ro0);
+        b1[ni][1] = rd(pb + ni * 16 * 128 + ro1);
+      }
+      if constexpr (EPI) epi(0, 1, 1, pm0, pn0);
+      issue(std::integral_constant<int, 3>{}, u + 1);
+      retire(EPI);
+      asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      mfma_q(b1, 0, 1);
+      asm volatile("s_barrier" ::: "memory");
+    }
+    {  // s2: A1 -> quadrant (1, 1)
+      const char* pa = buf + 3 * PIECE + wr * 64 * 128;
+#pragma unroll
+      for (int mi = 0; mi < 4; mi++) {
+        a[mi][0] = rd(pa + mi * 16 * 128 + ro0);
+        a[mi][1] = rd(pa + mi * 16 * 128 + ro1);
+      }
+      if constexpr (EPI) epi(1, 1, 0, pm0, pn0);
+      issue(std::integral_constant<int, 0>{}, u + 2);
+      retire(EPI);
+      asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      mfma_q(b1, 1, 1);
+      asm volatile("s_barrier" ::: "memory");
+    }
+    {  // s3: registers only -> quadrant (1, 0)
+      if constexpr (EPI) epi(1, 0, 1, pm0, pn0);
+      issue(std::integral_constant<int, 1>{}, u + 2);
+      retire(EPI);
+      asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      mfma_q(b0, 1, 0);
+      asm volatile("s_barrier" ::: "memory");
+    }
+    advance(true);
+    advance(false);
+  };
+
+  int u = 0;
+  for (int t = 0; t < my_tiles; t++) {
+    int k = 0;
+    if (t > 0) {
+      pm0 = cm0;
+      pn0 = cn0;
+      tile_mn(t, cm0, cn0);
+      ktile(u++, std::true_type{});
+      k = 1;
+    }
+    for (; k < nk; k++) ktile(u++, std::false_type{});
+  }
+  if (!wr) asm volatile("s_barrier" ::: "memory");  // both groups at the same barrier count
+  // the last tile: every wave stores its own quadrants (group 0's DMAs are all issued)
+  {
+    uint4 v[4];
+    pack_q(0, 0, v);
+    store_v(wr, 0, 0, cm0, cn0, v);
+    pack_q(0, 1, v);
+    store_v(wr, 0, 1, cm0, cn0, v);
+    pack_q(1, 1, v);
+    store_v(wr, 1, 1, cm0, cn0, v);
+    pack_q(1, 0, v);
+    store_v(wr, 1, 0, cm0, cn0, v);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail's zero-fill DMAs land before the LDS is released
+}
+
 int ppp_cus() {
   static int c = 0;
   if (!c) {
@@ -655,6 +949,13 @@ KFA_API int kfa_gemm_ppp(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int
   const PppArgs g{A, B, C, M, N, K, lda, ldb, ldc, (unsigned)cb, ws ? reinterpret_cast<float*>((char*)ws + 4096) : nullptr,
                   reinterpret_cast<int*>(ws), split};
   const dim3 gd(grid), bd(512);
+  if (probe == 9 || probe == 10) {  // wave-specialised stores (gemm_ppw_kernel): 256-wide, data-parallel tiles only
+    const int gw = (int)(tiles < cus ? tiles : cus);
+    const PppArgs gp{A, B, C, M, N, K, lda, ldb, ldc, (unsigned)cb, nullptr, nullptr, 1};
+    if (probe == 9) hipLaunchKernelGGL((gemm_ppw_kernel<false>), dim3(gw), dim3(512), 0, st, gp);
+    else hipLaunchKernelGGL((gemm_ppw_kernel<true>), dim3(gw), dim3(512), 0, st, gp);
+    return kfa_status();
+  }
   if (bn == 192) {  // three-phase k-tiles (P3); probe 7 / 8: the four-phase schedule (with / without stores)
     if (probe == 1 || probe == 6) hipLaunchKernelGGL((gemm_ppp_kernel<192, true, 0, true>), gd, bd, 0, st, g);
     else if (probe == 7) hipLaunchKernelGGL((gemm_ppp_kernel<192, false>), gd, bd, 0, st, g);

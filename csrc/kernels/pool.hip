@@ -325,7 +325,7 @@ __global__ __launch_bounds__(256) void maxpool3s2_bwd4(const bf16_t* __restrict_
   const int u = (int)(q % (unsigned)U);
   q /= (unsigned)U;
   const int t = (int)(q % (unsigned)T);
-  const int n = (int)(q / (unsigned)T);
+  const int n = live ? (int)(q / (unsigned)T) : 0;  // a STATS tail lane past the work only loads in-bounds rows
   uint4 g[4];
   uint2 pk[4];
   bool ok[4];

@@ -252,7 +252,10 @@ def _ppp_candidates(a, b):
     M, K = a.shape
     N = b.shape[0]
     L = _lib.lib()
-    c = [("ppp256", lambda: gemm_ppp(a, b, bn=256, split=False))]
+    c = [("ppp256", lambda: gemm_ppp(a, b, bn=256, split=False)),
+         # wave-specialised stores: group 0 all LDS-DMA, group 1 all C stores (plain / non-temporal)
+         ("ppw256", lambda: gemm_ppp(a, b, probe=9, split=False)),
+         ("ppw256-nt", lambda: gemm_ppp(a, b, probe=10, split=False))]
     if L.kfa_gemm_ppp_ws_bytes(M, N, K, 256, 0) > 0:
         c.append(("ppp256-split", lambda: gemm_ppp(a, b, bn=256)))
     if N % 192 == 0:

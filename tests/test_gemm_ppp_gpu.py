@@ -187,3 +187,25 @@ def test_dense_layer_small_batch_routes_own():
     _close(y, yr, 2e-2, "fc fwd")
     _close(x.grad, xr.grad, 2e-2, "fc dgrad")
     _close(lin.bias.grad, br.grad, 2e-2, "fc dbias")
+
+
+@pytest.mark.parametrize("M,N,K,blocks", [
+    (256, 256, 128, 0),       # one tile: only the after-loop stores
+    (512, 512, 128, 1),       # 4 tiles on one block, every k-tile a boundary one (hand-off each phase)
+    (1000, 776, 192, 3),      # edge tiles in M and N, uneven tile counts per block
+    (8192, 2304, 768, 0),     # 4.5 tiles per CU
+    (32768, 3072, 768, 0),    # BERT FFN-up: 6 tiles per CU
+    (2048, 768, 3072, 5),     # long k-loop, many tiles per block
+    (300, 8, 128, 0),         # N = 8
+])
+@pytest.mark.parametrize("probe", [9, 10], ids=["ppw", "ppw_nt"])
+def test_gemm_ppw_matches_fp32(M, N, K, blocks, probe):
+    """Wave-specialised persistent GEMM (gemm_ppw_kernel): group 0 issues every LDS-DMA
+    piece and hands its C quadrants to group 1 through LDS, group 1 issues every C store."""
+    from kubeflow_controller_amd.ops import gemm as G
+    torch.manual_seed(M + N + K + 3)
+    a, b = _bf(M, K), _bf(N, K, s=0.05)
+    c = G.gemm_ppp(a, b, blocks=blocks, probe=probe, split=False)
+    _close(c, a.float() @ b.float().t(), 1e-2, f"ppw {M}x{N}x{K} blocks={blocks} probe={probe}")
+    c2 = G.gemm_ppp(a, b, blocks=blocks, probe=probe, split=False)
+    assert torch.equal(c, c2)

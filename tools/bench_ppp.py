@@ -37,6 +37,7 @@ def main():
         w = torch.randn(N, K, device=d).to(torch.bfloat16)
         fl = 2.0 * M * N * K
         res = {}
+        res.pop("-", None)
         for rnd in range(3):
             for name, fn in (("hipblaslt", lambda: torch.mm(x, w.t())),
                              ("ppp-nosplit", lambda: G.gemm_ppp(x, w, bn=256, split=False)),
@@ -45,10 +46,15 @@ def main():
                              ("ppp192", lambda: G.gemm_ppp(x, w, bn=192)) if N % 192 == 0 else ("-", lambda: None),
                              ("ppp192-nost", lambda: G.gemm_ppp(x, w, bn=192, probe=1)) if N % 192 == 0 else ("-", lambda: None),
                              ("ppp-nostore", lambda: G.gemm_ppp(x, w, bn=256, probe=1)),
-                             ("ppp-nostore-nosplit", lambda: G.gemm_ppp(x, w, bn=256, probe=1, split=False))):
+                             ("ppp-nostore-nosplit", lambda: G.gemm_ppp(x, w, bn=256, probe=1, split=False)),
+                             ("ppw", lambda: G.gemm_ppp(x, w, probe=9, split=False)),
+                             ("ppw-nt", lambda: G.gemm_ppp(x, w, probe=10, split=False)),
+                             ("skinny", lambda: G.gemm_skinny(x, w)) if M <= 256 and N % 4 == 0 else ("-", lambda: None)):
                 res.setdefault(name, []).append(timeit(fn))
         ref = torch.mm(x, w.t()).float()
         err = max((G.gemm_ppp(x, w, bn=b).float() - ref).abs().max().item() for b in ((256, 192) if N % 192 == 0 else (256,)))
+        err = max(err, (G.gemm_ppp(x, w, probe=9, split=False).float() - ref).abs().max().item())
+        res.pop("-", None)
         line = " | ".join(f"{k} {min(v) * 1e3:7.1f} us {fl / min(v) / 1e9:6.0f} TF/s" for k, v in res.items())
         print(f"{M:6d} {N:5d} {K:5d} | {line} | ppp max|err| {err:.3g}", flush=True)
 
