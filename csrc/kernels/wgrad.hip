@@ -607,6 +607,18 @@ bool wide64() {
   return v == 1;
 }
 
+// KFA_WGRAD_WIDE64_ANY=1: 64x256 tiles for every Co <= 64 weight with N >= 512 (the
+// 3x3 64-channel convs, N = 576: the last tile is a quarter full) instead of 64x128
+// with 64x32 wave tiles, which read 1.5 LDS operands per MFMA
+bool wide64_any() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("KFA_WGRAD_WIDE64_ANY");
+    v = (e && e[0] == '1') ? 1 : 0;
+  }
+  return v == 1;
+}
+
 // KFA_WGRAD_PP=0: pointwise 256x256 weight gradients on the lockstep wgrad_kernel
 // instead of the ping-pong wgrad_pp_kernel
 static int wgrad_pp_mode() {  // 0 off, 1 size rule (default), 2 every pointwise weight (experiments)
@@ -638,7 +650,7 @@ WPlan plan(long K, int Co, int N, bool pointwise = false) {
   // 256x256 (8 waves of 128x64, one block per CU): half the operand bytes per
   // MFMA of the 128x128 tile — for the long reductions of big weights
   if ((Co % 256 == 0 && N % 256 == 0 && K >= 8192) || pp_shape(K, Co, N, pointwise)) p.variant = 4;
-  else if (Co <= 64 && N % 256 == 0 && wide64()) p.variant = 5;
+  else if (Co <= 64 && wide64() && (N % 256 == 0 || (N >= 512 && wide64_any()))) p.variant = 5;
   else p.variant = Co <= 64 ? (N <= 64 ? 3 : 1) : (N <= 64 ? 2 : 0);
   p.BM = p.variant == 4 ? 256 : ((p.variant == 1 || p.variant == 3 || p.variant == 5) ? 64 : 128);
   p.BN = (p.variant == 4 || p.variant == 5) ? 256 : ((p.variant == 2 || p.variant == 3) ? 64 : 128);

@@ -64,13 +64,29 @@ def ps_owner_ranks(num_workers: int, num_ps: int) -> List[int]:
     return [p * num_workers // num_ps for p in range(max(1, num_ps))]
 
 
-# Pull waits per module (opt-in, env KFA_PS_PULL_PER_MODULE=1): each module's
-# forward pre-hook waits only for the buckets holding its own parameters, so the
-# first layers compute while later buckets still arrive.  That is only correct if
-# no module reads another module's weight before that module's own forward has
-# run (tied or shared weights break it, silently), so the default is one wait for
-# every pull at the start of the forward.
-PER_MODULE_PULL_WAITS = os.environ.get("KFA_PS_PULL_PER_MODULE", "0") == "1"
+# Pull waits per module (default; env KFA_PS_PULL_PER_MODULE=0 turns them off):
+# each module's forward pre-hook waits only for the buckets holding its own
+# parameters, so the first layers compute while later buckets still arrive.  That
+# is only correct if no module reads another module's weight before that module's
+# own forward has run, so the model is checked first: a Parameter registered in
+# more than one module (tied / shared weights) keeps the single wait-all at the
+# start of every forward, and so does a model whose first forward does not show
+# every parameter-owning module running its own pre-hook.
+PER_MODULE_PULL_WAITS = os.environ.get("KFA_PS_PULL_PER_MODULE", "1") == "1"
+
+
+def shared_parameters(model: torch.nn.Module) -> List[str]:
+    """Names of parameters registered in more than one module (tied weights)."""
+    seen: Dict[int, str] = {}
+    shared: List[str] = []
+    for mname, m in model.named_modules(remove_duplicate=False):
+        for pname, p in m.named_parameters(recurse=False):
+            full = f"{mname}.{pname}" if mname else pname
+            if id(p) in seen and seen[id(p)] != full:
+                shared.append(f"{seen[id(p)]} = {full}")
+            else:
+                seen.setdefault(id(p), full)
+    return shared
 
 
 class ShardedGradSync:
@@ -132,8 +148,14 @@ class ShardedGradSync:
                 set_ready_callback(p, hook)
         self._pull_hooks = []
         self._stage: Dict[int, torch.Tensor] = {}  # per-bucket reduce-dtype staging (allocated once)
+        self.pull_mode = "wait-all"
         if model is not None and self.world > 1 and PER_MODULE_PULL_WAITS:
-            self._install_pull_waits(model)
+            tied = shared_parameters(model)
+            if tied:
+                self.pull_mode = f"wait-all (tied weights: {', '.join(tied[:3])})"
+            else:
+                self._install_pull_waits(model)
+                self.pull_mode = "per-module"
         self.reset()
 
     # ------------------------------------------------------------------ layout

@@ -442,7 +442,7 @@ def run_worker(spec: ClusterSpec, args) -> int:
     fixed = None if data is not None else synthetic_batch(args, model, device, rank)
     _log(f"Worker {rank}: {'local' if spec.is_local else f'{world} workers, {num_ps} ps'}, device {device}, "
          f"model {args.model}, {sum(p.numel() for p in model.parameters())} params, "
-         f"{'push/pull to ' + args.ps_placement + ' owners' if engine.sharded else 'all-reduce'}")
+         f"{'push/pull to ' + args.ps_placement + ' owners (pull waits: ' + getattr(engine.sync, 'pull_mode', '?') + ')' if engine.sharded else 'all-reduce'}")
     t_begin = time.time()
     _log(f"Training begins @ {t_begin:f}")
     global_step = resumed

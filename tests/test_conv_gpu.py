@@ -142,7 +142,7 @@ def test_wgrad_dense_shapes(rows, out_f, in_f):
     assert err < 2e-2 * ref.abs().max().item(), err
 
 
-@pytest.mark.parametrize("wide", ["1", "0"])
+@pytest.mark.parametrize("wide", ["1", "0", "any"])
 def test_wgrad_co64_gathered_taps(wide, monkeypatch):
     """Co = 64 weight gradients (1x1, gathered 3x3 / strided taps; N = R*S*Ci a
     multiple of 256) on the 64x256 tile and on the 64x128 one, both vs fp32.
@@ -152,7 +152,8 @@ def test_wgrad_co64_gathered_taps(wide, monkeypatch):
         "import torch, torch.nn.functional as F\n"
         "from kubeflow_controller_amd.ops.conv import wgrad_into\n"
         "torch.manual_seed(0); d = torch.device('cuda')\n"
-        "for (N, Ci, H, k, s, p) in [(4, 256, 14, 1, 1, 0), (3, 256, 13, 3, 2, 1), (2, 512, 9, 3, 1, 1)]:\n"
+        "for (N, Ci, H, k, s, p) in [(4, 256, 14, 1, 1, 0), (3, 256, 13, 3, 2, 1), (2, 512, 9, 3, 1, 1),\n"
+        "                            (4, 64, 20, 3, 1, 1)]:  # N = 576: a quarter-full last 256-wide tile\n"
         "    x = torch.randn(N, Ci, H, H, device=d).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)\n"
         "    w = torch.randn(64, Ci, k, k, device=d)\n"
         "    y = F.conv2d(x.float(), w, None, s, p)\n"
@@ -164,7 +165,7 @@ def test_wgrad_co64_gathered_taps(wide, monkeypatch):
         "    err = (out.permute(0, 3, 1, 2) - ref).abs().max().item()\n"
         "    assert err < 1e-2 * ref.abs().max().item(), (N, Ci, H, k, s, err)\n"
         "print('ok')\n")
-    env = dict(os.environ, KFA_WGRAD_WIDE64=wide)
+    env = dict(os.environ, KFA_WGRAD_WIDE64="0" if wide == "0" else "1", KFA_WGRAD_WIDE64_ANY="1" if wide == "any" else "0")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300,
                        cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-3000:]

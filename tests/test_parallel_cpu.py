@@ -359,3 +359,14 @@ def test_sharded_table_stays_out_of_flat_groups_after_deepcopy():
     flat = {id(p) for g in groups for p in g.params}
     assert id(m.tables.weight) not in flat
     assert m.tables.weight.dtype == torch.float32
+
+
+def test_pull_wait_mode_detects_tied_weights():
+    """Per-module pull waits are the default; a Parameter registered in two modules
+    (tied weights) keeps the wait-all pull."""
+    from kubeflow_controller_amd.parallel.ps import shared_parameters
+    a = torch.nn.Sequential(torch.nn.Linear(4, 4), torch.nn.Linear(4, 4))
+    assert shared_parameters(a) == []
+    b = torch.nn.Sequential(torch.nn.Linear(4, 4), torch.nn.Linear(4, 4))
+    b[1].weight = b[0].weight
+    assert shared_parameters(b) == ["0.weight = 1.weight"]
