@@ -306,6 +306,9 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(const bf16_t* __restri
 // through LDS (as dSᵀ [key][q]) for dQᵀ = Kᵀ·dSᵀ, computed after one barrier
 // by wave w for its queries 32w...  LDS = Q, K, dO images + dSᵀ = 80 KiB:
 // two workgroups per CU, so one loads while the other multiplies.
+// LDSD: D = rowsum(dO∘O) exchanged through the (not yet used) dSᵀ image instead of
+// a global scratch row — no vmcnt(0) + memory round trip before phase A.
+template <bool LDSD>
 __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(const bf16_t* __restrict__ qkv, const float* __restrict__ bqkv,
                                                           const float* __restrict__ kbias, const bf16_t* __restrict__ out,
                                                           const float* __restrict__ lse, const bf16_t* __restrict__ dout,
@@ -387,16 +390,21 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(const bf16_t* __restri
       for (int e = 0; e < 8; e++) acc += g[e] * o[e];
     }
     acc += __shfl_xor(acc, 1, 64);
-    if (!(lane & 1)) dwork[(long)bh * AS + dq] = acc;
+    if (!(lane & 1)) {
+      if constexpr (LDSD) reinterpret_cast<float*>(dST)[dq] = acc;
+      else dwork[(long)bh * AS + dq] = acc;
+    }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (!LDSD) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   float dd[2];
   {
-    const float2 d2 = *reinterpret_cast<const float2*>(dwork + (long)bh * AS + 2 * lane);
+    const float2 d2 = LDSD ? *reinterpret_cast<const float2*>(reinterpret_cast<const float*>(dST) + 2 * lane)
+                           : *reinterpret_cast<const float2*>(dwork + (long)bh * AS + 2 * lane);
     dd[0] = d2.x;
     dd[1] = d2.y;
   }
+  if constexpr (LDSD) __syncthreads();  // every wave has its D before phase A writes dSᵀ
   short8 kreg[2][2];
 #pragma unroll
   for (int kt = 0; kt < 2; kt++)
@@ -969,6 +977,20 @@ uint32_t attn_drop_thresh(float p) {
 
 }  // namespace
 
+// KFA_ATTN_PF=0: the S = 128 backward exchanges D through global scratch (the
+// pre-round-4 form) instead of LDS.  (A persistent forward that prefetched the
+// next (sequence, head)'s Q / K / V into registers measured 96.5 vs 80 us per
+// BERT-base layer: its 72 prefetch VGPRs cost the third workgroup per CU and
+// spilled — not kept.)
+static bool attn_pf() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("KFA_ATTN_PF");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+
 static bool attn_long_forced() {
   static int v = -1;
   if (v < 0) {
@@ -1008,9 +1030,14 @@ KFA_API int kfa_attn_bwd(const void* qkv, const float* bqkv, const float* key_bi
   const float ds = p > 0.f ? 1.f / (1.f - p) : 1.f;
   if (S == AS && !attn_long_forced()) {
     if (!work) return -3;
-    hipLaunchKernelGGL(attn_bwd_kernel, dim3((unsigned)(B * heads)), dim3(256), 0, st, (const bf16_t*)qkv, bqkv,
-                       key_bias, (const bf16_t*)out, lse, (const bf16_t*)dout, (bf16_t*)dqkv, dbqkv, work, heads,
-                       qscale, th, ds, (uint64_t)seed);
+    if (attn_pf())
+      hipLaunchKernelGGL(attn_bwd_kernel<true>, dim3((unsigned)(B * heads)), dim3(256), 0, st, (const bf16_t*)qkv,
+                         bqkv, key_bias, (const bf16_t*)out, lse, (const bf16_t*)dout, (bf16_t*)dqkv, dbqkv, work, heads,
+                         qscale, th, ds, (uint64_t)seed);
+    else
+      hipLaunchKernelGGL(attn_bwd_kernel<false>, dim3((unsigned)(B * heads)), dim3(256), 0, st, (const bf16_t*)qkv,
+                         bqkv, key_bias, (const bf16_t*)out, lse, (const bf16_t*)dout, (bf16_t*)dqkv, dbqkv, work, heads,
+                         qscale, th, ds, (uint64_t)seed);
     return kfa_status();
   }
   if (!work) return -3;

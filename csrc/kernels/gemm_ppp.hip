@@ -101,7 +101,18 @@ struct PppArgs {
   float* ws;
   int* flags;
   int split;
+  // experiment (kfa_gemm_ppp_set_stagger): blocks of odd logical index start this
+  // many s_memrealtime ticks (10 ns) late, so half the CUs cross their tile
+  // boundaries (and issue their C bursts) half a tile after the other half
+  int stagger;
 };
+
+__device__ __forceinline__ void ppp_stagger(int ticks, int lc) {
+  if (ticks > 0 && (lc & 1)) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)ticks) __builtin_amdgcn_s_sleep(4);
+  }
+}
 
 constexpr int kStoresPerPhase = 4;  // one 16-B store per 16-row block of a 64 x 32 quadrant
 
@@ -142,8 +153,9 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int q8 = nwg >> 3, r8 = nwg & 7, x8 = bid & 7;
   const int lc = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + (bid >> 3);
+  ppp_stagger(g.stagger, lc);
   const int ntn = (g.N + BN - 1) / BN, ntm = (g.M + 255) / 256, ntiles = ntm * ntn;
-  const int nk = g.K / BK;
+  const int nk = (g.K + BK - 1) / BK;  // K % 8 == 0; a partial last k-tile reads zeros past K
   // data-parallel tiles of this block (lc, lc + nwg, ...), then at most one split unit
   const int ns = g.split;
   const int ndp = ns > 1 ? ntiles / nwg : (lc < ntiles ? (ntiles - 1 - lc) / nwg + 1 : 0);
@@ -224,8 +236,10 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
     constexpr bool X = (p == 2 || p == 3);
     char* dst = smem + (gk & 1) * (4 * PIECE) + p * PIECE + wave * 8 * 128;
     const __amdgpu_buffer_rsrc_t r = (p == 0 || p == 3) ? rA : rB;
-    const int soff = (X ? xkt + xkb : ykt + ykb) * BK * 2;
-    const bool live = gk < J;
+    const int kt = X ? xkt + xkb : ykt + ykb;
+    const int soff = kt * BK * 2;
+    // K % 64 != 0: the last k-tile's chunks past K read zero (both operands)
+    const bool live = gk < J && kt * BK + lcx * 8 < g.K;
     dma16(r, dst, live ? voff[p][0] : (int)kOOB, soff);
     if constexpr (p != 2 || NB1 == 2) dma16(r, dst + 64 * 128, live ? voff[p][1] : (int)kOOB, soff);
   };
@@ -618,8 +632,9 @@ __global__ __launch_bounds__(512, 1) void gemm_ppw_kernel(PppArgs g) {
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int q8 = nwg >> 3, r8 = nwg & 7, x8 = bid & 7;
   const int lc = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + (bid >> 3);
+  ppp_stagger(g.stagger, lc);
   const int ntn = (g.N + BN - 1) / BN, ntm = (g.M + 255) / 256, ntiles = ntm * ntn;
-  const int nk = g.K / BK;
+  const int nk = (g.K + BK - 1) / BK;  // K % 8 == 0; a partial last k-tile reads zeros past K
   const int my_tiles = lc < ntiles ? (ntiles - 1 - lc) / nwg + 1 : 0;
   const int J = my_tiles * nk;
   if (J == 0) return;
@@ -677,8 +692,9 @@ __global__ __launch_bounds__(512, 1) void gemm_ppw_kernel(PppArgs g) {
     if (!loader) return;
     char* dst = smem + (gk & 1) * (4 * PIECE) + p * PIECE + wc * 8 * 128;
     const __amdgpu_buffer_rsrc_t r = (p == 0 || p == 3) ? rA : rB;
-    const int soff = (X ? xkt : ykt) * BK * 2;
-    const bool live = gk < J;
+    const int kt = X ? xkt : ykt;
+    const int soff = kt * BK * 2;
+    const bool live = gk < J && kt * BK + lcx * 8 < g.K;  // K tail: chunks past K read zero
 #pragma unroll
     for (int j = 0; j < DW; j++) dma16(r, dst + j * 32 * 128, live ? voff[p][j] : (int)kOOB, soff);
   };
@@ -890,7 +906,8 @@ int ppp_cus() {
 
 }  // namespace
 
-// C = A · Bᵀ (bf16 out) on the persistent ping-pong kernel.  K % 64 == 0,
+// C = A · Bᵀ (bf16 out) on the persistent ping-pong kernel.  K % 8 == 0 (a
+// partial last 64-deep k-tile reads zeros past K, e.g. the W&D MLP's K = 1680),
 // N % 8 == 0, every extent within 31-bit buffer offsets; grid = min(tiles, CUs)
 // (or `blocks` if > 0).  bn: tile width 256 or 192 (0 = pick: 192 when N is a
 // multiple of 192 and 256-wide tiles would leave a partial last round).
@@ -915,8 +932,8 @@ KFA_API long kfa_gemm_ppp_ws_bytes(int M, int N, int K, int bn, int blocks) {
   if (bn == 0) bn = kfa_gemm_ppp_pick_bn(M, N);
   const long tiles = (long)((M + 255) / 256) * ((N + bn - 1) / bn);
   const long cus = blocks > 0 ? blocks : ppp_cus();
-  if (tiles <= 0 || K % BK) return 0;
-  const int s = ppp_split(tiles, cus, K / BK);
+  if (tiles <= 0 || K % 8) return 0;
+  const int s = ppp_split(tiles, cus, (K + BK - 1) / BK);
   if (s == 1) return 0;
   const long r = tiles % cus;
   return 4096 + r * s * 256L * bn * 4;  // every part publishes (the last arriver is not known in advance)
@@ -931,27 +948,34 @@ KFA_API int kfa_gemm_ppp_pick_bn(int M, int N) {
   return r192 < r256 ? 192 : 256;
 }
 
+static int g_stagger = 0;
+// experiment knob (tools/bench_ppp.py): odd blocks start `ticks` x 10 ns late; 0 = off
+KFA_API int kfa_gemm_ppp_set_stagger(int ticks) {
+  g_stagger = ticks < 0 ? 0 : ticks;
+  return 0;
+}
+
 KFA_API int kfa_gemm_ppp(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int K, int lda, int ldb, int ldc,
                          int blocks, int probe, int bn, void* ws, long ws_bytes, int nosplit, hipStream_t st) {
   if (M <= 0 || N <= 0) return 0;
   // K >= 128: two k-tiles per tile at least (a tile's first two k-tiles carry its predecessor's stores)
-  if (K < 2 * BK || K % BK || N % 8 || lda % 8 || ldb % 8 || ldc % 8 || lda < K || ldb < K || ldc < N) return -1;
+  if (K < 2 * BK || K % 8 || N % 8 || lda % 8 || ldb % 8 || ldc % 8 || lda < K || ldb < K || ldc < N) return -1;
   const long cb = (long)M * ldc * 2;
   if (cb >= (long)kOOB || (long)M * lda * 2 >= (long)kOOB || (long)N * ldb * 2 >= (long)kOOB) return -2;
   if (bn == 0) bn = kfa_gemm_ppp_pick_bn(M, N);
   if (bn != 256 && bn != 192) return -1;
   const long tiles = (long)((M + 255) / 256) * ((N + bn - 1) / bn);
   const long cus = blocks > 0 ? blocks : ppp_cus();
-  int split = nosplit ? 1 : ppp_split(tiles, cus, K / BK);
+  int split = nosplit ? 1 : ppp_split(tiles, cus, (K + BK - 1) / BK);
   if (split > 1 && (ws == nullptr || ws_bytes < kfa_gemm_ppp_ws_bytes(M, N, K, bn, blocks))) return -3;
   // a split grid is the whole `cus` blocks (the split units fill the last round)
   const int grid = split > 1 ? (int)cus : (int)(tiles < cus ? tiles : cus);
   const PppArgs g{A, B, C, M, N, K, lda, ldb, ldc, (unsigned)cb, ws ? reinterpret_cast<float*>((char*)ws + 4096) : nullptr,
-                  reinterpret_cast<int*>(ws), split};
+                  reinterpret_cast<int*>(ws), split, g_stagger};
   const dim3 gd(grid), bd(512);
   if (probe == 9 || probe == 10) {  // wave-specialised stores (gemm_ppw_kernel): 256-wide, data-parallel tiles only
     const int gw = (int)(tiles < cus ? tiles : cus);
-    const PppArgs gp{A, B, C, M, N, K, lda, ldb, ldc, (unsigned)cb, nullptr, nullptr, 1};
+    const PppArgs gp{A, B, C, M, N, K, lda, ldb, ldc, (unsigned)cb, nullptr, nullptr, 1, g_stagger};
     if (probe == 9) hipLaunchKernelGGL((gemm_ppw_kernel<false>), dim3(gw), dim3(512), 0, st, gp);
     else hipLaunchKernelGGL((gemm_ppw_kernel<true>), dim3(gw), dim3(512), 0, st, gp);
     return kfa_status();

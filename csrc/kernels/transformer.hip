@@ -134,7 +134,11 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ 
 // launch).
 // dy2 (nullable): a second gradient summed into dy on the fly — a residual join
 // (dres + dbranch·W) whose GEMM then needs no addend epilogue (ops/transformer.py).
-template <int NV, bool TWO>
+// DEEP: rows of the wave in flight ahead of the one being reduced (1 or 2):
+// one row ahead leaves 8 waves x 1 row = ~36 KB of loads in flight per CU,
+// about half of what hides an HBM miss (MI355X_MICROARCH.md); two rows ahead
+// doubles it at +48 VGPRs (KFA_LN_BWD_DEEP).
+template <int NV, bool TWO, int DEEP>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ dy2,
                                                      const bf16_t* __restrict__ xs,
                                                      const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
@@ -143,6 +147,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
                                                      float* __restrict__ o_beta, float* __restrict__ o_bias, long rows,
                                                      int H, long rows_per_block, uint32_t thresh, float dscale,
                                                      uint64_t seed) {
+  static_assert(DEEP == 1 || DEEP == 2, "rows in flight");
   extern __shared__ float red[];  // [4][H]
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const long r0 = (long)blockIdx.x * rows_per_block;
@@ -160,34 +165,34 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
     const int c = (j * 64 + lane) * 8;
     if (c < H) load8f(gamma + c, gm[j]);
   }
-  // software pipeline: the next row's dy / x AND its mean / rstd are in flight
-  // while this row reduces (the row statistics were loaded at the top of their
-  // own iteration: one exposed memory latency per row)
-  uint4 nd[NV], nx[NV], ne[NV];
-  float nmean = 0.f, nrstd = 0.f;
-  auto fetch = [&](long row) {
+  // software pipeline: the next DEEP rows' dy / x AND their mean / rstd are in
+  // flight while this row reduces (slot S holds the rows row0 + S·4, + DEEP·4, ...)
+  uint4 nd[DEEP][NV], nx[DEEP][NV], ne[DEEP][NV];
+  float nmean[DEEP], nrstd[DEEP];
+  auto fetch = [&](auto sc, long row) __attribute__((always_inline)) {
+    constexpr int S = decltype(sc)::value;
     if (row < r1) {
-      nmean = mean_in[row];
-      nrstd = rstd_in[row];
+      nmean[S] = mean_in[row];
+      nrstd[S] = rstd_in[row];
     }
 #pragma unroll
     for (int j = 0; j < NV; j++) {
       const int c = (j * 64 + lane) * 8;
       if (c < H && row < r1) {
-        nd[j] = ld16(dy + row * (long)H + c);
-        if constexpr (TWO) ne[j] = ld16(dy2 + row * (long)H + c);
-        nx[j] = ld16(xs + row * (long)H + c);
+        nd[S][j] = ld16(dy + row * (long)H + c);
+        if constexpr (TWO) ne[S][j] = ld16(dy2 + row * (long)H + c);
+        nx[S][j] = ld16(xs + row * (long)H + c);
       }
     }
   };
-  fetch(r0 + w);
-  for (long row = r0 + w; row < r1; row += kRowsPerBlock) {
+  auto process = [&](auto sc, long row) __attribute__((always_inline)) {
+    constexpr int S = decltype(sc)::value;
     const long base = row * (long)H;
-    const float mean = nmean, rstd = nrstd;
+    const float mean = nmean[S], rstd = nrstd[S];
     uint4 cd[NV], cx[NV], ce[NV];
 #pragma unroll
-    for (int j = 0; j < NV; j++) { cd[j] = nd[j]; cx[j] = nx[j]; ce[j] = ne[j]; }
-    fetch(row + kRowsPerBlock);
+    for (int j = 0; j < NV; j++) { cd[j] = nd[S][j]; cx[j] = nx[S][j]; ce[j] = ne[S][j]; }
+    fetch(sc, row + DEEP * kRowsPerBlock);
     float xh[NV][8], g[NV][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -232,6 +237,13 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
         for (int e = 0; e < 8; e++) ad[j][e] += o[e];
       }
     }
+  };
+  fetch(std::integral_constant<int, 0>{}, r0 + w);
+  if constexpr (DEEP == 2) fetch(std::integral_constant<int, 1>{}, r0 + w + kRowsPerBlock);
+  for (long row = r0 + w; row < r1; row += DEEP * kRowsPerBlock) {
+    process(std::integral_constant<int, 0>{}, row);
+    if constexpr (DEEP == 2)
+      if (row + kRowsPerBlock < r1) process(std::integral_constant<int, 1>{}, row + kRowsPerBlock);
   }
   // block-reduce the three column accumulators
   auto reduce_out = [&](float (&acc)[NV][8], float* out) {
@@ -643,14 +655,20 @@ template <int NV>
 void launch_ln_bwd(dim3 g, size_t lds, hipStream_t s, const void* dy, const void* dy2, const void* xs,
                    const float* mean, const float* rstd, const float* gamma, void* dx, void* dbranch, float* o0,
                    float* o1, float* o2, long rows, int H, long rpb, uint32_t th, float ds, uint64_t seed) {
-  if (dy2)
-    hipLaunchKernelGGL((ln_bwd_kernel<NV, true>), g, dim3(256), lds, s, (const bf16_t*)dy, (const bf16_t*)dy2,
-                       (const bf16_t*)xs, mean, rstd, gamma, (bf16_t*)dx, (bf16_t*)dbranch, o0, o1, o2, rows, H, rpb,
-                       th, ds, seed);
-  else
-    hipLaunchKernelGGL((ln_bwd_kernel<NV, false>), g, dim3(256), lds, s, (const bf16_t*)dy, nullptr,
-                       (const bf16_t*)xs, mean, rstd, gamma, (bf16_t*)dx, (bf16_t*)dbranch, o0, o1, o2, rows, H, rpb,
-                       th, ds, seed);
+  static int deep = -1;
+  if (deep < 0) {
+    const char* e = getenv("KFA_LN_BWD_DEEP");
+    deep = (e && e[0] == '2') ? 2 : 1;
+  }
+#define KFA_LNB(TW, D)                                                                                              \
+  hipLaunchKernelGGL((ln_bwd_kernel<NV, TW, D>), g, dim3(256), lds, s, (const bf16_t*)dy,                          \
+                     TW ? (const bf16_t*)dy2 : nullptr, (const bf16_t*)xs, mean, rstd, gamma, (bf16_t*)dx,          \
+                     (bf16_t*)dbranch, o0, o1, o2, rows, H, rpb, th, ds, seed)
+  if (dy2 && deep == 2) KFA_LNB(true, 2);
+  else if (dy2) KFA_LNB(true, 1);
+  else if (deep == 2) KFA_LNB(false, 2);
+  else KFA_LNB(false, 1);
+#undef KFA_LNB
 }
 template <int G, int NV>
 void launch_sm_fwd(hipStream_t s, void* scores, const float* key_bias, void* pdrop, long rows, int S, int heads,

@@ -64,6 +64,151 @@ __global__ __launch_bounds__(256) void wd_input_bwd(const bf16_t* __restrict__ d
   }
 }
 
+// ---- output head + loss (the deep tower's 1-wide projection, the wide linear
+// over the dense features, sigmoid cross-entropy), forward and backward in one
+// pass each (+ a deterministic reduction of per-block partials), replacing two
+// GEMV-shaped hipBLASLt calls per direction and the ATen loss chain (~0.3 ms of
+// the 2.4 ms W&D step on hipBLASLt / ATen, profiles/r4_wide_deep_b65536_head.md).
+//   z_b    = x_b . w + out_b + wide_b + dpad_b . wd
+//   loss   = mean_b [ max(z, 0) - z y + log1p(exp(-|z|)) ]
+//   pmy_b  = sigmoid(z_b) - y_b  (saved for the backward)
+// Backward with g_b = dloss * pmy_b / B:
+//   dx_b = g_b w (bf16), dwide_b = g_b, dw = sum_b g_b x_b, dwd = sum_b g_b dpad_b, db = sum_b g_b
+// One 32-lane half-wave per row (H / 8 16-B pieces over its lanes); per-block partials.
+constexpr int kHeadRowsPerBlock = 8;  // half-waves of a 256-thread block
+constexpr int kHeadMaxPieces = 2;     // H <= 512
+constexpr int kHeadMaxDp = 64;
+
+__global__ __launch_bounds__(256) void wd_head_fwd(const bf16_t* __restrict__ x, const float* __restrict__ w,
+                                                   const float* __restrict__ ob, const float* __restrict__ wide,
+                                                   const float* __restrict__ dpad, const float* __restrict__ wd,
+                                                   const float* __restrict__ y, float* __restrict__ pmy,
+                                                   float* __restrict__ part, int B, int H, int Dp) {
+  __shared__ float red[kHeadRowsPerBlock];
+  const int hw = threadIdx.x >> 5, l = threadIdx.x & 31, npc = H / 8;
+  float lsum = 0.f;
+  for (long b = (long)blockIdx.x * kHeadRowsPerBlock + hw; b < B; b += (long)gridDim.x * kHeadRowsPerBlock) {
+    float s = 0.f;
+    for (int j = l; j < npc; j += 32) {
+      float f[8];
+      unpack8(*reinterpret_cast<const uint4*>(x + b * H + j * 8), f);
+      const float4 w0 = *reinterpret_cast<const float4*>(w + j * 8), w1 = *reinterpret_cast<const float4*>(w + j * 8 + 4);
+      s += f[0] * w0.x + f[1] * w0.y + f[2] * w0.z + f[3] * w0.w + f[4] * w1.x + f[5] * w1.y + f[6] * w1.z + f[7] * w1.w;
+    }
+    for (int j = l; j < Dp; j += 32) s += dpad[b * Dp + j] * wd[j];
+#pragma unroll
+    for (int o = 16; o; o >>= 1) s += __shfl_xor(s, o, 32);
+    if (l == 0) {
+      const float z = s + ob[0] + wide[b], yy = y[b];
+      pmy[b] = 1.f / (1.f + expf(-z)) - yy;
+      lsum += fmaxf(z, 0.f) - z * yy + log1pf(expf(-fabsf(z)));
+    }
+  }
+  if (l == 0) red[hw] = lsum;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int i = 0; i < kHeadRowsPerBlock; i++) t += red[i];
+    part[blockIdx.x] = t;
+  }
+}
+
+// loss[0] = sum(part[0..n)) / B in a fixed order (one block)
+__global__ __launch_bounds__(256) void wd_head_loss(const float* __restrict__ part, int n, int B,
+                                                    float* __restrict__ loss) {
+  __shared__ float red[256];
+  float t = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) t += part[i];
+  red[threadIdx.x] = t;
+  __syncthreads();
+  for (int o = 128; o; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) loss[0] = red[0] / (float)B;
+}
+
+// part: [gridDim.x][H + Dp + 1] = per-block (dw | dwd | db)
+__global__ __launch_bounds__(256) void wd_head_bwd(const bf16_t* __restrict__ x, const float* __restrict__ w,
+                                                   const float* __restrict__ dpad, const float* __restrict__ pmy,
+                                                   const float* __restrict__ dloss, bf16_t* __restrict__ dx,
+                                                   float* __restrict__ dwide, float* __restrict__ part, int B, int H,
+                                                   int Dp) {
+  extern __shared__ float sh[];  // [kHeadRowsPerBlock][H + Dp + 1]
+  const int hw = threadIdx.x >> 5, l = threadIdx.x & 31, npc = H / 8, W = H + Dp + 1;
+  const float gs = dloss[0] / (float)B;
+  float acc[kHeadMaxPieces][8] = {}, dacc[kHeadMaxDp / 32] = {}, bacc = 0.f;
+  float wr[kHeadMaxPieces][8];
+#pragma unroll
+  for (int q = 0; q < kHeadMaxPieces; q++) {
+    const int j = l + 32 * q;
+#pragma unroll
+    for (int e = 0; e < 8; e++) wr[q][e] = j < npc ? w[j * 8 + e] : 0.f;
+  }
+  for (long b = (long)blockIdx.x * kHeadRowsPerBlock + hw; b < B; b += (long)gridDim.x * kHeadRowsPerBlock) {
+    const float g = gs * pmy[b];
+#pragma unroll
+    for (int q = 0; q < kHeadMaxPieces; q++) {
+      const int j = l + 32 * q;
+      if (j < npc) {
+        float f[8], o[8];
+        unpack8(*reinterpret_cast<const uint4*>(x + b * H + j * 8), f);
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+          acc[q][e] += g * f[e];
+          o[e] = g * wr[q][e];
+        }
+        *reinterpret_cast<uint4*>(dx + b * H + j * 8) = pack8(o);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < kHeadMaxDp / 32; q++) {
+      const int j = l + 32 * q;
+      if (j < Dp) dacc[q] += g * dpad[b * Dp + j];
+    }
+    if (l == 0) {
+      dwide[b] = g;
+      bacc += g;
+    }
+  }
+  float* mine = sh + hw * W;
+#pragma unroll
+  for (int q = 0; q < kHeadMaxPieces; q++) {
+    const int j = l + 32 * q;
+    if (j < npc)
+#pragma unroll
+      for (int e = 0; e < 8; e++) mine[j * 8 + e] = acc[q][e];
+  }
+#pragma unroll
+  for (int q = 0; q < kHeadMaxDp / 32; q++) {
+    const int j = l + 32 * q;
+    if (j < Dp) mine[H + j] = dacc[q];
+  }
+  if (l == 0) mine[H + Dp] = bacc;
+  __syncthreads();
+  for (int c = threadIdx.x; c < W; c += 256) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < kHeadRowsPerBlock; i++) t += sh[i * W + c];
+    part[(long)blockIdx.x * W + c] = t;
+  }
+}
+
+// out[c] = sum over n blocks of part[blk][c] (fixed order), c < W
+__global__ __launch_bounds__(256) void wd_head_reduce(const float* __restrict__ part, int n, int W,
+                                                      float* __restrict__ out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= W) return;
+  float t = 0.f;
+  for (int i = 0; i < n; i++) t += part[(long)i * W + c];
+  out[c] = t;
+}
+
+int head_blocks(int B) {
+  const int b = (B + kHeadRowsPerBlock - 1) / kHeadRowsPerBlock;
+  return b < 1024 ? b : 1024;
+}
+
 int blocks_for(long n) {
   const long b = (n + 255) / 256;
   return (int)(b < 8192 ? (b < 1 ? 1 : b) : 8192);
@@ -77,6 +222,32 @@ KFA_API int kfa_wd_input_fwd(const bf16_t* rows, const float* dense, bf16_t* x, 
   if (E % 8 || Dp % 8 || B <= 0) return -1;
   hipLaunchKernelGGL(wd_input_fwd, dim3(blocks_for((long)B * ((Dp + F * E) / 8))), dim3(256), 0, st, rows, dense, x,
                      wide, B, F, E, Dp);
+  return kfa_status();
+}
+
+// blocks of the head kernels for B rows (the partial buffers hold this many rows)
+KFA_API int kfa_wd_head_blocks(int B) { return head_blocks(B); }
+
+// H % 8 == 0, H <= 512, Dp <= 64; x / dx 16-B aligned rows; part: head_blocks(B) floats;
+// loss: one float (written); pmy: B floats (written, for the backward)
+KFA_API int kfa_wd_head_fwd(const bf16_t* x, const float* w, const float* ob, const float* wide, const float* dpad,
+                            const float* wd, const float* y, float* pmy, float* part, float* loss, int B, int H, int Dp,
+                            hipStream_t st) {
+  if (B <= 0 || H % 8 || H > 8 * 32 * kHeadMaxPieces || Dp < 0 || Dp > kHeadMaxDp) return -1;
+  const int nb = head_blocks(B);
+  hipLaunchKernelGGL(wd_head_fwd, dim3(nb), dim3(256), 0, st, x, w, ob, wide, dpad, wd, y, pmy, part, B, H, Dp);
+  hipLaunchKernelGGL(wd_head_loss, dim3(1), dim3(256), 0, st, part, nb, B, loss);
+  return kfa_status();
+}
+
+// part: head_blocks(B) * (H + Dp + 1) floats of scratch; grads: H + Dp + 1 floats (dw | dwd | db)
+KFA_API int kfa_wd_head_bwd(const bf16_t* x, const float* w, const float* dpad, const float* pmy, const float* dloss,
+                            bf16_t* dx, float* dwide, float* part, float* grads, int B, int H, int Dp, hipStream_t st) {
+  if (B <= 0 || H % 8 || H > 8 * 32 * kHeadMaxPieces || Dp < 0 || Dp > kHeadMaxDp) return -1;
+  const int nb = head_blocks(B), W = H + Dp + 1;
+  hipLaunchKernelGGL(wd_head_bwd, dim3(nb), dim3(256), kHeadRowsPerBlock * W * 4, st, x, w, dpad, pmy, dloss, dx,
+                     dwide, part, B, H, Dp);
+  hipLaunchKernelGGL(wd_head_reduce, dim3((W + 255) / 256), dim3(256), 0, st, part, nb, W, grads);
   return kfa_status();
 }
 

@@ -29,6 +29,9 @@ from ..parallel.embedding import ShardedEmbedding
 
 _lib.register("kfa_wd_input_fwd", [_lib.P, _lib.P, _lib.P, _lib.P, _lib.I, _lib.I, _lib.I, _lib.I, _lib.P])
 _lib.register("kfa_wd_input_bwd", [_lib.P, _lib.P, _lib.P, _lib.I, _lib.I, _lib.I, _lib.I, _lib.P])
+_lib.register("kfa_wd_head_blocks", [_lib.I])
+_lib.register("kfa_wd_head_fwd", [_lib.P] * 10 + [_lib.I] * 3 + [_lib.P])
+_lib.register("kfa_wd_head_bwd", [_lib.P] * 9 + [_lib.I] * 3 + [_lib.P])
 
 
 class _WDInputFn(torch.autograd.Function):
@@ -56,6 +59,57 @@ class _WDInputFn(torch.autograd.Function):
         _lib.call("kfa_wd_input_bwd", _lib.ptr(dx), _lib.ptr(dwide), _lib.ptr(drows), B, F, E, Dp, _lib.stream())
         return drows, None, None, None, None
 
+
+class _WDHeadFn(torch.autograd.Function):
+    """Output head + loss in one HIP pass each way (``csrc/kernels/widedeep.hip``):
+    ``z = x . out_w + out_b + wide + dpad . wide_dense``, mean sigmoid cross-entropy
+    against ``labels``.  Replaces two GEMV-shaped hipBLASLt calls per direction and
+    the ATen loss / reduction chain.  Loss and every gradient reduce per-block
+    partials in a fixed order (deterministic)."""
+
+    @staticmethod
+    def forward(ctx, x, out_w, out_b, wide, dpad, wide_dense, labels):
+        B, H = x.shape
+        Dp = dpad.shape[1]
+        dev = x.device
+        w = out_w.detach().float().reshape(-1).contiguous()
+        ob = out_b.detach().float().reshape(-1).contiguous()
+        wd = wide_dense.detach().float().reshape(-1).contiguous()
+        y = labels.detach().float().reshape(-1).contiguous()
+        wide = wide.detach().float().contiguous()
+        pmy = torch.empty(B, dtype=torch.float32, device=dev)
+        part = torch.empty(_lib.lib().kfa_wd_head_blocks(B), dtype=torch.float32, device=dev)
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        _lib.call("kfa_wd_head_fwd", _lib.ptr(x), _lib.ptr(w), _lib.ptr(ob), _lib.ptr(wide), _lib.ptr(dpad), _lib.ptr(wd),
+                  _lib.ptr(y), _lib.ptr(pmy), _lib.ptr(part), _lib.ptr(loss), B, H, Dp, _lib.stream())
+        ctx.save_for_backward(x, w, dpad, pmy)
+        ctx.meta = (out_w.shape, out_w.dtype, out_b.shape, out_b.dtype, wide_dense.shape, wide_dense.dtype)
+        return loss
+
+    @staticmethod
+    def backward(ctx, dloss):
+        x, w, dpad, pmy = ctx.saved_tensors
+        wshape, wdt, bshape, bdt, wdshape, wddt = ctx.meta
+        B, H = x.shape
+        Dp = dpad.shape[1]
+        dl = dloss.detach().float().reshape(1).contiguous()
+        dx = torch.empty_like(x)
+        dwide = torch.empty(B, dtype=torch.float32, device=x.device)
+        nb = _lib.lib().kfa_wd_head_blocks(B)
+        part = _lib.workspace(4 * nb * (H + Dp + 1), x.device, "wd_head_part")
+        grads = torch.empty(H + Dp + 1, dtype=torch.float32, device=x.device)
+        _lib.call("kfa_wd_head_bwd", _lib.ptr(x), _lib.ptr(w), _lib.ptr(dpad), _lib.ptr(pmy), _lib.ptr(dl), _lib.ptr(dx),
+                  _lib.ptr(dwide), _lib.ptr(part), _lib.ptr(grads), B, H, Dp, _lib.stream())
+        return (dx, grads[:H].view(wshape).to(wdt), grads[H + Dp:].view(bshape).to(bdt), dwide, None,
+                grads[H:H + Dp].view(wdshape).to(wddt), None)
+
+
+def head_fusable(x: torch.Tensor, dpad: torch.Tensor) -> bool:
+    return (FUSED_HEAD and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 2 and x.is_contiguous()
+            and x.shape[1] % 8 == 0 and x.shape[1] <= 512 and dpad.shape[1] <= 64 and x.data_ptr() % 16 == 0)
+
+
+FUSED_HEAD = os.environ.get("KFA_WD_FUSED_HEAD", "1") != "0"  # csrc/kernels/widedeep.hip
 FUSED_INPUT = os.environ.get("KFA_WD_FUSED_INPUT", "1") != "0"  # csrc/kernels/widedeep.hip
 CRITEO_LIKE = (4_000_000,) * 4 + (1_000_000,) * 6 + (100_000,) * 8 + (10_000,) * 8
 
@@ -138,6 +192,9 @@ class WideDeep(nn.Module):
             x = x.float()
             for w, b in zip(self.weights, self.biases):
                 x = torch.relu(x @ w.float().t() + b.float())
+        dpad32 = dpad.float().contiguous()
+        if head_fusable(x, dpad32):
+            return _WDHeadFn.apply(x, self.out_w, self.out_b, wide, dpad32, self.wide_dense, labels)
         deep = (x @ self.out_w.to(x.dtype).t()).float().squeeze(1) + self.out_b.float()
         wide = wide + (dpad.float() @ self.wide_dense.float().t()).squeeze(1)
         return F.binary_cross_entropy_with_logits(deep + wide, labels.float())

@@ -46,12 +46,16 @@ ACTS = {None: 0, "none": 0, "gelu": 1, "tanh": 2, "relu": 3}
 #   "fused"  only the ones whose epilogue replaces a separate pass: the FFN-up
 #            forward (bias + GELU + pre-activation) and its dgrad (GELU' +
 #            bias-gradient column sums);
+#   "own"    as "auto", but the fastest OWN kernel is taken on every shape the
+#            own kernels cover, even where hipBLASLt times faster (A/B runs:
+#            what an all-own GEMM path costs end to end);
 #   "0"      none (hipBLASLt via torch.mm / addmm for all of them).
 # Measured on MI355X (tools/bench_gemm.py, tools/gpu_bert_gemm.sh; docs/kernels.md).
 _ROUTE = os.environ.get("KFA_GEMM", "auto")
 ROUTE_LAYERS = _ROUTE == "1"
 ROUTE_FUSED = _ROUTE in ("1", "fused")
-ROUTE_AUTO = _ROUTE == "auto"
+ROUTE_AUTO = _ROUTE in ("auto", "own")
+OWN_ONLY = _ROUTE == "own"
 TUNE_LOG = os.environ.get("KFA_GEMM_TUNE_LOG", "0") == "1"
 _choice: dict = {}
 
@@ -154,7 +158,8 @@ def gemm_nt(a, b, *, bias=None, act=None, addend=None, want_z=False, zin=None, d
 def gemm_ppp(a, b, *, out=None, blocks: int = 0, probe: int = 0, bn: int = 0, split: bool = True):
     """``a @ b.T`` (bf16) on the persistent ping-pong kernel (``csrc/kernels/gemm_ppp.hip``):
     one block per CU sweeps its tiles as one continuous k-tile pipeline, each tile's
-    C written from the accumulators during the next tile's first k-tile.  K % 64 == 0, K >= 128.
+    C written from the accumulators during the next tile's first k-tile.  K % 8 == 0, K >= 128
+    (a partial last 64-deep k-tile reads zeros past K).
     ``blocks`` > 0 caps the persistent grid (tests: many tiles per block).  ``probe=1``:
     timing probe with every C store dropped (C is left unwritten).  ``bn``: tile
     width 256 or 192 (0 = the kernel's pick: 192-wide tiles where N % 192 == 0 and
@@ -163,7 +168,7 @@ def gemm_ppp(a, b, *, out=None, blocks: int = 0, probe: int = 0, bn: int = 0, sp
     run by several blocks (fp32 partials combined in-kernel), so every CU runs
     about the same number of k-tiles — e.g. 384 tiles on 256 CUs: one full tile
     plus half a tile each instead of two tiles on half the CUs."""
-    if not gemm_ok(a, b) or a.shape[1] % 64 or a.shape[1] < 128:
+    if not gemm_ok(a, b) or a.shape[1] < 128:
         raise ValueError(f"gemm_ppp: unsupported operands {tuple(a.shape)} x {tuple(b.shape)}")
     M, K = a.shape
     N = b.shape[0]
@@ -204,9 +209,22 @@ def gemm_skinny(a, b, bias=None, *, splits: int = 0, out=None):
     return c
 
 
+def skinny_splits(a, b):
+    """``(name, splits)`` forms of :func:`gemm_skinny` worth timing for ``a @ b.T``:
+    the kernel's own pick (about one block per CU) and fixed 4 / 8 slices — fewer
+    slices leave the last-arriving slice less partial data to sum."""
+    M, K = a.shape
+    nks = K // 64
+    out = [("skinny", 0)]
+    for s in (4, 8):
+        if 2 * s <= nks:
+            out.append((f"skinny-s{s}", s))
+    return out
+
+
 def ppp_ok(a, b) -> bool:
     """Operands :func:`gemm_ppp` takes (plain ``a @ b.T``, bf16 out)."""
-    return gemm_ok(a, b) and a.shape[1] % 64 == 0 and a.shape[1] >= 128
+    return gemm_ok(a, b) and a.shape[1] >= 128
 
 
 def _agree_int(v: int, device) -> int:
@@ -236,7 +254,7 @@ def pick_fastest(kind: str, key: tuple, device, candidates) -> int:
     with torch.no_grad():
         ts = [_time_ms(fn, reps=10) for _, fn in candidates]
     best = min(range(1, len(ts)), key=lambda i: ts[i]) if len(ts) > 1 else 0
-    if best and not ts[best] < 0.99 * ts[0]:
+    if best and not ts[best] < 0.99 * ts[0] and not OWN_ONLY:
         best = 0
     hit = _choice[k] = _agree_int(best, device)
     if TUNE_LOG:
@@ -293,10 +311,10 @@ def dgrad_auto(dz, w, kind: str = "proj_dgrad"):
             return torch.mm(dz, w)
         wt = transpose_cached(w)
         own = []
-        if K % 64 == 0 and K >= 128:
+        if K >= 128:
             own += _ppp_candidates(dz, wt)
         if skinny_ok(dz, wt):
-            own.append(("skinny", lambda: gemm_skinny(dz, wt)))
+            own += [(n, (lambda s: lambda: gemm_skinny(dz, wt, splits=s))(s)) for n, s in skinny_splits(dz, wt)]
         if own:
             cands = [("hipblaslt", lambda: torch.mm(dz, w))] + own
             i = pick_fastest(kind, (M, N, K), dz.device, cands)

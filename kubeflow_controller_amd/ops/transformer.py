@@ -258,7 +258,7 @@ class DenseFn(torch.autograd.Function):
         fused = fusable and (_gemm.ROUTE_LAYERS or (_gemm.ROUTE_FUSED and has_act))
         _gemm.mark_weights_stale()  # the dgrad's cached weight transposes refresh at the next backward
         mm = None  # plain GEMM of the unfused path (None: hipBLASLt)
-        skinny = False  # the split-K skinny GEMM with the bias fused (M <= 256, e.g. the ResNet FC)
+        skinny = None  # split count of the split-K skinny GEMM with the bias fused (M <= 256, e.g. the ResNet FC)
         if fusable and _gemm.ROUTE_AUTO:
             # per shape, the fastest of: hipBLASLt + one bias/act pass, the MFMA GEMM with
             # the bias/act epilogue fused, the persistent MFMA GEMM + the bias/act pass,
@@ -269,24 +269,26 @@ class DenseFn(torch.autograd.Function):
             cands = ([("hipblaslt", lambda: ba(torch.mm(x2, weight.t()))),
                       ("gemm_nt-fused", lambda: _gemm.gemm_nt(x2, weight, bias=bias, act=act, want_z=has_act))]
                      + [(n, (lambda f: lambda: ba(f()))(f)) for n, f in own_pp])
-            if _gemm.skinny_ok(x2, weight):
-                cands.append(("skinny-bias", lambda: act_only(_gemm.gemm_skinny(x2, weight, bias))))
+            sk = _gemm.skinny_splits(x2, weight) if _gemm.skinny_ok(x2, weight) else []
+            cands += [(n + "-bias", (lambda s: lambda: act_only(_gemm.gemm_skinny(x2, weight, bias, splits=s)))(s))
+                      for n, s in sk]
             i = _gemm.pick_fastest("dense_fwd", (x2.shape[0], weight.shape[0], x2.shape[1], act, bias is not None),
                                    x2.device, cands)
             fused = i == 1
-            skinny = cands[i][0] == "skinny-bias"
+            ns = len(cands) - len(sk)
+            skinny = sk[i - ns][1] if i >= ns else None
             mm = own_pp[i - 2][1] if 2 <= i < 2 + len(own_pp) else None
         if fused:
             y, z = _gemm.gemm_nt(x2, weight, bias=bias, act=act, want_z=has_act)  # z includes the bias
-        elif skinny:
-            z = _gemm.gemm_skinny(x2, weight, bias)  # z includes the bias
+        elif skinny is not None:
+            z = _gemm.gemm_skinny(x2, weight, bias, splits=skinny)  # z includes the bias
             y = bias_act_fwd(z, None, act, p, seed) if (has_act or p > 0) else z
         else:
             z = mm() if mm is not None else torch.mm(x2, weight.t())
             y = bias_act_fwd(z, bias, act, p, seed) if (bias is not None or has_act or p > 0) else z
         ctx.save_for_backward(x2, weight, z if has_act else None)
         ctx.bias = bias
-        ctx.cfg = (act, p, seed, shp, fused, fused or skinny)
+        ctx.cfg = (act, p, seed, shp, fused, fused or skinny is not None)
         return y.view(*shp[:-1], weight.shape[0])
 
     @staticmethod

@@ -209,3 +209,23 @@ def test_gemm_ppw_matches_fp32(M, N, K, blocks, probe):
     _close(c, a.float() @ b.float().t(), 1e-2, f"ppw {M}x{N}x{K} blocks={blocks} probe={probe}")
     c2 = G.gemm_ppp(a, b, blocks=blocks, probe=probe, split=False)
     assert torch.equal(c, c2)
+
+
+@pytest.mark.parametrize("M,N,K", [
+    (65536, 1024, 1680),   # W&D MLP layer 1 forward: K = 26.25 k-tiles
+    (1000, 776, 200),      # partial k-tile of 8 columns + edge tiles in M and N
+    (512, 512, 136),       # two k-tiles, the second one 8 deep
+    (256, 512, 2056),      # split units whose last range ends in the partial k-tile
+])
+@pytest.mark.parametrize("form", ["ppp256", "ppp192", "split", "ppw", "ppw_nt"])
+def test_gemm_ppp_k_tail_matches_fp32(M, N, K, form):
+    """K % 64 != 0: the last k-tile's chunks past K are read as zeros on every kernel
+    form.  A and B are row-packed (lda = ldb = K), so what lies past K in a row is the
+    next row's data: reading it instead of zeros would show in C."""
+    from kubeflow_controller_amd.ops import gemm as G
+    torch.manual_seed(M + N + K + 9)
+    a, b = _bf(M, K), _bf(N, K, s=0.05)
+    kw = {"ppp256": dict(bn=256, split=False), "ppp192": dict(bn=192), "split": dict(bn=256),
+          "ppw": dict(probe=9, split=False), "ppw_nt": dict(probe=10, split=False)}[form]
+    c = G.gemm_ppp(a, b, **kw)
+    _close(c, a.float() @ b.float().t(), 1e-2, f"K-tail C {M}x{N}x{K} {form}")

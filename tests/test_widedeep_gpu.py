@@ -27,7 +27,7 @@ def test_wd_input_fwd_bwd_matches_torch(B, F, E, Dp):
 
 
 def test_wide_deep_step_fused_input_matches_unfused(monkeypatch):
-    """Same tiny W&D training steps with the fused input kernels and with the PyTorch chain."""
+    """Same tiny W&D training steps with the fused input / head kernels and with the PyTorch chain."""
     import copy
     from kubeflow_controller_amd.models import wide_deep as WD
     from kubeflow_controller_amd.trainer.engine import DistInfo, Engine
@@ -40,8 +40,47 @@ def test_wide_deep_step_fused_input_matches_unfused(monkeypatch):
     losses = {}
     for fused in (True, False):
         monkeypatch.setattr(WD, "FUSED_INPUT", fused)
+        monkeypatch.setattr(WD, "FUSED_HEAD", fused)
         eng = Engine(copy.deepcopy(base), WD.wide_deep_loss, optimizer="adam", lr=1e-2, channels_last=False,
                      dist_info=DistInfo(device=d))
         losses[fused] = [float(eng.train_step(*batch)) for _ in range(4)]
     for a, b in zip(losses[True], losses[False]):
         assert abs(a - b) < 2e-3 * max(1.0, abs(b)), losses
+
+
+@pytest.mark.parametrize("B,H,Dp", [(65536, 256, 16), (1000, 32, 8), (37, 512, 64), (8, 256, 0)])
+def test_wd_head_matches_fp32_reference(B, H, Dp):
+    """Fused output head + sigmoid cross-entropy (kfa_wd_head_fwd / _bwd) vs the plain
+    fp32 PyTorch chain it replaces: loss and every gradient."""
+    from kubeflow_controller_amd.models.wide_deep import _WDHeadFn
+    import torch.nn.functional as F
+    torch.manual_seed(B + H)
+    d = torch.device("cuda")
+    x = (torch.randn(B, H, device=d) * 0.5).to(torch.bfloat16).requires_grad_()
+    w = (torch.randn(1, H, device=d) * H ** -0.5).requires_grad_()
+    b = torch.randn(1, device=d).requires_grad_()
+    wide = torch.randn(B, device=d).requires_grad_()
+    dpad = torch.randn(B, Dp, device=d)
+    wd = (torch.randn(1, Dp, device=d) * 0.1).requires_grad_()
+    y = (torch.rand(B, device=d) < 0.3).float()
+    loss = _WDHeadFn.apply(x, w, b, wide, dpad, wd, y)
+    (loss * 3.0).backward()
+    xr = x.detach().float().requires_grad_()
+    wr, br, wider, wdr = (t.detach().clone().requires_grad_() for t in (w, b, wide, wd))
+    z = (xr @ wr.t()).squeeze(1) + br + wider + (dpad @ wdr.t()).squeeze(1)
+    ref = F.binary_cross_entropy_with_logits(z, y)
+    (ref * 3.0).backward()
+    torch.testing.assert_close(loss, ref, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=1e-6, rtol=1e-2)
+    torch.testing.assert_close(w.grad, wr.grad, atol=1e-5, rtol=1e-4)
+    torch.testing.assert_close(b.grad, br.grad, atol=1e-6, rtol=1e-4)
+    torch.testing.assert_close(wide.grad, wider.grad, atol=1e-7, rtol=1e-5)
+    if Dp:
+        torch.testing.assert_close(wd.grad, wdr.grad, atol=1e-5, rtol=1e-4)
+    # deterministic: a second run gives bit-identical loss and gradients
+    g1 = (w.grad.clone(), x.grad.clone())
+    w.grad = None
+    x.grad = None
+    loss2 = _WDHeadFn.apply(x, w, b, wide, dpad, wd, y)
+    (loss2 * 3.0).backward()
+    assert torch.equal(loss2, loss) and torch.equal(w.grad, g1[0]) and torch.equal(x.grad, g1[1])

@@ -70,6 +70,11 @@ def run(mode, transport, steps, batch, seq, model, timeout):
         print("\n-----\n".join(o[-2000:] for o in outs), file=sys.stderr)
         raise SystemExit(f"{mode}/{transport}: a replica failed")
     eps = [float(m.group(1)) for o in outs[1:] for m in re.finditer(r"Steady-state: .*?, ([\d.]+) examples/s", o)]
+    for o in outs[1:2]:  # worker 0's transport line (device / host per PS, and why)
+        for line in o.splitlines():
+            if "transport" in line:
+                print(f"    worker 0: {line.strip()[:200]}", file=sys.stderr, flush=True)
+                break
     return sum(eps), eps
 
 
@@ -80,12 +85,14 @@ def main():
     ap.add_argument("--seq", type=int, default=128)
     ap.add_argument("--model", default="bert_base")
     ap.add_argument("--timeout", type=float, default=240)
+    ap.add_argument("--modes", default="async:device,async:host,collective:-",
+                    help="comma list of mode:transport to run")
     a = ap.parse_args()
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     print(f"| mode ({a.model}, 2 workers + 1 PS on 1 GPU, batch {a.batch}/worker, seq {a.seq}) | "
           f"examples/s (sum) | per worker |", flush=True)
     print("|---|---|---|", flush=True)
-    for mode, tr in (("async", "device"), ("async", "host"), ("collective", "-")):
+    for mode, tr in (m.split(":") for m in a.modes.split(",")):
         tot, per = run(mode, tr, a.steps, a.batch, a.seq, a.model, a.timeout)
         print(f"| {mode} {tr} | {tot:.1f} | {', '.join(f'{x:.1f}' for x in per)} |", flush=True)
 

@@ -27,8 +27,30 @@ def timeit(fn, iters=20):
     return s.elapsed_time(e) / iters
 
 
+def stagger_sweep(d, shapes):
+    """KFA_PPP_STAGGER=1: odd blocks start late by 0 .. 12 us (the C-burst stagger experiment)."""
+    from kubeflow_controller_amd.ops import _lib
+    _lib.register("kfa_gemm_ppp_set_stagger", [_lib.I])
+    L = _lib.lib()
+    for M, N, K in shapes:
+        x = torch.randn(M, K, device=d).to(torch.bfloat16)
+        w = torch.randn(N, K, device=d).to(torch.bfloat16)
+        out = []
+        for ticks in (0, 300, 600, 900, 1200):
+            L.kfa_gemm_ppp_set_stagger(ticks)
+            t1 = min(timeit(lambda: G.gemm_ppp(x, w, bn=256, split=False)) for _ in range(3))
+            t2 = min(timeit(lambda: G.gemm_ppp(x, w, probe=9, split=False)) for _ in range(3))
+            out.append(f"{ticks * 10 / 1000:4.1f}us: ppp {t1 * 1e3:6.1f} ppw {t2 * 1e3:6.1f}")
+        L.kfa_gemm_ppp_set_stagger(0)
+        th = min(timeit(lambda: torch.mm(x, w.t())) for _ in range(3))
+        print(f"stagger {M}x{N}x{K} hipblaslt {th * 1e3:6.1f} | " + " | ".join(out), flush=True)
+
+
 def main():
     d = torch.device("cuda")
+    if os.environ.get("KFA_PPP_STAGGER") == "1":
+        stagger_sweep(d, [(32768, 3072, 768), (32768, 768, 3072), (32768, 2304, 768)])
+        return
     shapes = SHAPES
     if len(sys.argv) > 1:
         shapes = [tuple(int(v) for v in s.split("x")) for s in sys.argv[1:]]
@@ -49,7 +71,10 @@ def main():
                              ("ppp-nostore-nosplit", lambda: G.gemm_ppp(x, w, bn=256, probe=1, split=False)),
                              ("ppw", lambda: G.gemm_ppp(x, w, probe=9, split=False)),
                              ("ppw-nt", lambda: G.gemm_ppp(x, w, probe=10, split=False)),
-                             ("skinny", lambda: G.gemm_skinny(x, w)) if M <= 256 and N % 4 == 0 else ("-", lambda: None)):
+                             *([("skinny", lambda: G.gemm_skinny(x, w)), ("skinny-s2", lambda: G.gemm_skinny(x, w, splits=2)),
+                                ("skinny-s4", lambda: G.gemm_skinny(x, w, splits=4)),
+                                ("skinny-s8", lambda: G.gemm_skinny(x, w, splits=8))]
+                               if M <= 256 and N % 4 == 0 else [])):
                 res.setdefault(name, []).append(timeit(fn))
         ref = torch.mm(x, w.t()).float()
         err = max((G.gemm_ppp(x, w, bn=b).float() - ref).abs().max().item() for b in ((256, 192) if N % 192 == 0 else (256,)))

@@ -37,6 +37,32 @@ for s in $steps; do
     wd)
       log "Wide&Deep kernel trace"
       KFA_GEMM_TUNE_LOG=1 bash tools/gpu_prof_wd.sh 2> gpurun_out/wd_tune.err || exit 1 ;;
+    wdb)
+      log "Wide&Deep bench (unprofiled)"
+      timeout -k 10 300 python -u tools/bench_model.py --model wide_deep --batch 65536 --steps 30 --warmup 5 \
+        > gpurun_out/wdb.log 2> gpurun_out/wdb.err || { tail -30 gpurun_out/wdb.err; exit 1; }
+      tail -1 gpurun_out/wdb.log ;;
+    wdown)
+      log "Wide&Deep bench, own GEMMs on every covered shape (KFA_GEMM=own)"
+      KFA_GEMM=own KFA_GEMM_TUNE_LOG=1 timeout -k 10 300 python -u tools/bench_model.py --model wide_deep --batch 65536 \
+        --steps 30 --warmup 5 > gpurun_out/wdown.log 2> gpurun_out/wdown.err || { tail -30 gpurun_out/wdown.err; exit 1; }
+      tail -1 gpurun_out/wdown.log; grep "kfa gemm tune" gpurun_out/wdown.err | head -10 ;;
+    bertown)
+      log "BERT-base 256x128, own GEMMs on every covered shape (KFA_GEMM=own)"
+      KFA_GEMM=own KFA_GEMM_TUNE_LOG=1 timeout -k 10 300 python -u tools/bench_model.py --model bert_base --batch 256 \
+        --seq 128 --steps 20 --warmup 5 > gpurun_out/bertown.log 2> gpurun_out/bertown.err \
+        || { tail -30 gpurun_out/bertown.err; exit 1; }
+      tail -1 gpurun_out/bertown.log; grep "kfa gemm tune" gpurun_out/bertown.err | head -20 ;;
+    attn)
+      log "attention S=128: bwd D through LDS (PF=1) vs global scratch (PF=0)"
+      for v in 0 1 0 1; do
+        KFA_ATTN_PF=$v timeout -k 10 120 python -u tools/bench_attn.py 2>&1 | tee -a gpurun_out/attn.log | grep "attn PF" || exit 1
+      done ;;
+    stagger)
+      log "GEMM C-burst stagger sweep"
+      KFA_PPP_STAGGER=1 timeout -k 10 300 python -u tools/bench_ppp.py > gpurun_out/stagger.log 2>&1 \
+        || { tail -20 gpurun_out/stagger.log; exit 1; }
+      cat gpurun_out/stagger.log ;;
     ab)
       log "A/B conv wgrad side stream"
       bash tools/gpu_ab_env.sh "KFA_CONV_WGRAD_SIDE=0" "KFA_CONV_WGRAD_SIDE=1 KFA_CONV_OVERSUB=2" || exit 1 ;;
@@ -45,6 +71,17 @@ for s in $steps; do
       AB_ROUNDS=2 bash tools/gpu_ab_multi.sh "BASE=1" "KFA_CONV_WGRAD_SIDE=1 KFA_CONV_OVERSUB=2" \
         "KFA_WGRAD_WIDE64_ANY=1" "KFA_CONV_NARROW_LONGK=3" "KFA_CONV_BIG_AUTO_E=0" "KFA_POOL_BN_STATS=0 KFA_POOL_BWD4=0" \
         | tee gpurun_out/abm.log || exit 1 ;;
+    async)
+      log "async PS rehearsal (device transport), BERT-base 2w+1ps on one GPU"
+      timeout -k 10 400 python -u tools/async_rehearsal.py --modes async:device,collective:- 2>&1 \
+        | tee gpurun_out/async_rehearsal.log || exit 1 ;;
+    profb)
+      log "BERT-base kernel trace (HEAD)"
+      bash tools/gpu_prof_bert_head.sh || exit 1 ;;
+    abbert)
+      log "A/B/C BERT-base knobs"
+      AB_ROUNDS=2 AB_CMD="tools/bench_model.py --model bert_base --batch 256 --seq 128" bash tools/gpu_ab_multi.sh \
+        "BASE=1" "KFA_LN_BWD_DEEP=2" "KFA_GEMM=own" "KFA_ATTN_PF=0" | tee gpurun_out/abbert.log || exit 1 ;;
     gemm)
       log "GEMM shapes: hipBLASLt vs own"
       timeout -k 10 300 python -u tools/bench_ppp.py > gpurun_out/bench_ppp.log 2>&1 || { tail -20 gpurun_out/bench_ppp.log; exit 1; }
