@@ -3,8 +3,12 @@
 // [2048 x 1000] forward and data gradient; reference xw_plus_b of
 // mnist_replica.py:164-167 at the head of the network):
 //
-//   C[m][n] = bf16( Σ_k A[m][k] · B[n][k]  (+ bias[n]) )     M <= 256, A [M][lda], B [N][ldb]
+//   C[m][n] = bf16( Σ_k A[m][k] · B[n][k]  (+ bias[n]) )     A [M][lda], B [N][ldb]
 //
+// (Larger M runs as several 256-row bands, blockIdx.z: the same non-persistent
+// 256 x 64 tiles then serve the mid-size GEMMs whose 256 x 256 tiles would leave
+// most CUs idle — BERT's MLM transform 5120 x 768 x 768 has 60 of those, 240 of
+// these.)
 // With one 256-row band there are only ceil(N / 64) output tiles (16 for the
 // FC), far too few blocks for 256 CUs, and each tile's reduction (K = 2048) is
 // short.  So every tile's K is cut into S slices (S x tiles ~ the CU count):
@@ -54,8 +58,9 @@ __global__ __launch_bounds__(256, 2) void gemm_skinny_kernel(SkArgs g) {
   __shared__ __attribute__((aligned(16))) bf16_t smem[2 * (BM + BN) * BK];  // 80 KB: two k-steps of A and B
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int tile = blockIdx.x, slice = blockIdx.y;
-  const int n0 = tile * BN;
+  const int slice = blockIdx.y, band = blockIdx.z;
+  const int tile = band * gridDim.x + blockIdx.x;  // partial-slot / ticket index
+  const int n0 = blockIdx.x * BN, m0 = band * BM;
   const int kb = slice * g.kchunk;
   const int klen = min(g.kchunk, g.K - kb);
   const int nk = klen > 0 ? (klen + BK - 1) / BK : 0;
@@ -70,7 +75,7 @@ __global__ __launch_bounds__(256, 2) void gemm_skinny_kernel(SkArgs g) {
     const int row = 8 * (4 * i + wave) + lr;
     const int ck = (lane & 7) ^ ((row >> 1) & 7);
     a_ck[i] = ck * 8;
-    a_off[i] = row < g.M ? (row * g.lda + kb + ck * 8) * 2 : (int)kOOB;
+    a_off[i] = m0 + row < g.M ? ((m0 + row) * g.lda + kb + ck * 8) * 2 : (int)kOOB;
   }
 #pragma unroll
   for (int i = 0; i < 2; i++) {
@@ -175,7 +180,7 @@ __global__ __launch_bounds__(256, 2) void gemm_skinny_kernel(SkArgs g) {
     if (g.bias && nok) b = *reinterpret_cast<const float4*>(g.bias + n);
 #pragma unroll
     for (int mi = 0; mi < 4; mi++) {
-      const int m = wave * 64 + mi * 16 + fr;
+      const int m = m0 + wave * 64 + mi * 16 + fr;
       const floatx4 v = acc[ni][mi];
       uint2 o = make_uint2(pack2(v[0] + b.x, v[1] + b.y), pack2(v[2] + b.z, v[3] + b.w));
       const unsigned off = (m < g.M && nok) ? ((unsigned)m * (unsigned)g.ldc + (unsigned)n) * 2u : kOOB;
@@ -197,8 +202,9 @@ int sk_cus() {
 }
 
 // slices per tile: about one block per CU in total, each slice >= 2 k-steps
-void sk_plan(int N, int K, int want_splits, int& tiles, int& S, int& kchunk) {
-  tiles = (N + BN - 1) / BN;
+// (tiles = 256 x 64 output tiles over every 256-row band)
+void sk_plan(int M, int N, int K, int want_splits, int& tiles, int& S, int& kchunk) {
+  tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   const int nks = (K + BK - 1) / BK;
   S = want_splits > 0 ? want_splits : sk_cus() / tiles;
   if (S > nks / 2) S = nks / 2;
@@ -212,28 +218,28 @@ void sk_plan(int N, int K, int want_splits, int& tiles, int& S, int& kchunk) {
 
 // workspace bytes of kfa_gemm_skinny (counters, then the partial slots); 0: no split
 KFA_API long kfa_gemm_skinny_ws_bytes(int M, int N, int K, int splits) {
-  (void)M;
   int tiles, S, kc;
-  sk_plan(N, K, splits, tiles, S, kc);
+  sk_plan(M, N, K, splits, tiles, S, kc);
   if (S <= 1) return 0;
   return 4096 + (long)tiles * S * 16 * 256 * 16;
 }
 
-// C = A · Bᵀ (+ bias) for M <= 256; K % 8 == 0 (16-B DMA pieces), N % 4 == 0, strides % 8 == 0.
+// C = A · Bᵀ (+ bias); K % 8 == 0 (16-B DMA pieces), N % 4 == 0, strides % 8 == 0.
 // ws: kfa_gemm_skinny_ws_bytes bytes whose first 4096 are zero (the kernel leaves them zero).
 // splits: 0 = pick.  Returns 0, -1 on unsupported operands, -3 on a missing workspace.
 KFA_API int kfa_gemm_skinny(const bf16_t* A, const bf16_t* B, bf16_t* C, const float* bias, int M, int N, int K,
                             int lda, int ldb, int ldc, int splits, void* ws, long ws_bytes, hipStream_t st) {
   if (M <= 0 || N <= 0) return 0;
-  if (M > BM || K <= 0 || K % 8 || N % 4 || lda % 8 || ldb % 8 || ldc % 4 || lda < K || ldb < K || ldc < N) return -1;
+  if (K <= 0 || K % 8 || N % 4 || lda % 8 || ldb % 8 || ldc % 4 || lda < K || ldb < K || ldc < N) return -1;
   const long ab = ((long)(M - 1) * lda + K) * 2, bb = ((long)(N - 1) * ldb + K) * 2, cb = (long)M * ldc * 2;
   if (ab >= (long)kOOB || bb >= (long)kOOB || cb >= (long)kOOB) return -2;
   int tiles, S, kc;
-  sk_plan(N, K, splits, tiles, S, kc);
+  sk_plan(M, N, K, splits, tiles, S, kc);
   if ((long)tiles * S * 16 * 256 * 16 + 4096 > (1L << 40)) return -1;
   if (S > 1 && (ws == nullptr || ws_bytes < kfa_gemm_skinny_ws_bytes(M, N, K, splits) || tiles > 1024)) return -3;
   const SkArgs g{A, B, C, bias, M, N, K, lda, ldb, ldc, S, kc, (unsigned)ab, (unsigned)bb, (unsigned)cb,
                  S > 1 ? reinterpret_cast<float*>((char*)ws + 4096) : nullptr, S > 1 ? reinterpret_cast<int*>(ws) : nullptr};
-  hipLaunchKernelGGL(gemm_skinny_kernel, dim3(tiles, S), dim3(256), 0, st, g);
+  const int bands = (M + BM - 1) / BM;
+  hipLaunchKernelGGL(gemm_skinny_kernel, dim3(tiles / bands, S, bands), dim3(256), 0, st, g);
   return kfa_status();
 }

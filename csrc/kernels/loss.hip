@@ -132,6 +132,177 @@ __global__ __launch_bounds__(256) void argmax_kernel(const void* __restrict__ lo
   }
 }
 
+// ---- small classifier head + softmax cross-entropy (BERT's NSP: [B, H] x [2, H]ᵀ):
+//   logits[b][c] = x_b . W_c + bias_c,  loss = mean_b (logsumexp_c logits[b] - logits[b][y_b])
+// forward saves p = softmax(logits); backward with g[b][c] = dloss (p - [c == y_b]) / B:
+//   dx_b = Σ_c g[b][c] W_c (bf16),  dW_c = Σ_b g[b][c] x_b,  db_c = Σ_b g[b][c]
+// One 32-lane half-wave per row; per-block partials reduced in a fixed order.  C <= 8,
+// H % 8 == 0, H <= 1024.  Replaces an N = 2 hipBLASLt GEMM per direction + the loss chain.
+constexpr int kClsMaxC = 8, kClsMaxPieces = 4;  // H <= 32 lanes x 4 pieces x 8
+
+__device__ __forceinline__ int cls_blocks(int B) {
+  const int b = (B + 7) / 8;
+  return b < 256 ? b : 256;
+}
+
+template <int CM>
+__global__ __launch_bounds__(256) void cls_head_fwd(const bf16_t* __restrict__ x, const float* __restrict__ W,
+                                                    const float* __restrict__ bias, const long* __restrict__ y,
+                                                    float* __restrict__ prob, float* __restrict__ part, int B, int H,
+                                                    int C) {
+  __shared__ float red[8];
+  const int hw = threadIdx.x >> 5, l = threadIdx.x & 31, npc = H / 8;
+  float lsum = 0.f;
+  for (long b = (long)blockIdx.x * 8 + hw; b < B; b += (long)gridDim.x * 8) {
+    float z[CM];
+#pragma unroll
+    for (int c = 0; c < CM; c++) z[c] = 0.f;
+    for (int j = l; j < npc; j += 32) {
+      float f[8];
+      unpack8(*reinterpret_cast<const uint4*>(x + b * H + j * 8), f);
+#pragma unroll
+      for (int c = 0; c < CM; c++) {
+        if (c < C) {
+          const float4 w0 = *reinterpret_cast<const float4*>(W + (long)c * H + j * 8);
+          const float4 w1 = *reinterpret_cast<const float4*>(W + (long)c * H + j * 8 + 4);
+          z[c] += f[0] * w0.x + f[1] * w0.y + f[2] * w0.z + f[3] * w0.w + f[4] * w1.x + f[5] * w1.y + f[6] * w1.z +
+                  f[7] * w1.w;
+        }
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < CM; c++)
+#pragma unroll
+      for (int o = 16; o; o >>= 1) z[c] += __shfl_xor(z[c], o, 32);
+    if (l == 0) {
+      float mx = -3.0e38f;
+#pragma unroll
+      for (int c = 0; c < CM; c++)
+        if (c < C) {
+          z[c] += bias[c];
+          mx = fmaxf(mx, z[c]);
+        }
+      float se = 0.f;
+#pragma unroll
+      for (int c = 0; c < CM; c++)
+        if (c < C) se += expf(z[c] - mx);
+      const float lse = mx + logf(se);
+      const long yy = y[b];
+      float zy = 0.f;
+#pragma unroll
+      for (int c = 0; c < CM; c++)
+        if (c < C) {
+          prob[b * C + c] = expf(z[c] - lse);
+          if (c == yy) zy = z[c];
+        }
+      lsum += lse - zy;
+    }
+  }
+  if (l == 0) red[hw] = lsum;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int i = 0; i < 8; i++) t += red[i];
+    part[blockIdx.x] = t;
+  }
+}
+
+// loss[0] = sum(part[0..n)) / B, fixed order (one block)
+__global__ __launch_bounds__(256) void cls_head_loss(const float* __restrict__ part, int n, int B,
+                                                     float* __restrict__ loss) {
+  __shared__ float red[256];
+  float t = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) t += part[i];
+  red[threadIdx.x] = t;
+  __syncthreads();
+  for (int o = 128; o; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) loss[0] = red[0] / (float)B;
+}
+
+// part: [gridDim.x][C * H + C] = per-block (dW | db)
+template <int CM>
+__global__ __launch_bounds__(256) void cls_head_bwd(const bf16_t* __restrict__ x, const float* __restrict__ W,
+                                                    const long* __restrict__ y, const float* __restrict__ prob,
+                                                    const float* __restrict__ dloss, bf16_t* __restrict__ dx,
+                                                    float* __restrict__ part, int B, int H, int C) {
+  extern __shared__ float sh[];  // [8][C * H + C]
+  const int hw = threadIdx.x >> 5, l = threadIdx.x & 31, npc = H / 8, WC = C * H + C;
+  const float gs = dloss[0] / (float)B;
+  float acc[CM][kClsMaxPieces][8] = {};
+  float bacc[CM] = {};
+  for (long b = (long)blockIdx.x * 8 + hw; b < B; b += (long)gridDim.x * 8) {
+    const long yy = y[b];
+    float g[CM];
+#pragma unroll
+    for (int c = 0; c < CM; c++) {
+      g[c] = c < C ? gs * (prob[b * C + c] - (c == yy ? 1.f : 0.f)) : 0.f;
+      bacc[c] += g[c];
+    }
+#pragma unroll
+    for (int q = 0; q < kClsMaxPieces; q++) {
+      const int j = l + 32 * q;
+      if (j < npc) {
+        float f[8], o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        unpack8(*reinterpret_cast<const uint4*>(x + b * H + j * 8), f);
+#pragma unroll
+        for (int c = 0; c < CM; c++) {
+          if (c < C) {
+#pragma unroll
+            for (int e = 0; e < 8; e++) {
+              acc[c][q][e] += g[c] * f[e];
+              o[e] += g[c] * W[(long)c * H + j * 8 + e];
+            }
+          }
+        }
+        *reinterpret_cast<uint4*>(dx + b * H + j * 8) = pack8(o);
+      }
+    }
+  }
+  float* mine = sh + hw * WC;
+#pragma unroll
+  for (int c = 0; c < CM; c++) {
+    if (c < C) {
+#pragma unroll
+      for (int q = 0; q < kClsMaxPieces; q++) {
+        const int j = l + 32 * q;
+        if (j < npc)
+#pragma unroll
+          for (int e = 0; e < 8; e++) mine[c * H + j * 8 + e] = acc[c][q][e];
+      }
+      if (l == 0) mine[C * H + c] = bacc[c];
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < WC; i += 256) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; k++) t += sh[k * WC + i];
+    part[(long)blockIdx.x * WC + i] = t;
+  }
+}
+
+// out[c] = sum over n partial rows of part[i][c], fixed order (16 columns x 16 row groups per block)
+__global__ __launch_bounds__(256) void cls_head_reduce(const float* __restrict__ part, int n, int W,
+                                                       float* __restrict__ out) {
+  __shared__ float red[16][17];
+  const int cl = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
+  float t = 0.f;
+  if (c < W)
+    for (int i = g; i < n; i += 16) t += part[(long)i * W + c];
+  red[g][cl] = t;
+  __syncthreads();
+  if (g == 0 && c < W) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; k++) s += red[k][cl];
+    out[c] = s;
+  }
+}
+
 }  // namespace
 
 KFA_API int kfa_softmax_xent(const void* logits, int logits_bf16, const long* labels, const float* bias,
@@ -153,5 +324,41 @@ KFA_API int kfa_argmax(const void* logits, int logits_bf16, long* out, long rows
     hipLaunchKernelGGL(argmax_kernel<true>, dim3(rows), dim3(256), 0, s, logits, out, V);
   else
     hipLaunchKernelGGL(argmax_kernel<false>, dim3(rows), dim3(256), 0, s, logits, out, V);
+  return kfa_status();
+}
+
+// blocks of the classifier-head kernels for B rows (partial rows of the backward)
+KFA_API int kfa_cls_head_blocks(int B) { return (B + 7) / 8 < 256 ? (B + 7) / 8 : 256; }
+
+// x [B][H] bf16, W [C][H] fp32, bias [C] fp32, labels [B] int64 -> prob [B][C] fp32, loss (one float);
+// part: kfa_cls_head_blocks(B) floats.  C <= 8, H % 8 == 0, H <= 1024.
+KFA_API int kfa_cls_head_fwd(const bf16_t* x, const float* W, const float* bias, const long* y, float* prob, float* part,
+                             float* loss, int B, int H, int C, hipStream_t st) {
+  if (B <= 0 || C <= 0 || C > kClsMaxC || H % 8 || H > 8 * 32 * kClsMaxPieces) return -1;
+  const int nb = kfa_cls_head_blocks(B);
+  if (C <= 2) hipLaunchKernelGGL(cls_head_fwd<2>, dim3(nb), dim3(256), 0, st, x, W, bias, y, prob, part, B, H, C);
+  else hipLaunchKernelGGL(cls_head_fwd<kClsMaxC>, dim3(nb), dim3(256), 0, st, x, W, bias, y, prob, part, B, H, C);
+  hipLaunchKernelGGL(cls_head_loss, dim3(1), dim3(256), 0, st, part, nb, B, loss);
+  return kfa_status();
+}
+
+// dx [B][H] bf16 (written); grads [C * H + C] fp32 = (dW | db) (written); part: blocks x (C*H + C) floats.
+// C * H <= 4096 (the per-block LDS image of 8 half-waves' partials: 8 x (C·H + C) floats <= 131 KB)
+KFA_API int kfa_cls_head_bwd(const bf16_t* x, const float* W, const long* y, const float* prob, const float* dloss,
+                             bf16_t* dx, float* part, float* grads, int B, int H, int C, hipStream_t st) {
+  if (B <= 0 || C <= 0 || C > kClsMaxC || H % 8 || H > 8 * 32 * kClsMaxPieces || C * H > 4096) return -1;
+  const int nb = kfa_cls_head_blocks(B), WC = C * H + C;
+  const size_t lds = (size_t)8 * WC * 4;
+  if (lds > 65536) {
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&cls_head_bwd<kClsMaxC>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 8 * (4096 + kClsMaxC) * 4);
+      attr = true;
+    }
+  }
+  if (C <= 2) hipLaunchKernelGGL(cls_head_bwd<2>, dim3(nb), dim3(256), lds, st, x, W, y, prob, dloss, dx, part, B, H, C);
+  else hipLaunchKernelGGL(cls_head_bwd<kClsMaxC>, dim3(nb), dim3(256), lds, st, x, W, y, prob, dloss, dx, part, B, H, C);
+  hipLaunchKernelGGL(cls_head_reduce, dim3((WC + 15) / 16), dim3(256), 0, st, part, nb, WC, grads);
   return kfa_status();
 }

@@ -622,6 +622,53 @@ __global__ __launch_bounds__(256) void embed_bwd_fold_kernel(const long* __restr
   }
 }
 
+// Gradient of a SMALL table (R <= 512 rows: BERT's position and segment
+// embeddings) — grad[ids[r]] += dout[r] — without global atomics per element
+// (a handful of hot rows serialise them) and without the one-hot GEMM:
+// block (column group of 64, token chunk) accumulates its chunk's rows in an
+// LDS image [R][64] fp32 (lane = column: one wave-instruction adds one token
+// row's 128 B, 64 distinct banks), marks the ids it touched, then adds only the
+// touched rows into the fp32 gradient (one atomic per element per block).
+constexpr int kSmallTabMaxRows = 512;
+
+__global__ __launch_bounds__(256) void embed_small_bwd_kernel(const long* __restrict__ ids,
+                                                              const bf16_t* __restrict__ dout, long dstride,
+                                                              float* __restrict__ grad, long n, int D, int R,
+                                                              long rows_per_block) {
+  extern __shared__ float acc[];  // [R][64], then R touched flags
+  int* touched = reinterpret_cast<int*>(acc + R * 64);
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int c0 = blockIdx.x * 64;
+  for (int i = t; i < R * 64; i += 256) acc[i] = 0.f;
+  for (int i = t; i < R; i += 256) touched[i] = 0;
+  __syncthreads();
+  const long r0 = (long)blockIdx.y * rows_per_block, r1 = min(n, r0 + rows_per_block);
+  const bool live = c0 + lane < D;
+  // 4 rows per wave in flight: ids and values loaded before the LDS adds
+  for (long r = r0 + w; r < r1; r += 16) {
+    long id[4];
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const long rr = r + 4 * j;
+      id[j] = rr < r1 ? ids[rr] : -1;
+      v[j] = (rr < r1 && live) ? bf2f(dout[rr * dstride + c0 + lane]) : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      if (id[j] >= 0 && id[j] < R) {  // wave-uniform
+        atomicAdd(acc + id[j] * 64 + lane, v[j]);
+        if (lane == 0) touched[id[j]] = 1;
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = t; i < R * 64; i += 256) {
+    const int row = i >> 6, c = c0 + (i & 63);
+    if (touched[row] && c < D) atomicAdd(grad + (long)row * D + c, acc[i]);
+  }
+}
+
 int grid_for(long nvec) {
   long g = (nvec + 255) / 256;
   return (int)(g < 1 ? 1 : (g > 8192 ? 8192 : g));
@@ -867,6 +914,50 @@ KFA_API int kfa_embed_fwd(const long* i0, const void* t0, const long* i1, const 
 }
 
 // scratch: zero-initialised fp32 [rows_of_table, D], left zeroed on return.
+// dst (bf16 or fp32) += src (fp32); src zeroed (the scratch of kfa_embed_small_bwd for a bf16 gradient)
+__global__ __launch_bounds__(256) void fold_f32_kernel(float* __restrict__ src, void* __restrict__ dst, int dst_f32,
+                                                       long n) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const float v = src[i];
+    src[i] = 0.f;
+    if (dst_f32) {
+      reinterpret_cast<float*>(dst)[i] += v;
+    } else {
+      bf16_t* g = reinterpret_cast<bf16_t*>(dst) + i;
+      *g = (bf16_t)f2bf(bf2f(*g) + v);
+    }
+  }
+}
+
+KFA_API int kfa_fold_f32(float* src, void* dst, int dst_f32, long n, hipStream_t s) {
+  if (n <= 0) return 0;
+  const long b = (n + 255) / 256;
+  hipLaunchKernelGGL(fold_f32_kernel, dim3((unsigned)(b < 2048 ? b : 2048)), dim3(256), 0, s, src, dst, dst_f32, n);
+  return kfa_status();
+}
+
+// grad [R][D] fp32 (+)= sum of dout rows by id, R <= 512 (ids outside [0, R) skipped)
+KFA_API int kfa_embed_small_bwd(const long* ids, const void* dout, long dstride, float* grad, long n, int D, int R,
+                                hipStream_t s) {
+  if (n <= 0) return 0;
+  if (R <= 0 || R > kSmallTabMaxRows || D <= 0 || !ids) return -1;
+  const int cg = (D + 63) / 64;
+  long chunks = 128 / cg;
+  if (chunks < 1) chunks = 1;
+  if (chunks > (n + 63) / 64) chunks = (n + 63) / 64;
+  const long rpb = (n + chunks - 1) / chunks;
+  const size_t lds = (size_t)R * 64 * 4 + (size_t)R * 4;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&embed_small_bwd_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)((size_t)kSmallTabMaxRows * 65 * 4));
+    attr = true;
+  }
+  hipLaunchKernelGGL(embed_small_bwd_kernel, dim3(cg, (unsigned)chunks), dim3(256), lds, s, ids, (const bf16_t*)dout,
+                     dstride, grad, n, D, R, rpb);
+  return kfa_status();
+}
+
 KFA_API int kfa_embed_bwd(const long* ids, const void* dout, long dstride, float* scratch, void* grad, int grad_f32,
                           long n, int D, int accumulate, hipStream_t s) {
   if (n <= 0 || D % 8 || dstride % 8) return -1;

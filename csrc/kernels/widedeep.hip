@@ -194,19 +194,33 @@ __global__ __launch_bounds__(256) void wd_head_bwd(const bf16_t* __restrict__ x,
   }
 }
 
-// out[c] = sum over n blocks of part[blk][c] (fixed order), c < W
+// out[c] = sum over n blocks of part[blk][c] in a fixed order, c < W: block = 16
+// columns x 16 row groups; thread (row group g, column) sums partial rows g, g+16,
+// ... and the 16 group sums meet in LDS in group order (a single thread per column
+// walking all n partials was 235 us: n dependent loads)
 __global__ __launch_bounds__(256) void wd_head_reduce(const float* __restrict__ part, int n, int W,
                                                       float* __restrict__ out) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= W) return;
+  __shared__ float red[16][17];
+  const int cl = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
   float t = 0.f;
-  for (int i = 0; i < n; i++) t += part[(long)i * W + c];
-  out[c] = t;
+  if (c < W)
+    for (int i = g; i < n; i += 16) t += part[(long)i * W + c];
+  red[g][cl] = t;
+  __syncthreads();
+  if (g == 0 && c < W) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; k++) s += red[k][cl];
+    out[c] = s;
+  }
 }
 
+// blocks of the head kernels: 8 rows per block-iteration, at most 256 blocks (the
+// backward's partial rows: 256 x (H + Dp + 1) floats)
 int head_blocks(int B) {
   const int b = (B + kHeadRowsPerBlock - 1) / kHeadRowsPerBlock;
-  return b < 1024 ? b : 1024;
+  return b < 256 ? b : 256;
 }
 
 int blocks_for(long n) {
@@ -247,7 +261,7 @@ KFA_API int kfa_wd_head_bwd(const bf16_t* x, const float* w, const float* dpad, 
   const int nb = head_blocks(B), W = H + Dp + 1;
   hipLaunchKernelGGL(wd_head_bwd, dim3(nb), dim3(256), kHeadRowsPerBlock * W * 4, st, x, w, dpad, pmy, dloss, dx,
                      dwide, part, B, H, Dp);
-  hipLaunchKernelGGL(wd_head_reduce, dim3((W + 255) / 256), dim3(256), 0, st, part, nb, W, grads);
+  hipLaunchKernelGGL(wd_head_reduce, dim3((W + 15) / 16), dim3(256), 0, st, part, nb, W, grads);
   return kfa_status();
 }
 

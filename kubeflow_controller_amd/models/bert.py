@@ -26,7 +26,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import transformer as T
-from ..ops.loss import cross_entropy
+from ..ops.loss import classifier_xent
 
 
 @dataclass
@@ -175,8 +175,7 @@ class BertForPreTraining(nn.Module):
         # NSP on [CLS]
         cls_rows = torch.arange(B, device=dev) * S
         pooled = T.dense(h.index_select(0, cls_rows), self.pool_w, self.pool_b, "tanh")
-        nsp_logits = torch.mm(pooled, self.nsp_w.t()).float() + self.nsp_b
-        nsp = cross_entropy(nsp_logits, nsp_labels)
+        nsp = classifier_xent(pooled.contiguous(), self.nsp_w, self.nsp_b, nsp_labels)  # fused 2-way head + loss
         return mlm + nsp
 
     def forward_reference(self, input_ids, token_type_ids, attention_mask, mlm_positions, mlm_labels, nsp_labels):

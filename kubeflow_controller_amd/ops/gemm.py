@@ -39,16 +39,17 @@ _lib.register("kfa_gemm_skinny_ws_bytes", [I] * 4, restype=_lib.L)
 
 ACTS = {None: 0, "none": 0, "gelu": 1, "tanh": 2, "relu": 3}
 # Which dense-layer GEMMs run on this kernel (KFA_GEMM):
-#   "auto"   (default) the Linear layers (``DenseFn``: ResNet FC, MLP heads, W&D
-#            MLP) pick own-vs-library per shape, timed once at first use
-#            (:func:`prefer_own`); the BERT encoder projections stay on the library;
+#   "auto"   (default) every shape picks own-vs-library per shape, timed once at
+#            first use (an own kernel must beat hipBLASLt by 1 %);
+#   "own"    every shape an own kernel covers runs on the fastest OWN kernel
+#            (persistent / wave-specialised / skinny GEMMs); hipBLASLt is timed for
+#            the tuner log only.  Same box, 2 rounds: BERT-base 8,879-9,003 vs
+#            9,223-9,228 seq/s with "auto" (the FFN forward GEMMs lose 10-15 % to
+#            hipBLASLt); W&D 27.66 vs 27.71 M ex/s;
 #   "1"      every projection (forward and dgrad), encoder layers included;
 #   "fused"  only the ones whose epilogue replaces a separate pass: the FFN-up
 #            forward (bias + GELU + pre-activation) and its dgrad (GELU' +
 #            bias-gradient column sums);
-#   "own"    as "auto", but the fastest OWN kernel is taken on every shape the
-#            own kernels cover, even where hipBLASLt times faster (A/B runs:
-#            what an all-own GEMM path costs end to end);
 #   "0"      none (hipBLASLt via torch.mm / addmm for all of them).
 # Measured on MI355X (tools/bench_gemm.py, tools/gpu_bert_gemm.sh; docs/kernels.md).
 _ROUTE = os.environ.get("KFA_GEMM", "auto")
@@ -181,20 +182,25 @@ def gemm_ppp(a, b, *, out=None, blocks: int = 0, probe: int = 0, bn: int = 0, sp
     return c
 
 
+SKINNY_MAX_M = 16384  # the 256 x 64-tile kernel is a tuner candidate up to this many rows
+
+
 def skinny_ok(a, b) -> bool:
-    """Operands :func:`gemm_skinny` takes: M <= 256, N % 4 == 0 (bf16, K-contiguous)."""
+    """Operands :func:`gemm_skinny` takes: N % 4 == 0 (bf16, K-contiguous); tuned for
+    M <= SKINNY_MAX_M (one 256-row band for the ResNet FC, a few dozen for BERT's MLM head)."""
     return (a.is_cuda and b.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16
-            and a.dim() == 2 and b.dim() == 2 and a.shape[1] == b.shape[1] and 0 < a.shape[0] <= 256
+            and a.dim() == 2 and b.dim() == 2 and a.shape[1] == b.shape[1] and 0 < a.shape[0] <= SKINNY_MAX_M
             and a.shape[1] % 8 == 0 and b.shape[0] % 4 == 0 and a.stride(1) == 1 and b.stride(1) == 1
             and a.stride(0) % 8 == 0 and b.stride(0) % 8 == 0 and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0
             and b.shape[0] * b.stride(0) * 2 < (1 << 31))
 
 
 def gemm_skinny(a, b, bias=None, *, splits: int = 0, out=None):
-    """``a @ b.T (+ bias)`` (bf16 out, fp32 bias) for M <= 256 on the split-K skinny
-    kernel (``csrc/kernels/gemm_skinny.hip``): 256 x 64 output tiles, the reduction
-    cut into slices run by separate blocks, partials summed in slice order by the
-    last-arriving slice of each tile.  ``splits`` 0 = about one block per CU."""
+    """``a @ b.T (+ bias)`` (bf16 out, fp32 bias) on the split-K skinny kernel
+    (``csrc/kernels/gemm_skinny.hip``): 256 x 64 output tiles over 256-row bands, the
+    reduction cut into slices run by separate blocks when there are few tiles,
+    partials summed in slice order by the last-arriving slice of each tile.
+    ``splits`` 0 = about one block per CU."""
     if not skinny_ok(a, b):
         raise ValueError(f"gemm_skinny: unsupported operands {tuple(a.shape)} x {tuple(b.shape)}")
     M, K = a.shape
@@ -214,11 +220,14 @@ def skinny_splits(a, b):
     the kernel's own pick (about one block per CU) and fixed 4 / 8 slices — fewer
     slices leave the last-arriving slice less partial data to sum."""
     M, K = a.shape
+    N = b.shape[0]
     nks = K // 64
+    tiles = -(-M // 256) * -(-N // 64)
     out = [("skinny", 0)]
-    for s in (4, 8):
-        if 2 * s <= nks:
-            out.append((f"skinny-s{s}", s))
+    if tiles * 8 <= 256:  # fixed splits only where the tiles alone leave most CUs idle
+        for s in (4, 8):
+            if 2 * s <= nks:
+                out.append((f"skinny-s{s}", s))
     return out
 
 
@@ -288,6 +297,8 @@ def mm_auto(a, w, kind: str = "proj"):
     ``KFA_GEMM=0`` forces the library."""
     if ROUTE_AUTO and ppp_ok(a, w):
         cands = [("hipblaslt", lambda: torch.mm(a, w.t()))] + _ppp_candidates(a, w)
+        if skinny_ok(a, w):
+            cands += [(n, (lambda s: lambda: gemm_skinny(a, w, splits=s))(s)) for n, s in skinny_splits(a, w)]
         i = pick_fastest(kind, (a.shape[0], w.shape[0], a.shape[1]), a.device, cands)
         if i:
             return cands[i][1]()

@@ -16,6 +16,9 @@ from . import _lib
 _lib.register("kfa_softmax_xent", [_lib.P, _lib.I, _lib.P, _lib.P, _lib.P, _lib.P, _lib.L, _lib.I, _lib.F, _lib.F,
                                     _lib.P])
 _lib.register("kfa_argmax", [_lib.P, _lib.I, _lib.P, _lib.L, _lib.I, _lib.P])
+_lib.register("kfa_cls_head_blocks", [_lib.I])
+_lib.register("kfa_cls_head_fwd", [_lib.P] * 7 + [_lib.I] * 3 + [_lib.P])
+_lib.register("kfa_cls_head_bwd", [_lib.P] * 8 + [_lib.I] * 3 + [_lib.P])
 
 
 class _XentFn(torch.autograd.Function):
@@ -47,6 +50,54 @@ def cross_entropy(logits: torch.Tensor, labels: torch.Tensor, label_smoothing: f
     if logits.dtype not in (torch.bfloat16, torch.float32):
         logits = logits.float()
     return _XentFn.apply(logits, labels, label_smoothing)
+
+
+class _ClsHeadXentFn(torch.autograd.Function):
+    """``mean CE(x @ W.T + b, labels)`` for a small classifier (C <= 8 classes,
+    e.g. BERT's NSP head) in one HIP pass each way (``csrc/kernels/loss.hip``
+    ``cls_head_*``): no N = C GEMM on the library, no logits tensor."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, labels):
+        B, H = x.shape
+        C = w.shape[0]
+        w32 = w.detach().float().contiguous()
+        b32 = b.detach().float().reshape(-1).contiguous()
+        y = labels.reshape(-1).to(torch.int64).contiguous()
+        prob = torch.empty(B, C, dtype=torch.float32, device=x.device)
+        part = torch.empty(_lib.lib().kfa_cls_head_blocks(B), dtype=torch.float32, device=x.device)
+        loss = torch.empty((), dtype=torch.float32, device=x.device)
+        _lib.call("kfa_cls_head_fwd", _lib.ptr(x), _lib.ptr(w32), _lib.ptr(b32), _lib.ptr(y), _lib.ptr(prob),
+                  _lib.ptr(part), _lib.ptr(loss), B, H, C, _lib.stream())
+        ctx.save_for_backward(x, w32, y, prob)
+        ctx.meta = (w.shape, w.dtype, b.shape, b.dtype)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w32, y, prob = ctx.saved_tensors
+        wshape, wdt, bshape, bdt = ctx.meta
+        B, H = x.shape
+        C = w32.shape[0]
+        dl = g.detach().float().reshape(1).contiguous()
+        dx = torch.empty_like(x)
+        nb = _lib.lib().kfa_cls_head_blocks(B)
+        part = _lib.workspace(4 * nb * (C * H + C), x.device, "cls_head_part")
+        grads = torch.empty(C * H + C, dtype=torch.float32, device=x.device)
+        _lib.call("kfa_cls_head_bwd", _lib.ptr(x), _lib.ptr(w32), _lib.ptr(y), _lib.ptr(prob), _lib.ptr(dl), _lib.ptr(dx),
+                  _lib.ptr(part), _lib.ptr(grads), B, H, C, _lib.stream())
+        return dx, grads[:C * H].view(wshape).to(wdt), grads[C * H:].view(bshape).to(bdt), None
+
+
+def classifier_xent(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+    """Mean softmax cross-entropy of the classifier ``x @ w.T + b`` (fp32 scalar):
+    the fused HIP head for bf16 ``x`` with C <= 8 classes, else the PyTorch ops."""
+    if (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 2 and x.is_contiguous() and x.data_ptr() % 16 == 0
+            and 0 < w.shape[0] <= 8 and x.shape[1] % 8 == 0 and x.shape[1] <= 1024 and w.shape[1] == x.shape[1]
+            and w.shape[0] * x.shape[1] <= 4096):  # the backward's per-block LDS image: 8 x (C·H + C) floats
+        return _ClsHeadXentFn.apply(x, w, b, labels)
+    logits = x.float() @ w.float().t() + b.float()
+    return torch.nn.functional.cross_entropy(logits, labels.reshape(-1))
 
 
 class _ClippedSumXentFn(torch.autograd.Function):

@@ -53,6 +53,8 @@ _lib.register("kfa_attn_softmax_bwd", [P, P, L, I, Fl, U64, P])
 _lib.register("kfa_embed_fwd", [P, P, P, P, P, P, I, P, L, I, L, P])
 _lib.register("kfa_embed_bwd", [P, P, L, P, P, I, L, I, I, P])
 _lib.register("kfa_colsum", [P, P, P, L, I, I, P])
+_lib.register("kfa_embed_small_bwd", [P, P, _lib.L, P, _lib.L, I, I, P])
+_lib.register("kfa_fold_f32", [P, P, I, _lib.L, P])
 _lib.register("kfa_attn_fwd", [P, P, P, P, P, I, I, I, I, Fl, Fl, U64, P])
 _lib.register("kfa_attn_bwd", [P, P, P, P, P, P, P, P, I, I, I, I, Fl, Fl, U64, P, P])
 
@@ -61,6 +63,9 @@ FUSED_ATTN = os.environ.get("KFA_FUSED_ATTN", "1") != "0"
 
 ACTS = {None: 0, "none": 0, "gelu": 1, "tanh": 2, "relu": 3}
 SMALL_TABLE_ROWS = 1024
+# tables of <= 512 rows (BERT position / segment): kfa_embed_small_bwd instead of the
+# one-hot GEMM (KFA_EMB_SMALL=0 restores it)
+EMB_SMALL_KERNEL = os.environ.get("KFA_EMB_SMALL", "1") != "0"
 _MASK64 = (1 << 64) - 1
 
 
@@ -374,7 +379,18 @@ class EmbeddingSumFn(torch.autograd.Function):
                 grads.append(None)
                 continue
             g, _, direct = _grad_target(t)
-            if t.shape[0] <= SMALL_TABLE_ROWS:
+            if (EMB_SMALL_KERNEL and t.shape[0] <= 512 and g.dtype in (torch.float32, torch.bfloat16)
+                    and g.is_contiguous() and ids[k].dtype == torch.int64):
+                # LDS-accumulated per (column group, token chunk), touched rows added once per block;
+                # a bf16 gradient goes through a zeroed fp32 scratch folded in after
+                R = t.shape[0]
+                dst = g if g.dtype == torch.float32 else \
+                    _lib.workspace(R * D * 4, t.device, f"embed_small_scratch{k}").view(torch.float32)
+                _lib.call("kfa_embed_small_bwd", _lib.ptr(ids[k]), _lib.ptr(dout), D, _lib.ptr(dst), n, D, R,
+                          _lib.stream())
+                if dst is not g:
+                    _lib.call("kfa_fold_f32", _lib.ptr(dst), _lib.ptr(g), 0, R * D, _lib.stream())
+            elif t.shape[0] <= SMALL_TABLE_ROWS:
                 # few rows, many duplicates (position / segment tables): atomics would
                 # serialise on a handful of addresses; a one-hot GEMM (MFMA) reduces them
                 oh = torch.zeros(n, t.shape[0], dtype=dout.dtype, device=dout.device)
@@ -412,12 +428,18 @@ def _attn_biases(bqkv, key_bias, W3, T_, dev):
     """The kernels always read both biases (no branches around their prologue
     loads): absent ones become zeros."""
     if bqkv is None:
-        bqkv = torch.zeros(W3, dtype=torch.float32, device=dev)
+        bqkv = _zeros_f32(W3, dev)
     elif bqkv.dtype != torch.float32 or bqkv.numel() != W3 or not bqkv.is_contiguous():
         raise ValueError("attention: bqkv must be a contiguous fp32 [3H] vector")
-    if key_bias is None:
-        key_bias = torch.zeros(T_, dtype=torch.float32, device=dev)
+    if key_bias is None:  # no padding mask: one cached zero vector, not a fill kernel per call
+        key_bias = _zeros_f32(T_, dev)
     return bqkv, key_bias
+
+
+def _zeros_f32(n: int, dev) -> torch.Tensor:
+    """A read-only fp32 zero vector of ``n`` elements (grow-only workspace that no kernel
+    writes: the zero-initialised buffer stays zero)."""
+    return _lib.workspace(4 * n, dev, "const_zeros_f32").view(torch.float32)[:n]
 
 
 def attn_fwd(qkv, bqkv, key_bias, B, S, heads, p=0.0, seed=0):

@@ -194,7 +194,7 @@ def test_dense_auto_route_matches_fp32(monkeypatch):
     assert err < 3e-2, err
 
 
-@pytest.mark.parametrize("pick", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("pick", [0, 1, 2, 3, 4, 99])  # 99: the last candidate (skinny)
 def test_dense_every_route_matches_fp32(monkeypatch, pick):
     """Each DenseFn forward candidate (hipBLASLt + bias/act pass, fused-epilogue GEMM,
     persistent GEMM variants + bias/act pass) and each dgrad candidate, forced."""

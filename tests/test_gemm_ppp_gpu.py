@@ -152,10 +152,14 @@ def test_gemm_ppp_split_under_cu_hog():
     (100, 64, 520, 3, False),      # M < 256, uneven slices, k tail
     (256, 4, 8, 0, True),          # tiny
     (200, 1024, 4096, 16, False),  # many slices
+    (5120, 768, 768, 0, True),     # BERT MLM transform: 20 row bands x 12 tiles, no split
+    (1000, 200, 2048, 0, False),   # 4 bands (partial last), split slices over bands
+    (777, 96, 3000, 2, True),      # partial band, partial tile, k tail, 2 slices
 ])
 def test_gemm_skinny_matches_fp32(M, N, K, splits, bias):
     """Split-K skinny GEMM (csrc/kernels/gemm_skinny.hip): partials of K slices summed by
-    the last-arriving slice in slice order (bit-identical run to run), bias fused."""
+    the last-arriving slice in slice order (bit-identical run to run), bias fused;
+    M > 256 as several 256-row bands."""
     from kubeflow_controller_amd.ops import gemm as G
     torch.manual_seed(M + N + K)
     a, b = _bf(M, K), _bf(N, K, s=0.05)

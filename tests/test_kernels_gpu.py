@@ -335,3 +335,31 @@ def test_clipped_sum_xent_matches_fp32(dtype):
     torch.testing.assert_close(zz.grad.double().cpu(), zr.grad, atol=2e-2 if dtype == torch.bfloat16 else 1e-5,
                                rtol=2e-2 if dtype == torch.bfloat16 else 1e-4)
     assert float(zz.grad[5].float().abs().sum()) == 0.0
+
+
+@pytest.mark.parametrize("B,H,C", [(256, 768, 2), (37, 64, 5), (1000, 512, 8), (3, 8, 1)])
+def test_classifier_head_xent_matches_fp32(B, H, C):
+    """Fused small-classifier head + softmax CE (kfa_cls_head_fwd / _bwd, BERT's NSP)
+    vs the plain fp32 PyTorch chain: loss, dx, dW, db; bit-identical on a rerun."""
+    import torch.nn.functional as F
+    from kubeflow_controller_amd.ops.loss import classifier_xent
+    torch.manual_seed(B + H + C)
+    d = torch.device("cuda")
+    x = torch.randn(B, H, device=d).to(torch.bfloat16).requires_grad_()
+    w = (torch.randn(C, H, device=d) * H ** -0.5).to(torch.bfloat16).requires_grad_()
+    b = torch.randn(C, device=d).requires_grad_()
+    y = torch.randint(0, C, (B,), device=d)
+    loss = classifier_xent(x, w, b, y)
+    (loss * 2.0).backward()
+    xr, wr, br = (t.detach().float().requires_grad_() for t in (x, w, b))
+    ref = F.cross_entropy(xr @ wr.t() + br, y)
+    (ref * 2.0).backward()
+    torch.testing.assert_close(loss, ref, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=1e-5, rtol=1e-2)
+    torch.testing.assert_close(w.grad.float(), wr.grad, atol=1e-3, rtol=1e-2)
+    torch.testing.assert_close(b.grad, br.grad, atol=1e-5, rtol=1e-4)
+    g1 = (x.grad.clone(), w.grad.clone(), b.grad.clone())
+    x.grad = w.grad = b.grad = None
+    loss2 = classifier_xent(x, w, b, y)
+    (loss2 * 2.0).backward()
+    assert torch.equal(loss2, loss) and torch.equal(x.grad, g1[0]) and torch.equal(w.grad, g1[1])

@@ -195,6 +195,40 @@ def test_embedding_sum_sparse_grad():
     _close(w.grad, gref, 2e-2, "dW again")
 
 
+@pytest.mark.parametrize("R,Dm,pattern", [(512, 768, "positions"), (2, 768, "segments"), (300, 200, "random")])
+def test_embedding_small_table_grad(R, Dm, pattern, monkeypatch):
+    """kfa_embed_small_bwd (tables of <= 512 rows: LDS-accumulated per column group and
+    token chunk) vs a plain fp32 index_add, and vs the one-hot GEMM path it replaces."""
+    from kubeflow_controller_amd.ops import transformer as T
+    torch.manual_seed(R + Dm)
+    n = 32768 if pattern != "random" else 5000
+    if pattern == "positions":   # BERT: arange(128) per sequence of a 256 x 128 batch
+        ids = torch.arange(128, device=D).repeat(n // 128)
+    elif pattern == "segments":  # token types: two hot rows
+        ids = (torch.rand(n, device=D) < 0.4).long()
+    else:
+        ids = torch.randint(0, R, (n,), device=D)
+    t = torch.randn(R, Dm, device=D).requires_grad_()
+    dy = torch.randn(n, Dm, device=D).to(torch.bfloat16)
+    T.embedding_sum([t], [ids]).backward(dy)
+    ref = torch.zeros(R, Dm, device=D).index_add_(0, ids, dy.float())
+    _close(t.grad, ref, 1e-4, "small-table dT")
+    g_new = t.grad.clone()
+    t.grad = None
+    # a bf16 gradient buffer (flat-group params): fp32 scratch + fold
+    tb = t.detach().to(torch.bfloat16).requires_grad_()
+    monkeypatch.setattr(T, "_grad_target", lambda p: (torch.zeros(p.shape, dtype=torch.bfloat16, device=p.device), 1,
+                                                       False))
+    T.embedding_sum([tb], [ids]).backward(dy)
+    _close(tb.grad, ref, 1e-2, "small-table dT, bf16 gradient")
+    T.embedding_sum([tb], [ids]).backward(dy)  # the scratch was left zeroed: a second pass adds the same
+    _close(tb.grad, 2 * ref, 1e-2, "bf16 gradient, accumulated twice")
+    monkeypatch.undo()
+    monkeypatch.setattr(T, "EMB_SMALL_KERNEL", False)
+    T.embedding_sum([t], [ids]).backward(dy)
+    _close(g_new, t.grad, 2e-2, "vs one-hot path")
+
+
 def test_decoder_xent():
     from kubeflow_controller_amd.ops import transformer as T
     torch.manual_seed(0)
@@ -241,7 +275,7 @@ def test_bert_tiny_gpu_matches_reference(monkeypatch, side):
 
 def test_bert_own_gemm_routes_match_reference(monkeypatch):
     """Hidden 384 (a multiple of 192): with every per-shape choice forced to the own
-    kernels, the projections run on the persistent GEMM (192- and 256-wide tiles)
+    kernels, the projections run on the persistent / skinny GEMMs
     and the QKV dgrad of layer 1 reaches layer 0's LN2 backward through the
     ResidualJoin; gradients still match the fp32 reference."""
     from kubeflow_controller_amd.models.bert import BertConfig, BertForPreTraining, synthetic_mlm_batch
@@ -249,8 +283,10 @@ def test_bert_own_gemm_routes_match_reference(monkeypatch):
     monkeypatch.setattr(G, "prefer_own", lambda *a, **k: True)
     monkeypatch.setattr(G, "pick_fastest", lambda kind, key, dev, c: len(c) - 1)  # always an own variant
     calls = []
-    real = G.gemm_ppp
+    real, real_sk = G.gemm_ppp, G.gemm_skinny
     monkeypatch.setattr(G, "gemm_ppp", lambda a, b, **k: calls.append((a.shape[0], b.shape[0], a.shape[1])) or real(a, b, **k))
+    monkeypatch.setattr(G, "gemm_skinny",
+                        lambda a, b, *r, **k: calls.append((a.shape[0], b.shape[0], a.shape[1])) or real_sk(a, b, *r, **k))
     cfg = BertConfig(vocab_size=1000, hidden=384, layers=2, heads=6, intermediate=1536, max_position=128,
                      max_predictions=8, hidden_dropout=0.0, attn_dropout=0.0)
     torch.manual_seed(0)
@@ -269,7 +305,7 @@ def test_bert_own_gemm_routes_match_reference(monkeypatch):
     out.backward()
     for n, p in mg.named_parameters():
         _close(p.grad.cpu(), gref[n], 8e-2, n)
-    assert (512, 384, 1152) in calls and (512, 384, 384) in calls, calls  # QKV / out-proj dgrads on own GEMM
+    assert (512, 384, 1152) in calls and (512, 384, 384) in calls, calls  # QKV / out-proj dgrads on own GEMMs
 
 
 def test_bert_tiny_trains_with_flat_groups():

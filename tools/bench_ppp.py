@@ -11,7 +11,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from kubeflow_controller_amd.ops import gemm as G  # noqa: E402
 
 SHAPES = [(32768, 2304, 768), (32768, 768, 768), (32768, 3072, 768), (32768, 768, 3072), (32768, 768, 2304),
-          (5120, 30528, 768), (5120, 768, 30528), (256, 1000, 2048), (8192, 8192, 8192)]
+          (5120, 30528, 768), (5120, 768, 30528), (5120, 768, 768), (256, 1000, 2048), (8192, 8192, 8192)]
 
 
 def timeit(fn, iters=20):
@@ -71,7 +71,8 @@ def main():
                              ("ppp-nostore-nosplit", lambda: G.gemm_ppp(x, w, bn=256, probe=1, split=False)),
                              ("ppw", lambda: G.gemm_ppp(x, w, probe=9, split=False)),
                              ("ppw-nt", lambda: G.gemm_ppp(x, w, probe=10, split=False)),
-                             *([("skinny", lambda: G.gemm_skinny(x, w)), ("skinny-s2", lambda: G.gemm_skinny(x, w, splits=2)),
+                             *([("skinny", lambda: G.gemm_skinny(x, w))] if M <= 16384 and N % 4 == 0 else []),
+                             *([("skinny-s2", lambda: G.gemm_skinny(x, w, splits=2)),
                                 ("skinny-s4", lambda: G.gemm_skinny(x, w, splits=4)),
                                 ("skinny-s8", lambda: G.gemm_skinny(x, w, splits=8))]
                                if M <= 256 and N % 4 == 0 else [])):

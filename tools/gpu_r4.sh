@@ -81,7 +81,7 @@ for s in $steps; do
     abbert)
       log "A/B/C BERT-base knobs"
       AB_ROUNDS=2 AB_CMD="tools/bench_model.py --model bert_base --batch 256 --seq 128" bash tools/gpu_ab_multi.sh \
-        "BASE=1" "KFA_LN_BWD_DEEP=2" "KFA_GEMM=own" "KFA_ATTN_PF=0" | tee gpurun_out/abbert.log || exit 1 ;;
+        "BASE=1" "KFA_EMB_SMALL=0" "KFA_GEMM=own" | tee gpurun_out/abbert.log || exit 1 ;;
     gemm)
       log "GEMM shapes: hipBLASLt vs own"
       timeout -k 10 300 python -u tools/bench_ppp.py > gpurun_out/bench_ppp.log 2>&1 || { tail -20 gpurun_out/bench_ppp.log; exit 1; }
