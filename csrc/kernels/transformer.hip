@@ -622,50 +622,94 @@ __global__ __launch_bounds__(256) void embed_bwd_fold_kernel(const long* __restr
   }
 }
 
-// Gradient of a SMALL table (R <= 512 rows: BERT's position and segment
-// embeddings) — grad[ids[r]] += dout[r] — without global atomics per element
-// (a handful of hot rows serialise them) and without the one-hot GEMM:
-// block (column group of 64, token chunk) accumulates its chunk's rows in an
-// LDS image [R][64] fp32 (lane = column: one wave-instruction adds one token
-// row's 128 B, 64 distinct banks), marks the ids it touched, then adds only the
-// touched rows into the fp32 gradient (one atomic per element per block).
-constexpr int kSmallTabMaxRows = 512;
+// Gradient of a TINY table (R <= 8 rows: BERT's segment / token-type embedding)
+// — grad[ids[r]] += dout[r] — where every token hits one of a few rows: global
+// atomics serialise on them and the one-hot GEMM has M = R (hipBLASLt ran it at
+// ~140 us for R = 2).  Two launches:
+//  1. block (column group of 64, token chunk): a wave takes 8 rows x 64 columns per
+//     step (lane = row lane / 8, 8 columns lane % 8: 16-B loads, 4 steps in flight)
+//     and adds each row into register accumulators acc[R][8] (a select per table
+//     row: no dynamic register indexing); then the 8 row-lanes and the 4 waves of
+//     the block are summed (shuffles, LDS) and the block stores a partial [chunk][R][D];
+//  2. grad[r][c] += Σ_chunk partial[chunk][r][c] in chunk order (deterministic),
+//     into an fp32 or a bf16 gradient.
+// (An LDS-atomic version for tables up to 512 rows ran 174 us per table — slower
+// than the one-hot MFMA GEMM the position table keeps: 38 us.)
+constexpr int kSmallTabMaxRows = 8;
+constexpr int kSmallTabChunks = 32;
 
-__global__ __launch_bounds__(256) void embed_small_bwd_kernel(const long* __restrict__ ids,
-                                                              const bf16_t* __restrict__ dout, long dstride,
-                                                              float* __restrict__ grad, long n, int D, int R,
-                                                              long rows_per_block) {
-  extern __shared__ float acc[];  // [R][64], then R touched flags
-  int* touched = reinterpret_cast<int*>(acc + R * 64);
+template <int RM>
+__global__ __launch_bounds__(256) void embed_small_part_kernel(const long* __restrict__ ids,
+                                                               const bf16_t* __restrict__ dout, long dstride,
+                                                               float* __restrict__ part, long n, int D, int R,
+                                                               long rows_per_block) {
+  __shared__ float red[4][RM][64];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int c0 = blockIdx.x * 64;
-  for (int i = t; i < R * 64; i += 256) acc[i] = 0.f;
-  for (int i = t; i < R; i += 256) touched[i] = 0;
-  __syncthreads();
+  const int c0 = blockIdx.x * 64, rs = lane >> 3, cc = (lane & 7) * 8;
+  float acc[RM][8];
+#pragma unroll
+  for (int q = 0; q < RM; q++)
+#pragma unroll
+    for (int e = 0; e < 8; e++) acc[q][e] = 0.f;
   const long r0 = (long)blockIdx.y * rows_per_block, r1 = min(n, r0 + rows_per_block);
-  const bool live = c0 + lane < D;
-  // 4 rows per wave in flight: ids and values loaded before the LDS adds
-  for (long r = r0 + w; r < r1; r += 16) {
+  const bool live = c0 + cc < D;  // D % 8 == 0: a lane's 8 columns are all in or all out
+  for (long r = r0 + w * 8 + rs; r < r1 + 96; r += 128) {
     long id[4];
-    float v[4];
+    uint4 v[4];
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      const long rr = r + 4 * j;
-      id[j] = rr < r1 ? ids[rr] : -1;
-      v[j] = (rr < r1 && live) ? bf2f(dout[rr * dstride + c0 + lane]) : 0.f;
+      const long rr = r + 32 * j;
+      const bool ok = rr < r1 && live;
+      id[j] = ok ? ids[rr] : -1;
+      v[j] = ok ? *reinterpret_cast<const uint4*>(dout + rr * dstride + c0 + cc) : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      if (id[j] >= 0 && id[j] < R) {  // wave-uniform
-        atomicAdd(acc + id[j] * 64 + lane, v[j]);
-        if (lane == 0) touched[id[j]] = 1;
+      float f[8];
+      unpack8(v[j], f);
+#pragma unroll
+      for (int q = 0; q < RM; q++) {
+        const float m = id[j] == q ? 1.f : 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; e++) acc[q][e] = fmaf(m, f[e], acc[q][e]);
       }
     }
   }
+  // sum the 8 row-lanes sharing a column chunk (lane bits 3..5), then the 4 waves
+#pragma unroll
+  for (int q = 0; q < RM; q++)
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      float x = acc[q][e];
+      x += __shfl_xor(x, 8, 64);
+      x += __shfl_xor(x, 16, 64);
+      x += __shfl_xor(x, 32, 64);
+      acc[q][e] = x;
+    }
+  if (rs == 0)
+#pragma unroll
+    for (int q = 0; q < RM; q++)
+#pragma unroll
+      for (int e = 0; e < 8; e++) red[w][q][cc + e] = acc[q][e];
   __syncthreads();
+  float* dst = part + (long)blockIdx.y * R * D;
   for (int i = t; i < R * 64; i += 256) {
-    const int row = i >> 6, c = c0 + (i & 63);
-    if (touched[row] && c < D) atomicAdd(grad + (long)row * D + c, acc[i]);
+    const int q = i >> 6, c = i & 63;
+    if (c0 + c < D) dst[(long)q * D + c0 + c] = red[0][q][c] + red[1][q][c] + red[2][q][c] + red[3][q][c];
+  }
+}
+
+__global__ __launch_bounds__(256) void embed_small_reduce_kernel(const float* __restrict__ part, int chunks, long RD,
+                                                                 void* __restrict__ grad, int grad_f32) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < RD; i += (long)gridDim.x * 256) {
+    float s = 0.f;
+    for (int k = 0; k < chunks; k++) s += part[k * RD + i];
+    if (grad_f32) {
+      reinterpret_cast<float*>(grad)[i] += s;
+    } else {
+      bf16_t* g = reinterpret_cast<bf16_t*>(grad) + i;
+      *g = (bf16_t)f2bf(bf2f(*g) + s);
+    }
   }
 }
 
@@ -914,47 +958,26 @@ KFA_API int kfa_embed_fwd(const long* i0, const void* t0, const long* i1, const 
 }
 
 // scratch: zero-initialised fp32 [rows_of_table, D], left zeroed on return.
-// dst (bf16 or fp32) += src (fp32); src zeroed (the scratch of kfa_embed_small_bwd for a bf16 gradient)
-__global__ __launch_bounds__(256) void fold_f32_kernel(float* __restrict__ src, void* __restrict__ dst, int dst_f32,
-                                                       long n) {
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
-    const float v = src[i];
-    src[i] = 0.f;
-    if (dst_f32) {
-      reinterpret_cast<float*>(dst)[i] += v;
-    } else {
-      bf16_t* g = reinterpret_cast<bf16_t*>(dst) + i;
-      *g = (bf16_t)f2bf(bf2f(*g) + v);
-    }
-  }
-}
+// scratch floats kfa_embed_small_bwd needs (the per-chunk partial images)
+KFA_API long kfa_embed_small_ws_floats(int R, int D) { return (long)kSmallTabChunks * R * D; }
 
-KFA_API int kfa_fold_f32(float* src, void* dst, int dst_f32, long n, hipStream_t s) {
+// grad [R][D] (fp32 or bf16) += sum of dout rows by id, R <= 8, D % 8 == 0 (ids outside
+// [0, R) skipped); part: kfa_embed_small_ws_floats(R, D) floats of scratch
+KFA_API int kfa_embed_small_bwd(const long* ids, const void* dout, long dstride, void* grad, int grad_f32, long n,
+                                int D, int R, float* part, hipStream_t s) {
   if (n <= 0) return 0;
-  const long b = (n + 255) / 256;
-  hipLaunchKernelGGL(fold_f32_kernel, dim3((unsigned)(b < 2048 ? b : 2048)), dim3(256), 0, s, src, dst, dst_f32, n);
-  return kfa_status();
-}
-
-// grad [R][D] fp32 (+)= sum of dout rows by id, R <= 512 (ids outside [0, R) skipped)
-KFA_API int kfa_embed_small_bwd(const long* ids, const void* dout, long dstride, float* grad, long n, int D, int R,
-                                hipStream_t s) {
-  if (n <= 0) return 0;
-  if (R <= 0 || R > kSmallTabMaxRows || D <= 0 || !ids) return -1;
+  if (R <= 0 || R > kSmallTabMaxRows || D <= 0 || D % 8 || !ids || !part) return -1;
   const int cg = (D + 63) / 64;
-  long chunks = 128 / cg;
-  if (chunks < 1) chunks = 1;
-  if (chunks > (n + 63) / 64) chunks = (n + 63) / 64;
-  const long rpb = (n + chunks - 1) / chunks;
-  const size_t lds = (size_t)R * 64 * 4 + (size_t)R * 4;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&embed_small_bwd_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)((size_t)kSmallTabMaxRows * 65 * 4));
-    attr = true;
-  }
-  hipLaunchKernelGGL(embed_small_bwd_kernel, dim3(cg, (unsigned)chunks), dim3(256), lds, s, ids, (const bf16_t*)dout,
-                     dstride, grad, n, D, R, rpb);
+  const long rpb = (n + kSmallTabChunks - 1) / kSmallTabChunks;
+  if (R <= 2)
+    hipLaunchKernelGGL(embed_small_part_kernel<2>, dim3(cg, kSmallTabChunks), dim3(256), 0, s, ids,
+                       (const bf16_t*)dout, dstride, part, n, D, R, rpb);
+  else
+    hipLaunchKernelGGL(embed_small_part_kernel<kSmallTabMaxRows>, dim3(cg, kSmallTabChunks), dim3(256), 0, s, ids,
+                       (const bf16_t*)dout, dstride, part, n, D, R, rpb);
+  const long RD = (long)R * D, b = (RD + 255) / 256;
+  hipLaunchKernelGGL(embed_small_reduce_kernel, dim3((unsigned)(b < 2048 ? b : 2048)), dim3(256), 0, s, part,
+                     kSmallTabChunks, RD, grad, grad_f32);
   return kfa_status();
 }
 

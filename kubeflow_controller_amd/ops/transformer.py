@@ -53,8 +53,8 @@ _lib.register("kfa_attn_softmax_bwd", [P, P, L, I, Fl, U64, P])
 _lib.register("kfa_embed_fwd", [P, P, P, P, P, P, I, P, L, I, L, P])
 _lib.register("kfa_embed_bwd", [P, P, L, P, P, I, L, I, I, P])
 _lib.register("kfa_colsum", [P, P, P, L, I, I, P])
-_lib.register("kfa_embed_small_bwd", [P, P, _lib.L, P, _lib.L, I, I, P])
-_lib.register("kfa_fold_f32", [P, P, I, _lib.L, P])
+_lib.register("kfa_embed_small_ws_floats", [I, I], restype=_lib.L)
+_lib.register("kfa_embed_small_bwd", [P, P, _lib.L, P, I, _lib.L, I, I, P, P])
 _lib.register("kfa_attn_fwd", [P, P, P, P, P, I, I, I, I, Fl, Fl, U64, P])
 _lib.register("kfa_attn_bwd", [P, P, P, P, P, P, P, P, I, I, I, I, Fl, Fl, U64, P, P])
 
@@ -63,8 +63,8 @@ FUSED_ATTN = os.environ.get("KFA_FUSED_ATTN", "1") != "0"
 
 ACTS = {None: 0, "none": 0, "gelu": 1, "tanh": 2, "relu": 3}
 SMALL_TABLE_ROWS = 1024
-# tables of <= 512 rows (BERT position / segment): kfa_embed_small_bwd instead of the
-# one-hot GEMM (KFA_EMB_SMALL=0 restores it)
+# tables of <= 8 rows (BERT's segment table): kfa_embed_small_bwd instead of the one-hot
+# GEMM, whose M = R shape ran on hipBLASLt at ~140 us (KFA_EMB_SMALL=0 restores it)
 EMB_SMALL_KERNEL = os.environ.get("KFA_EMB_SMALL", "1") != "0"
 _MASK64 = (1 << 64) - 1
 
@@ -379,17 +379,13 @@ class EmbeddingSumFn(torch.autograd.Function):
                 grads.append(None)
                 continue
             g, _, direct = _grad_target(t)
-            if (EMB_SMALL_KERNEL and t.shape[0] <= 512 and g.dtype in (torch.float32, torch.bfloat16)
+            if (EMB_SMALL_KERNEL and t.shape[0] <= 8 and D % 8 == 0 and g.dtype in (torch.float32, torch.bfloat16)
                     and g.is_contiguous() and ids[k].dtype == torch.int64):
-                # LDS-accumulated per (column group, token chunk), touched rows added once per block;
-                # a bf16 gradient goes through a zeroed fp32 scratch folded in after
+                # per-chunk LDS images of the table's gradient, summed in chunk order into g
                 R = t.shape[0]
-                dst = g if g.dtype == torch.float32 else \
-                    _lib.workspace(R * D * 4, t.device, f"embed_small_scratch{k}").view(torch.float32)
-                _lib.call("kfa_embed_small_bwd", _lib.ptr(ids[k]), _lib.ptr(dout), D, _lib.ptr(dst), n, D, R,
-                          _lib.stream())
-                if dst is not g:
-                    _lib.call("kfa_fold_f32", _lib.ptr(dst), _lib.ptr(g), 0, R * D, _lib.stream())
+                part = _lib.workspace(4 * _lib.lib().kfa_embed_small_ws_floats(R, D), t.device, "embed_small_part")
+                _lib.call("kfa_embed_small_bwd", _lib.ptr(ids[k]), _lib.ptr(dout), D, _lib.ptr(g),
+                          int(g.dtype == torch.float32), n, D, R, _lib.ptr(part), _lib.stream())
             elif t.shape[0] <= SMALL_TABLE_ROWS:
                 # few rows, many duplicates (position / segment tables): atomics would
                 # serialise on a handful of addresses; a one-hot GEMM (MFMA) reduces them

@@ -195,10 +195,11 @@ def test_embedding_sum_sparse_grad():
     _close(w.grad, gref, 2e-2, "dW again")
 
 
-@pytest.mark.parametrize("R,Dm,pattern", [(512, 768, "positions"), (2, 768, "segments"), (300, 200, "random")])
+@pytest.mark.parametrize("R,Dm,pattern", [(512, 768, "positions"), (2, 768, "segments"), (8, 200, "random"), (5, 64, "random")])
 def test_embedding_small_table_grad(R, Dm, pattern, monkeypatch):
-    """kfa_embed_small_bwd (tables of <= 512 rows: LDS-accumulated per column group and
-    token chunk) vs a plain fp32 index_add, and vs the one-hot GEMM path it replaces."""
+    """Small-table embedding gradients vs a plain fp32 index_add: kfa_embed_small_bwd
+    (tables of <= 8 rows, register accumulators per column group and token chunk) and
+    the one-hot GEMM path (larger tables, and every table with KFA_EMB_SMALL=0)."""
     from kubeflow_controller_amd.ops import transformer as T
     torch.manual_seed(R + Dm)
     n = 32768 if pattern != "random" else 5000
@@ -215,13 +216,13 @@ def test_embedding_small_table_grad(R, Dm, pattern, monkeypatch):
     _close(t.grad, ref, 1e-4, "small-table dT")
     g_new = t.grad.clone()
     t.grad = None
-    # a bf16 gradient buffer (flat-group params): fp32 scratch + fold
+    # a bf16 gradient buffer (flat-group params): the reduce adds into bf16
     tb = t.detach().to(torch.bfloat16).requires_grad_()
     monkeypatch.setattr(T, "_grad_target", lambda p: (torch.zeros(p.shape, dtype=torch.bfloat16, device=p.device), 1,
                                                        False))
     T.embedding_sum([tb], [ids]).backward(dy)
     _close(tb.grad, ref, 1e-2, "small-table dT, bf16 gradient")
-    T.embedding_sum([tb], [ids]).backward(dy)  # the scratch was left zeroed: a second pass adds the same
+    T.embedding_sum([tb], [ids]).backward(dy)  # a second pass adds the same again
     _close(tb.grad, 2 * ref, 1e-2, "bf16 gradient, accumulated twice")
     monkeypatch.undo()
     monkeypatch.setattr(T, "EMB_SMALL_KERNEL", False)
