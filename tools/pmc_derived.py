@@ -43,7 +43,8 @@ def fmt(v, spec):
     return "—" if v is None else format(v, spec)
 
 
-def main(paths, keep=("gemm", "wgrad", "conv", "seg_", "radix", "scan_max", "bn_", "attn", "ln_", "bias_act")):
+def main(paths, keep=("gemm", "wgrad", "conv", "seg_", "radix", "scan_max", "bn_", "attn", "ln_", "bias_act",
+                      "maxpool", "pool", "stem", "sgd", "adam", "xent", "gap_")):
     rows = load(paths)
     print("| kernel | dispatches | mean us | MFMA busy | MFMA TF/s | LDS conflict | LDS-wait share | "
           "HBM read MB | HBM write MB | HBM TB/s |")
