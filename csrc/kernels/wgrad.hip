@@ -662,7 +662,15 @@ WPlan plan(long K, int Co, int N, bool pointwise = false) {
   const long steps = (K + BKW - 1) / BKW;
   long splits = ((long)p.blocks_per_cu * num_cus()) / p.tiles;
   splits = splits < 1 ? 1 : splits;
-  const long max_splits = steps / 4 > 0 ? steps / 4 : 1;
+  // each split >= min_steps k-steps (KFA_WGRAD_MIN_STEPS, default 4): more steps per
+  // split = fewer fp32 partial slabs to write and reduce, at the cost of idle CUs
+  static int min_steps = -1;
+  if (min_steps < 0) {
+    const char* e = getenv("KFA_WGRAD_MIN_STEPS");
+    min_steps = e ? atoi(e) : 4;
+    if (min_steps < 1) min_steps = 4;
+  }
+  const long max_splits = steps / min_steps > 0 ? steps / min_steps : 1;
   if (splits > max_splits) splits = max_splits;
   const long per = (steps + splits - 1) / splits;
   p.kchunk = (int)(per * BKW);

@@ -81,7 +81,13 @@ for s in $steps; do
     abbert)
       log "A/B/C BERT-base knobs"
       AB_ROUNDS=2 AB_CMD="tools/bench_model.py --model bert_base --batch 256 --seq 128" bash tools/gpu_ab_multi.sh \
-        "BASE=1" "KFA_EMB_SMALL=0" "KFA_GEMM=own" | tee gpurun_out/abbert.log || exit 1 ;;
+        "BASE=1" "KFA_WGRAD_MIN_STEPS=16" "KFA_WGRAD_MIN_STEPS=32" "KFA_WGRAD_MIN_STEPS=64" \
+        | tee gpurun_out/abbert.log || exit 1 ;;
+    abwd)
+      log "A/B/C Wide&Deep knobs"
+      AB_ROUNDS=2 AB_CMD="tools/bench_model.py --model wide_deep --batch 65536" bash tools/gpu_ab_multi.sh \
+        "BASE=1" "KFA_WGRAD_MIN_STEPS=16" "KFA_WGRAD_MIN_STEPS=32" "KFA_WGRAD_MIN_STEPS=64" \
+        | tee gpurun_out/abwd.log || exit 1 ;;
     gemm)
       log "GEMM shapes: hipBLASLt vs own"
       timeout -k 10 300 python -u tools/bench_ppp.py > gpurun_out/bench_ppp.log 2>&1 || { tail -20 gpurun_out/bench_ppp.log; exit 1; }
