@@ -105,6 +105,10 @@ struct PppArgs {
   // many s_memrealtime ticks (10 ns) late, so half the CUs cross their tile
   // boundaries (and issue their C bursts) half a tile after the other half
   int stagger;
+  // GELU epilogue (gemm_ppp_kernel<256, ..., GELU = true>): C = z = A·Bᵀ + bias (the
+  // pre-activation the backward needs), Y = gelu(z); bias fp32 [N], N <= 8192
+  bf16_t* Y;
+  const float* bias;
 };
 
 __device__ __forceinline__ void ppp_stagger(int ticks, int lc) {
@@ -135,9 +139,14 @@ constexpr int kStoresPerPhase = 4;  // one 16-B store per 16-row block of a 64 x
 // B0 (u+2) — each piece DMA'd 3 phases (one k-tile) before its read phase and
 // only into a buffer whose previous piece was read >= 2 phases earlier; every
 // phase retires the DMAs of three phases ago: steady vmcnt(D = 7).
-template <int BN = 256, bool NOST = false, int SMODE = 0, bool P3 = false>
+// GELU (BN = 256, SMODE = 0, no split): the bias + GELU epilogue — each quadrant
+// store writes z = acc + bias to C and gelu(z) to Y (8 stores per phase instead of
+// 4, counted in the retire waits), the bias staged once in the 32 KB of LDS the
+// 128 KB ring leaves free — so the BERT FFN-up forward needs no bias / GELU pass.
+template <int BN = 256, bool NOST = false, int SMODE = 0, bool P3 = false, bool GELU = false>
 __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
   static_assert(BN == 256 || BN == 192, "tile width");
+  static_assert(!GELU || (BN == 256 && SMODE == 0 && !P3 && !NOST), "GELU epilogue: plain 256-wide schedule");
   static_assert(!P3 || BN == 192, "three-phase k-tiles are the 192-wide schedule");
   static_assert(BN == 256 || !(SMODE & 2), "row pairs need two-block halves");
   constexpr int NB1 = BN == 256 ? 2 : 1;  // 16-column MFMA blocks in a wave's nh = 1 half
@@ -145,6 +154,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
   constexpr int TM = 8, TN = 2 + NB1;
   constexpr int D = 6 + NB1;              // DMAs per k-tile
   __shared__ __attribute__((aligned(16))) char smem[2 * 4 * PIECE];  // 128 KB: two k-tiles of four pieces
+  __shared__ __attribute__((aligned(16))) float sbias[GELU ? 8192 : 1];  // GELU: the bias vector (32 KB)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
@@ -176,6 +186,11 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
   const __amdgpu_buffer_rsrc_t rA = rsrc(g.A, (unsigned)(((long)(g.M - 1) * g.lda + g.K) * 2));
   const __amdgpu_buffer_rsrc_t rB = rsrc(g.B, (unsigned)(((long)(g.N - 1) * g.ldb + g.K) * 2));
   const __amdgpu_buffer_rsrc_t rC = rsrc(g.C, g.c_bytes);
+  const __amdgpu_buffer_rsrc_t rY = rsrc(GELU ? g.Y : g.C, GELU ? g.c_bytes : 0u);
+  if constexpr (GELU) {  // before any DMA is in flight: a plain load + LDS store + barrier
+    for (int i = tid; i < 8192; i += 512) sbias[i] = i < g.N ? g.bias[i] : 0.f;
+    __syncthreads();
+  }
   // DMA plan: instruction j of wave w fills piece rows j*64 + w*8 + lane/8,
   // physical chunk lane&7 <- logical chunk (lane&7) ^ ((row >> 1) & 7)
   const int prow = wave * 8 + (lane >> 3);
@@ -278,6 +293,41 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
     }
     const int n = n0 + wc * WN + nh * 32 + cb;
     const bool nok = n < g.N;
+    if constexpr (GELU) {
+      // before the swap, x holds columns 4fq..4fq+3 of the quadrant's first 16-column
+      // block, y the same of the second: their bias, then z = acc + bias -> C, gelu(z) -> Y
+      const int nq = n0 + wc * WN + nh * 32 + fq * 4;
+      const float4 bx = *reinterpret_cast<const float4*>(sbias + nq);
+      const float4 by = *reinterpret_cast<const float4*>(sbias + nq + 16);
+#pragma unroll
+      for (int mi = 0; mi < 4; mi++) {
+        floatx4& x = acc[nh * 2][mh * 4 + mi];
+        floatx4& y = acc[nh * 2 + 1][mh * 4 + mi];
+        const float zx0 = x[0] + bx.x, zx1 = x[1] + bx.y, zx2 = x[2] + bx.z, zx3 = x[3] + bx.w;
+        const float zy0 = y[0] + by.x, zy1 = y[1] + by.y, zy2 = y[2] + by.z, zy3 = y[3] + by.w;
+        const int m = m0 + wr * 128 + mh * 64 + mi * 16 + fr;
+        const unsigned off = (m < g.M && nok) ? ((unsigned)m * (unsigned)g.ldc + (unsigned)n) * 2u : kOOB;
+        const unsigned px0 = cvt2(zx0, zx1), px1 = cvt2(zx2, zx3), py0 = cvt2(zy0, zy1), py1 = cvt2(zy2, zy3);
+        {
+          const auto s0 = __builtin_amdgcn_permlane16_swap(px0, py0, false, false);
+          const auto s1 = __builtin_amdgcn_permlane16_swap(px1, py1, false, false);
+          store16(rC, off, make_uint4(s0[0], s1[0], s0[1], s1[1]));
+        }
+        {
+          // GELU of the bf16-rounded z (exactly the value the backward's gelu'(z) reads)
+          auto lo = [](unsigned w) { return __uint_as_float(w << 16); };
+          auto hi = [](unsigned w) { return __uint_as_float(w & 0xffff0000u); };
+          const auto s0 = __builtin_amdgcn_permlane16_swap(cvt2(gelu_f(lo(px0)), gelu_f(hi(px0))),
+                                                            cvt2(gelu_f(lo(py0)), gelu_f(hi(py0))), false, false);
+          const auto s1 = __builtin_amdgcn_permlane16_swap(cvt2(gelu_f(lo(px1)), gelu_f(hi(px1))),
+                                                            cvt2(gelu_f(lo(py1)), gelu_f(hi(py1))), false, false);
+          store16(rY, off, make_uint4(s0[0], s1[0], s0[1], s1[1]));
+        }
+        x = floatx4{0.f, 0.f, 0.f, 0.f};
+        y = floatx4{0.f, 0.f, 0.f, 0.f};
+      }
+      return;
+    }
 #pragma unroll
     for (int mi = 0; mi < 4; mi++) {
       floatx4& x = acc[nh * 2][mh * 4 + mi];
@@ -350,8 +400,9 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
       constexpr int s = decltype(sc)::value;
       // stores per phase: 4 each (quadrant per phase) or 8, 0, 8, 0 (row pairs)
       constexpr int RP = (SMODE & 2) ? 1 : 0;
-      constexpr int upto = RP ? 8 * (s / 2 + 1) : 4 * (s + 1);          // phases 0..s
-      constexpr int after = RP ? 8 * ((3 - s + (s % 2 == 0 ? 0 : 1)) / 2) : 4 * (3 - s);  // phases s+1..3
+      constexpr int SPP = GELU ? 8 : 4;  // stores per quadrant phase (GELU: z and gelu(z))
+      constexpr int upto = RP ? 8 * (s / 2 + 1) : SPP * (s + 1);          // phases 0..s
+      constexpr int after = RP ? 8 * ((3 - s + (s % 2 == 0 ? 0 : 1)) / 2) : SPP * (3 - s);  // phases s+1..3
       constexpr int n = D + (EPI ? upto : 0) + (PEPI ? after : 0);
       vm_wait<n>();
     };
@@ -953,6 +1004,25 @@ static int g_stagger = 0;
 KFA_API int kfa_gemm_ppp_set_stagger(int ticks) {
   g_stagger = ticks < 0 ? 0 : ticks;
   return 0;
+}
+
+// Z = A · Bᵀ + bias (bf16, the pre-activation), Y = gelu(Z) on the persistent kernel with
+// the bias + GELU epilogue (256-wide tiles, no split): K % 8 == 0, K >= 128, N % 8 == 0,
+// N <= 8192; Z and Y share ldc.  Returns 0, -1 on unsupported operands.
+KFA_API int kfa_gemm_ppp_gelu(const bf16_t* A, const bf16_t* B, bf16_t* Z, bf16_t* Y, const float* bias, int M, int N,
+                              int K, int lda, int ldb, int ldc, hipStream_t st) {
+  if (M <= 0 || N <= 0) return 0;
+  if (K < 2 * BK || K % 8 || N % 8 || N > 8192 || lda % 8 || ldb % 8 || ldc % 8 || lda < K || ldb < K || ldc < N ||
+      !bias || !Y)
+    return -1;
+  const long cb = (long)M * ldc * 2;
+  if (cb >= (long)kOOB || (long)M * lda * 2 >= (long)kOOB || (long)N * ldb * 2 >= (long)kOOB) return -2;
+  const long tiles = (long)((M + 255) / 256) * ((N + 255) / 256);
+  const long cus = ppp_cus();
+  const int grid = (int)(tiles < cus ? tiles : cus);
+  const PppArgs g{A, B, Z, M, N, K, lda, ldb, ldc, (unsigned)cb, nullptr, nullptr, 1, g_stagger, Y, bias};
+  hipLaunchKernelGGL((gemm_ppp_kernel<256, false, 0, false, true>), dim3(grid), dim3(512), 0, st, g);
+  return kfa_status();
 }
 
 KFA_API int kfa_gemm_ppp(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int K, int lda, int ldb, int ldc,

@@ -35,6 +35,7 @@ _lib.register("kfa_gemm_ppp", [P, P, P] + [I] * 9 + [P, _lib.L, I, P])
 _lib.register("kfa_gemm_ppp_ws_bytes", [I] * 5, restype=_lib.L)
 _lib.register("kfa_gemm_ppp_pick_bn", [I, I])
 _lib.register("kfa_gemm_skinny", [P, P, P, P] + [I] * 7 + [P, _lib.L, P])
+_lib.register("kfa_gemm_ppp_gelu", [P] * 5 + [I] * 6 + [P])
 _lib.register("kfa_gemm_skinny_ws_bytes", [I] * 4, restype=_lib.L)
 
 ACTS = {None: 0, "none": 0, "gelu": 1, "tanh": 2, "relu": 3}
@@ -183,6 +184,27 @@ def gemm_ppp(a, b, *, out=None, blocks: int = 0, probe: int = 0, bn: int = 0, sp
 
 
 SKINNY_MAX_M = 16384  # the 256 x 64-tile kernel is a tuner candidate up to this many rows
+
+
+def ppp_gelu_ok(a, b, bias) -> bool:
+    """Operands :func:`gemm_ppp_gelu` takes."""
+    return (ppp_ok(a, b) and b.shape[0] <= 8192 and bias is not None and bias.dtype == torch.float32
+            and bias.is_contiguous() and bias.numel() == b.shape[0])
+
+
+def gemm_ppp_gelu(a, b, bias):
+    """``(y, z)`` with ``z = a @ b.T + bias`` (bf16: the pre-activation, bias included)
+    and ``y = gelu(z)``, from ONE launch of the persistent GEMM with the bias + GELU
+    epilogue (``gemm_ppp_kernel<..., GELU>``): no separate bias / activation pass."""
+    if not ppp_gelu_ok(a, b, bias):
+        raise ValueError(f"gemm_ppp_gelu: unsupported operands {tuple(a.shape)} x {tuple(b.shape)}")
+    M, K = a.shape
+    N = b.shape[0]
+    z = torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
+    y = torch.empty_like(z)
+    _lib.call("kfa_gemm_ppp_gelu", _lib.ptr(a), _lib.ptr(b), _lib.ptr(z), _lib.ptr(y), _lib.ptr(bias), M, N, K,
+              a.stride(0), b.stride(0), N, _lib.stream())
+    return y, z
 
 
 def skinny_ok(a, b) -> bool:

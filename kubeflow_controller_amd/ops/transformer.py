@@ -66,6 +66,11 @@ SMALL_TABLE_ROWS = 1024
 # tables of <= 8 rows (BERT's segment table): kfa_embed_small_bwd instead of the one-hot
 # GEMM, whose M = R shape ran on hipBLASLt at ~140 us (KFA_EMB_SMALL=0 restores it)
 EMB_SMALL_KERNEL = os.environ.get("KFA_EMB_SMALL", "1") != "0"
+# KFA_FFN_GELU_EPI=1: the FFN-up forward also times the persistent GEMM with the bias +
+# GELU epilogue (one launch instead of GEMM + pass).  Off by default: measured 0.299 ms vs
+# 0.2255 for hipBLASLt + the bias/GELU pass (32768 x 3072 x 768) — its 8 stores per phase
+# sit in the counted vmcnt window of the DMA retires and stall the pipeline.
+FFN_GELU_EPI = os.environ.get("KFA_FFN_GELU_EPI", "0") == "1"
 _MASK64 = (1 << 64) - 1
 
 
@@ -476,6 +481,25 @@ def attn_bwd(qkv, bqkv, key_bias, out, lse, dout, dbqkv, B, S, heads, p=0.0, see
     return dqkv
 
 
+def _ffn_up(h, w, b):
+    """FFN-up forward ``(gelu(h @ w.T + b), z, z_has_bias)``: per shape the fastest of
+    the GEMM (hipBLASLt or an own persistent variant) + the bias/GELU pass, and the own
+    persistent GEMM with the bias + GELU epilogue (one launch, ``gemm_ppp_gelu``)."""
+    if _gemm.ROUTE_AUTO and FFN_GELU_EPI and _gemm.ppp_gelu_ok(h, w, b):
+        own_pp = _gemm._ppp_candidates(h, w)
+        cands = ([("hipblaslt+pass", lambda: bias_act_fwd(torch.mm(h, w.t()), b, "gelu"))]
+                 + [(n + "+pass", (lambda f: lambda: bias_act_fwd(f(), b, "gelu"))(f)) for n, f in own_pp]
+                 + [("ppp256-gelu", lambda: _gemm.gemm_ppp_gelu(h, w, b))])
+        i = _gemm.pick_fastest("ffn_up", (h.shape[0], w.shape[0], h.shape[1]), h.device, cands)
+        if i == len(cands) - 1:
+            y, z = _gemm.gemm_ppp_gelu(h, w, b)
+            return y, z, True
+        z = own_pp[i - 1][1]() if i > 0 else torch.mm(h, w.t())
+        return bias_act_fwd(z, b, "gelu"), z, False
+    z = _gemm.mm_auto(h, w)
+    return bias_act_fwd(z, b, "gelu"), z, False
+
+
 # ----------------------------------------------------------------------------- encoder layer
 class EncoderLayerFn(torch.autograd.Function):
     """Post-LN BERT encoder layer, forward + backward written out (see module doc).
@@ -535,16 +559,16 @@ class EncoderLayerFn(torch.autograd.Function):
         h1, h1s, m1, r1 = ln_fwd(ao, g1, be1, res=x, bias=bo, eps=eps, p=ph, seed=s_h1)
         del ao
         # feed-forward; f1 = pre-activation (GEMM path: bias included)
+        z_bias = use_f  # f1 includes b1 (the backward's GELU' then takes no bias)
         if use_f:
             f1a, f1 = _gemm.gemm_nt(h1, w1, bias=b1, act="gelu", want_z=True)
         else:
-            f1 = _gemm.mm_auto(h1, w1)                                     # [T, I]
-            f1a = bias_act_fwd(f1, b1, "gelu")
+            f1a, f1, z_bias = _ffn_up(h1, w1, b1)
         f2 = mm(f1a, w2)
         h2, h2s, m2, r2 = ln_fwd(f2, g2, be2, res=h1, bias=b2, eps=eps, p=ph, seed=s_h2)
         ctx.save_for_backward(x, ctxr, h1, h1s, m1, r1, f1, f1a, h2s, m2, r2, *att)
         ctx.params = (wqkv, bqkv, wo, bo, g1, be1, w1, b1, w2, b2, g2, be2)
-        ctx.cfg = (B, S, heads, ph, pa, (s_attn, s_h1, s_h2), qscale, use_g, use_f, fused)
+        ctx.cfg = (B, S, heads, ph, pa, (s_attn, s_h1, s_h2), qscale, use_g, use_f, fused, z_bias)
         ctx.key_bias = key_bias
         return h2
 
@@ -552,7 +576,7 @@ class EncoderLayerFn(torch.autograd.Function):
     def backward(ctx, dy):
         (x, ctxr, h1, h1s, m1, r1, f1, f1a, h2s, m2, r2, *att) = ctx.saved_tensors
         wqkv, bqkv, wo, bo, g1, be1, w1, b1, w2, b2, g2, be2 = ctx.params
-        B, S, heads, ph, pa, (s_attn, s_h1, s_h2), qscale, use_g, use_f, fused = ctx.cfg
+        B, S, heads, ph, pa, (s_attn, s_h1, s_h2), qscale, use_g, use_f, fused, z_bias = ctx.cfg
         key_bias = ctx.key_bias
         T, H = x.shape
         d = H // heads
@@ -570,7 +594,7 @@ class EncoderLayerFn(torch.autograd.Function):
         if use_f:   # df1 = (df2 · W2) * gelu'(z1), db1 += colsum(df1): one GEMM launch
             df1 = _gemm.gemm_nt(df2, _gemm.transpose(w2), zin=f1, dact="gelu", dbias=G(b1))[0]
         else:
-            df1 = bias_act_bwd(_gemm.dgrad_auto(df2, w2), f1, b1, "gelu", G(b1))
+            df1 = bias_act_bwd(_gemm.dgrad_auto(df2, w2), f1, None if z_bias else b1, "gelu", G(b1))
         del df2
         _wgrad_side_(G(w1), df1, h1)
         if use_g:   # residual-gradient join as the GEMM addend

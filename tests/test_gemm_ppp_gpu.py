@@ -233,3 +233,25 @@ def test_gemm_ppp_k_tail_matches_fp32(M, N, K, form):
           "ppw": dict(probe=9, split=False), "ppw_nt": dict(probe=10, split=False)}[form]
     c = G.gemm_ppp(a, b, **kw)
     _close(c, a.float() @ b.float().t(), 1e-2, f"K-tail C {M}x{N}x{K} {form}")
+
+
+@pytest.mark.parametrize("M,N,K", [
+    (32768, 3072, 768),    # BERT-base FFN-up: 6 tiles per CU
+    (1000, 776, 200),      # edge tiles in M and N, K tail
+    (512, 512, 128),       # 4 tiles, two k-tiles each (every other k-tile a boundary one)
+    (300, 8192, 256),      # the widest bias the LDS stage holds
+])
+def test_gemm_ppp_gelu_epilogue_matches_fp32(M, N, K):
+    """Persistent GEMM with the bias + GELU epilogue (8 stores per phase in the counted
+    retire waits): z = A·Bᵀ + bias and y = gelu(z) vs fp32; y is GELU of the stored bf16 z."""
+    import torch.nn.functional as F
+    from kubeflow_controller_amd.ops import gemm as G
+    torch.manual_seed(M + N + K + 11)
+    a, b = _bf(M, K), _bf(N, K, s=0.05)
+    bias = torch.randn(N, device=D)
+    y, z = G.gemm_ppp_gelu(a, b, bias)
+    zr = a.float() @ b.float().t() + bias
+    _close(z, zr, 1e-2, f"z {M}x{N}x{K}")
+    _close(y, F.gelu(z.float()), 1e-2, f"y {M}x{N}x{K}")
+    y2, z2 = G.gemm_ppp_gelu(a, b, bias)
+    assert torch.equal(y, y2) and torch.equal(z, z2)

@@ -81,8 +81,7 @@ for s in $steps; do
     abbert)
       log "A/B/C BERT-base knobs"
       AB_ROUNDS=2 AB_CMD="tools/bench_model.py --model bert_base --batch 256 --seq 128" bash tools/gpu_ab_multi.sh \
-        "BASE=1" "KFA_WGRAD_MIN_STEPS=16" "KFA_WGRAD_MIN_STEPS=32" "KFA_WGRAD_MIN_STEPS=64" \
-        | tee gpurun_out/abbert.log || exit 1 ;;
+        "BASE=1" "KFA_FFN_GELU_EPI=0" | tee gpurun_out/abbert.log || exit 1 ;;
     abwd)
       log "A/B/C Wide&Deep knobs"
       AB_ROUNDS=2 AB_CMD="tools/bench_model.py --model wide_deep --batch 65536" bash tools/gpu_ab_multi.sh \
