@@ -54,6 +54,18 @@ struct BnBwd {
   const uint8_t* emb;  // addend E masked by these ReLU bits (E = a block output's raw gradient), or nullptr
 };
 
+// BatchNorm-apply + ReLU prologue (PRO): T is a BatchNorm's RAW input x and the
+// A operand is relu(x * scale[c] + shift[c]) (bf16, rounded exactly as bn_apply
+// rounds it), applied on the register path between the global load and the LDS
+// store; padding taps stay 0.  The blocks of tile column 0 also write the
+// normalised value of every centre-tap slice to y (which then covers each input
+// pixel once — stride 1, P == H, Q == W, host-checked), so the backward's weight
+// gradient reads y as before and the BatchNorm's own apply pass is gone.
+struct Pro {
+  const float* ss;  // [scale | shift], 2C floats
+  bf16_t* y;        // normalised activation (same layout as T), or nullptr
+};
+
 struct Geo {
   int Nb, H, W, C;   // gathered tensor T
   int P, Q;          // GEMM row space (m = nb*P*Q + p*Q + q)
@@ -134,18 +146,20 @@ __device__ __forceinline__ int swz(int row, int chunk) { return row * BK + ((chu
 // main loop's LDS fragment reads on a reused register.
 constexpr unsigned kEpiE = 1, kEpiStats = 2, kEpiBnBwd = 4, kEpiEmb = 8, kEpiYMask = 16, kEpiAll = 31;
 
-template <int WM, int WN, int TM, int TN, unsigned EPI>
+template <int WM, int WN, int TM, int TN, unsigned EPI, bool PRO = false>
 __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_t* __restrict__ T,
                                                                      const bf16_t* __restrict__ B,
                                                                      bf16_t* __restrict__ D, const bf16_t* __restrict__ E,
                                                                      const bf16_t* __restrict__ Z,
-                                                                     float* __restrict__ stats, BnBwd bnb, Geo g) {
+                                                                     float* __restrict__ stats, BnBwd bnb, Geo g,
+                                                                     Pro pro = Pro{nullptr, nullptr}) {
   constexpr int NW = WM * WN, RPP = 8 * NW;  // waves; tile rows per staging pass (8 per wave)
   constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
   constexpr int AR = BM / RPP, BR = BN / RPP;  // 16-B chunks per thread per k-tile
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
   bf16_t* As = smem;                  // [2][BM][BK]
   bf16_t* Bs = smem + 2 * BM * BK;    // [2][BN][BK]
+  float* ssl = reinterpret_cast<float*>(smem + 2 * (BM + BN) * BK);  // PRO: [scale | shift] (2C floats)
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: LDS-DMA bases in SGPRs
@@ -224,6 +238,16 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
   // offset, tap) of the next slice is carried incrementally (wave-uniform) instead
   // of four scalar divisions per k-step
   int nx_ti = 0, nx_kt = 0, nx_c0 = 0, nx_r = 0, nx_s = 0;
+  // PRO register-path state of the slice in flight: raw A chunks, their source
+  // offsets (for the y write), valid-tap bits, the slice's scalar offset / channel base
+  uint4 pr_a[PRO ? AR : 1];
+  int pr_vo[PRO ? AR : 1];
+  unsigned pr_ok = 0;
+  int pr_soff = 0, pr_ch = 0;
+  bool pr_y = false;
+  const int pr_cs = (kc ^ ((rbase >> 1) & 7)) * 8;  // this lane's source chunk (the same for every i: RPP % 16 == 0)
+  auto ti_col0 = [&](int ti) { return tile_of(ti) % ntn == 0; };
+  const __amdgpu_buffer_rsrc_t rY = rsrc(pro.y ? pro.y : D, pro.y ? g.t_bytes : 0u);
   auto issue = [&](int st, int buf) {
     (void)st;
     const int ti = nx_ti, k0 = nx_kt * BK, c0 = nx_c0;
@@ -235,7 +259,27 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
       if (++nx_s == g.S) { nx_s = 0; nx_r++; }
     }
     if (++nx_kt == nk) { nx_kt = 0; nx_ti++; nx_c0 = 0; nx_r = 0; nx_s = 0; }
-    if (lin_a) {  // the whole offset but the slice's is fixed per tile (a_vo, setup)
+    if constexpr (PRO) {  // register path: loads now, normalised + stored to LDS by pro_store
+      pr_soff = (lin_a ? k0 : c0) * 2;
+      pr_ch = lin_a ? k0 : c0;
+      pr_y = pro.y && (ti_col0(ti) && (lin_a || (dh + g.oa == 0 && dw + g.ob == 0)));
+      pr_ok = 0;
+#pragma unroll
+      for (int i = 0; i < AR; i++) {
+        int vo = a_vo[i];
+        if (!lin_a) {
+          const int ih = a_hb[i] + dh, iw = a_wb[i] + dw;
+          const bool ok = (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+          vo = ok ? a_vo[i] + (ih * g.W + iw) * g.C * 2 : (int)kOOB;
+          pr_ok |= ok ? (1u << i) : 0u;
+        } else {
+          pr_ok |= 1u << i;
+        }
+        pr_vo[i] = vo;
+        auto v = __builtin_amdgcn_raw_buffer_load_b128(rT, (unsigned)vo, (unsigned)pr_soff, KFA_CONV_LOAD_AUX);
+        pr_a[i] = *reinterpret_cast<uint4*>(&v);
+      }
+    } else if (lin_a) {  // the whole offset but the slice's is fixed per tile (a_vo, setup)
 #pragma unroll
       for (int i = 0; i < AR; i++)
         buf_dma16_act(rT, As + buf * BM * BK + (i * RPP + wave * 8) * BK, a_vo[i], k0 * 2);
@@ -477,6 +521,46 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
       for (int j = 0; j < TM; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
   };
 
+  // PRO: the slice's A chunks landed -> relu(x * sc + sh) (0 on padding taps) into
+  // LDS `buf` at the positions the LDS-DMA would have filled; centre-tap slices of
+  // tile column 0 also go to y.
+  auto pro_store = [&](int buf) {
+    if constexpr (PRO) {
+      const int c = pr_ch + pr_cs;
+      float sc[8], sh[8];
+      {
+        const float4 a0 = *reinterpret_cast<const float4*>(ssl + c), a1 = *reinterpret_cast<const float4*>(ssl + c + 4);
+        const float4 b0 = *reinterpret_cast<const float4*>(ssl + g.C + c);
+        const float4 b1 = *reinterpret_cast<const float4*>(ssl + g.C + c + 4);
+        sc[0] = a0.x; sc[1] = a0.y; sc[2] = a0.z; sc[3] = a0.w; sc[4] = a1.x; sc[5] = a1.y; sc[6] = a1.z; sc[7] = a1.w;
+        sh[0] = b0.x; sh[1] = b0.y; sh[2] = b0.z; sh[3] = b0.w; sh[4] = b1.x; sh[5] = b1.y; sh[6] = b1.z; sh[7] = b1.w;
+      }
+#pragma unroll
+      for (int i = 0; i < AR; i++) {
+        float f[8];
+        unpack8(pr_a[i], f);
+        const bool ok = (pr_ok >> i) & 1u;
+#pragma unroll
+        for (int j = 0; j < 8; j++) f[j] = ok ? fmaxf(fmaf(f[j], sc[j], sh[j]), 0.f) : 0.f;
+        uint4 o = pack8(f);
+        *reinterpret_cast<uint4*>(As + buf * BM * BK + (i * RPP + wave * 8) * BK + lane * 8) = o;
+        if (pr_y) {
+          __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<decltype(__builtin_amdgcn_raw_buffer_load_b128(rY, 0, 0, 0))*>(&o),
+                                                 rY, (unsigned)pr_vo[i], (unsigned)pr_soff, 0);
+          // wait states for the store's data VGPRs before the next VALU write: hipcc's hazard
+          // pass misses this store-data hazard across the branch join inside the k-loop (the
+          // next chunk's first VALU op overwrote the 2nd data dword: tests/test_conv_gpu.py)
+          asm volatile("s_nop 4" ::: "memory");
+        }
+      }
+    }
+  };
+  auto pro_wait = [&]() {  // this slice's A loads retired (its BR B-operand DMAs may still be in flight)
+    if constexpr (BR == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if constexpr (BR == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+
   if (nk == 0) {  // no taps reach these outputs (strided dgrad parity class): D = 0 (+ E)
     for (int i = 0; i < my_tiles; i++) {
       epilogue(tile_of(i), 0);
@@ -484,7 +568,18 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
     }
     return;
   }
+  if constexpr (PRO) {
+    for (int i = tid; i < 2 * g.C; i += 64 * NW) ssl[i] = pro.ss[i];
+    __syncthreads();
+  }
   issue(0, 0);
+  if constexpr (PRO) {
+    if (total > 0) {
+      pro_wait();
+      pro_store(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the loop's first barrier publishes them
+    }
+  }
   for (int st = 0; st < total; st++) {
     const int buf = st & 1;
     if (st + 1 < total) {
@@ -497,6 +592,12 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
       asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
     }
     compute(buf);
+    if constexpr (PRO) {
+      if (st + 1 < total) {
+        pro_wait();
+        pro_store(buf ^ 1);
+      }
+    }
     if ((st + 1) % nk == 0) epilogue(tile_of(st / nk), buf);
     lds_barrier();  // every wave is done reading `buf` before slice st+2 is DMA'd into it
   }
@@ -628,6 +729,26 @@ static void launch_igemm(unsigned epi, dim3 grid, dim3 block, int lds, hipStream
 #undef KFA_IG
 }
 
+// PRO launches (forward convs reading a BatchNorm's raw input): EPI 0 or stats only
+template <int WM, int WN, int TM, int TN>
+static void launch_igemm_pro(unsigned epi, dim3 grid, dim3 block, int lds, hipStream_t st, const bf16_t* T,
+                             const bf16_t* B, bf16_t* D, float* stats, const Geo& g, const Pro& pro) {
+  const BnBwd bnb{nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr};
+#define KFA_IGP(EP)                                                                                                   \
+  {                                                                                                                   \
+    static bool attr = false;                                                                                         \
+    if (!attr && lds > 65536) {                                                                                       \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_igemm_kernel<WM, WN, TM, TN, EP, true>),          \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);                                     \
+      attr = true;                                                                                                    \
+    }                                                                                                                 \
+    hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, TM, TN, EP, true>), grid, block, lds, st, T, B, D, nullptr,          \
+                       zero_page(), stats, bnb, g, pro);                                                              \
+  }
+  if (epi & kEpiStats) KFA_IGP(kEpiStats) else KFA_IGP(0u)
+#undef KFA_IGP
+}
+
 // variant: 0 = 128x128 tile, 1 = 128x64 tile (N <= 64), 2 = 256x256 tile (8 waves), 3 = 256x64 (N <= 64)
 KFA_API int kfa_conv_igemm(const bf16_t* T, const bf16_t* B, bf16_t* D, const bf16_t* E, int Nb, int H, int W, int C,
                            int P, int Q, int R, int S, int sa, int ra, int oa, int ob, int N, int OH, int OW, int os,
@@ -689,6 +810,50 @@ KFA_API int kfa_conv_igemm(const bf16_t* T, const bf16_t* B, bf16_t* D, const bf
   } else {  // 128 x 128 tile: 2x2 waves of 64x64
     const int grid = pgrid((long)kfa_ceil_div(g.M, 128) * kfa_ceil_div(N, 128));
     launch_igemm<2, 2, 4, 4>(epi, dim3(grid), dim3(256), 2 * (128 + 128) * BK * 2, st, T, B, D, E, stats, bnb, g);
+  }
+  return kfa_status();
+}
+
+// Forward conv of relu(x * scale + shift) (a training BatchNorm + ReLU folded into
+// the A operand, see Pro): T = the BN's raw input x [Nb][H][W][C], ss = its
+// [scale | shift], y (optional) receives the normalised activation — only for
+// stride 1 with P == H, Q == W (the centre taps then cover every pixel).  D is
+// [Nb][P][Q][N]; stats as kfa_conv_igemm.
+KFA_API int kfa_conv_igemm_bnpro(const bf16_t* T, const bf16_t* B, bf16_t* D, const float* ss, bf16_t* y, int Nb,
+                                 int H, int W, int C, int P, int Q, int R, int S, int stride, int pad, int N,
+                                 int variant, float* stats, hipStream_t st) {
+  if (!ss || C % BK != 0 || N % 8 != 0 || C > 2048) return -1;
+  if (y && !(stride == 1 && P == H && Q == W && 2 * pad == R - 1 && 2 * pad == S - 1)) return -5;
+  Geo g{Nb, H, W, C, P, Q, R, S, stride, 1, -pad, -pad, Nb * P * Q, N, R * S * C, P, Q, 1, 0, 0, N, 0, 0, 0};
+  const long tb = (long)Nb * H * W * C * 2, bb = (long)N * R * S * C * 2, db = (long)Nb * P * Q * N * 2;
+  if (tb >= (long)kOOB || bb >= (long)kOOB || db >= (long)kOOB) return -2;
+  g.t_bytes = (unsigned)tb;
+  g.b_bytes = (unsigned)bb;
+  g.d_bytes = (unsigned)db;
+  if (g.M <= 0) return 0;
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  const Pro pro{ss, y};
+  const unsigned epi = stats ? kEpiStats : 0u;
+  const int tab = 8 * C;  // the [scale | shift] table behind the operand ring
+  auto cap = [&](long tiles, long slots) { return (int)(tiles < slots ? tiles : slots); };
+  if (variant == 3) {
+    const int grid = cap((long)kfa_ceil_div(g.M, 256) * kfa_ceil_div(N, 64), 2L * cus);
+    launch_igemm_pro<4, 1, 4, 4>(epi, dim3(grid), dim3(256), 2 * (256 + 64) * BK * 2 + tab, st, T, B, D, stats, g, pro);
+  } else if (variant == 1) {
+    const int grid = cap((long)kfa_ceil_div(g.M, 128) * kfa_ceil_div(N, 64), 3L * cus);
+    launch_igemm_pro<4, 1, 2, 4>(epi, dim3(grid), dim3(256), 2 * (128 + 64) * BK * 2 + tab, st, T, B, D, stats, g, pro);
+  } else if (variant == 2) {
+    const int grid = cap((long)kfa_ceil_div(g.M, 256) * kfa_ceil_div(N, 256), cus);
+    launch_igemm_pro<2, 4, 8, 4>(epi, dim3(grid), dim3(512), 2 * (256 + 256) * BK * 2 + tab, st, T, B, D, stats, g, pro);
+  } else {
+    const int grid = cap((long)kfa_ceil_div(g.M, 128) * kfa_ceil_div(N, 128), 2L * cus);
+    launch_igemm_pro<2, 2, 4, 4>(epi, dim3(grid), dim3(256), 2 * (128 + 128) * BK * 2 + tab, st, T, B, D, stats, g, pro);
   }
   return kfa_status();
 }

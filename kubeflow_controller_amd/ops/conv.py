@@ -34,6 +34,7 @@ from ..parallel.flat import direct_grad_view, notify_grad_ready
 
 P, I = _lib.P, _lib.I
 _lib.register("kfa_conv_igemm", [P, P, P, P] + [I] * 20 + [P, P, P, P, I, P, P, P, P])
+_lib.register("kfa_conv_igemm_bnpro", [P] * 5 + [I] * 12 + [P, P])
 _lib.register("kfa_zero_bf16", [P, _lib.L, P])
 _lib.register("kfa_weight_transpose", [P, P] + [I] * 10 + [P])
 _lib.register("kfa_weight_transpose_multi", [P, P, I, I, P])
@@ -186,6 +187,33 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, stats=None
     _lib.call("kfa_conv_igemm", _lib.ptr(x), _lib.ptr(w), _lib.ptr(y), None, Nb, H, W, C, Po, Qo, R, S, stride, 1,
               -pad, -pad, Co, Po, Qo, 1, 0, 0, Co, _variant(Nb * Po * Qo, Co, R * S * C), _lib.ptr(stats), None, None,
               None, 0, None, None, None, _lib.stream())
+    return y
+
+
+def bnpro_ok(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int) -> bool:
+    """``conv_fwd_bnpro`` covers this conv (and can write the normalised input as
+    a side output): NHWC bf16, C % 64 == 0, stride 1, 'same' padding."""
+    Co, C, R, S = w.shape
+    return (ENABLED and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and C % 64 == 0 and C <= 2048
+            and Co % 8 == 0 and stride == 1 and R == S and 2 * pad == R - 1)
+
+
+def conv_fwd_bnpro(x: torch.Tensor, ss: torch.Tensor, w: torch.Tensor, stride: int, pad: int, stats=None,
+                   y_out: "torch.Tensor | None" = None) -> torch.Tensor:
+    """Forward conv of ``relu(x * scale + shift)`` (per channel; ``ss`` = [scale | shift],
+    the BatchNorm's finalize output) with the BatchNorm-apply folded into the
+    implicit GEMM's A-operand load (``kfa_conv_igemm_bnpro``).  ``y_out`` (same
+    shape as ``x``) receives the normalised activation for the weight gradient."""
+    x, w = _cl(x), _cl(w)
+    Nb, C, H, W = x.shape
+    Co, _, R, S = w.shape
+    Po = (H + 2 * pad - R) // stride + 1
+    Qo = (W + 2 * pad - S) // stride + 1
+    y = torch.empty((Nb, Co, Po, Qo), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+    if y_out is not None and not y_out.is_contiguous(memory_format=torch.channels_last):
+        raise ValueError("conv_fwd_bnpro: y_out must be channels-last")
+    _lib.call("kfa_conv_igemm_bnpro", _lib.ptr(x), _lib.ptr(w), _lib.ptr(y), _lib.ptr(ss), _lib.ptr(y_out), Nb, H, W,
+              C, Po, Qo, R, S, stride, pad, Co, _variant(Nb * Po * Qo, Co, R * S * C), _lib.ptr(stats), _lib.stream())
     return y
 
 

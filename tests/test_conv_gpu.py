@@ -455,3 +455,52 @@ def test_batched_dgrad_weight_transpose_tracks_weight_updates(monkeypatch):
     for u, v in zip(ga, gb):
         assert torch.equal(u, v)
     assert len(convmod._tcache.entries) == 6  # a: 1; b (3x3/s2): 4 parity classes; c (1x1/s2): 1 class with taps
+
+
+@pytest.mark.parametrize("big", [False, True])
+@pytest.mark.parametrize("N,C,H,W,Co,k", [(4, 64, 14, 14, 64, 3), (2, 128, 14, 14, 256, 1), (3, 128, 7, 9, 128, 3),
+                                          (2, 64, 20, 20, 256, 1), (2, 256, 9, 11, 256, 3), (5, 64, 8, 8, 512, 1)])
+@pytest.mark.parametrize("with_y", [True, False])
+def test_conv_bn_apply_prologue(N, C, H, W, Co, k, big, with_y, monkeypatch):
+    """conv_fwd_bnpro(x, [scale|shift]) == conv_fwd(relu(x*scale+shift)) bit for bit
+    (same MFMA operands, same tile order), the fused BN statistics match, padding
+    taps stay zero (relu(shift) > 0 would leak there), and the side output is
+    exactly the bf16 activation bn_apply writes.  Also vs an fp32 PyTorch conv."""
+    from kubeflow_controller_amd.ops import _lib
+    from kubeflow_controller_amd.ops import conv as convmod
+    if big and Co % 256:
+        pytest.skip("256x256 tiles only for 256-multiple Cout")
+    monkeypatch.setattr(convmod, "BIG", big)
+    torch.manual_seed(1)
+    d = torch.device("cuda")
+    pad = k // 2
+    x = (torch.randn(N, C, H, W, device=d) * 2).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(Co, C, k, k, device=d) / (C * k * k) ** 0.5).to(torch.bfloat16)
+    w = w.contiguous(memory_format=torch.channels_last)
+    # the reference activation is bn_apply's own output (eval-mode BN + ReLU), ss its [scale | shift]
+    gamma, beta = torch.rand(C, device=d) + 0.25, torch.randn(C, device=d) * 0.5 + 0.3  # relu(shift) > 0 mostly
+    rm, rv = torch.randn(C, device=d) * 0.1, torch.rand(C, device=d) + 0.5
+    coef = torch.empty(3 * C, dtype=torch.float32, device=d)
+    yref = torch.empty_like(x)
+    _lib.call("kfa_bn_fwd_eval", _lib.ptr(x), None, _lib.ptr(yref), _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(rm),
+              _lib.ptr(rv), _lib.ptr(coef), N * H * W, C, 1e-5, 1, _lib.stream())
+    ss = coef[:2 * C]
+    sc, sh = ss[:C], ss[C:]
+    yf = torch.relu(x.float() * sc.view(1, C, 1, 1) + sh.view(1, C, 1, 1))
+    assert (yref.float() - yf).abs().max().item() <= 1e-2 * yf.abs().max().item()
+    nslot = _lib.lib().kfa_bn_slot_floats(Co)
+    st_a = torch.zeros(nslot, dtype=torch.float32, device=d)
+    st_b = torch.zeros(nslot, dtype=torch.float32, device=d)
+    y_out = torch.empty_like(x) if with_y else None
+    if y_out is not None:
+        y_out.fill_(float("nan"))
+    out = convmod.conv_fwd_bnpro(x, ss, w, 1, pad, st_a, y_out)
+    ref = convmod.conv_fwd(yref, w, 1, pad, st_b)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    if y_out is not None:
+        assert torch.equal(y_out, yref)
+    sa, sb = st_a.view(-1, 2 * Co).sum(0), st_b.view(-1, 2 * Co).sum(0)
+    torch.testing.assert_close(sa, sb, rtol=1e-4, atol=1e-2)
+    f32 = torch.nn.functional.conv2d(yref.float(), w.float(), None, 1, pad)
+    assert (out.float() - f32).abs().max().item() < 2e-2 * max(1.0, f32.abs().max().item())
