@@ -109,6 +109,11 @@ struct PppArgs {
   // pre-activation the backward needs), Y = gelu(z); bias fp32 [N], N <= 8192
   bf16_t* Y;
   const float* bias;
+  // GELU-backward epilogue (gemm_ppw_kernel<NT, DACT = true>): C = (A·Bᵀ) * gelu'(Zin + bias)
+  // with Zin the forward pre-activation (layout of C); column sums of C go to cpart
+  // ([ceil(M / 64)][N] fp32, one row per 64-row quadrant band, each entry written once)
+  const bf16_t* Zin;
+  float* cpart;
 };
 
 __device__ __forceinline__ void ppp_stagger(int ticks, int lc) {
@@ -671,7 +676,11 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
 // 32 KB hand-off = the CU's whole 160 KB.  No split remainder (data-parallel tiles).
 constexpr int HANDOFF = 16384;  // bytes per hand-off half: 4 waves x 64 rows x 32 cols x bf16
 
-template <bool NT>
+// DACT: the GELU-backward epilogue (the BERT FFN-down data gradient dz = (df2 · W2) *
+// gelu'(z1 + b1) and the FFN-up bias gradient's column sums): group 1 loads the
+// quadrant's z (and the bias) one phase ahead of its store phase (its counter holds no
+// DMA), multiplies, stores dz and writes the quadrant band's column sums to cpart.
+template <bool NT, bool DACT = false>
 __global__ __launch_bounds__(512, 1) void gemm_ppw_kernel(PppArgs g) {
   constexpr int BN = 256, WN = 64, TM = 8, TN = 4, NB1 = 2;
   constexpr int DW = 4;  // DMAs per piece per group-0 wave
@@ -699,6 +708,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ppw_kernel(PppArgs g) {
   const __amdgpu_buffer_rsrc_t rA = rsrc(g.A, (unsigned)(((long)(g.M - 1) * g.lda + g.K) * 2));
   const __amdgpu_buffer_rsrc_t rB = rsrc(g.B, (unsigned)(((long)(g.N - 1) * g.ldb + g.K) * 2));
   const __amdgpu_buffer_rsrc_t rC = rsrc(g.C, g.c_bytes);
+  const __amdgpu_buffer_rsrc_t rZ = rsrc(DACT ? g.Zin : g.C, DACT ? g.c_bytes : 0u);
   // DMA plan (group 0): instruction j of wave w fills piece rows j*32 + w*8 + lane/8
   const int prow = wc * 8 + (lane >> 3);
   const int lcx = (lane & 7) ^ ((prow >> 1) & 7);
@@ -773,17 +783,70 @@ __global__ __launch_bounds__(512, 1) void gemm_ppw_kernel(PppArgs g) {
       y = floatx4{0.f, 0.f, 0.f, 0.f};
     }
   };
-  // quadrant stores of wave-row group `grp` (a group-1 wave stores its partner's with grp = 0)
-  auto store_v = [&](int grp, int mh, int nh, int m0, int n0, const uint4 (&v)[4]) __attribute__((always_inline)) {
+  // byte offset of row block mi of quadrant (mh, nh) of wave-row group grp (kOOB past M / N)
+  auto q_off = [&](int grp, int mh, int nh, int m0, int n0, int mi) __attribute__((always_inline)) {
     const int n = n0 + wc * WN + nh * 32 + cb;
-    const bool nok = n < g.N;
+    const int m = m0 + grp * 128 + mh * 64 + mi * 16 + fr;
+    return (m < g.M && n < g.N) ? ((unsigned)m * (unsigned)g.ldc + (unsigned)n) * 2u : kOOB;
+  };
+  // DACT operands of a quadrant: zq[slot] its pre-activation rows, bq the bias of its 8 columns
+  uint4 zq[1][4];
+  float bq[8];
+  auto zload = [&](int slot, int grp, int mh, int nh, int m0, int n0) __attribute__((always_inline)) {
+    if constexpr (DACT) {
+#pragma unroll
+      for (int mi = 0; mi < 4; mi++) {
+        auto v = __builtin_amdgcn_raw_buffer_load_b128(rZ, q_off(grp, mh, nh, m0, n0, mi), 0, 0);
+        zq[slot][mi] = *reinterpret_cast<uint4*>(&v);
+      }
+    }
+  };
+  auto bload = [&](int nh, int n0) __attribute__((always_inline)) {
+    if constexpr (DACT) {
+      const int n = n0 + wc * WN + nh * 32 + cb;
+      if (g.bias && n < g.N) {
+        const float4 x = *reinterpret_cast<const float4*>(g.bias + n), y = *reinterpret_cast<const float4*>(g.bias + n + 4);
+        bq[0] = x.x; bq[1] = x.y; bq[2] = x.z; bq[3] = x.w; bq[4] = y.x; bq[5] = y.y; bq[6] = y.z; bq[7] = y.w;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; j++) bq[j] = 0.f;
+      }
+    }
+  };
+  // quadrant stores of wave-row group `grp` (a group-1 wave stores its partner's with grp = 0)
+  auto store_v = [&](int grp, int mh, int nh, int m0, int n0, const uint4 (&v)[4], int slot = 0)
+      __attribute__((always_inline)) {
+    float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int mi = 0; mi < 4; mi++) {
-      const int m = m0 + grp * 128 + mh * 64 + mi * 16 + fr;
-      const unsigned off = (m < g.M && nok) ? ((unsigned)m * (unsigned)g.ldc + (unsigned)n) * 2u : kOOB;
+      const unsigned off = q_off(grp, mh, nh, m0, n0, mi);
       using V = decltype(__builtin_amdgcn_raw_buffer_load_b128(rC, 0, 0, 0));
       uint4 w = v[mi];
+      if constexpr (DACT) {  // dz = c * gelu'(z + b) from the bf16 product, as bias_act_bwd evaluates it
+        float c[8], z[8];
+        unpack8(w, c);
+        unpack8(zq[slot][mi], z);
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+          c[j] *= gelu_grad(z[j] + bq[j]);
+          cs[j] += c[j];
+        }
+        w = pack8(c);
+      }
       __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<V*>(&w), rC, off, 0, NT ? 2 : 0);
+    }
+    if constexpr (DACT) {
+      // the 16 lanes of a column chunk (fr) hold 16 rows each x 4 row blocks: band total
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+        for (int j = 0; j < 8; j++) cs[j] += __shfl_xor(cs[j], o, 64);
+      const int n = n0 + wc * WN + nh * 32 + cb, mb = m0 + grp * 128 + mh * 64;
+      if (g.cpart && fr == 0 && n < g.N && mb < g.M) {
+        float* dst = g.cpart + (long)(mb >> 6) * g.N + n;
+        *reinterpret_cast<float4*>(dst) = make_float4(cs[0], cs[1], cs[2], cs[3]);
+        *reinterpret_cast<float4*>(dst + 4) = make_float4(cs[4], cs[5], cs[6], cs[7]);
+      }
     }
   };
   // hand-off area of phase parity `hp`: [wave column wc][mi][lane] 16-B slots (each wave its own 4 KB)
@@ -803,6 +866,25 @@ __global__ __launch_bounds__(512, 1) void gemm_ppw_kernel(PppArgs g) {
         asm volatile("ds_write_b128 %0, %1" ::"v"(ho_addr(hp, mi)), "v"(w) : "memory");
       }
     } else {
+      if constexpr (DACT) {
+        // own quadrant: its z + the bias (group 1's counter holds no DMA: plain waits), then the
+        // partner's z into the same registers and its hand-off — one operand set live at a time
+        zload(0, 1, mh, nh, pm0, pn0);
+        bload(nh, pn0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        store_v(1, mh, nh, pm0, pn0, v);
+        zload(0, 0, mh, nh, pm0, pn0);
+        u32x4 pw[4];
+#pragma unroll
+        for (int mi = 0; mi < 4; mi++) asm volatile("ds_read_b128 %0, %1" : "=v"(pw[mi]) : "v"(ho_addr(hp, mi)) : "memory");
+        asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" : "+v"(pw[0]), "+v"(pw[1]), "+v"(pw[2]), "+v"(pw[3]) :: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        uint4 pv[4];
+#pragma unroll
+        for (int mi = 0; mi < 4; mi++) pv[mi] = make_uint4(pw[mi][0], pw[mi][1], pw[mi][2], pw[mi][3]);
+        store_v(0, mh, nh, pm0, pn0, pv);
+        return;
+      }
       u32x4 pw[4];
 #pragma unroll
       for (int mi = 0; mi < 4; mi++) asm volatile("ds_read_b128 %0, %1" : "=v"(pw[mi]) : "v"(ho_addr(hp, mi)) : "memory");
@@ -853,7 +935,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ppw_kernel(PppArgs g) {
       if (ho) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
   };
-  auto ktile = [&](int u, auto mode) __attribute__((always_inline)) {
+  auto ktile = [&](int u, auto mode, bool pre = false) __attribute__((always_inline)) {
     constexpr bool EPI = decltype(mode)::value;
     const char* buf = smem + (u & 1) * (4 * PIECE);
     {  // s0: A0 + B0 -> quadrant (0, 0)
@@ -906,6 +988,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ppw_kernel(PppArgs g) {
     }
     {  // s3: registers only -> quadrant (1, 0)
       if constexpr (EPI) epi(1, 0, 1, pm0, pn0);
+      (void)pre;
       issue(std::integral_constant<int, 1>{}, u + 2);
       retire(EPI);
       asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
@@ -926,22 +1009,44 @@ __global__ __launch_bounds__(512, 1) void gemm_ppw_kernel(PppArgs g) {
       ktile(u++, std::true_type{});
       k = 1;
     }
-    for (; k < nk; k++) ktile(u++, std::false_type{});
+    for (; k < nk; k++) ktile(u++, std::false_type{}, DACT && k == nk - 1 && t + 1 < my_tiles);
   }
   if (!wr) asm volatile("s_barrier" ::: "memory");  // both groups at the same barrier count
   // the last tile: every wave stores its own quadrants (group 0's DMAs are all issued)
   {
     uint4 v[4];
-    pack_q(0, 0, v);
-    store_v(wr, 0, 0, cm0, cn0, v);
-    pack_q(0, 1, v);
-    store_v(wr, 0, 1, cm0, cn0, v);
-    pack_q(1, 1, v);
-    store_v(wr, 1, 1, cm0, cn0, v);
-    pack_q(1, 0, v);
-    store_v(wr, 1, 0, cm0, cn0, v);
+    auto tail = [&](int mh, int nh) __attribute__((always_inline)) {
+      if constexpr (DACT) {
+        zload(0, wr, mh, nh, cm0, cn0);
+        bload(nh, cn0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      pack_q(mh, nh, v);
+      store_v(wr, mh, nh, cm0, cn0, v);
+    };
+    tail(0, 0);
+    tail(0, 1);
+    tail(1, 1);
+    tail(1, 0);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail's zero-fill DMAs land before the LDS is released
+}
+
+// out[c] (+)= sum over rows of part[r][c] (the DACT epilogue's column-sum bands):
+// block = 64 columns x 4 row lanes, grid = ceil(N / 64); fixed summation order.
+__global__ __launch_bounds__(256) void colpart_reduce(const float* __restrict__ part, int R, int N,
+                                                      float* __restrict__ out, int accumulate) {
+  __shared__ float red[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), rl = threadIdx.x >> 6;
+  float s = 0.f;
+  if (c < N)
+    for (int r = rl; r < R; r += 4) s += part[(long)r * N + c];
+  red[rl][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (rl == 0 && c < N) {
+    const float t = (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
+    out[c] = accumulate ? out[c] + t : t;
+  }
 }
 
 int ppp_cus() {
@@ -1022,6 +1127,35 @@ KFA_API int kfa_gemm_ppp_gelu(const bf16_t* A, const bf16_t* B, bf16_t* Z, bf16_
   const int grid = (int)(tiles < cus ? tiles : cus);
   const PppArgs g{A, B, Z, M, N, K, lda, ldb, ldc, (unsigned)cb, nullptr, nullptr, 1, g_stagger, Y, bias};
   hipLaunchKernelGGL((gemm_ppp_kernel<256, false, 0, false, true>), dim3(grid), dim3(512), 0, st, g);
+  return kfa_status();
+}
+
+// dz = (A · Bᵀ) * gelu'(Zin + bias) (bf16; bias fp32 [N] or null) on the wave-specialised
+// persistent kernel with the GELU-backward epilogue; dbias (fp32 [N], nullable) (+)= the
+// column sums of dz (via cpart: kfa_gemm_ppw_dact_part_floats(M, N) floats of scratch).
+// K % 8 == 0, K >= 128, N % 8 == 0; Zin shares C's ldc.  Returns 0, -1 on unsupported operands.
+KFA_API long kfa_gemm_ppw_dact_part_floats(int M, int N) { return (long)((M + 63) / 64) * N; }
+
+KFA_API int kfa_gemm_ppw_dact(const bf16_t* A, const bf16_t* B, bf16_t* C, const bf16_t* Zin, const float* bias,
+                              float* cpart, float* dbias, int accumulate, int M, int N, int K, int lda, int ldb,
+                              int ldc, int nt, hipStream_t st) {
+  if (M <= 0 || N <= 0) return 0;
+  if (K < 2 * BK || K % 8 || N % 8 || lda % 8 || ldb % 8 || ldc % 8 || lda < K || ldb < K || ldc < N || !Zin ||
+      (dbias && !cpart))
+    return -1;
+  const long cb = (long)M * ldc * 2;
+  if (cb >= (long)kOOB || (long)M * lda * 2 >= (long)kOOB || (long)N * ldb * 2 >= (long)kOOB) return -2;
+  const long tiles = (long)((M + 255) / 256) * ((N + 255) / 256);
+  const long cus = ppp_cus();
+  PppArgs g{A, B, C, M, N, K, lda, ldb, ldc, (unsigned)cb, nullptr, nullptr, 1, g_stagger, nullptr, bias};
+  g.Zin = Zin;
+  g.cpart = dbias ? cpart : nullptr;
+  const int grid = (int)(tiles < cus ? tiles : cus);
+  if (nt) hipLaunchKernelGGL((gemm_ppw_kernel<true, true>), dim3(grid), dim3(512), 0, st, g);
+  else hipLaunchKernelGGL((gemm_ppw_kernel<false, true>), dim3(grid), dim3(512), 0, st, g);
+  if (dbias)
+    hipLaunchKernelGGL(colpart_reduce, dim3((N + 63) / 64), dim3(256), 0, st, cpart, (M + 63) / 64, N, dbias,
+                       accumulate);
   return kfa_status();
 }
 

@@ -36,6 +36,8 @@ _lib.register("kfa_gemm_ppp_ws_bytes", [I] * 5, restype=_lib.L)
 _lib.register("kfa_gemm_ppp_pick_bn", [I, I])
 _lib.register("kfa_gemm_skinny", [P, P, P, P] + [I] * 7 + [P, _lib.L, P])
 _lib.register("kfa_gemm_ppp_gelu", [P] * 5 + [I] * 6 + [P])
+_lib.register("kfa_gemm_ppw_dact", [P] * 7 + [I] * 8 + [P])
+_lib.register("kfa_gemm_ppw_dact_part_floats", [I, I], _lib.L)
 _lib.register("kfa_gemm_skinny_ws_bytes", [I] * 4, restype=_lib.L)
 
 ACTS = {None: 0, "none": 0, "gelu": 1, "tanh": 2, "relu": 3}
@@ -180,6 +182,35 @@ def gemm_ppp(a, b, *, out=None, blocks: int = 0, probe: int = 0, bn: int = 0, sp
     ws = _lib.workspace(nb, a.device, f"ppp_ws{_lib.stream() or 0}") if nb > 0 else None
     _lib.call("kfa_gemm_ppp", _lib.ptr(a), _lib.ptr(b), _lib.ptr(c), M, N, K, a.stride(0), b.stride(0), N,
               int(blocks), int(probe), int(bn), _lib.ptr(ws), nb, int(not split), _lib.stream())
+    return c
+
+
+def ppw_dact_ok(a, b, zin) -> bool:
+    """Operands :func:`gemm_ppw_dact` takes."""
+    return (ppp_ok(a, b) and zin is not None and zin.dtype == torch.bfloat16 and zin.is_contiguous()
+            and tuple(zin.shape) == (a.shape[0], b.shape[0]) and zin.data_ptr() % 16 == 0)
+
+
+def gemm_ppw_dact(a, b, zin, bias=None, dbias=None, *, nt: bool = False, accumulate: bool = True):
+    """``dz = (a @ b.T) * gelu'(zin + bias)`` (bf16) from ONE launch of the
+    wave-specialised persistent GEMM with the GELU-backward epilogue
+    (``gemm_ppw_kernel<..., DACT>``): no separate activation-gradient pass.
+    ``dbias`` (fp32 [N]) (+)= the column sums of dz (epilogue band partials + one
+    small reduce launch, fixed order)."""
+    if not ppw_dact_ok(a, b, zin):
+        raise ValueError(f"gemm_ppw_dact: unsupported operands {tuple(a.shape)} x {tuple(b.shape)}")
+    M, K = a.shape
+    N = b.shape[0]
+    _check_vec(bias, N, "bias")
+    c = torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
+    part = None
+    if dbias is not None:
+        _check_vec(dbias, N, "dbias")
+        part = _lib.workspace(_lib.lib().kfa_gemm_ppw_dact_part_floats(M, N) * 4, a.device,
+                              f"ppw_dact{_lib.stream() or 0}")
+    _lib.call("kfa_gemm_ppw_dact", _lib.ptr(a), _lib.ptr(b), _lib.ptr(c), _lib.ptr(zin), _lib.ptr(bias),
+              _lib.ptr(part), _lib.ptr(dbias), int(accumulate), M, N, K, a.stride(0), b.stride(0), N, int(nt),
+              _lib.stream())
     return c
 
 

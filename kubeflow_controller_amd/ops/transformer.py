@@ -71,6 +71,12 @@ EMB_SMALL_KERNEL = os.environ.get("KFA_EMB_SMALL", "1") != "0"
 # 0.2255 for hipBLASLt + the bias/GELU pass (32768 x 3072 x 768) — its 8 stores per phase
 # sit in the counted vmcnt window of the DMA retires and stall the pipeline.
 FFN_GELU_EPI = os.environ.get("KFA_FFN_GELU_EPI", "0") == "1"
+# KFA_DACT_EPI=1: the FFN-down data gradient through the GELU also times the
+# wave-specialised GEMM with the GELU-backward epilogue (gemm_ppw_dact) against GEMM +
+# bias_act_bwd.  Off by default: measured 392-425 vs 257-266 us (32768 x 3072 x 768) — the
+# GELU' arithmetic (~25 VALU ops per element) lands on the store waves' share of the MFMA
+# pipeline at the tile boundary, and the extra operand registers spill (docs/kernels.md).
+DACT_EPI = os.environ.get("KFA_DACT_EPI", "0") == "1"
 _MASK64 = (1 << 64) - 1
 
 
@@ -500,6 +506,28 @@ def _ffn_up(h, w, b):
     return bias_act_fwd(z, b, "gelu"), z, False
 
 
+def _ffn_down_dgrad_gelu(df2, w2, z, bias, dbias):
+    """``dz = (df2 @ w2) * gelu'(z + bias)`` and ``dbias += colsum(dz)`` — the FFN-down
+    data gradient through the GELU: per shape the faster of the data-gradient GEMM
+    (:func:`ops.gemm.dgrad_auto`) + the ``bias_act_bwd`` pass, and the wave-specialised
+    persistent GEMM with the GELU-backward epilogue (``gemm_ppw_dact``: one GEMM
+    launch, no 3-tensor pass).  The timing runs accumulate into a scratch bias gradient."""
+    if _gemm.ROUTE_AUTO and DACT_EPI and df2.is_cuda:
+        w2t = _gemm.transpose_cached(w2)
+        if _gemm.ppw_dact_ok(df2, w2t, z) and dbias is not None and dbias.dtype == torch.float32:
+            key = (df2.shape[0], w2.shape[1], df2.shape[1])
+            hit = _gemm._choice.get(("ffn_down_dgelu",) + key)
+            if hit is None:
+                scratch = torch.zeros_like(dbias)
+                cands = [("dgrad+pass", lambda: bias_act_bwd(_gemm.dgrad_auto(df2, w2), z, bias, "gelu", scratch)),
+                         ("ppw-dact", lambda: _gemm.gemm_ppw_dact(df2, w2t, z, bias, scratch)),
+                         ("ppw-dact-nt", lambda: _gemm.gemm_ppw_dact(df2, w2t, z, bias, scratch, nt=True))]
+                hit = _gemm.pick_fastest("ffn_down_dgelu", key, df2.device, cands)
+            if hit:
+                return _gemm.gemm_ppw_dact(df2, w2t, z, bias, dbias, nt=hit == 2)
+    return bias_act_bwd(_gemm.dgrad_auto(df2, w2), z, bias, "gelu", dbias)
+
+
 # ----------------------------------------------------------------------------- encoder layer
 class EncoderLayerFn(torch.autograd.Function):
     """Post-LN BERT encoder layer, forward + backward written out (see module doc).
@@ -594,7 +622,7 @@ class EncoderLayerFn(torch.autograd.Function):
         if use_f:   # df1 = (df2 · W2) * gelu'(z1), db1 += colsum(df1): one GEMM launch
             df1 = _gemm.gemm_nt(df2, _gemm.transpose(w2), zin=f1, dact="gelu", dbias=G(b1))[0]
         else:
-            df1 = bias_act_bwd(_gemm.dgrad_auto(df2, w2), f1, None if z_bias else b1, "gelu", G(b1))
+            df1 = _ffn_down_dgrad_gelu(df2, w2, f1, None if z_bias else b1, G(b1))
         del df2
         _wgrad_side_(G(w1), df1, h1)
         if use_g:   # residual-gradient join as the GEMM addend

@@ -255,3 +255,34 @@ def test_gemm_ppp_gelu_epilogue_matches_fp32(M, N, K):
     _close(y, F.gelu(z.float()), 1e-2, f"y {M}x{N}x{K}")
     y2, z2 = G.gemm_ppp_gelu(a, b, bias)
     assert torch.equal(y, y2) and torch.equal(z, z2)
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 3072, 768), (1000, 520, 136), (777, 256, 256), (2048, 1024, 512)])
+@pytest.mark.parametrize("with_bias", [True, False])
+@pytest.mark.parametrize("nt", [False, True])
+def test_ppw_gelu_backward_epilogue(M, N, K, with_bias, nt):
+    """gemm_ppw_dact: dz = (a @ b.T) * gelu'(z + bias) and dbias += colsum(dz), vs fp32
+    PyTorch (exact-erf GELU derivative) and vs the unfused bias_act_bwd path."""
+    from kubeflow_controller_amd.ops import gemm as G
+    from kubeflow_controller_amd.ops.transformer import bias_act_bwd
+    torch.manual_seed(3)
+    d = torch.device("cuda")
+    a = (torch.randn(M, K, device=d) / K ** 0.25).to(torch.bfloat16)
+    b = (torch.randn(N, K, device=d) / K ** 0.25).to(torch.bfloat16)
+    z = torch.randn(M, N, device=d).to(torch.bfloat16)
+    bias = torch.randn(N, device=d) * 0.5 if with_bias else None
+    dbias = torch.full((N,), 0.25, device=d)
+    dz = G.gemm_ppw_dact(a, b, z, bias, dbias, nt=nt)
+    zf = z.float() + (bias if with_bias else 0.0)
+    x = zf / 2 ** 0.5
+    gp = 0.5 * (1 + torch.erf(x)) + zf * torch.exp(-x * x) / (2 * torch.pi) ** 0.5
+    c = (a.float() @ b.float().t()).to(torch.bfloat16).float()
+    ref = c * gp
+    err = (dz.float() - ref).abs().max().item()
+    assert err <= 2e-2 * ref.abs().max().item() + 1e-2, err
+    dref = 0.25 + ref.sum(0)
+    torch.testing.assert_close(dbias, dref, rtol=2e-3, atol=2e-2 * (M ** 0.5))
+    # the unfused path (same bf16 product -> same GELU' arithmetic)
+    db2 = torch.full((N,), 0.25, device=d)
+    dz2 = bias_act_bwd(c.to(torch.bfloat16), z, bias, "gelu", db2)
+    assert (dz.float() - dz2.float()).abs().max().item() <= 2e-2 * dz2.float().abs().max().item() + 1e-2

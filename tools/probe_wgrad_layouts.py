@@ -22,11 +22,13 @@ def t(fn, it=20):
 
 
 d = torch.device("cuda")
-for (M, N, K) in [(16384, 3072, 768), (16384, 2304, 768), (16384, 768, 3072), (16384, 768, 768), (8192, 2304, 768)]:
+ROWS = int(os.environ.get("ROWS", "32768"))  # BERT-base 256 x 128 tokens
+for (M, N, K) in [(ROWS, 3072, 768), (ROWS, 2304, 768), (ROWS, 768, 3072), (ROWS, 768, 768)]:
     x = torch.randn(M, K, device=d, dtype=torch.bfloat16)
     dy = torch.randn(M, N, device=d, dtype=torch.bfloat16)
     gw = torch.zeros(N, K, device=d, dtype=torch.bfloat16)
     gwt = torch.zeros(K, N, device=d, dtype=torch.bfloat16)
+    gw32 = torch.zeros(N, K, device=d, dtype=torch.float32)  # the flat fp32 gradient bucket (the real target)
     fl = 2 * M * N * K
     res = {
         "addmm_(dyT,x)": t(lambda: gw.addmm_(dy.t(), x)),
@@ -35,5 +37,7 @@ for (M, N, K) in [(16384, 3072, 768), (16384, 2304, 768), (16384, 768, 3072), (1
         "addmm_T(xT,dy)": t(lambda: gwt.addmm_(x.t(), dy)),
         "mm(dyT.cont,x)": t(lambda: torch.mm(dy.t().contiguous(), x)),
         "kfa_wgrad": t(lambda: wgrad_into(x, dy, gw, 1, 1, M, K, 1, M, N, 1, 1, 1, 0, True)),
+        "kfa_wgrad_f32": t(lambda: wgrad_into(x, dy, gw32, 1, 1, M, K, 1, M, N, 1, 1, 1, 0, True)),
+        "mm+add_f32": t(lambda: gw32.add_(torch.mm(dy.t(), x))),
     }
     print(M, N, K, " | ".join(f"{k} {fl / v / 1e9:.0f}" for k, v in res.items()), flush=True)
