@@ -14,15 +14,18 @@ typedef __attribute__((ext_vector_type(16))) float floatx16;
 
 __device__ __forceinline__ float bf2f(uint32_t b) { return __uint_as_float(b << 16); }
 
-// round-to-nearest-even float -> bf16 (NaN kept quiet)
-__device__ __forceinline__ uint32_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (u >> 16) | 0x40u;
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return u >> 16;
+// float -> bf16, round to nearest even, NaN kept quiet: gfx950's v_cvt_pk_bf16_f32
+// (one VALU op per PAIR — the integer rounding sequence it replaces took ~7 per element,
+// a visible share of the VALU-bound attention kernels, profiles/pmc/r4_attention.md)
+typedef __attribute__((ext_vector_type(2))) __bf16 kfa_bf16x2_t;
+typedef __attribute__((ext_vector_type(2))) float kfa_floatx2_t;
+
+__device__ __forceinline__ uint32_t pack2(float lo, float hi) {
+  const kfa_floatx2_t f = {lo, hi};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f, kfa_bf16x2_t));
 }
 
-__device__ __forceinline__ uint32_t pack2(float lo, float hi) { return f2bf(lo) | (f2bf(hi) << 16); }
+__device__ __forceinline__ uint32_t f2bf(float f) { return pack2(f, 0.f) & 0xffffu; }
 
 // unpack a 16-byte vector of 8 bf16 into floats
 __device__ __forceinline__ void unpack8(const uint4 v, float f[8]) {
