@@ -640,6 +640,16 @@ KFA_API int kfa_bn_fwd_train_prestats(const bf16_t* x, const bf16_t* res, bf16_t
   return kfa_status();
 }
 
+// y = act(x * scale + shift) with a given [scale | shift] (2C floats): the apply pass of a
+// training BatchNorm whose finalize already ran (kfa_bn_finalize) and whose consumer could
+// not take the normalisation into its own operand load (ops/batchnorm.py, lazy outputs).
+KFA_API int kfa_bn_apply_ss(const bf16_t* x, bf16_t* y, const float* ss, long M, int C, int relu, hipStream_t s) {
+  if (!bn_shape_ok(M, C) || !ss) return -1;
+  Geom g = geom(M, C, max_row_blocks(C));
+  launch_apply(relu, nullptr, nullptr, dim3(g.gx), s, x, y, ss, ss + C, M, C, g.chunk, g.tpr, g.rpi);
+  return kfa_status();
+}
+
 KFA_API int kfa_bn_fwd_eval(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* gamma, const float* beta,
                             const float* rmean, const float* rvar, float* ws, long M, int C, float eps, int relu,
                             hipStream_t s) {

@@ -21,6 +21,9 @@ from ..ops.pool import MaxPool2d, global_avg_pool
 
 
 DUAL_BN = os.environ.get("KFA_BN_DUAL", "1") != "0"
+# bn2's output (read only by the 1x1 conv3) is left lazy: conv3 folds the BN-apply + ReLU
+# into its operand load where the per-shape tuner measured that faster (ops.conv._use_bnpro)
+LAZY_BN2 = os.environ.get("KFA_LAZY_BN2", "1") != "0"
 FUSED_STEM_POOL = os.environ.get("KFA_STEM_POOL_FUSED", "1") != "0"
 
 
@@ -59,7 +62,7 @@ class Bottleneck(nn.Module):
         st = self.training
         if self.downsample is None:
             y = self.bn1(self.conv1(x, join=join, bn_stats=st), bwd_link=st)
-            y = self.bn2(self.conv2(y, bn_stats=st), bwd_link=st)
+            y = self.bn2(self.conv2(y, bn_stats=st), bwd_link=st, lazy=st and LAZY_BN2)
             return self.bn3(self.conv3(y, bn_stats=st), residual=join.branch(x), bwd_link=st, res_join=join)
         # downsample block: relu(bn3(.) + bn_ds(.)) in ONE apply pass each way
         # (ops.batchnorm.bn_act_dual): the downsample conv's statistics wait in
@@ -68,7 +71,7 @@ class Bottleneck(nn.Module):
         r = self.downsample["conv"](x, join=join, bn_stats=(DS_SLOTS if dual else st))
         idn = None if dual else self.downsample["bn"](r)
         y = self.bn1(self.conv1(join.branch(x), bn_stats=st), bwd_link=st)
-        y = self.bn2(self.conv2(y, bn_stats=st), bwd_link=st)
+        y = self.bn2(self.conv2(y, bn_stats=st), bwd_link=st, lazy=st and LAZY_BN2)
         if dual:
             return bn_act_dual(self.bn3, self.conv3(y, bn_stats=st), self.downsample["bn"], r, bwd_link=st)
         return self.bn3(self.conv3(y, bn_stats=st), residual=idn, bwd_link=st)

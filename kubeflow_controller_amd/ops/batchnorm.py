@@ -47,6 +47,32 @@ _lib.register("kfa_bn_finalize", [_lib.P, _lib.P, _lib.L, _lib.I] + [_lib.P] * 7
 _lib.register("kfa_bn_fwd_train_dual", [_lib.P] * 11 + [_lib.L, _lib.I, _lib.F, _lib.F, _lib.I, _lib.P, _lib.P,
                                                         _lib.I, _lib.P])
 _lib.register("kfa_bn_bwd_rstats", [_lib.P] * 11 + [_lib.L, _lib.I, _lib.I, _lib.I] + [_lib.P] * 5 + [_lib.I, _lib.P])
+_lib.register("kfa_bn_apply_ss", [_lib.P, _lib.P, _lib.P, _lib.L, _lib.I, _lib.I, _lib.P])
+
+
+class LazyBN:
+    """A training BatchNorm + ReLU whose apply pass is deferred to its consumer: the
+    output tensor is allocated but NOT written; ``x`` (the BN input) and ``ss`` (its
+    [scale | shift]) let the one convolution that reads it fold relu(x·scale + shift)
+    into its A-operand load (``ops.conv.conv_fwd_bnpro``, which also fills the output
+    for the weight gradient), or :func:`materialize` runs the apply pass first.  Only a
+    model that guarantees that conv is the sole reader may ask for it (``lazy=True``)."""
+
+    __slots__ = ("x", "ss", "pending")
+
+    def __init__(self):
+        self.x = self.ss = None
+        self.pending = False
+
+
+def materialize(t: torch.Tensor) -> torch.Tensor:
+    """Write a lazy BatchNorm output (no-op for any other tensor)."""
+    lz = getattr(t, "_kfa_lazy", None)
+    if lz is not None and lz.pending:
+        M, C = _mc(lz.x)
+        _lib.call("kfa_bn_apply_ss", _lib.ptr(lz.x), _lib.ptr(t), _lib.ptr(lz.ss), M, C, 1, _lib.stream())
+        lz.pending = False
+    return t
 
 
 class BnBwdLink:
@@ -89,7 +115,7 @@ def _workspaces(C: int, device):
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, residual, training, momentum, eps, relu,
-                prestats=False, link=None, res_join=None):
+                prestats=False, link=None, res_join=None, lazy=None):
         x = _as_rows(x)
         M, C = _mc(x)
         if x.dtype != torch.bfloat16:
@@ -111,11 +137,17 @@ class _BNActFn(torch.autograd.Function):
             elif relu and MASK_FROM_X:
                 # with a residual the mask needs the output: keep it as bits (1/16 of y)
                 mb = torch.empty(M * C // 8, dtype=torch.uint8, device=x.device)
-            _lib.call("kfa_bn_fwd_train_prestats" if prestats else "kfa_bn_fwd_train", _lib.ptr(x), _lib.ptr(res),
-                      _lib.ptr(y), _lib.ptr(weight), _lib.ptr(bias),
-                      _lib.ptr(running_mean), _lib.ptr(running_var), _lib.ptr(mean), _lib.ptr(invstd),
-                      _lib.ptr(slots), _lib.ptr(coef if ss is None else ss), M, C, eps, momentum, int(relu),
-                      _lib.ptr(mb), s)
+            if lazy is not None and ss is not None:  # finalize only: the consumer conv applies it
+                _lib.call("kfa_bn_finalize", _lib.ptr(x), _lib.ptr(slots), M, C, _lib.ptr(weight), _lib.ptr(bias),
+                          _lib.ptr(running_mean), _lib.ptr(running_var), _lib.ptr(mean), _lib.ptr(invstd),
+                          _lib.ptr(ss), eps, momentum, int(prestats), s)
+                lazy.x, lazy.ss, lazy.pending = x, ss, True
+            else:
+                _lib.call("kfa_bn_fwd_train_prestats" if prestats else "kfa_bn_fwd_train", _lib.ptr(x),
+                          _lib.ptr(res), _lib.ptr(y), _lib.ptr(weight), _lib.ptr(bias),
+                          _lib.ptr(running_mean), _lib.ptr(running_var), _lib.ptr(mean), _lib.ptr(invstd),
+                          _lib.ptr(slots), _lib.ptr(coef if ss is None else ss), M, C, eps, momentum, int(relu),
+                          _lib.ptr(mb), s)
         else:
             _lib.call("kfa_bn_fwd_eval", _lib.ptr(x), _lib.ptr(res), _lib.ptr(y), _lib.ptr(weight), _lib.ptr(bias),
                       _lib.ptr(running_mean), _lib.ptr(running_var), _lib.ptr(coef), M, C, eps, int(relu), s)
@@ -168,14 +200,14 @@ class _BNActFn(torch.autograd.Function):
         if direct:
             notify_grad_ready(ctx.params[0])
             notify_grad_ready(ctx.params[1])
-            return dx, None, None, None, None, dres, None, None, None, None, None, None, None
+            return dx, None, None, None, None, dres, None, None, None, None, None, None, None, None
         if dgamma is not None and weight is not None and weight.dtype != torch.float32:
             dgamma, dbeta = dgamma.to(weight.dtype), dbeta.to(weight.dtype)
-        return dx, dgamma, dbeta, None, None, dres, None, None, None, None, None, None, None
+        return dx, dgamma, dbeta, None, None, dres, None, None, None, None, None, None, None, None
 
 
 def bn_act(x, weight, bias, running_mean, running_var, residual=None, training=True, momentum=0.1, eps=1e-5,
-           relu=True, prestats=False, bwd_link=False, res_join=None):
+           relu=True, prestats=False, bwd_link=False, res_join=None, lazy=False):
     """``prestats``: the statistics of ``x`` already sit in the BN slot workspace
     (accumulated by the producing convolution's epilogue).  ``bwd_link``: the
     output feeds exactly one igemm convolution, whose dgrad epilogue may compute
@@ -186,10 +218,13 @@ def bn_act(x, weight, bias, running_mean, running_var, residual=None, training=T
         bn_slot_workspace(x.shape[1], x.device).zero_()
         prestats = False
     link = BnBwdLink() if (bwd_link and training) else None
+    lz = LazyBN() if (lazy and training and relu and residual is None and MASK_FROM_X and x.is_cuda) else None
     y = _BNActFn.apply(x, weight, bias, running_mean, running_var, residual, training, momentum, eps, relu,
-                       prestats, link, res_join)
+                       prestats, link, res_join, lz)
     if link is not None:
         y._kfa_bn_link = link
+    if lz is not None and lz.pending:
+        y._kfa_lazy = lz
     return y
 
 
@@ -417,11 +452,13 @@ class BatchNorm2dAct(nn.Module):
         self.register_buffer("running_mean", torch.zeros(num_features))
         self.register_buffer("running_var", torch.ones(num_features))
 
-    def forward(self, x, residual=None, bwd_link: bool = False, res_join=None):
+    def forward(self, x, residual=None, bwd_link: bool = False, res_join=None, lazy: bool = False):
+        """``lazy``: the output feeds exactly one ``ops.conv.conv2d`` next, which folds the
+        BN-apply + ReLU into its operand load where that measured faster (``LazyBN``)."""
         if x.is_cuda:
             pre = getattr(x, "_kfa_prestats", False) and getattr(x, "_kfa_prestats_tag", "bn_slots") == "bn_slots"
             return bn_act(x, self.weight, self.bias, self.running_mean, self.running_var, residual,
-                          self.training, self.momentum, self.eps, self.relu, pre, bwd_link, res_join)
+                          self.training, self.momentum, self.eps, self.relu, pre, bwd_link, res_join, lazy)
         # CPU path (plumbing tests / CPU-only MNIST-style jobs): plain PyTorch.
         y = torch.nn.functional.batch_norm(x, self.running_mean, self.running_var, self.weight.to(x.dtype),
                                            self.bias.to(x.dtype), self.training, self.momentum, self.eps)

@@ -479,9 +479,43 @@ class _Branch(torch.autograd.Function):
         return None, None
 
 
+# KFA_CONV_BNPRO=0: lazy BatchNorm outputs are always materialised by the apply pass
+BNPRO = os.environ.get("KFA_CONV_BNPRO", "1") != "0"
+_bnpro_choice = {}
+
+
+def _use_bnpro(lz, x, w, stride, pad, stats) -> bool:
+    """Fold the lazy BatchNorm's apply into this conv (``conv_fwd_bnpro``)?  Per shape, the
+    faster of (apply pass + conv) and the fused conv, timed once at first use (scratch
+    outputs and statistics; rank 0's choice everywhere).  Measured: a win for the 1x1
+    bn2 -> conv3 layers up to 256 channels, a loss for every 3x3 (the transform is redone
+    per tap) — ``profiles/r4_bn_apply_prologue.md``."""
+    if not (BNPRO and bnpro_ok(x, w, stride, pad) and not torch.cuda.is_current_stream_capturing()):
+        return False
+    key = (tuple(x.shape), tuple(w.shape), stride, pad, stats is not None)
+    hit = _bnpro_choice.get(key)
+    if hit is None:
+        M, C = x.numel() // x.shape[1], x.shape[1]
+        yy = torch.empty_like(lz.x)
+        st = None
+        if stats is not None:
+            st = torch.zeros_like(stats)
+        Co = w.shape[0]
+
+        def sep():
+            _lib.call("kfa_bn_apply_ss", _lib.ptr(lz.x), _lib.ptr(yy), _lib.ptr(lz.ss), M, C, 1, _lib.stream())
+            conv_fwd(yy, w, stride, pad, st)
+
+        t_sep = _time_ms(sep)
+        t_pro = _time_ms(lambda: conv_fwd_bnpro(lz.x, lz.ss, w, stride, pad, st, yy))
+        hit = _bnpro_choice[key] = _agree(t_pro < 0.98 * t_sep, x.device)
+        del yy, st, Co
+    return hit
+
+
 class _ConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, stride, pad, join, stats, vendor=False):
+    def forward(ctx, x, w, stride, pad, join, stats, vendor=False, lazy=None):
         ctx.save_for_backward(x, w)
         ctx.stride, ctx.pad, ctx.join = stride, pad, join
         ctx.wparam = w  # the Parameter itself (for the direct flat-gradient write)
@@ -489,6 +523,9 @@ class _ConvFn(torch.autograd.Function):
         if ctx.bn_link is not None:
             ctx.bn_link.convs += 1
         _tcache.mark_stale()  # weights may have changed since the last backward
+        if lazy is not None:  # x is a lazy BN output: this launch also writes it (for the wgrad)
+            lazy.pending = False
+            return conv_fwd_bnpro(lazy.x, lazy.ss, w, stride, pad, stats, x)
         if vendor:
             return _cl(F.conv2d(_cl(x), _cl(w), None, stride, pad))
         return conv_fwd(x, w, stride, pad, stats)
@@ -526,7 +563,7 @@ class _ConvFn(torch.autograd.Function):
                     torch.cuda.current_stream(x.device).wait_stream(_streams.side_stream(x.device))
             else:
                 dw = conv_wgrad(x, dy, w, ctx.stride, ctx.pad, ctx.wparam)
-        return dx, dw, None, None, None, None, None
+        return dx, dw, None, None, None, None, None, None
 
 
 def apply_bit_mask(t: torch.Tensor, bits: torch.Tensor) -> torch.Tensor:
@@ -612,6 +649,21 @@ def conv2d(x, w, stride: int = 1, pad: int = 0, join: "GradJoin | None" = None, 
     for a BN whose finalize runs later than the next BN's (the downsample BN of
     ``bn_act_dual``); True = the shared one."""
     tag = bn_stats if isinstance(bn_stats, str) else "bn_slots"
+    lz = getattr(x, "_kfa_lazy", None)
+    if lz is not None and lz.pending and join is None and igemm_ok(x, w):
+        stats = None
+        if bn_stats:
+            from .batchnorm import bn_slot_workspace
+            stats = bn_slot_workspace(w.shape[0], x.device, tag)
+        if _use_bnpro(lz, x, w, stride, pad, stats):
+            y = _ConvFn.apply(x, w, stride, pad, None, stats, False, lz)
+            if stats is not None:
+                y._kfa_prestats = True
+                y._kfa_prestats_tag = tag
+            return y
+    if lz is not None and lz.pending:
+        from .batchnorm import materialize
+        materialize(x)
     if stem_ok(x, w, stride, pad) and join is None:
         stats = None
         if bn_stats:

@@ -504,3 +504,53 @@ def test_conv_bn_apply_prologue(N, C, H, W, Co, k, big, with_y, monkeypatch):
     torch.testing.assert_close(sa, sb, rtol=1e-4, atol=1e-2)
     f32 = torch.nn.functional.conv2d(yref.float(), w.float(), None, 1, pad)
     assert (out.float() - f32).abs().max().item() < 2e-2 * max(1.0, f32.abs().max().item())
+
+
+@pytest.mark.parametrize("cin,mid,stride", [(256, 64, 1), (128, 64, 2)])
+def test_resnet_block_lazy_bn2_fused_into_conv3(cin, mid, stride, monkeypatch):
+    """bn2 -> conv3 with the BN-apply folded into conv3's operand load (lazy bn2 output,
+    conv_fwd_bnpro) vs the apply pass + conv: same block output and gradients, the lazy
+    output is filled for the weight gradient, and the BN slot workspace ends clean."""
+    import copy
+    from kubeflow_controller_amd.models import resnet as R
+    from kubeflow_controller_amd.ops import conv as convmod
+    from kubeflow_controller_amd.ops.batchnorm import bn_slot_workspace
+    torch.manual_seed(0)
+    d = torch.device("cuda")
+    blk = R.Bottleneck(cin, mid, stride).to(d)
+    for m in blk.modules():
+        if isinstance(m, convmod.Conv2d):
+            m.weight.data = m.weight.data.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    for m in blk.modules():  # non-trivial BN parameters (bn3 is zero-initialised)
+        if hasattr(m, "running_var"):
+            m.weight.data.uniform_(0.5, 1.5)
+            m.bias.data.uniform_(-0.5, 0.5)
+    blk2 = copy.deepcopy(blk)
+    x = (torch.randn(4, cin, 20, 20, device=d)).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    calls = {"pro": 0}
+    real = convmod.conv_fwd_bnpro
+
+    def counting(*a, **k):
+        calls["pro"] += 1
+        return real(*a, **k)
+
+    outs = []
+    g = None
+    for fused, b in ((True, blk), (False, blk2)):
+        monkeypatch.setattr(convmod, "_use_bnpro", lambda *a, f=fused, **k: f)
+        monkeypatch.setattr(convmod, "conv_fwd_bnpro", counting)
+        xr = x.clone().requires_grad_()
+        y = b(xr)
+        if g is None:  # ONE output gradient for both runs
+            g = torch.randn(y.shape, device=d).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        y.backward(g)
+        torch.cuda.synchronize()
+        outs.append((y.float(), xr.grad.float(), [p.grad.float().clone() for p in b.parameters()]))
+    assert calls["pro"] == 1
+    (ya, ga, pa), (yb, gb, pb) = outs
+    assert (ya - yb).abs().max().item() <= 2e-2 * max(1.0, yb.abs().max().item())
+    assert (ga - gb).abs().max().item() <= 3e-2 * max(1.0, gb.abs().max().item())
+    for u, v in zip(pa, pb):
+        assert (u - v).abs().max().item() <= 3e-2 * max(1.0, v.abs().max().item())
+    for C in (mid, 4 * mid):
+        assert bn_slot_workspace(C, d).abs().max().item() == 0
