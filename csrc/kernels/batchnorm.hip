@@ -490,13 +490,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply(const bf16_t* __restrict__ dy
 #pragma unroll
     for (int j = 0; j < 8; j++) { ca[j] = coef[c0 + j]; cb[j] = coef[C + c0 + j]; ck[j] = coef[2 * C + c0 + j]; }
     load_ss<MASK>(ss, C, c0, sc, sf);
-    for (long r = rb + r0; r < re; r += rpi) {
-      const long o = r * C + c0;
-      uint4 yv = make_uint4(0, 0, 0, 0);
-      if (MASK == 1) yv = ld16(y + o);
-      const unsigned bits = MASK == 3 ? (unsigned)mb[o >> 3] : 0u;
-      const uint4 dv = ld16(dy + o);
-      const uint4 xv = ld16(x + o);
+    auto one = [&](long o, const uint4 dv, const uint4 xv, const uint4 yv, unsigned bits) {
       float dz[8], xf[8], out[8];
       unpack8(xv, xf);
       masked_dy<MASK>(dv, yv, xf, sc, sf, bits, dz);
@@ -504,6 +498,25 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply(const bf16_t* __restrict__ dy
       for (int j = 0; j < 8; j++) out[j] = fmaf(ca[j], dz[j], fmaf(cb[j], xf[j], ck[j]));
       st16(dx + o, pack8(out));
       if (DRES) st16(dres + o, pack8(dz));
+    };
+    // two rows per iteration with all four (six) loads issued before either row is
+    // computed, as bn_apply: twice the bytes in flight per thread
+    long r = rb + r0;
+    for (; r + rpi < re; r += 2L * rpi) {
+      const long o0 = r * C + c0, o1 = (r + rpi) * C + c0;
+      uint4 y0 = make_uint4(0, 0, 0, 0), y1 = y0;
+      if (MASK == 1) { y0 = ld16(y + o0); y1 = ld16(y + o1); }
+      const unsigned b0 = MASK == 3 ? (unsigned)mb[o0 >> 3] : 0u, b1 = MASK == 3 ? (unsigned)mb[o1 >> 3] : 0u;
+      const uint4 d0 = ld16(dy + o0), d1 = ld16(dy + o1);
+      const uint4 x0 = ld16(x + o0), x1 = ld16(x + o1);
+      one(o0, d0, x0, y0, b0);
+      one(o1, d1, x1, y1, b1);
+    }
+    for (; r < re; r += rpi) {
+      const long o = r * C + c0;
+      uint4 yv = make_uint4(0, 0, 0, 0);
+      if (MASK == 1) yv = ld16(y + o);
+      one(o, ld16(dy + o), ld16(x + o), yv, MASK == 3 ? (unsigned)mb[o >> 3] : 0u);
     }
   }
 }
