@@ -554,12 +554,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_rstats(const bf16_t* __restri
         mu[j] = rmean[c0 + j];
       }
       load_ss<MASK>(ss, C, c0, sc, sf);
-      for (long row = rb + r0; row < re; row += rpi) {
-        const long o = row * C + c0;
-        uint4 yv = make_uint4(0, 0, 0, 0);
-        if (MASK == 1) yv = ld16(y + o);
-        const unsigned bits = MASK == 3 ? (unsigned)mb[o >> 3] : 0u;
-        const uint4 dv = ld16(dy + o), xv = ld16(x + o), rv = ld16(r + o);
+      auto one = [&](long o, const uint4 dv, const uint4 xv, const uint4 rv, const uint4 yv, unsigned bits) {
         float dz[8], xf[8], rf[8], out[8];
         unpack8(xv, xf);
         unpack8(rv, rf);
@@ -571,6 +566,23 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_rstats(const bf16_t* __restri
           s2[j] += dz[j] * (rf[j] - mu[j]);
         }
         st16(dx + o, pack8(out));
+      };
+      long row = rb + r0;
+      for (; row + rpi < re; row += 2L * rpi) {  // two rows in flight (see bn_bwd_apply)
+        const long o0 = row * C + c0, o1 = (row + rpi) * C + c0;
+        uint4 y0 = make_uint4(0, 0, 0, 0), y1 = y0;
+        if (MASK == 1) { y0 = ld16(y + o0); y1 = ld16(y + o1); }
+        const unsigned b0 = MASK == 3 ? (unsigned)mb[o0 >> 3] : 0u, b1 = MASK == 3 ? (unsigned)mb[o1 >> 3] : 0u;
+        const uint4 d0 = ld16(dy + o0), d1 = ld16(dy + o1), x0 = ld16(x + o0), x1 = ld16(x + o1);
+        const uint4 q0 = ld16(r + o0), q1 = ld16(r + o1);
+        one(o0, d0, x0, q0, y0, b0);
+        one(o1, d1, x1, q1, y1, b1);
+      }
+      for (; row < re; row += rpi) {
+        const long o = row * C + c0;
+        uint4 yv = make_uint4(0, 0, 0, 0);
+        if (MASK == 1) yv = ld16(y + o);
+        one(o, ld16(dy + o), ld16(x + o), ld16(r + o), yv, MASK == 3 ? (unsigned)mb[o >> 3] : 0u);
       }
     }
     if (active) {
