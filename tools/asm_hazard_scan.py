@@ -1,5 +1,7 @@
-"""Scan gfx950 device assembly for a VMEM store whose data VGPRs a VALU op
-overwrites before two wait states have passed.
+"""Scan gfx950 device assembly for a VMEM store of more than 64 bits of data
+(dwordx3 / dwordx4) whose data VGPRs a VALU op overwrites before two wait states
+have passed (the rule: cdna_hip_programming.md §5.7 — such a store ends with
+`s_nop 1` in inline asm).
 
 hipcc's hazard pass inserts those wait states inside a basic block but missed
 them across a branch join inside a loop (conv_igemm_kernel's PRO side store:
@@ -17,7 +19,7 @@ import subprocess
 import sys
 import tempfile
 
-_STORE = re.compile(r"(buffer|global|flat)_store_dwordx(2|3|4)$")
+_STORE = re.compile(r"(buffer|global|flat)_store_dwordx(3|4)$")  # data wider than 64 bits
 
 
 def _regs(tok: str) -> set:
@@ -46,6 +48,8 @@ def scan_asm(text: str, need: int = 2):
             if not u or u.startswith((";", ".")) or u.endswith(":"):
                 continue
             p = u.replace(",", " ").split()
+            if p[0] in ("s_endpgm", "s_branch", "s_setpc_b64"):  # the next line is not the next instruction
+                break
             if p[0] == "s_nop":
                 ws += int(p[1], 0) + 1
             else:
