@@ -186,9 +186,19 @@ __global__ __launch_bounds__(64 * kGroups) void bn_finalize(const bf16_t* __rest
                             float* __restrict__ save_invstd, float* __restrict__ scale, float* __restrict__ shift,
                             float eps, float momentum) {
   const int c = blockIdx.x * 64 + threadIdx.x;
+  // the per-channel operands are loaded BEFORE the slot exchanges, so their latency
+  // overlaps the atomics' round trip instead of following it
+  const bool own = threadIdx.y == 0 && c < C;
+  float g = 1.f, bt = 0.f, rm0 = 0.f, rv0 = 0.f, kx = 0.f;
+  if (own) {
+    if (gamma) g = gamma[c];
+    if (beta) bt = beta[c];
+    if (rmean) { rm0 = rmean[c]; rv0 = rvar[c]; }
+    if (x) kx = bf2f(x[c]);
+  }
   double a, b;
   if (!combine2(part, C, c, a, b)) return;
-  const double K = x ? (double)bf2f(x[c]) : 0.0;  // x == nullptr: un-shifted sums (fused in the conv epilogue)
+  const double K = x ? (double)kx : 0.0;  // x == nullptr: un-shifted sums (fused in the conv epilogue)
   const double m1 = a / (double)M;
   double var = b / (double)M - m1 * m1;
   if (var < 0.0) var = 0.0;
@@ -196,14 +206,12 @@ __global__ __launch_bounds__(64 * kGroups) void bn_finalize(const bf16_t* __rest
   const float invstd = (float)(1.0 / sqrt(var + (double)eps));
   save_mean[c] = (float)mean;
   save_invstd[c] = invstd;
-  const float g = gamma ? gamma[c] : 1.f;
-  const float bt = beta ? beta[c] : 0.f;
   scale[c] = g * invstd;
   shift[c] = bt - (float)mean * g * invstd;
   if (rmean) {
     const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
-    rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mean;
-    rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unbiased;
+    rmean[c] = (1.f - momentum) * rm0 + momentum * (float)mean;
+    rvar[c] = (1.f - momentum) * rv0 + momentum * (float)unbiased;
   }
 }
 
@@ -455,17 +463,24 @@ __global__ __launch_bounds__(64 * kGroups) void bn_bwd_finalize(float* __restric
                                 float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ coef,
                                 int accumulate) {
   const int c = blockIdx.x * 64 + threadIdx.x;
+  const bool own = threadIdx.y == 0 && c < C;  // operands ahead of the slot exchanges (see bn_finalize)
+  float inv = 0.f, g = 1.f, mu = 0.f, dg0 = 0.f, db0 = 0.f;
+  if (own) {
+    inv = invstd[c];
+    if (gamma) g = gamma[c];
+    mu = mean[c];
+    if (accumulate && dgamma) dg0 = dgamma[c];
+    if (accumulate && dbeta) db0 = dbeta[c];
+  }
   double sdy, sdx;
   if (!combine2(part, C, c, sdy, sdx)) return;
-  const float inv = invstd[c];
-  const float g = gamma ? gamma[c] : 1.f;
   const float dg = (float)sdx * inv;  // sum(dz * xhat)
   // accumulate: the outputs are views into the flat gradient bucket (+=)
-  if (dgamma) dgamma[c] = accumulate ? dgamma[c] + dg : dg;
-  if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)sdy : (float)sdy;
+  if (dgamma) dgamma[c] = accumulate ? dg0 + dg : dg;
+  if (dbeta) dbeta[c] = accumulate ? db0 + (float)sdy : (float)sdy;
   const float a = g * inv;
   const float b = -g * inv * inv * inv * (float)(sdx / (double)M);
-  const float k = -a * (float)(sdy / (double)M) - b * mean[c];
+  const float k = -a * (float)(sdy / (double)M) - b * mu;
   coef[c] = a;
   coef[C + c] = b;
   coef[2 * C + c] = k;
