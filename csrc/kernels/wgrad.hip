@@ -547,6 +547,14 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   __shared__ floatx4 red[4][64];
   const int el = threadIdx.x & 63, sl = threadIdx.x >> 6;
   const long i = (long)blockIdx.x * 64 + el;  // float4 index
+  // the gradient being accumulated into is read up front (lanes that write it), so its
+  // round trip overlaps the partial loads instead of following the block reduction
+  floatx4 g0 = floatx4{0.f, 0.f, 0.f, 0.f};
+  uint2 gb = make_uint2(0u, 0u);
+  if (accumulate && sl == 0 && i < total / 4) {
+    if (grad_f32) g0 = reinterpret_cast<const floatx4*>(grad)[i];
+    else gb = reinterpret_cast<const uint2*>(grad)[i];
+  }
   floatx4 s = floatx4{0.f, 0.f, 0.f, 0.f};
   if (i < total / 4) {
     int k = sl;
@@ -564,15 +572,12 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   if (sl != 0 || i >= total / 4) return;
   s = red[0][el] + red[1][el] + red[2][el] + red[3][el];
   if (grad_f32) {
-    floatx4* g = reinterpret_cast<floatx4*>(grad) + i;
-    *g = accumulate ? *g + s : s;
+    reinterpret_cast<floatx4*>(grad)[i] = accumulate ? g0 + s : s;
   } else {
-    uint2* g = reinterpret_cast<uint2*>(grad) + i;
     if (accumulate) {
-      const uint2 o = *g;
-      s[0] += bf2f(o.x & 0xffff); s[1] += bf2f(o.x >> 16); s[2] += bf2f(o.y & 0xffff); s[3] += bf2f(o.y >> 16);
+      s[0] += bf2f(gb.x & 0xffff); s[1] += bf2f(gb.x >> 16); s[2] += bf2f(gb.y & 0xffff); s[3] += bf2f(gb.y >> 16);
     }
-    *g = make_uint2(pack2(s[0], s[1]), pack2(s[2], s[3]));
+    reinterpret_cast<uint2*>(grad)[i] = make_uint2(pack2(s[0], s[1]), pack2(s[2], s[3]));
   }
 }
 
