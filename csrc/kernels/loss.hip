@@ -350,11 +350,19 @@ KFA_API int kfa_cls_head_bwd(const bf16_t* x, const float* W, const long* y, con
   const int nb = kfa_cls_head_blocks(B), WC = C * H + C;
   const size_t lds = (size_t)8 * WC * 4;
   if (lds > 65536) {
-    static bool attr = false;
-    if (!attr) {
+    // the attribute is per function AND per device: both instances (C <= 2 reaches 65,600 B at
+    // H = 1024, BERT-large NSP), raised once on every device this process launches on
+    static unsigned long long done = 0;  // bit d: device d has both attributes
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const unsigned long long bit = 1ull << (dev & 63);
+    if (!(__atomic_load_n(&done, __ATOMIC_ACQUIRE) & bit)) {
+      const int cap = 8 * (4096 + kClsMaxC) * 4;
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&cls_head_bwd<kClsMaxC>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 8 * (4096 + kClsMaxC) * 4);
-      attr = true;
+                                hipFuncAttributeMaxDynamicSharedMemorySize, cap);
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&cls_head_bwd<2>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, cap);
+      __atomic_fetch_or(&done, bit, __ATOMIC_RELEASE);
     }
   }
   if (C <= 2) hipLaunchKernelGGL(cls_head_bwd<2>, dim3(nb), dim3(256), lds, st, x, W, y, prob, dloss, dx, part, B, H, C);

@@ -226,15 +226,18 @@ inline void pass(const unsigned* kin, const int* vin, unsigned* kout, int* vout,
 inline int sort_pairs(unsigned* k0, int* v0, unsigned* k1, int* v1, int n, int nbits, int* hist, hipStream_t s) {
   if (n <= 0) return 0;
   const int np = passes(nbits);
-  const int db = (nbits + np - 1) / np;
+  // digit widths balanced over the passes and summing to exactly nbits (25 -> 9 / 8 / 8):
+  // bits at and above nbits never take part (hipCUB end_bit semantics)
+  const int base = nbits / np, extra = nbits % np;
   unsigned* ks[2] = {k0, k1};
   int* vs[2] = {v0, v1};
+  int sh = 0;
   for (int p = 0; p < np; ++p) {
     const unsigned* ki = ks[p & 1];
     const int* vi = vs[p & 1];
     unsigned* ko = ks[(p + 1) & 1];
     int* vo = vs[(p + 1) & 1];
-    const int sh = p * db;
+    const int db = base + (p < extra ? 1 : 0);
     switch (db) {
       case 1: pass<1>(ki, vi, ko, vo, n, sh, hist, s); break;
       case 2: pass<2>(ki, vi, ko, vo, n, sh, hist, s); break;
@@ -246,6 +249,7 @@ inline int sort_pairs(unsigned* k0, int* v0, unsigned* k1, int* v1, int n, int n
       case 8: pass<8>(ki, vi, ko, vo, n, sh, hist, s); break;
       default: pass<9>(ki, vi, ko, vo, n, sh, hist, s); break;
     }
+    sh += db;
   }
   if (np % 2 == 0) {  // the result is back in (k0, v0)
     hipError_t e = hipMemcpyAsync(k1, k0, (size_t)n * 4, hipMemcpyDeviceToDevice, s);

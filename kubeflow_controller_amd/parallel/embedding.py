@@ -85,7 +85,13 @@ class _LookupFn(torch.autograd.Function):
             # local row of each id on its owner; key = owner-major (owner, local row)
             key = (ids % emb.owners) * emb.rows_per_owner + torch.div(ids, emb.owners, rounding_mode="floor")
             if emb.dedup:   # each distinct id crosses the fabric once per sender, both ways
-                ukey, inv = torch.unique(key, sorted=True, return_inverse=True)
+                if plan is not None and len(plan) == 4 and plan[2] is not None:
+                    # keys / inverse from the host plan: torch.unique on the device needs its
+                    # output size on the host, i.e. a stream drain per lookup
+                    ukey, inv = (t.pin_memory().to(ids.device, non_blocking=True) if ids.is_cuda else t
+                                 for t in (plan[2], plan[3]))
+                else:
+                    ukey, inv = torch.unique(key, sorted=True, return_inverse=True)
                 send_ids = ukey
             else:
                 order = torch.argsort(key, stable=True)
@@ -93,7 +99,7 @@ class _LookupFn(torch.autograd.Function):
             owner_s = torch.div(send_ids, emb.rows_per_owner, rounding_mode="floor")
             send_ids = send_ids - owner_s * emb.rows_per_owner
             if plan is not None:   # split sizes known on the host already: no device sync
-                send_l, recv_l = plan
+                send_l, recv_l = plan[0], plan[1]
             else:                  # derive them on the device (one D2H sync per lookup)
                 send = torch.bincount(owner_s, minlength=emb.world)
                 recv = torch.empty_like(send)
@@ -321,18 +327,24 @@ class ShardedEmbedding(nn.Module):
         data loader's batch before its H2D copy): the per-owner counts come from a
         CPU bincount and the receive counts from an all-to-all on a gloo (host)
         group, so the lookup itself never waits for the GPU (``.tolist()`` of a
-        device tensor would drain the stream every step)."""
+        device tensor would drain the stream every step).  With dedup the plan also
+        carries the sorted distinct keys and the inverse map (CPU tensors), which
+        the lookup copies instead of running ``torch.unique`` on the device.
+
+        Returns ``(send_counts, recv_counts, unique_keys | None, inverse | None)``."""
         if self.world == 1:
             return None
         ids_cpu = ids_cpu.reshape(-1).cpu()
         owner = ids_cpu % self.owners
+        ukey = inv = None
         if self.dedup:
-            owner = torch.unique(owner * self.rows_per_owner + torch.div(ids_cpu, self.owners, rounding_mode="floor"))
-            owner = torch.div(owner, self.rows_per_owner, rounding_mode="floor")
+            key = owner * self.rows_per_owner + torch.div(ids_cpu, self.owners, rounding_mode="floor")
+            ukey, inv = torch.unique(key, sorted=True, return_inverse=True)
+            owner = torch.div(ukey, self.rows_per_owner, rounding_mode="floor")
         send = torch.bincount(owner, minlength=self.world)
         recv = torch.empty_like(send)
         dist.all_to_all_single(recv, send, group=self._meta_group())
-        return send.tolist(), recv.tolist()
+        return send.tolist(), recv.tolist(), ukey, inv
 
     def _meta_group(self):
         if getattr(self, "_meta", None) is None:

@@ -148,15 +148,27 @@ class ShardedGradSync:
                 set_ready_callback(p, hook)
         self._pull_hooks = []
         self._stage: Dict[int, torch.Tensor] = {}  # per-bucket reduce-dtype staging (allocated once)
-        self.pull_mode = "wait-all"
+        self._static_mode = "wait-all"
+        self._verified = False
         if model is not None and self.world > 1 and PER_MODULE_PULL_WAITS:
             tied = shared_parameters(model)
             if tied:
-                self.pull_mode = f"wait-all (tied weights: {', '.join(tied[:3])})"
+                self._static_mode = f"wait-all (tied weights: {', '.join(tied[:3])})"
             else:
                 self._install_pull_waits(model)
-                self.pull_mode = "per-module"
+                self._static_mode = None
         self.reset()
+
+    @property
+    def pull_mode(self) -> str:
+        """What the forward actually waits on: decided by the first forward (see
+        ``_root_post``), ``"pending first forward"`` until then."""
+        if self._static_mode is not None:
+            return self._static_mode
+        if not self._verified:
+            return "wait-all (pending first forward)"
+        n = len(self._root_mods)
+        return "per-module" if n == 0 else f"per-module ({n} modules read without their own forward: waited at the root)"
 
     # ------------------------------------------------------------------ layout
     def _my_chunks(self, gi: int):
@@ -284,13 +296,19 @@ class ShardedGradSync:
         holding its own parameters.  That is only safe if every module that owns
         parameters runs its own ``forward`` (a model may read a submodule's
         weight directly), so the root module waits for EVERY pull until one
-        forward pass has shown that all parameter-owning modules fired their hook."""
+        forward pass has shown which parameter-owning modules fired their hook.
+        Modules that did NOT (their weights are read by another module, e.g.
+        ResNet's ``bn_act_dual`` reading bn3 / the downsample BN) have their
+        buckets waited at the root from then on; the rest wait in their own hook."""
         by_param = {}
         for gi, g in enumerate(self.groups):
             for pi, p in enumerate(g.params):
                 by_param[id(p)] = self._of_param.get((gi, pi), [])
         self._param_modules = set()
+        self._mod_buckets: Dict[int, List[Bucket]] = {}
         self._fired = set()
+        self._root_mods: set = set()
+        self._root_buckets: List[Bucket] = []
         self._verified = False
         for m in model.modules():
             bs = []
@@ -300,6 +318,7 @@ class ShardedGradSync:
                         bs.append(b)
             if bs:
                 self._param_modules.add(id(m))
+                self._mod_buckets[id(m)] = bs
                 self._pull_hooks.append(m.register_forward_pre_hook(
                     lambda _m, _i, bs=bs: self._module_wait(_m, bs)))
         self._pull_hooks.append(model.register_forward_pre_hook(lambda _m, _i: self._root_pre()))
@@ -313,10 +332,20 @@ class ShardedGradSync:
         if not self._verified:
             self.wait_pull()
             self._fired.clear()
+        elif self._root_buckets:
+            self.wait_pull(self._root_buckets)
 
     def _root_post(self) -> None:
-        if not self._verified and self._param_modules <= self._fired:
-            self._verified = True
+        if self._verified:
+            return
+        self._root_mods = self._param_modules - self._fired
+        rb: List[Bucket] = []
+        for mid in self._root_mods:
+            for b in self._mod_buckets[mid]:
+                if b not in rb:
+                    rb.append(b)
+        self._root_buckets = rb
+        self._verified = True
 
     # ------------------------------------------------------------------ checkpoint helpers
     def full_master(self, gi: int) -> torch.Tensor:

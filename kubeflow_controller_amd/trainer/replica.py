@@ -491,6 +491,8 @@ def run_worker(spec: ClusterSpec, args) -> int:
         global_step += inc
         if store is not None and spec.is_chief:
             store.add(STEP_KEY, inc)
+        if local_step == 0 and engine.sharded and spec.is_chief:  # decided by the first forward
+            _log(f"Worker {rank}: pull waits after the first forward: {getattr(engine.sync, 'pull_mode', '?')}")
         if local_step + 1 == warm:
             if device.type == "cuda":
                 torch.cuda.synchronize()
@@ -623,14 +625,17 @@ def main(argv: Optional[list] = None) -> int:
         if spec.is_ps:  # a PS serves for as long as the workers train: no step-level guard
             return run_ps_async(spec, args)
         _arm_watchdog(args)
-        rc = run_worker_async(spec, args)
+        try:
+            return run_worker_async(spec, args)
+        finally:  # an in-process caller must not be left with a live exit=True timer
+            _disarm_watchdog()
     elif spec.is_ps:
         return run_ps(spec, args)
-    else:
-        _arm_watchdog(args)
-        rc = run_worker(spec, args)
-    _disarm_watchdog()
-    return rc
+    _arm_watchdog(args)
+    try:
+        return run_worker(spec, args)
+    finally:
+        _disarm_watchdog()
 
 
 if __name__ == "__main__":

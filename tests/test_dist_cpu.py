@@ -242,3 +242,47 @@ def test_tuner_decision_broadcast_only_in_lockstep_jobs(lockstep):
     out = mgr.dict()
     mp.spawn(_agree_worker, args=(2, _free_port(), lockstep, out), nprocs=2, join=True)
     assert dict(out) == ({0: (True, 3), 1: (True, 3)} if lockstep else {0: (True, 3), 1: (False, 1)})
+
+
+def _pull_mode_worker(rank, world, port, out):
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from kubeflow_controller_amd.models.bert import BertConfig, BertForPreTraining, bert_loss, synthetic_mlm_batch
+    from kubeflow_controller_amd.models.resnet import resnet_tiny
+    from kubeflow_controller_amd.ops.loss import cross_entropy
+    from kubeflow_controller_amd.trainer.engine import DistInfo, Engine
+    modes = {}
+    torch.manual_seed(0)
+    r = Engine(resnet_tiny(10), lambda m, x, y: cross_entropy(m(x), y), optimizer="sgd", lr=0.01,
+               compute_dtype=torch.bfloat16, channels_last=True, bucket_mb=0.05,
+               dist_info=DistInfo(rank=rank, world=world), ps=1, ps_placement="sharded")
+    modes["resnet_before"] = r.sync.pull_mode
+    x = torch.randn(2, 3, 32, 32).contiguous(memory_format=torch.channels_last)
+    for _ in range(2):
+        r.train_step(x, torch.randint(0, 10, (2,)))
+    modes["resnet"] = r.sync.pull_mode
+    modes["resnet_root"] = len(r.sync._root_buckets)
+    cfg = BertConfig.tiny()
+    b = Engine(BertForPreTraining(cfg), bert_loss, optimizer="adam", lr=1e-4, compute_dtype=torch.bfloat16,
+               channels_last=False, bucket_mb=0.05, dist_info=DistInfo(rank=rank, world=world), ps=1,
+               ps_placement="sharded")
+    batch = synthetic_mlm_batch(cfg, 2, 16, generator=torch.Generator().manual_seed(rank))
+    b.train_step(*batch)
+    modes["bert"] = b.sync.pull_mode
+    torch.save(modes, f"{out}.{rank}")
+    dist.destroy_process_group()
+
+
+def test_ps_pull_waits_engage_per_module_for_resnet_and_bert(tmp_path):
+    """the per-module pull waits must actually engage after the first
+    forward.  ResNet's fused ``bn_act_dual`` reads bn3 / downsample-BN weights
+    without their own forward: those modules' buckets are waited at the root,
+    every other module waits in its own pre-hook (mode "per-module ...")."""
+    out = str(tmp_path / "pm")
+    mp.start_processes(_pull_mode_worker, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    m = torch.load(f"{out}.0", weights_only=True)
+    assert m["resnet_before"].startswith("wait-all (pending"), m
+    assert m["resnet"].startswith("per-module"), m
+    assert m["bert"].startswith("per-module") or m["bert"].startswith("wait-all (tied"), m

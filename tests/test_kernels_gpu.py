@@ -337,7 +337,7 @@ def test_clipped_sum_xent_matches_fp32(dtype):
     assert float(zz.grad[5].float().abs().sum()) == 0.0
 
 
-@pytest.mark.parametrize("B,H,C", [(256, 768, 2), (37, 64, 5), (1000, 512, 8), (3, 8, 1)])
+@pytest.mark.parametrize("B,H,C", [(256, 768, 2), (37, 64, 5), (1000, 512, 8), (3, 8, 1), (64, 1024, 2)])
 def test_classifier_head_xent_matches_fp32(B, H, C):
     """Fused small-classifier head + softmax CE (kfa_cls_head_fwd / _bwd, BERT's NSP)
     vs the plain fp32 PyTorch chain: loss, dx, dW, db; bit-identical on a rerun."""

@@ -90,6 +90,28 @@ def test_own_radix_sort_pairs_matches_stable_sort(n, nbits):
     assert torch.equal(vd.cpu().to(torch.int64), ref_i)
 
 
+@pytest.mark.parametrize("n,nbits", [(5000, 25), (70000, 17), (4097, 10)])
+def test_own_radix_sort_ignores_bits_above_nbits(n, nbits):
+    """hipCUB end_bit semantics: keys carrying bits at and above nbits sort on the
+    low nbits only (stable), the high bits travel with the key unchanged."""
+    from kubeflow_controller_amd.ops import _lib
+    _lib.register("kfa_radix_ws_bytes", [_lib.L], restype=_lib.L)
+    _lib.register("kfa_radix_sort_pairs", [_lib.P, _lib.P, _lib.L, _lib.I, _lib.P, _lib.L, _lib.P])
+    g = torch.Generator().manual_seed(n * 3 + nbits)
+    low = torch.randint(0, 1 << nbits, (n,), generator=g, dtype=torch.int64)
+    low[: n // 4] = low[: n // 4] % 13
+    high = torch.randint(0, 1 << (32 - nbits), (n,), generator=g, dtype=torch.int64) << nbits
+    k32 = (low | high).bitwise_and(0xFFFFFFFF)
+    _, ref_i = torch.sort(low, stable=True)
+    kd = k32.to(torch.int32).cuda()
+    vd = torch.arange(n, dtype=torch.int32, device="cuda")
+    ws = torch.empty(_lib.lib().kfa_radix_ws_bytes(n), dtype=torch.uint8, device="cuda")
+    _lib.call("kfa_radix_sort_pairs", kd.data_ptr(), vd.data_ptr(), n, nbits, ws.data_ptr(), ws.numel(),
+              _lib.stream())
+    assert torch.equal(vd.cpu().to(torch.int64), ref_i)
+    assert torch.equal(kd.cpu().to(torch.int64).bitwise_and(0xFFFFFFFF), k32[ref_i])
+
+
 @pytest.mark.parametrize("n", [1, 63, 1024, 1025, 26561, 300000])
 def test_scan_max_exclusive(n):
     from kubeflow_controller_amd.ops import _lib
