@@ -3,6 +3,8 @@
 * ``_native_runtime`` — C++ control-plane runtime (core in
   ``csrc/runtime/runtime_core.h``, bindings in ``runtime.cpp``), compiled with
   g++ against pybind11.
+* ``parallel/_kfc_comm.so`` — the first-party collective layer (``csrc/comm/comm.cpp``:
+  bootstrap, RCCL resolved at run time, host-TCP backend for CPU tests), g++.
 * ``ops/_hip_kernels.so`` — the hand-written CDNA4 kernels (``csrc/kernels/*.hip``)
   compiled by ``hipcc --offload-arch=gfx950`` into ONE shared object with a C
   ABI; Python binds it with ``ctypes`` (``ops/_lib.py``), so no torch headers
@@ -86,6 +88,30 @@ def build_runtime(force: bool = False) -> str:
         _run(cmd, quiet=True)
         os.replace(tmp, tgt)
         _write_stamp(tgt, srcs)
+    return tgt
+
+
+def comm_target() -> str:
+    return os.path.join(PKG, "parallel", "_kfc_comm.so")
+
+
+def build_comm(force: bool = False) -> str:
+    """The first-party collective layer (``csrc/comm/comm.cpp``: TCP bootstrap,
+    RCCL backend resolved at run time, host-TCP backend for CPU) as a C-ABI
+    shared object bound with ctypes (``parallel/comm.py``).  Plain g++: it
+    includes no HIP / RCCL header (RCCL is dlopen'ed), so it builds and its host
+    backend runs on a machine without ROCm devices."""
+    src = os.path.join(CSRC, "comm", "comm.cpp")
+    tgt = comm_target()
+    with _lock:
+        if not force and _up_to_date(tgt, [src]):
+            return tgt
+        cxx = os.environ.get("CXX", "g++")
+        tmp = tgt + f".tmp{os.getpid()}"
+        _run([cxx, "-O2", "-std=c++17", "-shared", "-fPIC", "-Wall", "-Wextra", "-Wno-unused-parameter",
+              "-fvisibility=hidden", src, "-o", tmp, "-ldl", "-lpthread"], quiet=True)
+        os.replace(tmp, tgt)
+        _write_stamp(tgt, [src])
     return tgt
 
 
@@ -212,6 +238,7 @@ def run_sanitized(kind: str, timeout: float = 300.0, canary: bool = False) -> su
 
 def build_all(force: bool = False) -> None:
     build_runtime(force)
+    build_comm(force)
     build_kernels(force)
 
 

@@ -1,0 +1,364 @@
+"""Communicators for the gradient / parameter traffic (SURVEY §1.2 L0 comm, §2.5, §2.7, §5.8).
+
+Two implementations of one small interface (``all_reduce``, ``reduce_scatter_tensor``,
+``all_gather_into_tensor``, ``broadcast``, ``reduce``, ``all_to_all_single``,
+``send`` / ``recv``, ``barrier``; every collective takes ``async_op`` and returns a
+work object with ``wait()``):
+
+* :class:`Communicator` — the first-party layer, ``csrc/comm/comm.cpp``
+  (``parallel/_kfc_comm.so``).  Bootstrap: rank 0 (the chief) opens a TCP
+  listener and publishes ``host:port`` in the job's rendezvous store — the store
+  every replica already reaches on the chief's cluster-spec endpoint, the
+  kube-dns stand-in of ``kubelet/endpoints.py``; every other rank connects and
+  receives the RCCL unique id (one exchange per communicator, the analogue of the
+  reference's ``tf.train.Server`` bind, ``mnist_replica.py:117-122``).  Then
+  RCCL's collectives run directly on the caller's flat buffers on this
+  communicator's OWN HIP stream: it first waits for the caller's stream (the
+  kernels that produced the bucket), and hands the result back through an event
+  that ``Work.wait()`` makes the caller's stream wait on — the optimizer (or the
+  next forward) waits for exactly the buckets it reads.  On a CPU the same C++
+  layer runs its host-TCP backend (``backend="host"``) so it is tested against
+  gloo without a GPU (``tests/test_comm_cpu.py``).
+* :class:`TorchComm` — ``torch.distributed`` on a process group (gloo on the
+  CPU: the test double; ``KFA_COMM=torch`` also selects it on GPUs for A/B).
+
+:func:`make_comm` picks one: ``KFA_COMM`` = ``native`` | ``torch``; default
+native on GPUs (RCCL), torch (gloo) on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import itertools
+import os
+from typing import Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+_P, _L, _I, _S = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_size_t
+_LIB = None
+
+_DT = {torch.int8: 0, torch.uint8: 1, torch.int32: 2, torch.int64: 4, torch.float16: 6, torch.float32: 7,
+       torch.float64: 8, torch.bfloat16: 9, torch.bool: 1}
+_OPS = {"sum": 0, "prod": 1, "max": 2, "min": 3, "avg": 4}
+
+
+def _op_code(op) -> int:
+    if isinstance(op, str):
+        return _OPS[op.lower()]
+    name = str(op).split(".")[-1].lower()   # dist.ReduceOp.SUM / RedOpType.SUM
+    for k, v in (("sum", 0), ("product", 1), ("prod", 1), ("max", 2), ("min", 3), ("avg", 4)):
+        if name.startswith(k):
+            return v
+    raise ValueError(f"unsupported reduction op {op!r}")
+
+
+def lib() -> ctypes.CDLL:
+    """The comm library (built in-tree by ``_build.build_comm``; built here if
+    missing and a compiler is present — it is plain C++, no ROCm toolchain)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    from .. import _build
+    path = _build.comm_target()
+    if not os.path.exists(path):
+        _build.build_comm()
+    L = ctypes.CDLL(path)
+    sig = {
+        "kfc_last_error": ([], ctypes.c_char_p), "kfc_listen": ([ctypes.c_char_p, _I, ctypes.POINTER(_I)], _I),
+        "kfc_close_fd": ([_I], None), "kfc_rccl_path": ([], ctypes.c_char_p), "kfc_rccl_version": ([], _I),
+        "kfc_comm_init": ([ctypes.c_char_p, _I, _I, ctypes.c_char_p, _I, _I, _I], _P),
+        "kfc_backend": ([_P], ctypes.c_char_p),
+        "kfc_all_reduce": ([_P, _P, _P, _S, _I, _I, _P], _I),
+        "kfc_reduce_scatter": ([_P, _P, _P, _S, _I, _I, _P], _I),
+        "kfc_all_gather": ([_P, _P, _P, _S, _I, _P], _I),
+        "kfc_broadcast": ([_P, _P, _P, _S, _I, _I, _P], _I),
+        "kfc_reduce": ([_P, _P, _P, _S, _I, _I, _I, _P], _I),
+        "kfc_send": ([_P, _P, _S, _I, _I, _P], _I), "kfc_recv": ([_P, _P, _S, _I, _I, _P], _I),
+        "kfc_all_to_all_v": ([_P, _P, _P, _P, _P, _P, _P, _I, _P], _I),
+        "kfc_group_start": ([_P], _I), "kfc_group_end": ([_P], _I), "kfc_async_error": ([_P], _I),
+        "kfc_comm_abort": ([_P], None), "kfc_comm_destroy": ([_P], None),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes, f.restype = args, res
+    _LIB = L
+    return L
+
+
+class CommError(RuntimeError):
+    pass
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise CommError(f"{what}: {lib().kfc_last_error().decode(errors='replace')} (code {rc})")
+
+
+class Work:
+    """Completion of one collective: ``wait()`` orders the caller's CURRENT stream
+    after it (no host wait); CPU collectives are complete on return."""
+    __slots__ = ("event", "device")
+
+    def __init__(self, event=None, device=None):
+        self.event, self.device = event, device
+
+    def wait(self) -> bool:
+        if self.event is not None:
+            torch.cuda.current_stream(self.device).wait_event(self.event)
+        return True
+
+    def is_completed(self) -> bool:
+        return self.event is None or self.event.query()
+
+
+def _ptr(t: torch.Tensor):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+_KEYS = itertools.count()
+
+
+class Communicator:
+    """One communicator of the first-party layer (see the module docstring)."""
+
+    native = True
+
+    def __init__(self, handle, rank: int, world: int, device: torch.device, backend: str):
+        self._h = handle
+        self.rank, self.world, self.device, self.backend = rank, world, device, backend
+        self.stream = torch.cuda.Stream(device=device) if device.type == "cuda" else None
+
+    @classmethod
+    def create(cls, store, rank: int, world: int, device: torch.device, backend: Optional[str] = None,
+               advertise_host: Optional[str] = None, key: Optional[str] = None,
+               timeout_s: float = 300.0) -> "Communicator":
+        """Collective over every rank: rank 0 listens and publishes its address under
+        ``key`` in ``store`` (a ``torch.distributed`` Store); the others read it and
+        connect.  Every rank must create its communicators in the same order."""
+        backend = backend or ("rccl" if device.type == "cuda" else "host")
+        key = key or f"kfc/comm/{next(_KEYS)}"
+        L = lib()
+        tmo = int(timeout_s * 1000)
+        if rank == 0:
+            port = ctypes.c_int(0)
+            fd = L.kfc_listen(b"", 0, ctypes.byref(port))
+            if fd < 0:
+                _check(-fd, "kfc_listen")
+            host = advertise_host or os.environ.get("MASTER_ADDR", "127.0.0.1")
+            store.set(key, f"{host}:{port.value}")
+            h = L.kfc_comm_init(backend.encode(), world, 0, None, 0, fd, tmo)
+        else:
+            addr = store.get(key).decode()
+            host, _, port = addr.rpartition(":")
+            h = L.kfc_comm_init(backend.encode(), world, rank, host.encode(), int(port), -1, tmo)
+        if not h:
+            raise CommError(f"kfc_comm_init({backend}, rank {rank}/{world}): {L.kfc_last_error().decode()}")
+        return cls(h, rank, world, device, backend)
+
+    # -------------------------------------------------------------- plumbing
+    def _stream_arg(self):
+        return ctypes.c_void_p(self.stream.cuda_stream) if self.stream is not None else None
+
+    def _run(self, tensors: Sequence[torch.Tensor], fn, what: str, async_op: bool) -> Work:
+        if self._h is None:
+            raise CommError("communicator destroyed")
+        if self.stream is None:
+            _check(fn(None), what)
+            return Work()
+        cur = torch.cuda.current_stream(self.device)
+        self.stream.wait_stream(cur)           # the producing kernels first
+        _check(fn(self._stream_arg()), what)
+        for t in tensors:                       # keep the caching allocator off these until the comm stream is done
+            t.record_stream(self.stream)
+        ev = torch.cuda.Event()
+        ev.record(self.stream)
+        w = Work(ev, self.device)
+        if not async_op:
+            cur.wait_event(ev)
+        return w
+
+    @staticmethod
+    def _dt(t: torch.Tensor) -> int:
+        if t.dtype not in _DT:
+            raise CommError(f"unsupported dtype {t.dtype}")
+        if not t.is_contiguous():
+            raise CommError("collective buffers must be contiguous")
+        return _DT[t.dtype]
+
+    # -------------------------------------------------------------- collectives
+    def all_reduce(self, t: torch.Tensor, op="sum", async_op: bool = False) -> Work:
+        dt, oc = self._dt(t), _op_code(op)
+        return self._run([t], lambda s: lib().kfc_all_reduce(self._h, _ptr(t), _ptr(t), t.numel(), dt, oc, s),
+                         "all_reduce", async_op)
+
+    def reduce_scatter_tensor(self, out: torch.Tensor, inp: torch.Tensor, op="sum", async_op: bool = False) -> Work:
+        dt, oc = self._dt(inp), _op_code(op)
+        if out.dtype != inp.dtype or inp.numel() != out.numel() * self.world:
+            raise CommError(f"reduce_scatter: input {inp.numel()} != world {self.world} x output {out.numel()}")
+        return self._run([out, inp], lambda s: lib().kfc_reduce_scatter(self._h, _ptr(inp), _ptr(out), out.numel(),
+                                                                         dt, oc, s), "reduce_scatter", async_op)
+
+    def all_gather_into_tensor(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False) -> Work:
+        dt = self._dt(inp)
+        if out.dtype != inp.dtype or out.numel() != inp.numel() * self.world:
+            raise CommError(f"all_gather: output {out.numel()} != world {self.world} x input {inp.numel()}")
+        return self._run([out, inp], lambda s: lib().kfc_all_gather(self._h, _ptr(inp), _ptr(out), inp.numel(), dt,
+                                                                     s), "all_gather", async_op)
+
+    def broadcast(self, t: torch.Tensor, src: int, async_op: bool = False) -> Work:
+        dt = self._dt(t)
+        return self._run([t], lambda s: lib().kfc_broadcast(self._h, _ptr(t), _ptr(t), t.numel(), dt, src, s),
+                         "broadcast", async_op)
+
+    def reduce(self, t: torch.Tensor, dst: int, op="sum", async_op: bool = False) -> Work:
+        dt, oc = self._dt(t), _op_code(op)
+        return self._run([t], lambda s: lib().kfc_reduce(self._h, _ptr(t), _ptr(t), t.numel(), dt, oc, dst, s),
+                         "reduce", async_op)
+
+    def send(self, t: torch.Tensor, dst: int, async_op: bool = False) -> Work:
+        dt = self._dt(t)
+        return self._run([t], lambda s: lib().kfc_send(self._h, _ptr(t), t.numel(), dt, dst, s), "send", async_op)
+
+    def recv(self, t: torch.Tensor, src: int, async_op: bool = False) -> Work:
+        dt = self._dt(t)
+        return self._run([t], lambda s: lib().kfc_recv(self._h, _ptr(t), t.numel(), dt, src, s), "recv", async_op)
+
+    def all_to_all_single(self, out: torch.Tensor, inp: torch.Tensor, out_splits: Sequence[int],
+                          in_splits: Sequence[int], async_op: bool = False) -> Work:
+        """Rows of ``inp`` (``in_splits[p]`` of them to rank p) -> rows of ``out``
+        (``out_splits[p]`` from rank p): one grouped send / recv batch, the local
+        block copied on the communicator's stream."""
+        dt = self._dt(inp)
+        row = inp[0].numel() if inp.dim() > 1 and inp.shape[0] else (out[0].numel() if out.dim() > 1 and out.shape[0]
+                                                                    else 1)
+        W = self.world
+        sc = (ctypes.c_int64 * W)(*[int(n) * row for n in in_splits])
+        rc = (ctypes.c_int64 * W)(*[int(n) * row for n in out_splits])
+        so = (ctypes.c_int64 * W)(*[sum(in_splits[:p]) * row for p in range(W)])
+        ro = (ctypes.c_int64 * W)(*[sum(out_splits[:p]) * row for p in range(W)])
+        r = self.rank
+
+        def fn(s):
+            rc_ = lib().kfc_all_to_all_v(self._h, _ptr(inp), sc, so, _ptr(out), rc, ro, dt, s)
+            if rc_ == 0 and in_splits[r]:
+                src = inp.reshape(-1)[so[r]:so[r] + sc[r]]
+                dst = out.reshape(-1)[ro[r]:ro[r] + rc[r]]
+                if self.stream is not None:
+                    with torch.cuda.stream(self.stream):
+                        dst.copy_(src)
+                else:
+                    dst.copy_(src)
+            return rc_
+        return self._run([out, inp], fn, "all_to_all", async_op)
+
+    def barrier(self) -> None:
+        t = torch.ones(1, dtype=torch.int32, device=self.device)
+        self.all_reduce(t)
+        if self.stream is not None:
+            torch.cuda.current_stream(self.device).synchronize()
+        if int(t.item()) != self.world:
+            raise CommError(f"barrier: {int(t.item())} of {self.world} ranks")
+
+    def check(self) -> None:
+        """Raise if the backend recorded an asynchronous error (RCCL)."""
+        _check(lib().kfc_async_error(self._h), "async error")
+
+    def destroy(self, abort: bool = False) -> None:
+        if self._h is not None:
+            (lib().kfc_comm_abort if abort else lib().kfc_comm_destroy)(self._h)
+            self._h = None
+
+    def __repr__(self) -> str:
+        return f"Communicator({self.backend}, rank {self.rank}/{self.world}, {self.device})"
+
+
+class TorchComm:
+    """The same interface over ``torch.distributed`` (gloo on the CPU: the test double)."""
+
+    native = False
+    backend = "torch"
+
+    def __init__(self, process_group=None):
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(process_group) if dist.is_initialized() else 0
+
+    @staticmethod
+    def _rop(op):
+        if not isinstance(op, str):
+            return op
+        return {"sum": dist.ReduceOp.SUM, "prod": dist.ReduceOp.PRODUCT, "max": dist.ReduceOp.MAX,
+                "min": dist.ReduceOp.MIN, "avg": dist.ReduceOp.AVG}[op]
+
+    def all_reduce(self, t, op="sum", async_op=False):
+        return dist.all_reduce(t, op=self._rop(op), group=self.pg, async_op=async_op) or Work()
+
+    def reduce_scatter_tensor(self, out, inp, op="sum", async_op=False):
+        return dist.reduce_scatter_tensor(out, inp, op=self._rop(op), group=self.pg, async_op=async_op) or Work()
+
+    def all_gather_into_tensor(self, out, inp, async_op=False):
+        return dist.all_gather_into_tensor(out, inp, group=self.pg, async_op=async_op) or Work()
+
+    def broadcast(self, t, src, async_op=False):
+        return dist.broadcast(t, src, group=self.pg, async_op=async_op) or Work()
+
+    def reduce(self, t, dst, op="sum", async_op=False):
+        return dist.reduce(t, dst, op=self._rop(op), group=self.pg, async_op=async_op) or Work()
+
+    def send(self, t, dst, async_op=False):
+        if async_op:
+            return dist.isend(t, dst, group=self.pg)
+        dist.send(t, dst, group=self.pg)
+        return Work()
+
+    def recv(self, t, src, async_op=False):
+        if async_op:
+            return dist.irecv(t, src, group=self.pg)
+        dist.recv(t, src, group=self.pg)
+        return Work()
+
+    def all_to_all_single(self, out, inp, out_splits, in_splits, async_op=False):
+        return dist.all_to_all_single(out, inp, list(out_splits), list(in_splits), group=self.pg,
+                                      async_op=async_op) or Work()
+
+    def barrier(self):
+        dist.barrier(group=self.pg)
+
+    def check(self):
+        pass
+
+    def destroy(self, abort=False):
+        pass
+
+    def __repr__(self) -> str:
+        return f"TorchComm({dist.get_backend(self.pg) if dist.is_initialized() else 'none'}, {self.world} ranks)"
+
+
+def comm_mode(device: torch.device) -> str:
+    m = os.environ.get("KFA_COMM", "").lower()
+    if m in ("native", "torch"):
+        return m
+    return "native" if device.type == "cuda" else "torch"
+
+
+def default_store():
+    """The rendezvous store of the default process group (rank 0 hosts it on the
+    chief's endpoint)."""
+    try:
+        return dist.distributed_c10d._get_default_store()
+    except Exception:  # noqa: BLE001 - older / private API: connect a client to MASTER_ADDR:PORT
+        return dist.TCPStore(os.environ.get("MASTER_ADDR", "127.0.0.1"), int(os.environ["MASTER_PORT"]),
+                             is_master=False)
+
+
+def make_comm(device: torch.device, process_group=None, store=None, mode: Optional[str] = None):
+    """The communicator for a job's gradient / parameter traffic (see module doc)."""
+    mode = mode or comm_mode(device)
+    if not dist.is_initialized() or dist.get_world_size(process_group) == 1 or mode == "torch":
+        return TorchComm(process_group)
+    if process_group is not None and process_group is not dist.group.WORLD:
+        raise CommError("the native communicator spans the default group's ranks only")
+    t = float(os.environ.get("KFA_DIST_INIT_TIMEOUT", "300"))
+    return Communicator.create(store or default_store(), dist.get_rank(), dist.get_world_size(), device,
+                               timeout_s=t)

@@ -41,11 +41,16 @@ def _join_side_streams(t: torch.Tensor) -> None:
 
 
 class GradSync:
+    """``comm``: the communicator the buckets' all-reduces run on (``parallel/comm.py``:
+    the first-party RCCL layer on GPUs, ``TorchComm`` = torch.distributed otherwise)."""
+
     def __init__(self, groups: Sequence[FlatGroup], process_group=None, bucket_mb: float = 32.0,
-                 overlap: bool = True, reduce_dtype: Optional[torch.dtype] = torch.float32):
+                 overlap: bool = True, reduce_dtype: Optional[torch.dtype] = torch.float32, comm=None):
+        from .comm import TorchComm
         self.groups = list(groups)
         self.pg = process_group
-        self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        self.comm = comm if comm is not None else TorchComm(process_group)
+        self.world = self.comm.world
         self.overlap = overlap and self.world > 1
         self.reduce_dtype = reduce_dtype
         if self.world > 1 and reduce_dtype is not None:
@@ -92,7 +97,7 @@ class GradSync:
             red.copy_(view)
         else:
             red = view
-        b.work = dist.all_reduce(red, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+        b.work = self.comm.all_reduce(red, "sum", async_op=True)
 
     def finish(self) -> float:
         """Wait for (or issue) every bucket's collective; return the grad scale (1/world)."""
@@ -130,12 +135,15 @@ class GradSync:
         return out
 
 
-def broadcast_params(groups: Sequence[FlatGroup], src: int = 0, process_group=None) -> None:
+def broadcast_params(groups: Sequence[FlatGroup], src: int = 0, process_group=None, comm=None) -> None:
     """Initial parameter sync from rank ``src`` (owner-initialised
     params broadcast once before the first step)."""
     if not dist.is_initialized() or dist.get_world_size(process_group) == 1:
         return
     for g in groups:
-        dist.broadcast(g.fp32, src, group=process_group)
+        if comm is not None:
+            comm.broadcast(g.fp32, src)
+        else:
+            dist.broadcast(g.fp32, src, group=process_group)
         if g.master is not None:
             g.data.copy_(g.master)

@@ -70,8 +70,13 @@ def _segment_path(n: int, dim: int) -> bool:
     return os.environ.get("KFA_SPARSE_ATOMIC", "0") != "1" and dim % 8 == 0 and dim <= 248 and n < 2 ** 31
 
 
-def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits: List[int], in_splits: List[int], pg) -> None:
-    dist.all_to_all_single(out, inp, out_splits, in_splits, group=pg)
+def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits: List[int], in_splits: List[int], pg, comm=None) -> None:
+    """The id / row / gradient exchange: on the job's communicator when the Engine
+    attached one (``ShardedEmbedding.comm``, parallel/comm.py), else torch.distributed."""
+    if comm is not None:
+        comm.all_to_all_single(out, inp, out_splits, in_splits)
+    else:
+        dist.all_to_all_single(out, inp, out_splits, in_splits, group=pg)
 
 
 class _LookupFn(torch.autograd.Function):
@@ -103,13 +108,13 @@ class _LookupFn(torch.autograd.Function):
             else:                  # derive them on the device (one D2H sync per lookup)
                 send = torch.bincount(owner_s, minlength=emb.world)
                 recv = torch.empty_like(send)
-                dist.all_to_all_single(recv, send, group=emb.pg)
+                _a2a(recv, send, [1] * emb.world, [1] * emb.world, emb.pg, emb.comm)
                 send_l, recv_l = send.tolist(), recv.tolist()
             if sum(send_l) != send_ids.numel():
                 raise RuntimeError(f"ShardedEmbedding: plan sends {sum(send_l)} ids, lookup has {send_ids.numel()} "
                                    f"({'unique ' if emb.dedup else ''}ids); plan and dedup setting disagree")
             local = torch.empty(sum(recv_l), dtype=ids.dtype, device=ids.device)
-            _a2a(local, send_ids, recv_l, send_l, emb.pg)
+            _a2a(local, send_ids, recv_l, send_l, emb.pg, emb.comm)
         else:
             send_l, recv_l = None, None
             local = torch.div(ids, emb.owners, rounding_mode="floor") if emb.owners > 1 else ids
@@ -118,7 +123,7 @@ class _LookupFn(torch.autograd.Function):
         rows = emb.gather(local)
         if comm:
             back = torch.empty(sum(send_l), D, dtype=rows.dtype, device=rows.device)
-            _a2a(back, rows, send_l, recv_l, emb.pg)
+            _a2a(back, rows, send_l, recv_l, emb.pg, emb.comm)
             if inv is not None:
                 out = back.index_select(0, inv)
             else:
@@ -150,7 +155,7 @@ class _LookupFn(torch.autograd.Function):
             else:
                 d_send = dout.index_select(0, order)
             g = torch.empty(local.numel(), emb.dim, dtype=dout.dtype, device=dout.device)
-            _a2a(g, d_send, recv_l, send_l, emb.pg)
+            _a2a(g, d_send, recv_l, send_l, emb.pg, emb.comm)
         else:
             g = dout
         emb.apply_sparse(local, g, prep=ctx.prep)
@@ -166,6 +171,7 @@ class ShardedEmbedding(nn.Module):
                  device=None):
         super().__init__()
         self.pg = process_group
+        self.comm = None  # the job's communicator (parallel/comm.py), attached by the Engine
         init = dist.is_initialized()
         self.world = dist.get_world_size(process_group) if init else 1
         self.rank = dist.get_rank(process_group) if init else 0

@@ -94,13 +94,15 @@ class ShardedGradSync:
 
     def __init__(self, groups: Sequence[FlatGroup], process_group=None, *, bucket_mb: float = 32.0,
                  placement: str = "sharded", num_ps: int = 1, reduce_dtype: Optional[torch.dtype] = torch.float32,
-                 model: Optional[torch.nn.Module] = None, overlap: bool = True):
+                 model: Optional[torch.nn.Module] = None, overlap: bool = True, comm=None):
+        from .comm import TorchComm
         if placement not in ("sharded", "ps"):
             raise ValueError(f"placement must be 'sharded' or 'ps', got {placement!r}")
         self.groups = list(groups)
         self.pg = process_group
-        self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
-        self.rank = dist.get_rank(process_group) if dist.is_initialized() else 0
+        self.comm = comm if comm is not None else TorchComm(process_group)  # parallel/comm.py
+        self.world = self.comm.world
+        self.rank = self.comm.rank
         self.placement = placement if self.world > 1 else "sharded"
         self.num_ps = max(1, num_ps)
         self.owners = ps_owner_ranks(self.world, self.num_ps) if self.placement == "ps" else []
@@ -233,7 +235,7 @@ class ShardedGradSync:
             src = self._staged(b, view, rd)
             out = self.gshard[b.group][b.shard_off:b.shard_off + c]
             b.tmp = src
-            b.work = dist.reduce_scatter_tensor(out, src, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+            b.work = self.comm.reduce_scatter_tensor(out, src, "sum", async_op=True)
         else:
             if b.owner == self.rank:
                 buf = self.gshard[b.group][b.shard_off:b.shard_off + b.numel]
@@ -241,7 +243,7 @@ class ShardedGradSync:
             else:
                 buf = self._staged(b, view, rd)
             b.tmp = buf
-            b.work = dist.reduce(buf, b.owner, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+            b.work = self.comm.reduce(buf, b.owner, "sum", async_op=True)
 
     def push(self) -> float:
         """Issue what backward did not, wait for every push; returns the grad scale 1/world."""
@@ -276,12 +278,12 @@ class ShardedGradSync:
             out = g.data[b.start:b.end]
             if b.owner == -1:
                 c = b.numel // self.world
-                b.pull_work = dist.all_gather_into_tensor(out, src_buf[b.shard_off:b.shard_off + c],
-                                                          group=self.pg, async_op=True)
+                b.pull_work = self.comm.all_gather_into_tensor(out, src_buf[b.shard_off:b.shard_off + c],
+                                                               async_op=True)
             else:
                 if b.owner == self.rank:
                     out.copy_(src_buf[b.shard_off:b.shard_off + b.numel])
-                b.pull_work = dist.broadcast(out, b.owner, group=self.pg, async_op=True)
+                b.pull_work = self.comm.broadcast(out, b.owner, async_op=True)
         if not self._pull_hooks:
             self.wait_pull()
 
@@ -361,11 +363,11 @@ class ShardedGradSync:
             out = full[b.start:b.end]
             if b.owner == -1:
                 c = b.numel // self.world
-                dist.all_gather_into_tensor(out, self.w32[gi][b.shard_off:b.shard_off + c], group=self.pg)
+                self.comm.all_gather_into_tensor(out, self.w32[gi][b.shard_off:b.shard_off + c])
             else:
                 if b.owner == self.rank:
                     out.copy_(self.w32[gi][b.shard_off:b.shard_off + b.numel])
-                dist.broadcast(out, b.owner, group=self.pg)
+                self.comm.broadcast(out, b.owner)
         return full
 
     def load_full_master(self, gi: int, full: torch.Tensor) -> None:

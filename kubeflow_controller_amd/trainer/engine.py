@@ -82,7 +82,7 @@ class Engine:
                  momentum: float = 0.9, weight_decay: float = 5e-5, betas=(0.9, 0.999), eps: float = 1e-8,
                  compute_dtype=torch.bfloat16, bucket_mb: float = 32.0, dist_info: Optional[DistInfo] = None,
                  channels_last: bool = True, ps: int = 0, ps_placement: str = "ps",
-                 grad_reduce_dtype: Optional[torch.dtype] = torch.float32):
+                 grad_reduce_dtype: Optional[torch.dtype] = torch.float32, comm=None):
         from ..ops.optim import FusedAdam, FusedSGD
         from ..parallel.ddp import GradSync, broadcast_params
 
@@ -96,14 +96,23 @@ class Engine:
         self.loss_fn = loss_fn
         # pad so every group splits evenly into per-rank reduce-scatter shards
         self.groups: List[FlatGroup] = split_params(self.model, compute_dtype, pad_to=8 * max(1, self.info.world))
-        broadcast_params(self.groups)
+        # gradient / parameter traffic: the first-party communicator (RCCL on GPUs,
+        # parallel/comm.py) unless KFA_COMM=torch; torch.distributed (gloo) on the CPU
+        if comm is None:
+            from ..parallel.comm import make_comm
+            comm = make_comm(self.info.device)
+        self.comm = comm
+        for m in self.model.modules():  # sparse tables exchange rows on the same communicator
+            if getattr(m, "kfa_sparse_module", False) and getattr(m, "world", 1) > 1:
+                m.comm = comm
+        broadcast_params(self.groups, comm=comm)
         self.sharded = ps > 0 and self.info.world > 1
         if self.sharded:
             from ..parallel.ps import ShardedGradSync
             self.sync = ShardedGradSync(self.groups, bucket_mb=bucket_mb, placement=ps_placement, num_ps=ps,
-                                        reduce_dtype=grad_reduce_dtype, model=self.model)
+                                        reduce_dtype=grad_reduce_dtype, model=self.model, comm=comm)
         else:
-            self.sync = GradSync(self.groups, bucket_mb=bucket_mb, reduce_dtype=grad_reduce_dtype)
+            self.sync = GradSync(self.groups, bucket_mb=bucket_mb, reduce_dtype=grad_reduce_dtype, comm=comm)
         spaces = self.sync.spaces()
         if optimizer == "sgd":
             self.opt = FusedSGD(spaces, lr=lr, momentum=momentum, weight_decay=weight_decay)
