@@ -240,6 +240,7 @@ def run_rank(args) -> int:
     import torch
 
     from kubeflow_controller_amd.models.resnet import resnet50, resnet_tiny
+    from kubeflow_controller_amd.ops import routes
     from kubeflow_controller_amd.ops.loss import cross_entropy
     from kubeflow_controller_amd.trainer.engine import Engine, init_distributed, timed_steps
 
@@ -294,11 +295,14 @@ def run_rank(args) -> int:
                        "grad_reduce": args.grad_reduce if info.world > 1 else None,
                        "backend": (torch.distributed.get_backend() if torch.distributed.is_initialized()
                                    else None),
+                       "comm": repr(engine.comm) if info.world > 1 else None,
+                       "routes": routes.summary(),
                        "optimizer": "SGD momentum 0.9 (fused HIP), fp32 master",
                        "hip_graph": engine._graph is not None,
                        "loss": r["loss"]},
         }
         print(json.dumps(out), flush=True)
+    engine.comm.destroy()
     if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
     import faulthandler

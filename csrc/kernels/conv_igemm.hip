@@ -146,6 +146,174 @@ __device__ __forceinline__ int swz(int row, int chunk) { return row * BK + ((chu
 // main loop's LDS fragment reads on a reused register.
 constexpr unsigned kEpiE = 1, kEpiStats = 2, kEpiBnBwd = 4, kEpiEmb = 8, kEpiYMask = 16, kEpiAll = 31;
 
+struct EpiRes {  // buffer resources of the epilogue's output / addend / BN input / BN output
+  __amdgpu_buffer_rsrc_t d, e, bx, by;
+};
+
+// Epilogue of one wave tile through LDS: MFMA leaves each lane 4 consecutive
+// channels of one pixel (acc[ni][mi][r] = D(m = mw + 16 mi + fr, n = nw + 16 ni
+// + 4 fq + r)); staging the wave's tile in LDS (XOR-swizzled 16-B chunks,
+// conflict-free both ways) lets every lane store 16 B and a wave cover 128-B row
+// segments, so the HBM writes of the memory-bound layers (K = 64..256) coalesce.
+// NHALF staging passes over the wave's rows (1 for 64-row wave tiles; 4 for the
+// 128-row ones, keeping the epilogue's in-flight loads at 48 VGPRs).  `stage`:
+// this wave's 256 * (TM / NHALF) * TN staged elements; `first_barrier`: the
+// first pass waits at a workgroup barrier before its LDS writes (the stage
+// aliases an operand buffer other waves may still be reading).  Also: the
+// residual-gradient addend (kEpiE, masked by ReLU bits with kEpiEmb) and the
+// fused BatchNorm statistics (kEpiStats; kEpiBnBwd: backward statistics of the
+// BN this dgrad feeds).  The accumulators are zeroed for the next tile.
+template <int TM, int TN, int NHALF, unsigned EPI>
+__device__ __forceinline__ void conv_epilogue(const Geo& g, floatx4 (&acc)[TN][TM], char* stage, bool first_barrier,
+                                              int lane, int mw, int nw, int PQ, float rPQ, float rQ, bool lin_d,
+                                              const bf16_t* E, float* stats, const BnBwd& bnb, const EpiRes& er) {
+  constexpr int TMH = TM / NHALF;     // MFMA row tiles per pass
+  constexpr int RB = 32 * TN;         // staged row bytes
+  constexpr int CPR = 2 * TN;         // 16-B chunks per staged row
+  constexpr int IT = (16 * TMH * CPR) / 64;  // 16-B row pieces per lane per pass
+  const int fr = lane & 15, fq = lane >> 4;
+  const int c = lane % CPR;
+  const int n = nw + c * 8;
+  float mu[8] = {0, 0, 0, 0, 0, 0, 0, 0}, msc[8], msf[8];
+  constexpr bool kE = EPI & kEpiE, kST = EPI & kEpiStats, kBS = EPI & kEpiBnBwd, kEM = EPI & kEpiEmb;
+  constexpr bool kYM = EPI & kEpiYMask;  // ReLU mask read from the BN output (else bits / recomputed from x)
+  const bool bstat = kBS && kST && stats && bnb.x;
+  const bool ymask = kYM && bnb.relu && bnb.y;       // mask from the output y
+  const bool bmask = bnb.relu && !bnb.y && bnb.mb;   // from the output bit mask
+  // else (relu) recomputed from x with the saved scale / shift
+  if (bstat)
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      mu[j] = n + j < g.N ? bnb.mean[n + j] : 0.f;
+      msc[j] = (bnb.relu && !ymask && !bmask && n + j < g.N) ? bnb.ss[n + j] : 0.f;
+      msf[j] = (bnb.relu && !ymask && !bmask && n + j < g.N) ? bnb.ss[g.N + n + j] : 0.f;
+    }
+  float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // fused BN statistics
+#pragma unroll
+  for (int hh = 0; hh < NHALF; hh++) {
+    // output offsets first, so the epilogue's global loads (residual-grad addend,
+    // BN input / output for the fused backward statistics) are all in flight
+    // while the tile is staged through LDS
+    unsigned offs[IT];
+#pragma unroll
+    for (int it = 0; it < IT; it++) {
+      const int m = mw + hh * TMH * 16 + it * (64 / CPR) + lane / CPR;
+      unsigned orow;  // byte offset of output row m
+      if (lin_d) {
+        orow = (unsigned)m * (unsigned)g.ldd * 2u;
+      } else {
+        const int nb = fdiv(m, PQ, rPQ), rem = m - nb * PQ;
+        const int p = fdiv(rem, g.Q, rQ), q = rem - p * g.Q;
+        orow = (unsigned)((nb * g.OH + p * g.os + g.oph) * g.OW + (q * g.os + g.opw)) * (unsigned)g.ldd * 2u;
+      }
+      offs[it] = (m >= g.M || n >= g.N) ? kOOB : orow + (unsigned)n * 2u;
+    }
+    uint4 ev[IT], bx[IT], by[IT];
+    unsigned mbits[IT], ebits[IT];
+    if (kE && E)
+#pragma unroll
+      for (int it = 0; it < IT; it++) {
+        ev[it] = bload16(er.e, offs[it]);
+        if (kEM && bnb.emb) ebits[it] = offs[it] != kOOB ? (unsigned)bnb.emb[offs[it] >> 4] : 0u;
+      }
+    if (bstat)
+#pragma unroll
+      for (int it = 0; it < IT; it++) {
+        bx[it] = bload16(er.bx, offs[it]);
+        if (ymask) by[it] = bload16(er.by, offs[it]);
+        if (bmask) mbits[it] = offs[it] != kOOB ? (unsigned)bnb.mb[offs[it] >> 4] : 0u;  // 8 bf16 = 16 B per bit byte
+      }
+
+    if (hh == 0 && first_barrier) lds_barrier();  // every wave is done reading the operand buffer under `stage`
+    else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave read back its previous pass
+#pragma unroll
+    for (int mj = 0; mj < TMH; mj++)
+#pragma unroll
+      for (int ni = 0; ni < TN; ni++) {
+        const int mi = hh * TMH + mj;
+        const int row = mj * 16 + fr, col = ni * 16 + fq * 4;
+        const uint2 o = make_uint2(pack2(acc[ni][mi][0], acc[ni][mi][1]), pack2(acc[ni][mi][2], acc[ni][mi][3]));
+        *reinterpret_cast<uint2*>(stage + row * RB + (((col >> 3) ^ (row & (CPR - 1))) << 4) + (col & 7) * 2) = o;
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int it = 0; it < IT; it++) {
+      const int r = it * (64 / CPR) + lane / CPR;
+      const uint4 v = *reinterpret_cast<const uint4*>(stage + r * RB + ((c ^ (r & (CPR - 1))) << 4));
+      const unsigned off = offs[it];
+      uint4 o = v;
+      if (kE && E) {  // wave-uniform branch
+        float f[8], h[8];
+        unpack8(v, f);
+        unpack8(ev[it], h);
+        if (kEM && bnb.emb) {  // residual gradient dz = dy * relu-mask, formed here instead of by the BN backward
+#pragma unroll
+          for (int j = 0; j < 8; j++) f[j] += ((ebits[it] >> j) & 1u) ? h[j] : 0.f;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; j++) f[j] += h[j];
+        }
+        o = pack8(f);
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<decltype(__builtin_amdgcn_raw_buffer_load_b128(er.d, 0, 0, 0))*>(&o), er.d, off, 0, KFA_CONV_STORE_AUX);
+      if (kST && stats && off != kOOB) {  // wave-uniform pointer test; per-lane row mask
+        float f[8];
+        unpack8(o, f);  // the bf16-rounded values the BatchNorm will see
+        if (bstat) {    // backward statistics of the BN this dgrad feeds
+          float xf[8];
+          unpack8(bx[it], xf);
+          if (ymask) {
+            float yf[8];
+            unpack8(by[it], yf);
+#pragma unroll
+            for (int j = 0; j < 8; j++) f[j] = yf[j] > 0.f ? f[j] : 0.f;
+          } else if (bmask) {
+#pragma unroll
+            for (int j = 0; j < 8; j++) f[j] = ((mbits[it] >> j) & 1u) ? f[j] : 0.f;
+          } else if (bnb.relu) {  // y = relu(fma(x, sc, sh)) exactly as bn_apply evaluated it
+#pragma unroll
+            for (int j = 0; j < 8; j++) f[j] = fmaf(xf[j], msc[j], msf[j]) > 0.f ? f[j] : 0.f;
+          }
+#pragma unroll
+          for (int j = 0; j < 8; j++) { s1[j] += f[j]; s2[j] += f[j] * (xf[j] - mu[j]); }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; j++) { s1[j] += f[j]; s2[j] += f[j] * f[j]; }
+        }
+      }
+    }
+  }
+  if (kST && stats) {
+    // Butterfly-reduce over the lanes sharing channel chunk c = lane % CPR (xor
+    // 8, 16, 32): every lane ends with its chunk's wave totals.  Lane L then
+    // publishes channel (L % 8) * 8 + L / 8 — its own chunk, register L / 8
+    // (a select chain, no shuffles) — so ONE 64-lane atomic instruction per
+    // statistic covers the wave's 64 channels (CPR == 8: TN == 4).
+    static_assert(CPR == 8, "fused BN statistics assume 64-channel wave tiles");
+#pragma unroll
+    for (int o = CPR; o < 64; o <<= 1)
+#pragma unroll
+      for (int j = 0; j < 8; j++) { s1[j] += __shfl_xor(s1[j], o, 64); s2[j] += __shfl_xor(s2[j], o, 64); }
+    const int jj = lane >> 3;
+    float a = s1[0], b = s2[0];
+#pragma unroll
+    for (int j = 1; j < 8; j++) {
+      a = jj == j ? s1[j] : a;
+      b = jj == j ? s2[j] : b;
+    }
+    const int nc = n + jj;
+    if (nc < g.N) {
+      float* slot = stats + (long)(blockIdx.x % kBnSlots) * 2 * g.N;
+      __hip_atomic_fetch_add(slot + nc, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(slot + g.N + nc, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < TN; i++)
+#pragma unroll
+    for (int j = 0; j < TM; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+}
+
 template <int WM, int WN, int TM, int TN, unsigned EPI, bool PRO = false>
 __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_t* __restrict__ T,
                                                                      const bf16_t* __restrict__ B,
@@ -358,167 +526,18 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
       }
     }
   };
-  // Epilogue through LDS: MFMA leaves each lane 4 consecutive channels of one
-  // pixel (8-B pieces, 32-B row segments per store instruction); staging the
-  // wave's tile in LDS (XOR-swizzled 16-B chunks, conflict-free both ways)
-  // lets every lane store 16 B and a wave cover 128-B row segments, so the
-  // HBM writes of the memory-bound layers (K = 64..256) coalesce.
-  // staging passes over the wave's rows: 1 for the 4-wave tiles; 4 for the 8-wave
-  // 128-row wave tiles (keeps the epilogue's in-flight loads at 48 VGPRs)
+  // Epilogue: conv_epilogue (below the kernel) over this wave's tile, staged in
+  // ring buffer `buf` once every wave is done reading it (its first pass's barrier)
   constexpr int NHALF = NW == 4 ? 1 : TM / 2;
-  constexpr int TMH = TM / NHALF;     // MFMA row tiles per pass
-  constexpr int WT = 256 * TMH * TN;  // staged elements per wave per pass (16TMH rows x 16TN channels)
-  constexpr int RB = 32 * TN;         // staged row bytes
-  constexpr int CPR = 2 * TN;         // 16-B chunks per staged row
+  constexpr int WT = 256 * (TM / NHALF) * TN;  // staged elements per wave per pass
   static_assert(NW * WT <= (BM + BN) * BK, "conv epilogue stage must fit one ring buffer");
+  const EpiRes er{rD, rE, rBX, rBY};
   auto epilogue = [&](int tile, int buf) {
-    constexpr int IT = (16 * TMH * CPR) / 64;  // 16-B row pieces per lane per pass
     const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
-    const int c = lane % CPR;
-    const int n = n0 + wn * TN * 16 + c * 8;
-    float mu[8] = {0, 0, 0, 0, 0, 0, 0, 0}, msc[8], msf[8];
-    constexpr bool kE = EPI & kEpiE, kST = EPI & kEpiStats, kBS = EPI & kEpiBnBwd, kEM = EPI & kEpiEmb;
-    constexpr bool kYM = EPI & kEpiYMask;  // ReLU mask read from the BN output (else bits / recomputed from x)
-    const bool bstat = kBS && kST && stats && bnb.x;
-    const bool ymask = kYM && bnb.relu && bnb.y;       // mask from the output y
-    const bool bmask = bnb.relu && !bnb.y && bnb.mb;   // from the output bit mask
-    // else (relu) recomputed from x with the saved scale / shift
-    if (bstat)
-#pragma unroll
-      for (int j = 0; j < 8; j++) {
-        mu[j] = n + j < g.N ? bnb.mean[n + j] : 0.f;
-        msc[j] = (bnb.relu && !ymask && !bmask && n + j < g.N) ? bnb.ss[n + j] : 0.f;
-        msf[j] = (bnb.relu && !ymask && !bmask && n + j < g.N) ? bnb.ss[g.N + n + j] : 0.f;
-      }
-    float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // fused BN statistics
-    char* stage;
-    {
-      const int e = wave * WT;
-      stage = reinterpret_cast<char*>(e < BM * BK ? As + buf * BM * BK + e : Bs + buf * BN * BK + (e - BM * BK));
-    }
-#pragma unroll
-    for (int hh = 0; hh < NHALF; hh++) {
-      // output offsets first, so the epilogue's global loads (residual-grad addend,
-      // BN input / output for the fused backward statistics) are all in flight
-      // while the tile is staged through LDS
-      unsigned offs[IT];
-#pragma unroll
-      for (int it = 0; it < IT; it++) {
-        const int m = m0 + wm * TM * 16 + hh * TMH * 16 + it * (64 / CPR) + lane / CPR;
-        unsigned orow;  // byte offset of output row m
-        if (lin_d) {
-          orow = (unsigned)m * (unsigned)g.ldd * 2u;
-        } else {
-          const int nb = fdiv(m, PQ, rPQ), rem = m - nb * PQ;
-          const int p = fdiv(rem, g.Q, rQ), q = rem - p * g.Q;
-          orow = (unsigned)((nb * g.OH + p * g.os + g.oph) * g.OW + (q * g.os + g.opw)) * (unsigned)g.ldd * 2u;
-        }
-        offs[it] = (m >= g.M || n >= g.N) ? kOOB : orow + (unsigned)n * 2u;
-      }
-      uint4 ev[IT], bx[IT], by[IT];
-      unsigned mbits[IT], ebits[IT];
-      if (kE && E)
-#pragma unroll
-        for (int it = 0; it < IT; it++) {
-          ev[it] = bload16(rE, offs[it]);
-          if (kEM && bnb.emb) ebits[it] = offs[it] != kOOB ? (unsigned)bnb.emb[offs[it] >> 4] : 0u;
-        }
-      if (bstat)
-#pragma unroll
-        for (int it = 0; it < IT; it++) {
-          bx[it] = bload16(rBX, offs[it]);
-          if (ymask) by[it] = bload16(rBY, offs[it]);
-          if (bmask) mbits[it] = offs[it] != kOOB ? (unsigned)bnb.mb[offs[it] >> 4] : 0u;  // 8 bf16 = 16 B per bit byte
-        }
-
-      if (hh == 0) lds_barrier();  // every wave is done reading `buf`: reuse it as the staging area
-      else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave read back its previous pass
-#pragma unroll
-      for (int mj = 0; mj < TMH; mj++)
-#pragma unroll
-        for (int ni = 0; ni < TN; ni++) {
-          const int mi = hh * TMH + mj;
-          const int row = mj * 16 + fr, col = ni * 16 + fq * 4;
-          const uint2 o = make_uint2(pack2(acc[ni][mi][0], acc[ni][mi][1]), pack2(acc[ni][mi][2], acc[ni][mi][3]));
-          *reinterpret_cast<uint2*>(stage + row * RB + (((col >> 3) ^ (row & (CPR - 1))) << 4) + (col & 7) * 2) = o;
-        }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int it = 0; it < IT; it++) {
-        const int r = it * (64 / CPR) + lane / CPR;
-        const uint4 v = *reinterpret_cast<const uint4*>(stage + r * RB + ((c ^ (r & (CPR - 1))) << 4));
-        const unsigned off = offs[it];
-        uint4 o = v;
-        if (kE && E) {  // wave-uniform branch
-          float f[8], h[8];
-          unpack8(v, f);
-          unpack8(ev[it], h);
-          if (kEM && bnb.emb) {  // residual gradient dz = dy * relu-mask, formed here instead of by the BN backward
-#pragma unroll
-            for (int j = 0; j < 8; j++) f[j] += ((ebits[it] >> j) & 1u) ? h[j] : 0.f;
-          } else {
-#pragma unroll
-            for (int j = 0; j < 8; j++) f[j] += h[j];
-          }
-          o = pack8(f);
-        }
-        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<decltype(__builtin_amdgcn_raw_buffer_load_b128(rD, 0, 0, 0))*>(&o), rD, off, 0, KFA_CONV_STORE_AUX);
-        if (kST && stats && off != kOOB) {  // wave-uniform pointer test; per-lane row mask
-          float f[8];
-          unpack8(o, f);  // the bf16-rounded values the BatchNorm will see
-          if (bstat) {    // backward statistics of the BN this dgrad feeds
-            float xf[8];
-            unpack8(bx[it], xf);
-            if (ymask) {
-              float yf[8];
-              unpack8(by[it], yf);
-#pragma unroll
-              for (int j = 0; j < 8; j++) f[j] = yf[j] > 0.f ? f[j] : 0.f;
-            } else if (bmask) {
-#pragma unroll
-              for (int j = 0; j < 8; j++) f[j] = ((mbits[it] >> j) & 1u) ? f[j] : 0.f;
-            } else if (bnb.relu) {  // y = relu(fma(x, sc, sh)) exactly as bn_apply evaluated it
-#pragma unroll
-              for (int j = 0; j < 8; j++) f[j] = fmaf(xf[j], msc[j], msf[j]) > 0.f ? f[j] : 0.f;
-            }
-#pragma unroll
-            for (int j = 0; j < 8; j++) { s1[j] += f[j]; s2[j] += f[j] * (xf[j] - mu[j]); }
-          } else {
-#pragma unroll
-            for (int j = 0; j < 8; j++) { s1[j] += f[j]; s2[j] += f[j] * f[j]; }
-          }
-        }
-      }
-    }
-    if (kST && stats) {
-      // Butterfly-reduce over the lanes sharing channel chunk c = lane % CPR (xor
-      // 8, 16, 32): every lane ends with its chunk's wave totals.  Lane L then
-      // publishes channel (L % 8) * 8 + L / 8 — its own chunk, register L / 8
-      // (a select chain, no shuffles) — so ONE 64-lane atomic instruction per
-      // statistic covers the wave's 64 channels (CPR == 8: TN == 4).
-      static_assert(CPR == 8, "fused BN statistics assume 64-channel wave tiles");
-#pragma unroll
-      for (int o = CPR; o < 64; o <<= 1)
-#pragma unroll
-        for (int j = 0; j < 8; j++) { s1[j] += __shfl_xor(s1[j], o, 64); s2[j] += __shfl_xor(s2[j], o, 64); }
-      const int jj = lane >> 3;
-      float a = s1[0], b = s2[0];
-#pragma unroll
-      for (int j = 1; j < 8; j++) {
-        a = jj == j ? s1[j] : a;
-        b = jj == j ? s2[j] : b;
-      }
-      const int nc = n + jj;
-      if (nc < g.N) {
-        float* slot = stats + (long)(blockIdx.x % kBnSlots) * 2 * g.N;
-        __hip_atomic_fetch_add(slot + nc, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add(slot + g.N + nc, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < TN; i++)
-#pragma unroll
-      for (int j = 0; j < TM; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    const int e = wave * WT;
+    char* stage = reinterpret_cast<char*>(e < BM * BK ? As + buf * BM * BK + e : Bs + buf * BN * BK + (e - BM * BK));
+    conv_epilogue<TM, TN, NHALF, EPI>(g, acc, stage, true, lane, m0 + wm * TM * 16, n0 + wn * TN * 16, PQ, rPQ, rQ,
+                                      lin_d, E, stats, bnb, er);
   };
 
   // PRO: the slice's A chunks landed -> relu(x * sc + sh) (0 on padding taps) into
@@ -601,6 +620,240 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
     if ((st + 1) % nk == 0) epilogue(tile_of(st / nk), buf);
     lds_barrier();  // every wave is done reading `buf` before slice st+2 is DMA'd into it
   }
+}
+
+// ---------------------------------------------------------------------------
+// Ping-pong implicit GEMM (256 x 256 tiles): gemm_pp_kernel's two-wave-group
+// schedule (gemm.hip, "Ping-pong 256x256 kernel") with the A operand gathered
+// from the NHWC activation as in conv_igemm_kernel.  512 threads = two wave
+// GROUPS (waves 0-3: tile rows 0-127, waves 4-7: rows 128-255; wave w owns the
+// 128 x 64 tile at (w >> 2, w & 3)), one block per CU, BK = 64 = one tap's 64
+// channels.  Each k-tile is four 16 KB pieces ordered by first use
+//   A0: A rows {0-63, 128-191}   B0: B rows {64c + 0..31}
+//   B1: B rows {64c + 32..63}    A1: A rows {64-127, 192-255}
+// consumed in four phases of 16 MFMAs per wave; group 1 runs one barrier
+// behind group 0, so on every SIMD one wave's MFMAs run under the other's LDS
+// fragment reads and DMA issue, and four pieces (8 DMAs per lane) stay in
+// flight across the barriers (never vmcnt(0) in the main loop).  Compared
+// with the 4-wave 128 x 128 conv_igemm_kernel (two blocks per CU, ONE k-step
+// of prefetch, 19-24 % MFMA busy at 3.6-4.4 VALU per MFMA,
+// profiles/pmc/r4_resnet50_step.md): 128 x 64 wave tiles read 0.375 LDS
+// fragments per MFMA instead of 0.5, the tile moves half the L2 -> LDS bytes
+// per FLOP, and the load latency is covered by ~a k-tile of work.
+// Gather: the A piece of k-tile kt reads tap (r, s), channels c0..c0+63, at
+// per-lane 32-bit offsets (rows past M and padding taps go past the buffer
+// and read 0); the tap walk is carried incrementally (wave-uniform) — the A0
+// piece of a k-tile advances it, its A1 piece (issued three phases later, no
+// other A0 in between) reuses it.  Epilogue: conv_epilogue (LDS-staged 16-B
+// stores + fused addend / BN statistics), 4 staging passes per 128-row wave tile.
+template <unsigned EPI>
+__global__ __launch_bounds__(512, 1) void conv_pp_kernel(const bf16_t* __restrict__ T, const bf16_t* __restrict__ B,
+                                                         bf16_t* __restrict__ D, const bf16_t* __restrict__ E,
+                                                         float* __restrict__ stats, BnBwd bnb, Geo g) {
+  constexpr int TM = 8, TN = 4, PIECE = 128 * BK * 2;
+  __shared__ __attribute__((aligned(16))) char smem[2 * 4 * PIECE];  // 128 KB: two k-tile buffers
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  // T1 XCD remap + grouped raster (as gemm_pp_kernel): the blocks of one XCD take
+  // consecutive tiles, GM row panels wide
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q8 = nwg >> 3, r8 = nwg & 7, x8 = bid & 7;
+  const int wg = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + (bid >> 3);
+  const int ntn = (g.N + 255) / 256, ntm = (g.M + 255) / 256;
+  constexpr int GM = 4;
+  const int grp = wg / (GM * ntn), gm0 = grp * GM, gmn = min(GM, ntm - gm0), rem = wg - grp * GM * ntn;
+  const int m0 = (gm0 + rem % gmn) * 256, n0 = (rem / gmn) * 256;
+
+  const __amdgpu_buffer_rsrc_t rT = rsrc(T, g.t_bytes), rB = rsrc(B, g.b_bytes), rD = rsrc(D, g.d_bytes);
+  const int PQ = g.P * g.Q;
+  const float rPQ = 1.f / (float)PQ, rQ = 1.f / (float)g.Q;
+  const bool lin_a = g.R == 1 && g.S == 1 && g.sa == 1 && g.oa == 0 && g.ob == 0 && g.H == g.P && g.W == g.Q;
+  const bool lin_d = g.os == 1 && g.oph == 0 && g.opw == 0 && g.OH == g.P && g.OW == g.Q;
+  // DMA plan: instruction j of wave w fills piece rows j*64 + w*8 + lane/8,
+  // physical chunk lane&7 <- logical chunk (lane&7) ^ ((row >> 1) & 7)
+  const int prow = wave * 8 + (lane >> 3);
+  const int lc = (lane & 7) ^ ((prow >> 1) & 7);
+  int a_hb[2][2], a_wb[2][2], a_vo[2][2];  // [h: A0 / A1][j]
+  int b_vo[2][2];                          // [h: B0 / B1][j]
+#pragma unroll
+  for (int h = 0; h < 2; h++)
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      const int m = m0 + j * 128 + h * 64 + prow;
+      if (m < g.M && lin_a) {
+        a_hb[h][j] = 0;
+        a_wb[h][j] = 0;
+        a_vo[h][j] = (m * g.C + lc * 8) * 2;
+      } else if (m < g.M) {  // a_vo: the row's offset at tap (0, 0) (may lie outside the image)
+        const int nb = fdiv(m, PQ, rPQ), rm = m - nb * PQ;
+        const int p = fdiv(rm, g.Q, rQ), q = rm - p * g.Q;
+        a_hb[h][j] = p * g.sa + g.oa;
+        a_wb[h][j] = q * g.sa + g.ob;
+        a_vo[h][j] = ((nb * g.H * g.W + a_hb[h][j] * g.W + a_wb[h][j]) * g.C + lc * 8) * 2;
+      } else {
+        a_hb[h][j] = -(1 << 28);  // forces out-of-range
+        a_wb[h][j] = 0;
+        a_vo[h][j] = (int)kOOB;
+      }
+      const int n = n0 + (2 * j + (prow >> 5)) * 64 + h * 32 + (prow & 31);
+      b_vo[h][j] = n < g.N ? (n * g.K + lc * 8) * 2 : (int)kOOB;
+    }
+  const int nk = g.K / BK;
+  const int plast = 4 * nk - 7;  // last phase that issues a piece
+  // tap walk of the A pieces (wave-uniform): next k-tile's (channel offset, r, s)
+  int tw_c0 = 0, tw_r = 0, tw_s = 0;
+  int ta_dh = 0, ta_dw = 0, ta_off = 0, ta_soff = 0;  // the tap of the last A0 piece issued
+  auto issue = [&](int P, auto pc, auto steady) __attribute__((always_inline)) {
+    constexpr int p = decltype(pc)::value;
+    const int kt = (P + 6) >> 2;
+    if (decltype(steady)::value || kt < nk) {
+      char* dst = smem + (kt & 1) * (4 * PIECE) + p * PIECE + wave * 8 * 128;
+      if constexpr (p == 0 || p == 3) {
+        constexpr int h = p == 3;
+        if constexpr (h == 0) {  // A0 of k-tile kt: advance the tap walk
+          ta_dh = tw_r * g.ra;
+          ta_dw = tw_s * g.ra;
+          ta_off = (ta_dh * g.W + ta_dw) * g.C * 2;
+          ta_soff = (lin_a ? kt * BK : tw_c0) * 2;
+          tw_c0 += BK;
+          if (tw_c0 >= g.C) {
+            tw_c0 = 0;
+            if (++tw_s == g.S) { tw_s = 0; tw_r++; }
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+          int vo = a_vo[h][j];
+          if (!lin_a) {  // selects, no branch: the tap offset is one scalar add
+            const int ih = a_hb[h][j] + ta_dh, iw = a_wb[h][j] + ta_dw;
+            const bool ok = (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+            vo = ok ? vo + ta_off : (int)kOOB;
+          }
+          buf_dma16_act(rT, reinterpret_cast<bf16_t*>(dst + j * 64 * 128), vo, ta_soff);
+        }
+      } else {
+        constexpr int h = p == 2;
+        buf_dma16(rB, reinterpret_cast<bf16_t*>(dst), b_vo[h][0], kt * BK * 2);
+        buf_dma16(rB, reinterpret_cast<bf16_t*>(dst + 64 * 128), b_vo[h][1], kt * BK * 2);
+      }
+    }
+  };
+  auto retire = [&](int P, auto steady) __attribute__((always_inline)) {
+    if constexpr (decltype(steady)::value) {
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      const int younger = min(P, plast) - (P - 3) + 1;
+      const int y = younger < 0 ? 0 : younger;
+      if (y >= 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if (y == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else if (y == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else if (y == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  };
+
+  // this lane's fragment read offsets in a piece: row fr, logical chunk 4 ks + fq
+  const int fr = lane & 15, fq = lane >> 4;
+  const int ro0 = fr * 128 + ((fq ^ (fr >> 1)) << 4), ro1 = fr * 128 + (((4 + fq) ^ (fr >> 1)) << 4);
+  floatx4 acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; i++)
+#pragma unroll
+    for (int j = 0; j < TM; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  short8 a[4][2], b0[2][2], b1[2][2];
+
+  // prologue: pieces of phases -6..-1 (A0 B0 B1 A1 of k-tile 0, A0 B0 of k-tile 1)
+  issue(-6, std::integral_constant<int, 0>{}, std::false_type{});
+  issue(-5, std::integral_constant<int, 1>{}, std::false_type{});
+  issue(-4, std::integral_constant<int, 2>{}, std::false_type{});
+  issue(-3, std::integral_constant<int, 3>{}, std::false_type{});
+  issue(-2, std::integral_constant<int, 0>{}, std::false_type{});
+  issue(-1, std::integral_constant<int, 1>{}, std::false_type{});
+  retire(-1, std::false_type{});
+  asm volatile("s_barrier" ::: "memory");
+  if (wr) asm volatile("s_barrier" ::: "memory");  // group 1 runs one barrier behind
+
+  auto mfma_q = [&](short8 (&bb)[2][2], int mh, int nh) __attribute__((always_inline)) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ks++)
+#pragma unroll
+      for (int ni = 0; ni < 2; ni++)
+#pragma unroll
+        for (int mi = 0; mi < 4; mi++)
+          acc[nh * 2 + ni][mh * 4 + mi] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[ni][ks], a[mi][ks], acc[nh * 2 + ni][mh * 4 + mi], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto rd = [&](const char* p) -> short8 { return *reinterpret_cast<const short8*>(p); };
+
+  // one k-tile = four phases (st: std::true_type when every phase of k-tile u
+  // issues a piece, i.e. u + 2 < nk)
+  auto ktile = [&](int u, auto st) __attribute__((always_inline)) {
+    const char* buf = smem + (u & 1) * (4 * PIECE);
+    const int P = 4 * u;
+    {  // s0: A0 + B0
+      const char* pa = buf + wr * 64 * 128;
+      const char* pb = buf + PIECE + wc * 32 * 128;
+#pragma unroll
+      for (int ni = 0; ni < 2; ni++) {
+        b0[ni][0] = rd(pb + ni * 16 * 128 + ro0);
+        b0[ni][1] = rd(pb + ni * 16 * 128 + ro1);
+      }
+#pragma unroll
+      for (int mi = 0; mi < 4; mi++) {
+        a[mi][0] = rd(pa + mi * 16 * 128 + ro0);
+        a[mi][1] = rd(pa + mi * 16 * 128 + ro1);
+      }
+      issue(P, std::integral_constant<int, 2>{}, st);
+      retire(P, st);
+      asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      mfma_q(b0, 0, 0);
+      asm volatile("s_barrier" ::: "memory");
+    }
+    {  // s1: B1
+      const char* pb = buf + 2 * PIECE + wc * 32 * 128;
+#pragma unroll
+      for (int ni = 0; ni < 2; ni++) {
+        b1[ni][0] = rd(pb + ni * 16 * 128 + ro0);
+        b1[ni][1] = rd(pb + ni * 16 * 128 + ro1);
+      }
+      issue(P + 1, std::integral_constant<int, 3>{}, st);
+      retire(P + 1, st);
+      asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      mfma_q(b1, 0, 1);
+      asm volatile("s_barrier" ::: "memory");
+    }
+    {  // s2: A1
+      const char* pa = buf + 3 * PIECE + wr * 64 * 128;
+#pragma unroll
+      for (int mi = 0; mi < 4; mi++) {
+        a[mi][0] = rd(pa + mi * 16 * 128 + ro0);
+        a[mi][1] = rd(pa + mi * 16 * 128 + ro1);
+      }
+      issue(P + 2, std::integral_constant<int, 0>{}, st);
+      retire(P + 2, st);
+      asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      mfma_q(b1, 1, 1);
+      asm volatile("s_barrier" ::: "memory");
+    }
+    {  // s3: registers only
+      issue(P + 3, std::integral_constant<int, 1>{}, st);
+      retire(P + 3, st);
+      asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      mfma_q(b0, 1, 0);
+      asm volatile("s_barrier" ::: "memory");
+    }
+  };
+  int u = 0;
+  for (; u + 2 < nk; u++) ktile(u, std::true_type{});
+  for (; u < nk; u++) ktile(u, std::false_type{});
+  if (!wr) asm volatile("s_barrier" ::: "memory");  // both groups at the same barrier count: the ring is idle
+  const EpiRes er{rD, rsrc(E ? E : D, E ? g.d_bytes : 0u), rsrc(bnb.x ? bnb.x : D, bnb.x ? g.d_bytes : 0u),
+                  rsrc(bnb.y ? bnb.y : D, bnb.y ? g.d_bytes : 0u)};
+  conv_epilogue<TM, TN, 4, EPI>(g, acc, smem + wave * (256 * 2 * TN) * 2, false, lane, m0 + wr * 128, n0 + wc * 64,
+                                PQ, rPQ, rQ, lin_d, E, stats, bnb, er);
 }
 
 // zero-fill D rows of the output pixel mapping that the GEMM does not cover
@@ -749,7 +1002,32 @@ static void launch_igemm_pro(unsigned epi, dim3 grid, dim3 block, int lds, hipSt
 #undef KFA_IGP
 }
 
-// variant: 0 = 128x128 tile, 1 = 128x64 tile (N <= 64), 2 = 256x256 tile (8 waves), 3 = 256x64 (N <= 64)
+template <unsigned EP>
+static void launch_pp1(dim3 grid, hipStream_t st, const bf16_t* T, const bf16_t* B, bf16_t* D, const bf16_t* E,
+                       float* stats, const BnBwd& bnb, const Geo& g) {
+  hipLaunchKernelGGL((conv_pp_kernel<EP>), grid, dim3(512), 0, st, T, B, D, E, stats, bnb, g);
+}
+
+static void launch_pp(unsigned epi, dim3 grid, hipStream_t st, const bf16_t* T, const bf16_t* B, bf16_t* D,
+                      const bf16_t* E, float* stats, const BnBwd& bnb, const Geo& g) {
+  switch (pick_epi(epi)) {
+    case 0u: launch_pp1<0u>(grid, st, T, B, D, E, stats, bnb, g); break;
+    case kEpiStats: launch_pp1<kEpiStats>(grid, st, T, B, D, E, stats, bnb, g); break;
+    case kEpiE: launch_pp1<kEpiE>(grid, st, T, B, D, E, stats, bnb, g); break;
+    case kEpiE | kEpiEmb: launch_pp1<kEpiE | kEpiEmb>(grid, st, T, B, D, E, stats, bnb, g); break;
+    case kEpiStats | kEpiBnBwd: launch_pp1<kEpiStats | kEpiBnBwd>(grid, st, T, B, D, E, stats, bnb, g); break;
+    case kEpiE | kEpiStats | kEpiBnBwd:
+      launch_pp1<kEpiE | kEpiStats | kEpiBnBwd>(grid, st, T, B, D, E, stats, bnb, g);
+      break;
+    case kEpiE | kEpiEmb | kEpiStats | kEpiBnBwd:
+      launch_pp1<kEpiE | kEpiEmb | kEpiStats | kEpiBnBwd>(grid, st, T, B, D, E, stats, bnb, g);
+      break;
+    default: launch_pp1<kEpiAll>(grid, st, T, B, D, E, stats, bnb, g); break;
+  }
+}
+
+// variant: 0 = 128x128 tile, 1 = 128x64 tile (N <= 64), 2 = 256x256 tile (8 waves), 3 = 256x64 (N <= 64),
+// 4 = 256x256 ping-pong (conv_pp_kernel: C % 64 == 0, K > 0; one block per tile)
 KFA_API int kfa_conv_igemm(const bf16_t* T, const bf16_t* B, bf16_t* D, const bf16_t* E, int Nb, int H, int W, int C,
                            int P, int Q, int R, int S, int sa, int ra, int oa, int ob, int N, int OH, int OW, int os,
                            int oph, int opw, int ldd, int variant, float* stats, const bf16_t* bn_x,
@@ -796,7 +1074,9 @@ KFA_API int kfa_conv_igemm(const bf16_t* T, const bf16_t* B, bf16_t* D, const bf
   auto pgrid = [&](long tiles) { return (int)(tiles < slots ? tiles : slots); };
   const unsigned epi = (E ? kEpiE : 0u) | (stats ? kEpiStats : 0u) | (bn_x ? kEpiBnBwd : 0u) |
                        ((E && add_mb) ? kEpiEmb : 0u) | ((bn_x && bn_y && bn_relu) ? kEpiYMask : 0u);
-  if (variant == 3) {  // 256 x 64 tile (Cout <= 64): 4 waves of 64x64, 80 KB LDS -> 2 blocks / CU
+  if (variant == 4 && C % BK == 0 && g.K > 0) {  // ping-pong 256 x 256 (grid = tiles, one block per CU resident)
+    launch_pp(epi, dim3((unsigned)((long)kfa_ceil_div(g.M, 256) * kfa_ceil_div(N, 256))), st, T, B, D, E, stats, bnb, g);
+  } else if (variant == 3) {  // 256 x 64 tile (Cout <= 64): 4 waves of 64x64, 80 KB LDS -> 2 blocks / CU
     const int grid = pgrid((long)kfa_ceil_div(g.M, 256) * kfa_ceil_div(N, 64));
     launch_igemm<4, 1, 4, 4>(epi, dim3(grid), dim3(256), 2 * (256 + 64) * BK * 2, st, T, B, D, E, stats, bnb, g);
   } else if (variant == 1) {  // 128 x 64 tile (Cout <= 64): 4 waves of 32x64

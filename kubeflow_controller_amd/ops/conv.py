@@ -159,8 +159,51 @@ BIG_AUTO = os.environ.get("KFA_CONV_BIG_AUTO", "1") != "0"
 BIG_AUTO_E = os.environ.get("KFA_CONV_BIG_AUTO_E", "1") != "0"  # also for launches with an addend
 
 
+# Ping-pong 256x256 implicit GEMM (conv_pp_kernel, variant 4): "1" = every launch with
+# N >= PP_MIN_N, "0" = never, "auto" = per launch shape from the committed routing table
+# (ops/routes.py; timed at first use when the shape is not in it) vs the default tile.
+# Per ResNet-50 shape (profiles/r5_conv_pp_layers.md): 1.4x on the 14x14 3x3s and the
+# wide 1x1s, slower where 256x256 tiles leave CUs idle (7x7, N = 128).
+PP = os.environ.get("KFA_CONV_PP", "auto")
+PP_MIN_N = int(os.environ.get("KFA_CONV_PP_MIN_N", "256"))
+_IG_VARIANT, _IG_STATS = 23, 24  # argument positions in kfa_conv_igemm
+_pp_scratch: dict = {}
+
+
+def _igemm(args: list, stats_t=None, kind: str = "conv") -> None:
+    """One ``kfa_conv_igemm`` launch; with ``KFA_CONV_PP=auto`` the tile variant of this
+    launch shape (geometry + epilogue features) is the routed one: the default tile vs
+    the ping-pong kernel, from the table or timed once (statistics into a scratch
+    slot buffer, so the real BatchNorm slots only see the real launch)."""
+    N, K, C = args[16], args[10] * args[11] * args[7], args[7]
+    if PP == "auto" and N >= PP_MIN_N and K > 0 and C % 64 == 0:
+        from . import routes
+        flags = tuple(int(args[i] is not None) for i in (3, _IG_STATS, 25, 31))
+        key = tuple(args[4:23]) + flags
+        dev = stats_t.device if stats_t is not None else torch.device("cuda", torch.cuda.current_device())
+        sc = None
+        if stats_t is not None:
+            sc = _pp_scratch.get((stats_t.numel(), dev))
+            if sc is None:
+                sc = _pp_scratch[(stats_t.numel(), dev)] = torch.zeros_like(stats_t)
+
+        def run(v):
+            a = list(args)
+            a[_IG_VARIANT] = v
+            if sc is not None:
+                a[_IG_STATS] = _lib.ptr(sc)
+            return lambda: _lib.call("kfa_conv_igemm", *a)
+        i = routes.decide(kind, key, dev, [("igemm", run(args[_IG_VARIANT])), ("pp", run(4))])
+        if i == 1:
+            args = list(args)
+            args[_IG_VARIANT] = 4
+    _lib.call("kfa_conv_igemm", *args)
+
+
 def _variant(M: int, N: int, K: int = 0, addend: bool = False) -> int:
     """Tile shape of one implicit-GEMM launch: M output pixels x N channels, reduction K."""
+    if PP == "1" and N >= PP_MIN_N and K > 0:
+        return 4
     if N <= 64:
         return NARROW_LONGK if K >= 512 else NARROW
     if BIG and N % 256 == 0 and K >= BIG_MIN_K:
@@ -184,9 +227,9 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, stats=None
     Po = (H + 2 * pad - R) // stride + 1
     Qo = (W + 2 * pad - S) // stride + 1
     y = torch.empty((Nb, Co, Po, Qo), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
-    _lib.call("kfa_conv_igemm", _lib.ptr(x), _lib.ptr(w), _lib.ptr(y), None, Nb, H, W, C, Po, Qo, R, S, stride, 1,
-              -pad, -pad, Co, Po, Qo, 1, 0, 0, Co, _variant(Nb * Po * Qo, Co, R * S * C), _lib.ptr(stats), None, None,
-              None, 0, None, None, None, _lib.stream())
+    _igemm([_lib.ptr(x), _lib.ptr(w), _lib.ptr(y), None, Nb, H, W, C, Po, Qo, R, S, stride, 1,
+            -pad, -pad, Co, Po, Qo, 1, 0, 0, Co, _variant(Nb * Po * Qo, Co, R * S * C), _lib.ptr(stats), None, None,
+            None, 0, None, None, None, _lib.stream()], stats, "conv_fwd")
     return y
 
 
@@ -305,16 +348,18 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride: int, pad: int
         raise ValueError(f"conv_dgrad: addend mask of {EM.numel()} bytes for {dx.numel()} elements")
     st = _lib.stream()
     bn_args = (None, None, None, None, 0, None, None)
+    bn_ws = None
     if bn is not None:
         from .batchnorm import bn_slot_workspace
-        bn_args = (_lib.ptr(bn_slot_workspace(Ci, dy.device)), _lib.ptr(bn.x), _lib.ptr(bn.y), _lib.ptr(bn.mean),
+        bn_ws = bn_slot_workspace(Ci, dy.device)
+        bn_args = (_lib.ptr(bn_ws), _lib.ptr(bn.x), _lib.ptr(bn.y), _lib.ptr(bn.mean),
                    int(bn.relu), _lib.ptr(bn.ss), _lib.ptr(bn.mb))
         bn.prestats = True
     if stride == 1:
         wt = _transposed_weight(w, 0, 1, R, 0, 1, S)
-        _lib.call("kfa_conv_igemm", _lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), _lib.ptr(E), Nb, Po, Qo, Co, H, W, R, S,
-                  1, -1, pad, pad, Ci, H, W, 1, 0, 0, Ci, _variant(Nb * H * W, Ci, R * S * Co, E is not None), *bn_args,
-                  _lib.ptr(EM), st)
+        _igemm([_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), _lib.ptr(E), Nb, Po, Qo, Co, H, W, R, S,
+                1, -1, pad, pad, Ci, H, W, 1, 0, 0, Ci, _variant(Nb * H * W, Ci, R * S * Co, E is not None), *bn_args,
+                _lib.ptr(EM), st], bn_ws, "conv_dgrad")
         return dx
     # stride s: output parity classes.  For class (ph, pw) the rows h = s*i + ph
     # receive taps r with (ph + pad - r) % s == 0, from dY row i + (ph + pad - r)/s.
@@ -333,10 +378,10 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride: int, pad: int
             wt = _transposed_weight(w, r0, stride, Rs, s0, stride, Ss) if Rs * Ss else w
             oa_h = (ph + pad - r0) // stride
             oa_w = (pw + pad - s0) // stride
-            _lib.call("kfa_conv_igemm", _lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), _lib.ptr(E), Nb, Po, Qo, Co, Hc, Wc,
-                      Rs, Ss, 1, -1, oa_h, oa_w, Ci, H, W, stride, ph, pw, Ci,
-                      _variant(Nb * Hc * Wc, Ci, Rs * Ss * Co, E is not None),
-                      *bn_args, _lib.ptr(EM), st)
+            _igemm([_lib.ptr(dy), _lib.ptr(wt), _lib.ptr(dx), _lib.ptr(E), Nb, Po, Qo, Co, Hc, Wc,
+                    Rs, Ss, 1, -1, oa_h, oa_w, Ci, H, W, stride, ph, pw, Ci,
+                    _variant(Nb * Hc * Wc, Ci, Rs * Ss * Co, E is not None),
+                    *bn_args, _lib.ptr(EM), st], bn_ws, "conv_dgrad")
     return dx
 
 
@@ -506,9 +551,11 @@ def _use_bnpro(lz, x, w, stride, pad, stats) -> bool:
             _lib.call("kfa_bn_apply_ss", _lib.ptr(lz.x), _lib.ptr(yy), _lib.ptr(lz.ss), M, C, 1, _lib.stream())
             conv_fwd(yy, w, stride, pad, st)
 
-        t_sep = _time_ms(sep)
-        t_pro = _time_ms(lambda: conv_fwd_bnpro(lz.x, lz.ss, w, stride, pad, st, yy))
-        hit = _bnpro_choice[key] = _agree(t_pro < 0.98 * t_sep, x.device)
+        from . import routes  # committed table first, else timed (median of 3 x 30 launches)
+        i = routes.decide("bnpro", key, x.device,
+                          [("sep", sep), ("pro", lambda: conv_fwd_bnpro(lz.x, lz.ss, w, stride, pad, st, yy))],
+                          margin=0.98)
+        hit = _bnpro_choice[key] = i == 1
         del yy, st, Co
     return hit
 

@@ -73,16 +73,11 @@ def prefer_own(kind: str, key: tuple, device, run_own, run_lib) -> bool:
     hit = _choice.get(k)
     if hit is not None:
         return hit
-    if torch.cuda.is_current_stream_capturing():
-        return False
-    from .conv import _agree, _time_ms
-    with torch.no_grad():
-        t_own, t_lib = _time_ms(run_own), _time_ms(run_lib)
-    hit = _choice[k] = _agree(t_own < 0.97 * t_lib, device)
-    if TUNE_LOG:
-        import sys
-        print(f"[kfa gemm tune] {kind} {key}: own {t_own:.4f} ms, library {t_lib:.4f} ms -> "
-              f"{'own' if hit else 'library'}", file=sys.stderr, flush=True)
+    from . import routes  # committed per-arch table first, else timed (median of 3 x 30 launches)
+    i = routes.decide(kind, key, device, [("library", run_lib), ("own", run_own)], margin=0.97, log=TUNE_LOG)
+    if torch.cuda.is_current_stream_capturing() and i == 0:
+        return False  # not cached: decided for real outside the capture
+    hit = _choice[k] = i == 1
     return hit
 
 
@@ -289,41 +284,22 @@ def ppp_ok(a, b) -> bool:
     return gemm_ok(a, b) and a.shape[1] >= 128
 
 
-def _agree_int(v: int, device) -> int:
-    """Rank 0's choice among several kernels (see ``ops.conv._agree``)."""
-    import torch.distributed as dist
-    from . import conv as _c
-    if not _c._LOCKSTEP or not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
-        return v
-    dev = device if dist.get_backend() == "nccl" else torch.device("cpu")
-    t = torch.tensor([int(v)], dtype=torch.int32, device=dev)
-    dist.broadcast(t, 0)
-    return int(t.item())
-
-
 def pick_fastest(kind: str, key: tuple, device, candidates) -> int:
     """Index of the fastest of ``candidates`` (``[(name, fn), ...]``, index 0 =
-    the library form) for this shape, timed once at first use outside any graph
-    capture; rank 0's choice is applied on every rank.  An own kernel must beat
-    the library by 1 % to be picked (timing noise never flips a tie to it)."""
+    the library form) for this shape: the committed routing table's pick
+    (``ops/routes.py``), else timed once at first use outside any graph capture;
+    rank 0's choice is applied on every rank.  An own kernel must beat the library
+    by 1 % to be picked (timing noise never flips a tie to it)."""
     k = (kind,) + tuple(key)
     hit = _choice.get(k)
     if hit is not None:
         return hit
-    if torch.cuda.is_current_stream_capturing():
+    from . import routes  # committed per-arch table first, else timed (median of 3 x 30 launches)
+    i = routes.decide(kind, key, device, candidates, margin=1e9 if OWN_ONLY else 0.99, log=TUNE_LOG)
+    if torch.cuda.is_current_stream_capturing() and i == 0:
         return 0
-    from .conv import _time_ms
-    with torch.no_grad():
-        ts = [_time_ms(fn, reps=10) for _, fn in candidates]
-    best = min(range(1, len(ts)), key=lambda i: ts[i]) if len(ts) > 1 else 0
-    if best and not ts[best] < 0.99 * ts[0] and not OWN_ONLY:
-        best = 0
-    hit = _choice[k] = _agree_int(best, device)
-    if TUNE_LOG:
-        import sys
-        desc = ", ".join(f"{n} {t:.4f} ms" for (n, _), t in zip(candidates, ts))
-        print(f"[kfa gemm tune] {kind} {key}: {desc} -> {candidates[hit][0]}", file=sys.stderr, flush=True)
-    return hit
+    _choice[k] = i
+    return i
 
 
 def _ppp_candidates(a, b):

@@ -28,14 +28,21 @@ SHAPES = [
 ]
 
 
-@pytest.mark.parametrize("big", [False, True])
+@pytest.mark.parametrize("big", [False, True, "pp"])
 @pytest.mark.parametrize("N,Cin,H,W,Cout,k,stride,pad", SHAPES)
 def test_conv_igemm_fwd_dgrad(N, Cin, H, W, Cout, k, stride, pad, big, monkeypatch):
+    """fwd + dgrad (+ the wgrad) of the implicit GEMM vs fp32 PyTorch; big = the
+    8-wave 256x256 tile, "pp" = the ping-pong 256x256 kernel (conv_pp_kernel) on
+    every launch with >= 64 output channels (tails in M and N included)."""
     from kubeflow_controller_amd.ops import conv as convmod
     from kubeflow_controller_amd.ops.conv import conv2d
-    if big and not (Cout % 256 == 0 or Cin % 256 == 0):
+    if big is True and not (Cout % 256 == 0 or Cin % 256 == 0):
         pytest.skip("256x256 tiles only for 256-multiple channel counts")
-    monkeypatch.setattr(convmod, "BIG", big)
+    if big == "pp":
+        monkeypatch.setattr(convmod, "PP", "1")
+        monkeypatch.setattr(convmod, "PP_MIN_N", 64)
+    else:
+        monkeypatch.setattr(convmod, "BIG", big)
     torch.manual_seed(0)
     d = torch.device("cuda")
     x = torch.randn(N, Cin, H, W, device=d).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
@@ -200,15 +207,19 @@ def test_wgrad_direct_into_flat_buffer(vendor, monkeypatch):
     assert err < 3e-2 * wf.grad.abs().max().item(), err
 
 
+@pytest.mark.parametrize("pp", [False, True])
 @pytest.mark.parametrize("Cin,Cout,k,stride", [(64, 256, 1, 1), (128, 128, 3, 2), (64, 64, 3, 1), (256, 256, 3, 1)])
-def test_bn_stats_fused_into_conv_epilogue(Cin, Cout, k, stride, monkeypatch):
+def test_bn_stats_fused_into_conv_epilogue(Cin, Cout, k, stride, pp, monkeypatch):
     """conv(bn_stats=True) accumulates the BN statistics in its epilogue; the BN
     then skips its stats pass — same outputs / running stats as the unfused pair,
-    and the self-cleaning slot workspace is left zeroed."""
+    and the self-cleaning slot workspace is left zeroed (pp: the ping-pong kernel's epilogue)."""
     from kubeflow_controller_amd.ops import conv as convmod
     from kubeflow_controller_amd.ops.batchnorm import BatchNorm2dAct, bn_slot_workspace
     from kubeflow_controller_amd.ops.conv import Conv2d
     monkeypatch.setattr(convmod, "BIG", Cout % 256 == 0)  # the 256x256 tiles' epilogue too
+    if pp:
+        monkeypatch.setattr(convmod, "PP", "1")
+        monkeypatch.setattr(convmod, "PP_MIN_N", 64)
     d = torch.device("cuda")
     torch.manual_seed(0)
     conv = Conv2d(Cin, Cout, k, stride=stride, padding=k // 2).to(d)
@@ -228,14 +239,19 @@ def test_bn_stats_fused_into_conv_epilogue(Cin, Cout, k, stride, monkeypatch):
     assert bn_slot_workspace(Cout, d).abs().max().item() == 0
 
 
+@pytest.mark.parametrize("pp", [False, True])
 @pytest.mark.parametrize("C,Cout,k,stride", [(64, 64, 3, 1), (128, 128, 3, 2), (64, 256, 1, 1), (256, 256, 3, 1)])
-def test_bn_bwd_stats_fused_into_dgrad_epilogue(C, Cout, k, stride, monkeypatch):
+def test_bn_bwd_stats_fused_into_dgrad_epilogue(C, Cout, k, stride, pp, monkeypatch):
     """BN(+ReLU) -> conv: the conv's dgrad epilogue accumulates the BN's backward
-    statistics (BnBwdLink); gradients match the unfused pair and the slots end clean."""
+    statistics (BnBwdLink); gradients match the unfused pair and the slots end clean
+    (pp: the ping-pong kernel's dgrad epilogue)."""
     from kubeflow_controller_amd.ops import conv as convmod
     from kubeflow_controller_amd.ops.batchnorm import BatchNorm2dAct, bn_slot_workspace
     from kubeflow_controller_amd.ops.conv import Conv2d
     monkeypatch.setattr(convmod, "BIG", C % 256 == 0)
+    if pp:
+        monkeypatch.setattr(convmod, "PP", "1")
+        monkeypatch.setattr(convmod, "PP_MIN_N", 64)
     d = torch.device("cuda")
     torch.manual_seed(0)
     bn = BatchNorm2dAct(C).to(d)

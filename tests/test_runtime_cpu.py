@@ -65,3 +65,29 @@ def test_spec_model_dir_reaches_replicas():
     env = {e.name: e.value for e in lj.get_template().spec.containers[0].env}
     assert env["KFA_MODEL_DIR"] == "/m"
     assert checkpoint.latest("") is None
+
+
+def test_routes_table_lookup_dump_and_summary(tmp_path, monkeypatch):
+    """ops/routes.py: a committed table entry is applied by candidate NAME without
+    timing (no GPU needed), summary() names the table by hash and counts table vs
+    timed / own vs library picks, dump() writes a re-loadable table."""
+    import json
+    from kubeflow_controller_amd.ops import routes
+    tab = tmp_path / "routes_test.json"
+    tab.write_text(json.dumps({"arch": "gfx950", "routes": {"proj|32768,2304,768": "ppp256",
+                                                            "conv_fwd|1,2,3": "igemm"}}))
+    monkeypatch.setattr(routes, "TABLE_PATH", str(tab))
+    monkeypatch.setattr(routes, "MODE", "on")
+    monkeypatch.setattr(routes, "_table", None)
+    monkeypatch.setattr(routes, "_made", {})
+    boom = lambda: (_ for _ in ()).throw(AssertionError("timed a table hit"))  # noqa: E731
+    i = routes.decide("proj", (32768, 2304, 768), None, [("hipblaslt", boom), ("ppp192", boom), ("ppp256", boom)])
+    assert i == 2
+    assert routes.decide("conv_fwd", (1, 2, 3), None, [("igemm", boom), ("pp", boom)]) == 0
+    s = routes.summary()
+    assert s["from_table"] == 2 and s["timed"] == 0 and s["own"] == 2 and s["library"] == 0
+    assert s["table"] == "routes_test.json" and len(s["table_sha"]) == 12
+    out = tmp_path / "dumped.json"
+    routes.dump(str(out))
+    doc = json.loads(out.read_text())
+    assert doc["routes"] == {"conv_fwd|1,2,3": "igemm", "proj|32768,2304,768": "ppp256"}

@@ -58,6 +58,7 @@ def main(argv=None) -> int:
         metric = f"{args.model} training examples/sec (whole node)"
     engine = Engine(model, loss_fn, optimizer="adam", lr=args.lr, weight_decay=0.01, bucket_mb=args.bucket_mb,
                     dist_info=info, channels_last=False, ps=args.ps)
+    from kubeflow_controller_amd.ops import routes as _routes
     r = timed_steps(engine, batch, args.steps, args.warmup)
     ms = r["elapsed"] / args.steps * 1e3
     value = args.batch * info.world * args.steps / r["elapsed"]
@@ -68,7 +69,7 @@ def main(argv=None) -> int:
                "config": {"model": args.model, "global_batch": args.batch * info.world,
                           "seq_len": args.seq if args.model.startswith("bert") else None,
                           "parallelism": (f"{info.world}w+{args.ps}ps" if args.ps else f"dp{info.world}"),
-                          "loss": r["loss"]}}
+                          "routes": _routes.summary(), "loss": r["loss"]}}
         if flops:
             out["tflops_per_gpu"] = round(flops / (ms / 1e3) / 1e12, 1)
         print(json.dumps(out), flush=True)
