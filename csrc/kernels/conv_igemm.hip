@@ -1008,8 +1008,8 @@ static void launch_pp1(dim3 grid, hipStream_t st, const bf16_t* T, const bf16_t*
   hipLaunchKernelGGL((conv_pp_kernel<EP>), grid, dim3(512), 0, st, T, B, D, E, stats, bnb, g);
 }
 
-static void launch_pp(unsigned epi, dim3 grid, hipStream_t st, const bf16_t* T, const bf16_t* B, bf16_t* D,
-                      const bf16_t* E, float* stats, const BnBwd& bnb, const Geo& g) {
+static void launch_pp(unsigned epi, dim3 grid, hipStream_t st, const bf16_t* T, const bf16_t* B,
+                      bf16_t* D, const bf16_t* E, float* stats, const BnBwd& bnb, const Geo& g) {
   switch (pick_epi(epi)) {
     case 0u: launch_pp1<0u>(grid, st, T, B, D, E, stats, bnb, g); break;
     case kEpiStats: launch_pp1<kEpiStats>(grid, st, T, B, D, E, stats, bnb, g); break;
@@ -1075,7 +1075,8 @@ KFA_API int kfa_conv_igemm(const bf16_t* T, const bf16_t* B, bf16_t* D, const bf
   const unsigned epi = (E ? kEpiE : 0u) | (stats ? kEpiStats : 0u) | (bn_x ? kEpiBnBwd : 0u) |
                        ((E && add_mb) ? kEpiEmb : 0u) | ((bn_x && bn_y && bn_relu) ? kEpiYMask : 0u);
   if (variant == 4 && C % BK == 0 && g.K > 0) {  // ping-pong 256 x 256 (grid = tiles, one block per CU resident)
-    launch_pp(epi, dim3((unsigned)((long)kfa_ceil_div(g.M, 256) * kfa_ceil_div(N, 256))), st, T, B, D, E, stats, bnb, g);
+    launch_pp(epi, dim3((unsigned)((long)kfa_ceil_div(g.M, 256) * kfa_ceil_div(N, 256))), st, T, B, D, E, stats, bnb,
+              g);
   } else if (variant == 3) {  // 256 x 64 tile (Cout <= 64): 4 waves of 64x64, 80 KB LDS -> 2 blocks / CU
     const int grid = pgrid((long)kfa_ceil_div(g.M, 256) * kfa_ceil_div(N, 64));
     launch_igemm<4, 1, 4, 4>(epi, dim3(grid), dim3(256), 2 * (256 + 64) * BK * 2, st, T, B, D, E, stats, bnb, g);

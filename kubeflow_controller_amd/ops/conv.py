@@ -193,10 +193,11 @@ def _igemm(args: list, stats_t=None, kind: str = "conv") -> None:
             if sc is not None:
                 a[_IG_STATS] = _lib.ptr(sc)
             return lambda: _lib.call("kfa_conv_igemm", *a)
-        i = routes.decide(kind, key, dev, [("igemm", run(args[_IG_VARIANT])), ("pp", run(4))])
-        if i == 1:
+        cands = [("igemm", run(args[_IG_VARIANT]), args[_IG_VARIANT]), ("pp", run(4), 4)]
+        i = routes.decide(kind, key, dev, [(n, f) for n, f, _ in cands])
+        if i:
             args = list(args)
-            args[_IG_VARIANT] = 4
+            args[_IG_VARIANT] = cands[i][2]
     _lib.call("kfa_conv_igemm", *args)
 
 
