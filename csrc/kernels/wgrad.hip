@@ -348,6 +348,12 @@ __device__ __forceinline__ void wp_retire(int younger) {  // all but the pieces 
   else wp_vmcnt<0>();
 }
 
+// GATHER: X is the implicit im2col of an NHWC activation (3x3 / strided / padded
+// convs): an X column n is a fixed (r, s, ci) per lane and piece, its row a pixel k
+// whose (image, p, q) each lane carries per DMA row across k-tiles (the B0 / B1
+// pieces of one k-tile are issued back to back, then the rows advance 64 pixels);
+// taps outside the image and pixels past K read 0 through the buffer range check.
+template <bool GATHER>
 __global__ __launch_bounds__(512, 1) void wgrad_pp_kernel(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X,
                                                           float* __restrict__ part, void* __restrict__ grad,
                                                           int grad_f32, int accumulate, WGeo g) {
@@ -368,10 +374,14 @@ __global__ __launch_bounds__(512, 1) void wgrad_pp_kernel(const bf16_t* __restri
   const int nk = (ke - kb + WP_BK - 1) / WP_BK;
 
   const __amdgpu_buffer_rsrc_t rA = wrsrc(dY, (unsigned)g.K * (unsigned)g.Co * 2u);
-  const __amdgpu_buffer_rsrc_t rB = wrsrc(X, (unsigned)g.K * (unsigned)g.Ci * 2u);
+  const __amdgpu_buffer_rsrc_t rB = wrsrc(X, GATHER ? g.x_bytes : (unsigned)g.K * (unsigned)g.Ci * 2u);
   // DMA plan: instruction j (0, 1) of wave w fills piece rows 4 (2w + j) + lane / 16,
   // physical chunk lane & 15 <- logical chunk (lane & 15) ^ img_swz<128>(row)
   int voff[4][2];
+  // GATHER (Ci % 64 == 0, host-checked: a 64-channel group never straddles taps, so the
+  // B0 / B1 columns of a lane share (r, s) and differ by 32 channels):
+  int gx_rs[2], gx_ci[2];            // [j] tap (r - pad) << 16 | (s - pad) & 0xffff, channel of the lane's B0 column
+  int gk_img[2], gk_p[2], gk_q[2];   // [j] pixel of the lane's X row in the next k-tile
 #pragma unroll
   for (int j = 0; j < 2; j++) {
     const int row = 4 * (2 * wave + j) + (lane >> 4);
@@ -382,18 +392,53 @@ __global__ __launch_bounds__(512, 1) void wgrad_pp_kernel(const bf16_t* __restri
       voff[h ? 3 : 0][j] = m < g.Co ? (row * g.Co + m) * 2 : (int)kOOB;
       const int n = n0 + (c >> 5) * 64 + h * 32 + (c & 31);
       voff[h ? 2 : 1][j] = n < g.N ? (row * g.Ci + n) * 2 : (int)kOOB;
+      if (GATHER && h == 0) {
+        const int tap = n / g.Ci, r = tap / g.S, sx = tap - r * g.S;
+        gx_ci[j] = n - tap * g.Ci;
+        // past the last tap: r - pad = 0x4000, never in range (H < 2^14 host-checked)
+        gx_rs[j] = (int)((unsigned)(n < g.N ? r - g.pad : 0x4000) << 16) | ((sx - g.pad) & 0xffff);
+      }
+    }
+    if constexpr (GATHER) {
+      const int PQ = g.P * g.Q;
+      const int k = kb + row;
+      const int img = fdiv(k, PQ, 1.f / (float)PQ), rem = k - img * PQ;
+      gk_img[j] = img;
+      gk_p[j] = fdiv(rem, g.Q, 1.f / (float)g.Q);
+      gk_q[j] = rem - gk_p[j] * g.Q;
     }
   }
+  const int nimg = g.K / (g.P * g.Q);  // pixels past K belong to image nimg and beyond
+  const int dq = WP_BK % g.Q, dp = (WP_BK / g.Q) % g.P, dimg = WP_BK / (g.P * g.Q);  // 64 pixels in digits
   const int plast = 4 * nk - 7;  // last phase that issues a piece
   auto issue = [&](int P, auto pc, auto steady) __attribute__((always_inline)) {
     constexpr int p = decltype(pc)::value;
     const int kt = (P + 6) >> 2;
     if (decltype(steady)::value || kt < nk) {
       char* dst = smem + (kt & 1) * (4 * WP_PIECE) + p * WP_PIECE + wave * 2 * 1024;
-      const bool isA = p == 0 || p == 3;
-      const int soff = (kb + kt * WP_BK) * (isA ? g.Co : g.Ci) * 2;
-      buf_dma16<0>(isA ? rA : rB, reinterpret_cast<bf16_t*>(dst), voff[p][0], soff);
-      buf_dma16<0>(isA ? rA : rB, reinterpret_cast<bf16_t*>(dst + 1024), voff[p][1], soff);
+      constexpr bool isA = p == 0 || p == 3;
+      if constexpr (GATHER && !isA) {
+        constexpr int h = p == 2;
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+          const int hh = gk_p[j] * g.st + (gx_rs[j] >> 16), ww = gk_q[j] * g.st + (int)(short)(gx_rs[j] & 0xffff);
+          const bool ok = gk_img[j] < nimg && (unsigned)hh < (unsigned)g.H && (unsigned)ww < (unsigned)g.W;
+          const int vo = ok ? (((gk_img[j] * g.H + hh) * g.W + ww) * g.Ci + gx_ci[j] + h * 32) * 2 : (int)kOOB;
+          buf_dma16<0>(rB, reinterpret_cast<bf16_t*>(dst + j * 1024), vo, 0);
+          if constexpr (h == 1) {  // B1 closes this k-tile's X rows: advance them 64 pixels
+            int q = gk_q[j] + dq, pp = gk_p[j] + dp, img = gk_img[j] + dimg;
+            if (q >= g.Q) { q -= g.Q; pp++; }
+            if (pp >= g.P) { pp -= g.P; img++; }
+            gk_q[j] = q;
+            gk_p[j] = pp;
+            gk_img[j] = img;
+          }
+        }
+      } else {
+        const int soff = (kb + kt * WP_BK) * (isA ? g.Co : g.Ci) * 2;
+        buf_dma16<0>(isA ? rA : rB, reinterpret_cast<bf16_t*>(dst), voff[p][0], soff);
+        buf_dma16<0>(isA ? rA : rB, reinterpret_cast<bf16_t*>(dst + 1024), voff[p][1], soff);
+      }
     }
   };
   auto retire = [&](int P, auto steady) __attribute__((always_inline)) {
@@ -642,9 +687,22 @@ struct WPlan {
   int BM, BN, tiles, splits, kchunk, threads, blocks_per_cu;
 };
 
-// pointwise weights the ping-pong kernel takes (edge tiles masked, so any Co / N)
-static bool pp_shape(long K, int Co, int N, bool pointwise) {
-  if (!pointwise || !wgrad_pp_on()) return false;
+// KFA_WGRAD_PP_GATHER=0: gathered (3x3 / strided) big weights stay on the lockstep
+// 8-wave wgrad_kernel instead of wgrad_pp_kernel<true>
+static bool wgrad_pp_gather() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("KFA_WGRAD_PP_GATHER");
+    v = e ? atoi(e) : 1;
+  }
+  return v != 0;
+}
+
+// pointwise weights the ping-pong kernel takes (edge tiles masked, so any Co / N);
+// gathered ones (wgrad_pp_kernel<true>) where the lockstep kernel would take 256x256 tiles
+static bool pp_shape(long K, int Co, int N, bool pointwise, int Ci = 0, int H = 0, int W = 0) {
+  if (!wgrad_pp_on()) return false;
+  if (!pointwise) return wgrad_pp_gather() && Ci % 64 == 0 && Co % 256 == 0 && N % 256 == 0 && K >= 8192 && H < 16384 && W < 16384;
   // per-shape table (tools/bench_wgrad_pp.py, 1x MI355X): wins from 256 x 256 channels up (BERT dW -4..-9 %,
   // ResNet-50 1x1s at 50176 / 200704 pixels -2..-5 %); the 128-channel ResNet shapes lose 10-24 %
   return wgrad_pp_mode() == 2 ? (Co >= 128 && N >= 128) : (K >= 8192 && Co >= 256 && N >= 256);
@@ -731,10 +789,13 @@ KFA_API int kfa_conv_wgrad(const bf16_t* dY, const bf16_t* X, void* grad, int gr
     hipLaunchKernelGGL((wgrad_kernel<1, 4, 4, 4>), grid, dim3(256), lds, s, dY, X, pp, grad, grad_f32, accumulate,
                        zero_page(), g);
   }
-  else if (pp_shape(K, Co, g.N, pointwise)) {
+  else if (pp_shape(K, Co, g.N, pointwise, Ci, H, W)) {
     // pointwise, long reduction, big weight: ping-pong 256x256 (BERT-base dW: 2304x768 142 -> 129 us,
     // 3072x768 176 -> 168; the ResNet 1x1 shapes measured equal or slower: tools/bench_wgrad_pp.py)
-    hipLaunchKernelGGL(wgrad_pp_kernel, grid, dim3(512), 0, s, dY, X, pp, grad, grad_f32, accumulate, g);
+    if (pointwise)
+      hipLaunchKernelGGL(wgrad_pp_kernel<false>, grid, dim3(512), 0, s, dY, X, pp, grad, grad_f32, accumulate, g);
+    else
+      hipLaunchKernelGGL(wgrad_pp_kernel<true>, grid, dim3(512), 0, s, dY, X, pp, grad, grad_f32, accumulate, g);
   }
   else {
     static bool attr = false;  // 128 KiB of dynamic LDS

@@ -149,6 +149,38 @@ def test_wgrad_dense_shapes(rows, out_f, in_f):
     assert err < 2e-2 * ref.abs().max().item(), err
 
 
+@pytest.mark.parametrize("N,Cin,H,W,Cout,k,stride,pad", [
+    (8, 256, 32, 32, 256, 3, 1, 1),    # 14x14-stage-like 3x3: 8192 pixels, Co = 256, N = 2304
+    (5, 256, 33, 31, 512, 3, 2, 1),    # strided 3x3, odd sizes: a tail k-tile, taps off both edges
+    (24, 512, 14, 14, 512, 3, 2, 1),   # ResNet stage-4 entry shape, tail k-tile
+    (9, 512, 30, 30, 1024, 1, 2, 0),   # strided 1x1 (downsample): gathered, not pointwise
+    (2, 512, 64, 64, 256, 3, 1, 1),    # 18 weight tiles -> pixel split-K partials of the gathered kernel
+])
+def test_wgrad_gathered_pingpong(N, Cin, H, W, Cout, k, stride, pad):
+    """Gathered (3x3 / strided) big weight gradients on wgrad_pp_kernel<true> (Co % 256 == 0,
+    N % 256 == 0, >= 8192 pixels) vs the fp32 PyTorch weight gradient, fp32 accumulate
+    and bf16 overwrite."""
+    from kubeflow_controller_amd.ops.conv import wgrad_into
+    torch.manual_seed(1)
+    d = torch.device("cuda")
+    x = torch.randn(N, Cin, H, W, device=d).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    P_ = (H + 2 * pad - k) // stride + 1
+    Q_ = (W + 2 * pad - k) // stride + 1
+    dy = torch.randn(N, Cout, P_, Q_, device=d).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    ref = torch.ops.aten.convolution_backward(dy.float(), x.float(), torch.empty(Cout, Cin, k, k, device=d), None,
+                                              [stride, stride], [pad, pad], [1, 1], False, [0, 0], 1,
+                                              [False, True, False])[1]
+    ref = ref.permute(0, 2, 3, 1).contiguous()  # [Co][R][S][Ci]
+    out = torch.full((Cout, k, k, Cin), 0.25, device=d)
+    wgrad_into(x, dy, out, N, H, W, Cin, P_, Q_, Cout, k, k, stride, pad, accumulate=True)
+    err = (out - 0.25 - ref).abs().max().item()
+    assert err < 1e-2 * ref.abs().max().item(), err
+    outb = torch.zeros(Cout, k, k, Cin, device=d, dtype=torch.bfloat16)
+    wgrad_into(x, dy, outb, N, H, W, Cin, P_, Q_, Cout, k, k, stride, pad, accumulate=False)
+    err = (outb.float() - ref).abs().max().item()
+    assert err < 2e-2 * ref.abs().max().item(), err
+
+
 @pytest.mark.parametrize("wide", ["1", "0", "any"])
 def test_wgrad_co64_gathered_taps(wide, monkeypatch):
     """Co = 64 weight gradients (1x1, gathered 3x3 / strided taps; N = R*S*Ci a

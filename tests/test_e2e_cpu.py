@@ -380,3 +380,55 @@ def test_local_ordinal_of_ps_gpu(monkeypatch):
     monkeypatch.delenv("KFA_GPUS")
     monkeypatch.delenv("HIP_VISIBLE_DEVICES", raising=False)
     assert local_ordinal("4")[0] == 4
+
+
+@pytest.mark.parametrize("yml,nw,nps,owners", [("resnet50-2w1ps.yml", 2, 1, [0]),
+                                               ("wide-deep-8w4ps.yml", 8, 4, [0, 2, 4, 6])])
+def test_baseline_ps_layouts_bind_gpus_ranks_and_owners(tmp_path, yml, nw, nps, owners):
+    """The BASELINE PS layouts through the real controller + kubelet on an 8-GPU node
+    (replica commands swapped for a probe that parses its cluster spec exactly as
+    trainer/replica.py does): every worker gets ONE exclusive GPU (HIP_VISIBLE_DEVICES),
+    its collective rank is its task index, the PS replicas get no GPU, and the PS
+    tasks' variables live on worker ranks ps_owner_ranks(W, P) (co-located owners,
+    SURVEY §7.3 H1a)."""
+    st = ObjectStore()
+    n = Node(st, kubelet=True, root_dir=str(tmp_path), num_gpus=8, resync=30).start()
+    try:
+        job = serde.load_file(os.path.join(ROOT, "examples", "tfjob", yml), env=ENV)[0]
+        probe = textwrap.dedent("""
+            import os, sys
+            sys.path.insert(0, %r)
+            from kubeflow_controller_amd.trainer.cluster import add_cluster_flags, parse_cluster
+            from kubeflow_controller_amd.parallel.ps import ps_owner_ranks
+            import argparse
+            ap = argparse.ArgumentParser(); add_cluster_flags(ap)
+            a, _ = ap.parse_known_args()
+            s = parse_cluster(a)
+            env = s.torch_env()
+            print('PROBE', s.job_name, s.task_index, env['RANK'], env['WORLD_SIZE'],
+                  os.environ.get('HIP_VISIBLE_DEVICES', '-') or '-', len(s.ps),
+                  ','.join(map(str, ps_owner_ranks(s.num_workers, len(s.ps)))))
+        """ % ROOT)
+        for spec in job.spec.specs:
+            spec.template.spec.containers[0].command = [sys.executable, "-c", probe]
+        st.create(job)
+        wait_for_phase(st, "default", job.metadata.name, {"Succeeded"}, 90)
+        pods = st.list("Pod")
+        seen = {}
+        for p in pods:
+            line = [l for l in _logs(str(tmp_path), p).splitlines() if l.startswith("PROBE")][-1].split()
+            seen[(line[1], int(line[2]))] = (line[3], line[4], line[5], int(line[6]), line[7], p.status.gpus)
+        assert sorted(k for k in seen if k[0] == "worker") == [("worker", i) for i in range(nw)]
+        assert sorted(k for k in seen if k[0] == "ps") == [("ps", i) for i in range(nps)]
+        gpus = []
+        for i in range(nw):
+            rank, world, hip, ps_n, own, bound = seen[("worker", i)]
+            assert rank == str(i) and world == str(nw) and ps_n == nps
+            assert hip == str(bound[0]) and len(bound) == 1, (hip, bound)
+            assert own == ",".join(map(str, owners))
+            gpus.append(bound[0])
+        assert sorted(gpus) == list(range(nw))           # exclusive, all distinct
+        for i in range(nps):
+            assert seen[("ps", i)][2] == "-" and seen[("ps", i)][5] == []
+    finally:
+        n.shutdown()
