@@ -294,8 +294,9 @@ class AsyncPSClient(_ClientSteps):
                     off += n
 
     def push(self) -> int:
-        """Send every PS its gradient shard; returns the global step reported by PS 0."""
-        step = -1
+        """Send every PS its gradient shard (all shards first, then the replies, so the
+        PS tasks apply concurrently); returns the global step reported by PS 0."""
+        live = []
         for k, (rank, ps, buf) in enumerate(self.plan):
             if not ps:
                 continue
@@ -309,6 +310,9 @@ class AsyncPSClient(_ClientSteps):
                 off += n
             self._header(rank, PUSH, self.tags[k])
             dist.send(buf, rank, group=self.group, tag=TAG_DATA)
+            live.append((k, rank))
+        step = -1
+        for k, rank in live:
             s = self._await_reply(k, rank)
             if k == 0:
                 step = s
@@ -590,23 +594,35 @@ class DeviceAsyncPSClient(_ClientSteps):
 
     @torch.no_grad()
     def push(self) -> int:
-        step = -1
-        for k, (rank, groups, _, mail, stage) in enumerate(self.plan):
-            if not groups:
-                continue
+        """Every PS shard at once: all mailbox copies (peer D2D writes over xGMI) are
+        enqueued first and covered by ONE host wait per device, then every PS gets its
+        header, then the replies are collected — the PS tasks apply their shards
+        concurrently instead of one after another (round 4 did copy / wait / header /
+        reply per PS in turn)."""
+        live = [(k, rank, groups, mail, stage) for k, (rank, groups, _, mail, stage) in enumerate(self.plan) if groups]
+        devs = set()
+        for k, rank, groups, mail, stage in live:
             dst = stage if stage is not None else mail
             for g, start in groups:
                 dst[start:start + g.numel].copy_(g.grad)
             if stage is None:
-                # the mailbox is written before the header: host wait on the copies' events only
-                for d in {mail.device, groups[0][0].grad.device}:
-                    ev = self._ev.setdefault(d, torch.cuda.Event())
-                    ev.record(torch.cuda.current_stream(d))
-                    ev.synchronize()
+                devs |= {mail.device, groups[0][0].grad.device}
+        # the mailboxes are written before any header: one host wait on the copies' events
+        evs = []
+        for d in devs:
+            ev = self._ev.setdefault(d, torch.cuda.Event())
+            ev.record(torch.cuda.current_stream(d))
+            evs.append(ev)
+        for ev in evs:
+            ev.synchronize()
+        for k, rank, groups, mail, stage in live:
+            if stage is None:
                 self._header(rank, PUSH_DEV, self.tags[k])
             else:
                 self._header(rank, PUSH, self.tags[k])
                 dist.send(stage, rank, group=self.group, tag=TAG_DATA)
+        step = -1
+        for k, rank, *_ in live:
             s = self._await_reply(k, rank)
             if k == 0:
                 step = s
