@@ -646,6 +646,9 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
 // piece of a k-tile advances it, its A1 piece (issued three phases later, no
 // other A0 in between) reuses it.  Epilogue: conv_epilogue (LDS-staged 16-B
 // stores + fused addend / BN statistics), 4 staging passes per 128-row wave tile.
+#ifndef KFA_CONV_PP_NHALF
+#define KFA_CONV_PP_NHALF 4  // epilogue staging passes over the 128-row wave tile (8 KB of LDS per wave per pass at 2)
+#endif
 template <unsigned EPI>
 __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const bf16_t* __restrict__ T, const bf16_t* __restrict__ B,
                                                          bf16_t* __restrict__ D, const bf16_t* __restrict__ E,
@@ -852,7 +855,8 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const bf16_t* __restric
   if (!wr) asm volatile("s_barrier" ::: "memory");  // both groups at the same barrier count: the ring is idle
   const EpiRes er{rD, rsrc(E ? E : D, E ? g.d_bytes : 0u), rsrc(bnb.x ? bnb.x : D, bnb.x ? g.d_bytes : 0u),
                   rsrc(bnb.y ? bnb.y : D, bnb.y ? g.d_bytes : 0u)};
-  conv_epilogue<TM, TN, 4, EPI>(g, acc, smem + wave * (256 * 2 * TN) * 2, false, lane, m0 + wr * 128, n0 + wc * 64,
+  conv_epilogue<TM, TN, KFA_CONV_PP_NHALF, EPI>(g, acc, smem + wave * (256 * (TM / KFA_CONV_PP_NHALF) * TN) * 2, false,
+                                                lane, m0 + wr * 128, n0 + wc * 64,
                                 PQ, rPQ, rQ, lin_d, E, stats, bnb, er);
 }
 
