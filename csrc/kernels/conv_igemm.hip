@@ -649,24 +649,53 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
 #ifndef KFA_CONV_PP_NHALF
 #define KFA_CONV_PP_NHALF 4  // epilogue staging passes over the 128-row wave tile (8 KB of LDS per wave per pass at 2)
 #endif
-template <unsigned EPI>
+// WR wave-rows x WC = 8 / WR wave-columns of 128 x 64 wave tiles: WR = 2 is the
+// 256 x 256 tile above (one wave-row per group); WR = 4 the 512 x 128 tile of the
+// 128-channel layers (two wave-rows per group, 2 x 2 waves), the SAME wave tile and
+// phase schedule with A pieces of 256 rows (32 KB, 4 DMAs per lane) and B pieces of
+// 64 rows (8 KB, 1 DMA): 2 x 80 KB = the whole 160 KB of LDS, 104 FLOP per operand
+// byte (the 128 x 128 tile: 64).
+template <int WR>
+__device__ __forceinline__ void pp_vm_wait(int n) {  // s_waitcnt vmcnt(n), n in [0, 2*WR + 8/WR]
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+  }
+}
+
+template <unsigned EPI, int WR = 2>
 __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const bf16_t* __restrict__ T, const bf16_t* __restrict__ B,
                                                          bf16_t* __restrict__ D, const bf16_t* __restrict__ E,
                                                          float* __restrict__ stats, BnBwd bnb, Geo g) {
-  constexpr int TM = 8, TN = 4, PIECE = 128 * BK * 2;
-  __shared__ __attribute__((aligned(16))) char smem[2 * 4 * PIECE];  // 128 KB: two k-tile buffers
+  constexpr int TM = 8, TN = 4, WC = 8 / WR, MT = 128 * WR, NT = 64 * WC;
+  constexpr int AP = WR * 64 * 128, BP = WC * 32 * 128;  // A / B piece bytes (64-deep rows of 128 B)
+  constexpr int KTB = 2 * (AP + BP);                     // one k-tile buffer: [A0][B0][B1][A1]
+  constexpr int OFF[4] = {0, AP, AP + BP, AP + 2 * BP};
+  constexpr int NDMA[4] = {WR, WC / 2, WC / 2, WR};      // DMA instructions per lane of each piece
+  constexpr int STEADY = 2 * WR + WC;                    // DMAs of any four consecutive phases
+  __shared__ __attribute__((aligned(16))) char smem[2 * KTB];  // 128 KB (WR 2) / 160 KB (WR 4)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 2, wc = wave & 3;
+  const int wr = WR == 2 ? wave >> 2 : ((wave >> 2) << 1) | ((wave >> 1) & 1);  // group = wave >> 2
+  const int wc = wave & (WC - 1);
   // T1 XCD remap + grouped raster (as gemm_pp_kernel): the blocks of one XCD take
   // consecutive tiles, GM row panels wide
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int q8 = nwg >> 3, r8 = nwg & 7, x8 = bid & 7;
   const int wg = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + (bid >> 3);
-  const int ntn = (g.N + 255) / 256, ntm = (g.M + 255) / 256;
+  const int ntn = (g.N + NT - 1) / NT, ntm = (g.M + MT - 1) / MT;
   constexpr int GM = 4;
   const int grp = wg / (GM * ntn), gm0 = grp * GM, gmn = min(GM, ntm - gm0), rem = wg - grp * GM * ntn;
-  const int m0 = (gm0 + rem % gmn) * 256, n0 = (rem / gmn) * 256;
+  const int m0 = (gm0 + rem % gmn) * MT, n0 = (rem / gmn) * NT;
 
   const __amdgpu_buffer_rsrc_t rT = rsrc(T, g.t_bytes), rB = rsrc(B, g.b_bytes), rD = rsrc(D, g.d_bytes);
   const int PQ = g.P * g.Q;
@@ -674,15 +703,17 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const bf16_t* __restric
   const bool lin_a = g.R == 1 && g.S == 1 && g.sa == 1 && g.oa == 0 && g.ob == 0 && g.H == g.P && g.W == g.Q;
   const bool lin_d = g.os == 1 && g.oph == 0 && g.opw == 0 && g.OH == g.P && g.OW == g.Q;
   // DMA plan: instruction j of wave w fills piece rows j*64 + w*8 + lane/8,
-  // physical chunk lane&7 <- logical chunk (lane&7) ^ ((row >> 1) & 7)
+  // physical chunk lane&7 <- logical chunk (lane&7) ^ ((row >> 1) & 7).
+  // A piece h, instruction j: wave-row j's rows h*64 + [0, 64);  B piece h,
+  // instruction j: wave-columns 2j, 2j+1's columns h*32 + [0, 32).
   const int prow = wave * 8 + (lane >> 3);
   const int lc = (lane & 7) ^ ((prow >> 1) & 7);
-  int a_hb[2][2], a_wb[2][2], a_vo[2][2];  // [h: A0 / A1][j]
-  int b_vo[2][2];                          // [h: B0 / B1][j]
+  int a_hb[2][WR], a_wb[2][WR], a_vo[2][WR];  // [h: A0 / A1][j]
+  int b_vo[2][WC / 2];                        // [h: B0 / B1][j]
 #pragma unroll
-  for (int h = 0; h < 2; h++)
+  for (int h = 0; h < 2; h++) {
 #pragma unroll
-    for (int j = 0; j < 2; j++) {
+    for (int j = 0; j < WR; j++) {
       const int m = m0 + j * 128 + h * 64 + prow;
       if (m < g.M && lin_a) {
         a_hb[h][j] = 0;
@@ -699,9 +730,13 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const bf16_t* __restric
         a_wb[h][j] = 0;
         a_vo[h][j] = (int)kOOB;
       }
+    }
+#pragma unroll
+    for (int j = 0; j < WC / 2; j++) {
       const int n = n0 + (2 * j + (prow >> 5)) * 64 + h * 32 + (prow & 31);
       b_vo[h][j] = n < g.N ? (n * g.K + lc * 8) * 2 : (int)kOOB;
     }
+  }
   const int nk = g.K / BK;
   const int plast = 4 * nk - 7;  // last phase that issues a piece
   // tap walk of the A pieces (wave-uniform): next k-tile's (channel offset, r, s)
@@ -711,7 +746,7 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const bf16_t* __restric
     constexpr int p = decltype(pc)::value;
     const int kt = (P + 6) >> 2;
     if (decltype(steady)::value || kt < nk) {
-      char* dst = smem + (kt & 1) * (4 * PIECE) + p * PIECE + wave * 8 * 128;
+      char* dst = smem + (kt & 1) * KTB + OFF[p] + wave * 8 * 128;
       if constexpr (p == 0 || p == 3) {
         constexpr int h = p == 3;
         if constexpr (h == 0) {  // A0 of k-tile kt: advance the tap walk
@@ -726,7 +761,7 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const bf16_t* __restric
           }
         }
 #pragma unroll
-        for (int j = 0; j < 2; j++) {
+        for (int j = 0; j < WR; j++) {
           int vo = a_vo[h][j];
           if (!lin_a) {  // selects, no branch: the tap offset is one scalar add
             const int ih = a_hb[h][j] + ta_dh, iw = a_wb[h][j] + ta_dw;
@@ -737,22 +772,23 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const bf16_t* __restric
         }
       } else {
         constexpr int h = p == 2;
-        buf_dma16(rB, reinterpret_cast<bf16_t*>(dst), b_vo[h][0], kt * BK * 2);
-        buf_dma16(rB, reinterpret_cast<bf16_t*>(dst + 64 * 128), b_vo[h][1], kt * BK * 2);
+#pragma unroll
+        for (int j = 0; j < WC / 2; j++)
+          buf_dma16(rB, reinterpret_cast<bf16_t*>(dst + j * 64 * 128), b_vo[h][j], kt * BK * 2);
       }
     }
   };
   auto retire = [&](int P, auto steady) __attribute__((always_inline)) {
     if constexpr (decltype(steady)::value) {
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    } else {
-      const int younger = min(P, plast) - (P - 3) + 1;
-      const int y = younger < 0 ? 0 : younger;
-      if (y >= 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else if (y == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      else if (y == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else if (y == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      pp_vm_wait<WR>(STEADY);
+    } else {  // keep the pieces of phases [P - 3, min(P, plast)] in flight
+      int n = 0;
+#pragma unroll
+      for (int d = 0; d < 4; d++) {
+        const int q = P - d;
+        if (q <= plast) n += NDMA[(q + 2) & 3];  // phase q issues piece (q + 2) & 3
+      }
+      pp_vm_wait<WR>(n);
     }
   };
 
@@ -775,7 +811,7 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const bf16_t* __restric
   issue(-1, std::integral_constant<int, 1>{}, std::false_type{});
   retire(-1, std::false_type{});
   asm volatile("s_barrier" ::: "memory");
-  if (wr) asm volatile("s_barrier" ::: "memory");  // group 1 runs one barrier behind
+  if (wave >> 2) asm volatile("s_barrier" ::: "memory");  // group 1 runs one barrier behind
 
   auto mfma_q = [&](short8 (&bb)[2][2], int mh, int nh) __attribute__((always_inline)) {
     __builtin_amdgcn_s_setprio(1);
@@ -794,11 +830,11 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const bf16_t* __restric
   // one k-tile = four phases (st: std::true_type when every phase of k-tile u
   // issues a piece, i.e. u + 2 < nk)
   auto ktile = [&](int u, auto st) __attribute__((always_inline)) {
-    const char* buf = smem + (u & 1) * (4 * PIECE);
+    const char* buf = smem + (u & 1) * KTB;
     const int P = 4 * u;
     {  // s0: A0 + B0
-      const char* pa = buf + wr * 64 * 128;
-      const char* pb = buf + PIECE + wc * 32 * 128;
+      const char* pa = buf + OFF[0] + wr * 64 * 128;
+      const char* pb = buf + OFF[1] + wc * 32 * 128;
 #pragma unroll
       for (int ni = 0; ni < 2; ni++) {
         b0[ni][0] = rd(pb + ni * 16 * 128 + ro0);
@@ -816,7 +852,7 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const bf16_t* __restric
       asm volatile("s_barrier" ::: "memory");
     }
     {  // s1: B1
-      const char* pb = buf + 2 * PIECE + wc * 32 * 128;
+      const char* pb = buf + OFF[2] + wc * 32 * 128;
 #pragma unroll
       for (int ni = 0; ni < 2; ni++) {
         b1[ni][0] = rd(pb + ni * 16 * 128 + ro0);
@@ -829,7 +865,7 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const bf16_t* __restric
       asm volatile("s_barrier" ::: "memory");
     }
     {  // s2: A1
-      const char* pa = buf + 3 * PIECE + wr * 64 * 128;
+      const char* pa = buf + OFF[3] + wr * 64 * 128;
 #pragma unroll
       for (int mi = 0; mi < 4; mi++) {
         a[mi][0] = rd(pa + mi * 16 * 128 + ro0);
@@ -852,12 +888,12 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const bf16_t* __restric
   int u = 0;
   for (; u + 2 < nk; u++) ktile(u, std::true_type{});
   for (; u < nk; u++) ktile(u, std::false_type{});
-  if (!wr) asm volatile("s_barrier" ::: "memory");  // both groups at the same barrier count: the ring is idle
+  if (!(wave >> 2)) asm volatile("s_barrier" ::: "memory");  // both groups at the same barrier count: the ring is idle
   const EpiRes er{rD, rsrc(E ? E : D, E ? g.d_bytes : 0u), rsrc(bnb.x ? bnb.x : D, bnb.x ? g.d_bytes : 0u),
                   rsrc(bnb.y ? bnb.y : D, bnb.y ? g.d_bytes : 0u)};
   conv_epilogue<TM, TN, KFA_CONV_PP_NHALF, EPI>(g, acc, smem + wave * (256 * (TM / KFA_CONV_PP_NHALF) * TN) * 2, false,
-                                                lane, m0 + wr * 128, n0 + wc * 64,
-                                PQ, rPQ, rQ, lin_d, E, stats, bnb, er);
+                                                lane, m0 + wr * 128, n0 + wc * 64, PQ, rPQ, rQ, lin_d, E, stats, bnb,
+                                                er);
 }
 
 // zero-fill D rows of the output pixel mapping that the GEMM does not cover
@@ -1007,31 +1043,33 @@ static void launch_igemm_pro(unsigned epi, dim3 grid, dim3 block, int lds, hipSt
 }
 
 template <unsigned EP>
-static void launch_pp1(dim3 grid, hipStream_t st, const bf16_t* T, const bf16_t* B, bf16_t* D, const bf16_t* E,
-                       float* stats, const BnBwd& bnb, const Geo& g) {
-  hipLaunchKernelGGL((conv_pp_kernel<EP>), grid, dim3(512), 0, st, T, B, D, E, stats, bnb, g);
+static void launch_pp1(int wr, dim3 grid, hipStream_t st, const bf16_t* T, const bf16_t* B, bf16_t* D,
+                       const bf16_t* E, float* stats, const BnBwd& bnb, const Geo& g) {
+  if (wr == 4) hipLaunchKernelGGL((conv_pp_kernel<EP, 4>), grid, dim3(512), 0, st, T, B, D, E, stats, bnb, g);
+  else hipLaunchKernelGGL((conv_pp_kernel<EP, 2>), grid, dim3(512), 0, st, T, B, D, E, stats, bnb, g);
 }
 
-static void launch_pp(unsigned epi, dim3 grid, hipStream_t st, const bf16_t* T, const bf16_t* B,
+static void launch_pp(int wr, unsigned epi, dim3 grid, hipStream_t st, const bf16_t* T, const bf16_t* B,
                       bf16_t* D, const bf16_t* E, float* stats, const BnBwd& bnb, const Geo& g) {
   switch (pick_epi(epi)) {
-    case 0u: launch_pp1<0u>(grid, st, T, B, D, E, stats, bnb, g); break;
-    case kEpiStats: launch_pp1<kEpiStats>(grid, st, T, B, D, E, stats, bnb, g); break;
-    case kEpiE: launch_pp1<kEpiE>(grid, st, T, B, D, E, stats, bnb, g); break;
-    case kEpiE | kEpiEmb: launch_pp1<kEpiE | kEpiEmb>(grid, st, T, B, D, E, stats, bnb, g); break;
-    case kEpiStats | kEpiBnBwd: launch_pp1<kEpiStats | kEpiBnBwd>(grid, st, T, B, D, E, stats, bnb, g); break;
+    case 0u: launch_pp1<0u>(wr, grid, st, T, B, D, E, stats, bnb, g); break;
+    case kEpiStats: launch_pp1<kEpiStats>(wr, grid, st, T, B, D, E, stats, bnb, g); break;
+    case kEpiE: launch_pp1<kEpiE>(wr, grid, st, T, B, D, E, stats, bnb, g); break;
+    case kEpiE | kEpiEmb: launch_pp1<kEpiE | kEpiEmb>(wr, grid, st, T, B, D, E, stats, bnb, g); break;
+    case kEpiStats | kEpiBnBwd: launch_pp1<kEpiStats | kEpiBnBwd>(wr, grid, st, T, B, D, E, stats, bnb, g); break;
     case kEpiE | kEpiStats | kEpiBnBwd:
-      launch_pp1<kEpiE | kEpiStats | kEpiBnBwd>(grid, st, T, B, D, E, stats, bnb, g);
+      launch_pp1<kEpiE | kEpiStats | kEpiBnBwd>(wr, grid, st, T, B, D, E, stats, bnb, g);
       break;
     case kEpiE | kEpiEmb | kEpiStats | kEpiBnBwd:
-      launch_pp1<kEpiE | kEpiEmb | kEpiStats | kEpiBnBwd>(grid, st, T, B, D, E, stats, bnb, g);
+      launch_pp1<kEpiE | kEpiEmb | kEpiStats | kEpiBnBwd>(wr, grid, st, T, B, D, E, stats, bnb, g);
       break;
-    default: launch_pp1<kEpiAll>(grid, st, T, B, D, E, stats, bnb, g); break;
+    default: launch_pp1<kEpiAll>(wr, grid, st, T, B, D, E, stats, bnb, g); break;
   }
 }
 
 // variant: 0 = 128x128 tile, 1 = 128x64 tile (N <= 64), 2 = 256x256 tile (8 waves), 3 = 256x64 (N <= 64),
-// 4 = 256x256 ping-pong (conv_pp_kernel: C % 64 == 0, K > 0; one block per tile)
+// 4 = 256x256 ping-pong (conv_pp_kernel: C % 64 == 0, K > 0; one block per tile),
+// 6 = 512x128 ping-pong (conv_pp_kernel<.., 4>: the 128-channel layers, same conditions)
 KFA_API int kfa_conv_igemm(const bf16_t* T, const bf16_t* B, bf16_t* D, const bf16_t* E, int Nb, int H, int W, int C,
                            int P, int Q, int R, int S, int sa, int ra, int oa, int ob, int N, int OH, int OW, int os,
                            int oph, int opw, int ldd, int variant, float* stats, const bf16_t* bn_x,
@@ -1079,8 +1117,11 @@ KFA_API int kfa_conv_igemm(const bf16_t* T, const bf16_t* B, bf16_t* D, const bf
   const unsigned epi = (E ? kEpiE : 0u) | (stats ? kEpiStats : 0u) | (bn_x ? kEpiBnBwd : 0u) |
                        ((E && add_mb) ? kEpiEmb : 0u) | ((bn_x && bn_y && bn_relu) ? kEpiYMask : 0u);
   if (variant == 4 && C % BK == 0 && g.K > 0) {  // ping-pong 256 x 256 (grid = tiles, one block per CU resident)
-    launch_pp(epi, dim3((unsigned)((long)kfa_ceil_div(g.M, 256) * kfa_ceil_div(N, 256))), st, T, B, D, E, stats, bnb,
-              g);
+    launch_pp(2, epi, dim3((unsigned)((long)kfa_ceil_div(g.M, 256) * kfa_ceil_div(N, 256))), st, T, B, D, E, stats,
+              bnb, g);
+  } else if (variant == 6 && C % BK == 0 && g.K > 0) {  // ping-pong 512 x 128
+    launch_pp(4, epi, dim3((unsigned)((long)kfa_ceil_div(g.M, 512) * kfa_ceil_div(N, 128))), st, T, B, D, E, stats,
+              bnb, g);
   } else if (variant == 3) {  // 256 x 64 tile (Cout <= 64): 4 waves of 64x64, 80 KB LDS -> 2 blocks / CU
     const int grid = pgrid((long)kfa_ceil_div(g.M, 256) * kfa_ceil_div(N, 64));
     launch_igemm<4, 1, 4, 4>(epi, dim3(grid), dim3(256), 2 * (256 + 64) * BK * 2, st, T, B, D, E, stats, bnb, g);

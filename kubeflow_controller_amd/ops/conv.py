@@ -163,7 +163,8 @@ BIG_AUTO_E = os.environ.get("KFA_CONV_BIG_AUTO_E", "1") != "0"  # also for launc
 # N >= PP_MIN_N, "0" = never, "auto" = per launch shape from the committed routing table
 # (ops/routes.py; timed at first use when the shape is not in it) vs the default tile.
 # Per ResNet-50 shape (profiles/r5_conv_pp_layers.md): 1.4x on the 14x14 3x3s and the
-# wide 1x1s, slower where 256x256 tiles leave CUs idle (7x7, N = 128).
+# wide 1x1s, slower where 256x256 tiles leave CUs idle (7x7, N = 128).  "512": force the
+# 512x128 ping-pong tile (variant 6, the 128-channel layers) instead.
 PP = os.environ.get("KFA_CONV_PP", "auto")
 PP_MIN_N = int(os.environ.get("KFA_CONV_PP_MIN_N", "256"))
 _IG_VARIANT, _IG_STATS = 23, 24  # argument positions in kfa_conv_igemm
@@ -176,7 +177,7 @@ def _igemm(args: list, stats_t=None, kind: str = "conv") -> None:
     the ping-pong kernel, from the table or timed once (statistics into a scratch
     slot buffer, so the real BatchNorm slots only see the real launch)."""
     N, K, C = args[16], args[10] * args[11] * args[7], args[7]
-    if PP == "auto" and N >= PP_MIN_N and K > 0 and C % 64 == 0:
+    if PP == "auto" and N >= 64 and K > 0 and C % 64 == 0:
         from . import routes
         flags = tuple(int(args[i] is not None) for i in (3, _IG_STATS, 25, 31))
         key = tuple(args[4:23]) + flags
@@ -193,7 +194,12 @@ def _igemm(args: list, stats_t=None, kind: str = "conv") -> None:
             if sc is not None:
                 a[_IG_STATS] = _lib.ptr(sc)
             return lambda: _lib.call("kfa_conv_igemm", *a)
+        # every ping-pong form competes, even with part of its tile width empty: on the
+        # 64-channel 3x3s the 512x128 tile (half empty) still beats the 128x64 one by 10 %
+        # (profiles/r5_conv_pp_layers.md)
         cands = [("igemm", run(args[_IG_VARIANT]), args[_IG_VARIANT]), ("pp", run(4), 4)]
+        if N <= 512:  # 512 x 128 ping-pong: the 64 / 128-channel layers and narrow N <= 512 grids
+            cands.append(("pp512", run(6), 6))
         i = routes.decide(kind, key, dev, [(n, f) for n, f, _ in cands])
         if i:
             args = list(args)
@@ -203,8 +209,8 @@ def _igemm(args: list, stats_t=None, kind: str = "conv") -> None:
 
 def _variant(M: int, N: int, K: int = 0, addend: bool = False) -> int:
     """Tile shape of one implicit-GEMM launch: M output pixels x N channels, reduction K."""
-    if PP == "1" and N >= PP_MIN_N and K > 0:
-        return 4
+    if PP in ("1", "512") and N >= PP_MIN_N and K > 0:
+        return 4 if PP == "1" else 6
     if N <= 64:
         return NARROW_LONGK if K >= 512 else NARROW
     if BIG and N % 256 == 0 and K >= BIG_MIN_K:

@@ -28,18 +28,19 @@ SHAPES = [
 ]
 
 
-@pytest.mark.parametrize("big", [False, True, "pp"])
+@pytest.mark.parametrize("big", [False, True, "pp", "pp512"])
 @pytest.mark.parametrize("N,Cin,H,W,Cout,k,stride,pad", SHAPES)
 def test_conv_igemm_fwd_dgrad(N, Cin, H, W, Cout, k, stride, pad, big, monkeypatch):
     """fwd + dgrad (+ the wgrad) of the implicit GEMM vs fp32 PyTorch; big = the
     8-wave 256x256 tile, "pp" = the ping-pong 256x256 kernel (conv_pp_kernel) on
-    every launch with >= 64 output channels (tails in M and N included)."""
+    every launch with >= 64 output channels (tails in M and N included), "pp512" = its
+    512x128 form (two wave-rows per group)."""
     from kubeflow_controller_amd.ops import conv as convmod
     from kubeflow_controller_amd.ops.conv import conv2d
     if big is True and not (Cout % 256 == 0 or Cin % 256 == 0):
         pytest.skip("256x256 tiles only for 256-multiple channel counts")
-    if big == "pp":
-        monkeypatch.setattr(convmod, "PP", "1")
+    if big in ("pp", "pp512"):
+        monkeypatch.setattr(convmod, "PP", "1" if big == "pp" else "512")
         monkeypatch.setattr(convmod, "PP_MIN_N", 64)
     else:
         monkeypatch.setattr(convmod, "BIG", big)
@@ -239,7 +240,7 @@ def test_wgrad_direct_into_flat_buffer(vendor, monkeypatch):
     assert err < 3e-2 * wf.grad.abs().max().item(), err
 
 
-@pytest.mark.parametrize("pp", [False, True])
+@pytest.mark.parametrize("pp", [False, True, "512"])
 @pytest.mark.parametrize("Cin,Cout,k,stride", [(64, 256, 1, 1), (128, 128, 3, 2), (64, 64, 3, 1), (256, 256, 3, 1)])
 def test_bn_stats_fused_into_conv_epilogue(Cin, Cout, k, stride, pp, monkeypatch):
     """conv(bn_stats=True) accumulates the BN statistics in its epilogue; the BN
@@ -250,7 +251,7 @@ def test_bn_stats_fused_into_conv_epilogue(Cin, Cout, k, stride, pp, monkeypatch
     from kubeflow_controller_amd.ops.conv import Conv2d
     monkeypatch.setattr(convmod, "BIG", Cout % 256 == 0)  # the 256x256 tiles' epilogue too
     if pp:
-        monkeypatch.setattr(convmod, "PP", "1")
+        monkeypatch.setattr(convmod, "PP", "1" if pp is True else "512")
         monkeypatch.setattr(convmod, "PP_MIN_N", 64)
     d = torch.device("cuda")
     torch.manual_seed(0)
@@ -271,7 +272,7 @@ def test_bn_stats_fused_into_conv_epilogue(Cin, Cout, k, stride, pp, monkeypatch
     assert bn_slot_workspace(Cout, d).abs().max().item() == 0
 
 
-@pytest.mark.parametrize("pp", [False, True])
+@pytest.mark.parametrize("pp", [False, True, "512"])
 @pytest.mark.parametrize("C,Cout,k,stride", [(64, 64, 3, 1), (128, 128, 3, 2), (64, 256, 1, 1), (256, 256, 3, 1)])
 def test_bn_bwd_stats_fused_into_dgrad_epilogue(C, Cout, k, stride, pp, monkeypatch):
     """BN(+ReLU) -> conv: the conv's dgrad epilogue accumulates the BN's backward
@@ -282,7 +283,7 @@ def test_bn_bwd_stats_fused_into_dgrad_epilogue(C, Cout, k, stride, pp, monkeypa
     from kubeflow_controller_amd.ops.conv import Conv2d
     monkeypatch.setattr(convmod, "BIG", C % 256 == 0)
     if pp:
-        monkeypatch.setattr(convmod, "PP", "1")
+        monkeypatch.setattr(convmod, "PP", "1" if pp is True else "512")
         monkeypatch.setattr(convmod, "PP_MIN_N", 64)
     d = torch.device("cuda")
     torch.manual_seed(0)

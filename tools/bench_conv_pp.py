@@ -19,7 +19,7 @@ SH = [  # Cin, H, Cout, k, stride, pad, count in RN50
     (2048, 7, 512, 1, 1, 0, 2), (512, 7, 512, 3, 1, 1, 2),
 ]
 d = torch.device("cuda")
-VARS = [int(v) for v in os.environ.get("VARS", "-1,4").split(",")]
+VARS = [int(v) for v in os.environ.get("VARS", "-1,4,6").split(",")]
 
 
 def t(fn, it=20):
