@@ -336,10 +336,17 @@ class TorchComm:
 
 
 def comm_mode(device: torch.device) -> str:
+    """``KFA_COMM`` if set; else native on GPUs whose process group runs RCCL — a job
+    that forced gloo on GPUs (``KFA_DIST_BACKEND=gloo``: several ranks sharing one
+    GPU, which RCCL refuses) keeps torch.distributed — and torch (gloo) on the CPU."""
     m = os.environ.get("KFA_COMM", "").lower()
     if m in ("native", "torch"):
         return m
-    return "native" if device.type == "cuda" else "torch"
+    if device.type != "cuda":
+        return "torch"
+    if dist.is_initialized() and dist.get_backend() != "nccl":
+        return "torch"
+    return "native"
 
 
 def default_store():

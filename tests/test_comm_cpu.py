@@ -196,3 +196,22 @@ def test_engine_native_comm_matches_gloo_training(tmp_path):
             assert a[ps]["comm"].startswith("Communicator(host") and b[ps]["comm"].startswith("TorchComm")
             for x, y in zip(a[ps]["params"], b[ps]["params"]):
                 torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-6)
+
+
+def test_comm_mode_selection(monkeypatch):
+    """native only on GPUs with an RCCL process group (a gloo-on-GPU rehearsal keeps
+    torch.distributed: RCCL refuses two ranks on one device); KFA_COMM overrides."""
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    from kubeflow_controller_amd.parallel import comm as C
+    monkeypatch.delenv("KFA_COMM", raising=False)
+    assert C.comm_mode(torch.device("cpu")) == "torch"
+    monkeypatch.setattr(dist, "is_initialized", lambda: True)
+    monkeypatch.setattr(dist, "get_backend", lambda *a: "gloo")
+    assert C.comm_mode(torch.device("cuda", 0)) == "torch"
+    monkeypatch.setattr(dist, "get_backend", lambda *a: "nccl")
+    assert C.comm_mode(torch.device("cuda", 0)) == "native"
+    monkeypatch.setenv("KFA_COMM", "torch")
+    assert C.comm_mode(torch.device("cuda", 0)) == "torch"
+    monkeypatch.setenv("KFA_COMM", "native")
+    assert C.comm_mode(torch.device("cpu")) == "native"
