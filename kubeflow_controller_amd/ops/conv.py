@@ -200,6 +200,8 @@ def _igemm(args: list, stats_t=None, kind: str = "conv") -> None:
         cands = [("igemm", run(args[_IG_VARIANT]), args[_IG_VARIANT]), ("pp", run(4), 4)]
         if N <= 512:  # 512 x 128 ping-pong: the 64 / 128-channel layers and narrow N <= 512 grids
             cands.append(("pp512", run(6), 6))
+        if args[_IG_VARIANT] == 2:  # the static rule chose the 8-wave 256x256 tile: the 128x128 one competes too
+            cands.append(("igemm128", run(0), 0))
         i = routes.decide(kind, key, dev, [(n, f) for n, f, _ in cands])
         if i:
             args = list(args)
