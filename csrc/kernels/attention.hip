@@ -193,10 +193,53 @@ __device__ __forceinline__ short8 pack_pair(floatx4 x, floatx4 y) {
   return *reinterpret_cast<const short8*>(&u);
 }
 
+// Dropout of the attention probabilities (every kernel of this file): ONE 32-bit
+// counter hash per PAIR of scores (q, k) and (q, k + 16), k with bit 4 clear, whose
+// 16-bit halves decide the two keeps: keep iff half >= t16 = round(p·2^16) (drop
+// probability t16 / 2^16, kept values scaled by 2^16 / (2^16 − t16)).  Every lane
+// layout below holds both keys of a pair in one lane (key tiles kt and kt + 1 of 16),
+// so a pair costs one hash — half the quarter-rate v_mul_lo_u32 work of a per-score
+// hash, which was ~40 % of the forward's VALU cycles.
+__device__ __forceinline__ uint32_t attn_pair_hash(uint64_t seed, uint64_t row, int S, int key_lo) {
+  return drop_hash(seed, row * (uint64_t)S + (uint64_t)key_lo);
+}
+// S = 128: the index row·128 + key never carries across a 2^32 boundary, so
+// drop_hash's 64-bit index splits into lo = (row << 7) ^ key and hi = row >> 25 —
+// per row (lane) once; a pair is then one xor-add plus the 32-bit finaliser.
+struct RowKey {
+  uint32_t a, b;
+};
+__device__ __forceinline__ RowKey row_key128(uint64_t seed, uint64_t row) {
+  return RowKey{(uint32_t)(row << 7) ^ (uint32_t)seed, (uint32_t)(seed >> 32) + __umul24((uint32_t)(row >> 25), 0x9E3779u)};
+}
+__device__ __forceinline__ uint32_t pair_hash128(RowKey k, uint32_t key_lo) {
+  uint32_t x = (k.a ^ key_lo) + k.b;  // == drop_hash(seed, row·128 + key_lo)
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ bool keep_lo(uint32_t h, uint32_t t16) { return (h & 0xffffu) >= t16; }
+__device__ __forceinline__ bool keep_hi(uint32_t h, uint32_t t16) { return (h >> 16) >= t16; }
+
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+
+// Packed keep mask (S = 128): word [bh][c][q] (c = (key >> 2) & 3) holds bit
+// (key >> 4)·4 + (key & 3) for the 32 keys with that c — exactly the 32 keys one
+// forward lane (fq = c) owns for query q, so the forward stores one dword per lane
+// and query, and a backward lane reads its 4 consecutive queries as one 16-B chunk.
+// 2 KiB per head (6 MiB per BERT-base layer at 256 x 128): the backward reads bits
+// instead of re-hashing every score.
+//
+// DROP: 0 no dropout, 1 pair hash, 2 pair hash + write the packed mask.
+template <int DROP>
 __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(const bf16_t* __restrict__ qkv, const float* __restrict__ bqkv,
                                                           const float* __restrict__ kbias, bf16_t* __restrict__ out,
-                                                          float* __restrict__ lse, int heads, float qscale,
-                                                          uint32_t thresh, float dscale, uint64_t seed) {
+                                                          float* __restrict__ lse, uint32_t* __restrict__ mask, int heads,
+                                                          float qscale, uint32_t thresh, float dscale, uint64_t seed) {
   // Q, K, V images only (48 KiB: three workgroups per CU): the probabilities
   // feed P·V straight from registers and O is staged in the Q image afterwards
   __shared__ __attribute__((aligned(16))) char sm[3 * 16384];
@@ -210,7 +253,9 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(const bf16_t* __restri
   const int col[3] = {h * AD, H + h * AD, 2 * H + h * AD};
   const bool ub[3] = {true, true, true};
   const bool tf[3] = {true, true, true};
-  const float sc[3] = {qscale, 1.f, 1.f};
+  // scores in log2 units: q is scaled by log2(e)/sqrt(d) and the key mask by log2(e),
+  // so the softmax exponent is one subtraction + v_exp_f32 per score
+  const float sc[3] = {qscale * kLog2e, 1.f, 1.f};
   char* const img[3] = {Qi, Ki, Vi};
   const bf16_t* const src[3] = {qkv, qkv, qkv};
   const long ld[3] = {3L * H, 3L * H, 3L * H};
@@ -219,6 +264,10 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(const bf16_t* __restri
   float kb[8][4];
   load_key_bias(kbias, row0, fq, kb);
   images_commit<3>(L, tf, sc, img, tid);
+#pragma unroll
+  for (int kt = 0; kt < 8; kt++)
+#pragma unroll
+    for (int r = 0; r < 4; r++) kb[kt][r] *= kLog2e;
   __syncthreads();
 
   floatx4 s[8][2];
@@ -241,23 +290,36 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(const bf16_t* __restri
     for (int kt = 0; kt < 8; kt++)
 #pragma unroll
       for (int r = 0; r < 4; r++) {
-        const float e = __expf(s[kt][qt][r] - mx);
+        const float e = __builtin_amdgcn_exp2f(s[kt][qt][r] - mx);
         s[kt][qt][r] = e;
         sum += e;
       }
     sum += __shfl_xor(sum, 16, 64);
     sum += __shfl_xor(sum, 32, 64);
-    if (fq == 0) lse[(long)bh * AS + q] = mx + __logf(sum);
+    if (fq == 0) lse[(long)bh * AS + q] = (mx + __log2f(sum)) * kLn2;  // natural-log units
     const float inv = 1.f / sum;
+    if constexpr (DROP == 0) {
 #pragma unroll
-    for (int kt = 0; kt < 8; kt++)
+      for (int kt = 0; kt < 8; kt++)
 #pragma unroll
-      for (int r = 0; r < 4; r++) {
-        float v = s[kt][qt][r] * inv;
-        if (thresh)
-          v = drop_hash(seed, ((uint64_t)bh * AS + q) * AS + kt * 16 + 4 * fq + r) >= thresh ? v * dscale : 0.f;
-        s[kt][qt][r] = v;
-      }
+        for (int r = 0; r < 4; r++) s[kt][qt][r] *= inv;
+    } else {
+      const float invd = inv * dscale;
+      RowKey rk = row_key128(seed, (uint64_t)bh * AS + q);
+      rk.a ^= 4 * fq;  // this lane's keys 32kp + 4fq + r: the fq bits are disjoint from 32kp + r
+      uint32_t bits = 0;
+#pragma unroll
+      for (int kp = 0; kp < 4; kp++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const uint32_t hh = pair_hash128(rk, 32 * kp + r);
+          const bool k0 = keep_lo(hh, thresh), k1 = keep_hi(hh, thresh);
+          s[2 * kp][qt][r] = k0 ? s[2 * kp][qt][r] * invd : 0.f;
+          s[2 * kp + 1][qt][r] = k1 ? s[2 * kp + 1][qt][r] * invd : 0.f;
+          if constexpr (DROP == 2) bits |= ((uint32_t)k0 << (8 * kp + r)) | ((uint32_t)k1 << (8 * kp + 4 + r));
+        }
+      if constexpr (DROP == 2) mask[((long)bh * 4 + fq) * AS + q] = bits;
+    }
   }
 
   // Oᵀ[d][q] = Σ_key V[key][d] · Pd[q][key]:  o[dt][qt][r] = O(q = qb + 16qt + fr, d = 16dt + 4fq + r).
@@ -306,27 +368,36 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(const bf16_t* __restri
 // through LDS (as dSᵀ [key][q]) for dQᵀ = Kᵀ·dSᵀ, computed after one barrier
 // by wave w for its queries 32w...  LDS = Q, K, dO images + dSᵀ = 80 KiB:
 // two workgroups per CU, so one loads while the other multiplies.
-// LDSD: D = rowsum(dO∘O) exchanged through the (not yet used) dSᵀ image instead of
-// a global scratch row — no vmcnt(0) + memory round trip before phase A.
-template <bool LDSD>
+//
+// Per-query operands through the not-yet-written part of dSᵀ: step j's dS lands in
+// the query columns 32j..32j+31 of the wave's own 32 key rows, so before phase A
+// each wave parks, in THOSE columns of its rows kw..kw+11, what step j will read:
+// D and lse·log2(e) of the step's 32 queries (rows kw..kw+3) and, with a forward
+// mask (DROP 2), the step's keep-mask words (rows kw+4..kw+11).  A step reads its
+// block (one ds_read_b128 per 4 queries) before it overwrites it with dS — the
+// reads replace 64 ds_bpermute lane shuffles and 64 per-score hashes per lane.
+// DROP: 0 no dropout, 1 pair hash (no mask), 2 packed mask from the forward (parked
+// in LDS), 3 packed mask read from memory per step (one step ahead).
+template <int DROP>
 __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(const bf16_t* __restrict__ qkv, const float* __restrict__ bqkv,
                                                           const float* __restrict__ kbias, const bf16_t* __restrict__ out,
                                                           const float* __restrict__ lse, const bf16_t* __restrict__ dout,
                                                           bf16_t* __restrict__ dqkv, float* __restrict__ dbqkv,
-                                                          float* __restrict__ dwork, int heads, float qscale,
+                                                          const uint32_t* __restrict__ mask, int heads, float qscale,
                                                           uint32_t thresh, float dscale, uint64_t seed) {
   __shared__ __attribute__((aligned(16))) char sm[3 * 16384 + 32768];  // 80 KiB
   char* Qi = sm;            // [128 q][64]      q·scale (+ bias)
   char* Ki = sm + 16384;    // [128 key][64]    k (+ bias)
   char* Gi = sm + 32768;    // [128 q][64]      dO
   char* dST = sm + 49152;   // [128 key][128 q] dL/dS, transposed
+  float* Dx = reinterpret_cast<float*>(dST + 12 * 256);  // D exchange: rows 12-13 (no parked block there)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
   const int bh = blockIdx.x, b = bh / heads, h = bh - b * heads, H = heads * AD;
   const long row0 = (long)b * AS, W3 = 3L * H;
   const int kw = wave * 32;
   // every global load up front, in consumption order: biases, Q / K / dO image
   // rows, this lane's V operand pieces V[kw + 16kt + fr][32ks + 8fq ..] (+ bias),
-  // the O rows 2·lane, 2·lane + 1 (for D) and their lse
+  // the O half-row for D, the lse / mask chunks this lane parks
   const int icol[3] = {h * AD, H + h * AD, h * AD};
   const bool iub[3] = {true, true, false};
   const bool itf[3] = {true, true, false};
@@ -345,9 +416,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(const bf16_t* __restri
     vb[ks][4] = b1.x; vb[ks][5] = b1.y; vb[ks][6] = b1.z; vb[ks][7] = b1.w;
   }
   // D = rowsum(dO∘O) is formed ONCE per workgroup: wave w takes queries 32w..32w+31,
-  // a lane half a row (32 d), the pair combines with one shuffle and D goes through
-  // a global scratch row of this head (every wave then reads all 128) — each wave
-  // used to load all 128 O rows itself (64 KiB of O per workgroup instead of 16)
+  // a lane half a row (32 d), the pair combines with one shuffle
   uint4 vraw[2][2], oraw[4];
 #pragma unroll
   for (int kt = 0; kt < 2; kt++)
@@ -358,10 +427,29 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(const bf16_t* __restri
   const int dq = wave * 32 + (lane >> 1), dh = (lane & 1) * 32;  // this lane's D row and half
 #pragma unroll
   for (int c = 0; c < 4; c++) oraw[c] = *reinterpret_cast<const uint4*>(out + (row0 + dq) * H + h * AD + dh + c * 8);
-  const float2 lse2 = *reinterpret_cast<const float2*>(lse + (long)bh * AS + 2 * lane);
+  // parked D / lse chunk of this lane: step cj, kind cw (0 D, 1 lse), queries cq..cq+3
+  const int cj = lane >> 4, cw = (lane >> 3) & 1, cqt = (lane >> 2) & 1, cf = lane & 3;
+  const int cq = 32 * cj + 16 * cqt + 4 * cf;
+  const float4 lse4 = *reinterpret_cast<const float4*>(lse + (long)bh * AS + cq);
+  // parked mask chunks: ids lane, lane + 64 -> (step, c, qt, f): words [bh][c][32 step + 16 qt + 4 f ..]
+  uint4 mraw[2];
+  if constexpr (DROP == 2) {
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+      const int id = lane + 64 * t, mj = id >> 5, mc = (id >> 3) & 3, mqt = (id >> 2) & 1, mf = id & 3;
+      mraw[t] = *reinterpret_cast<const uint4*>(mask + ((long)bh * 4 + mc) * AS + 32 * mj + 16 * mqt + 4 * mf);
+    }
+  }
+  // DROP 3: this lane's mask words straight from memory, one step ahead
+  const uint32_t* const mlane = mask + ((long)bh * 4 + ((fr >> 2) & 3)) * AS + 4 * fq;
+  uint4 mg[2] = {};
+  if constexpr (DROP == 3) {
+#pragma unroll
+    for (int qt = 0; qt < 2; qt++) mg[qt] = *reinterpret_cast<const uint4*>(mlane + 16 * qt);
+  }
   float kbv[2];
 #pragma unroll
-  for (int kt = 0; kt < 2; kt++) kbv[kt] = kbias[row0 + kw + kt * 16 + fr];
+  for (int kt = 0; kt < 2; kt++) kbv[kt] = kbias[row0 + kw + kt * 16 + fr] * kLog2e;
   images_commit<3>(L, itf, isc, iimg, tid);
   short8 vreg[2][2];
 #pragma unroll
@@ -377,8 +465,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(const bf16_t* __restri
     }
   __syncthreads();
 
-  // D[q] = Σ_d dO[q][d]·O[q][d]: this wave's 32 queries -> the head's scratch row,
-  // then every wave keeps q = 2·lane, 2·lane + 1
+  // D[q] = Σ_d dO[q][d]·O[q][d]: this wave's 32 queries -> the exchange row
   {
     float acc = 0.f;
 #pragma unroll
@@ -390,32 +477,49 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(const bf16_t* __restri
       for (int e = 0; e < 8; e++) acc += g[e] * o[e];
     }
     acc += __shfl_xor(acc, 1, 64);
-    if (!(lane & 1)) {
-      if constexpr (LDSD) reinterpret_cast<float*>(dST)[dq] = acc;
-      else dwork[(long)bh * AS + dq] = acc;
+    if (!(lane & 1)) Dx[dq] = acc;
+  }
+  if constexpr (DROP == 2) {
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+      const int id = lane + 64 * t, mj = id >> 5, mc = (id >> 3) & 3, mqt = (id >> 2) & 1, mf = id & 3;
+      *reinterpret_cast<uint4*>(dST + off128(kw + 4 + 2 * mc + mqt, 32 * mj + 8 * mf)) = mraw[t];
     }
   }
-  if constexpr (!LDSD) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  float dd[2];
   {
-    const float2 d2 = LDSD ? *reinterpret_cast<const float2*>(reinterpret_cast<const float*>(dST) + 2 * lane)
-                           : *reinterpret_cast<const float2*>(dwork + (long)bh * AS + 2 * lane);
-    dd[0] = d2.x;
-    dd[1] = d2.y;
+    const float4 d4 = *reinterpret_cast<const float4*>(Dx + cq);
+    const float4 v = cw ? make_float4(lse4.x * kLog2e, lse4.y * kLog2e, lse4.z * kLog2e, lse4.w * kLog2e) : d4;
+    *reinterpret_cast<float4*>(dST + off128(kw + 2 * cw + cqt, 32 * cj + 8 * cf)) = v;
   }
-  if constexpr (LDSD) __syncthreads();  // every wave has its D before phase A writes dSᵀ
+  __syncthreads();  // every wave has read the D exchange row before phase A writes dSᵀ over it
   short8 kreg[2][2];
 #pragma unroll
   for (int kt = 0; kt < 2; kt++)
 #pragma unroll
     for (int ks = 0; ks < 2; ks++) kreg[kt][ks] = rd_row<64>(Ki, kw + kt * 16 + fr, ks * 32 + fq * 8);
+  const int mbit = 8 * wave + (fr & 3), mrow = kw + 4 + 2 * ((fr >> 2) & 3);  // mask bit of key tile 0 / parked row
+  const int dsbits = __float_as_int(dscale);
 
   // ---- phase A: 4 steps of 32 queries; dvT / dkT[dt][kt][r] = dV / dK(key = kw + 16kt + fr, d = 16dt + 4fq + r)
   floatx4 dvT[4][2], dkT[4][2];
 #pragma unroll
   for (int dt = 0; dt < 4; dt++) dvT[dt][0] = dvT[dt][1] = dkT[dt][0] = dkT[dt][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
   for (int j = 0; j < 4; j++) {
+    // this step's parked operands (read before the step's dS overwrites them)
+    float4 Dv[2], Lv[2];
+    uint4 mw[2] = {};
+#pragma unroll
+    for (int qt = 0; qt < 2; qt++) {
+      Dv[qt] = *reinterpret_cast<const float4*>(dST + off128(kw + qt, 32 * j + 8 * fq));
+      Lv[qt] = *reinterpret_cast<const float4*>(dST + off128(kw + 2 + qt, 32 * j + 8 * fq));
+      if constexpr (DROP == 2) mw[qt] = *reinterpret_cast<const uint4*>(dST + off128(mrow + qt, 32 * j + 8 * fq));
+      if constexpr (DROP == 3) {
+        mw[qt] = mg[qt];
+        if (j < 3) mg[qt] = *reinterpret_cast<const uint4*>(mlane + 32 * (j + 1) + 16 * qt);
+      }
+    }
     // s / dp[qt][kt][r]: (q = 32j + 16qt + 4fq + r, key = kw + 16kt + fr)
     floatx4 s[2][2], dp[2][2];
 #pragma unroll
@@ -435,23 +539,28 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(const bf16_t* __restri
     floatx4 pd[2][2], ds[2][2];
 #pragma unroll
     for (int qt = 0; qt < 2; qt++) {
-      const int qb4 = 32 * j + 16 * qt + 4 * fq;
+      const float Dr[4] = {Dv[qt].x, Dv[qt].y, Dv[qt].z, Dv[qt].w};
+      const float Lr[4] = {Lv[qt].x, Lv[qt].y, Lv[qt].z, Lv[qt].w};
+      const uint32_t Mr[4] = {mw[qt].x, mw[qt].y, mw[qt].z, mw[qt].w};
 #pragma unroll
       for (int r = 0; r < 4; r++) {
-        const float Dq = __shfl(dd[r & 1], (qb4 + r) >> 1, 64);
-        const float lq = __shfl(r & 1 ? lse2.y : lse2.x, (qb4 + r) >> 1, 64);
+        uint32_t hh = 0;
+        if constexpr (DROP == 1)
+          hh = pair_hash128(row_key128(seed, (uint64_t)bh * AS + 32 * j + 16 * qt + 4 * fq + r), kw + fr);
 #pragma unroll
         for (int kt = 0; kt < 2; kt++) {
-          const float p = __expf(s[qt][kt][r] + kbv[kt] - lq);
-          float g = dp[qt][kt][r], pv = p;
-          if (thresh) {
-            const bool keep =
-                drop_hash(seed, ((uint64_t)bh * AS + qb4 + r) * AS + kw + kt * 16 + fr) >= thresh;
-            pv = keep ? p * dscale : 0.f;
-            g = keep ? g * dscale : 0.f;
+          const float p = __builtin_amdgcn_exp2f(fmaf(s[qt][kt][r], kLog2e, kbv[kt]) - Lr[r]);
+          const float g = dp[qt][kt][r];
+          if constexpr (DROP == 0) {
+            pd[qt][kt][r] = p;
+            ds[qt][kt][r] = p * (g - Dr[r]);
+          } else {
+            float m;
+            if constexpr (DROP == 1) m = (kt ? keep_hi(hh, thresh) : keep_lo(hh, thresh)) ? dscale : 0.f;
+            else m = __int_as_float(__builtin_amdgcn_sbfe((int)Mr[r], mbit + 4 * kt, 1) & dsbits);
+            pd[qt][kt][r] = p * m;
+            ds[qt][kt][r] = p * fmaf(g, m, -Dr[r]);
           }
-          pd[qt][kt][r] = pv;
-          ds[qt][kt][r] = p * (g - Dq);
         }
       }
     }
@@ -513,20 +622,25 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(const bf16_t* __restri
     }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   const int c = lane & 7;
+  bf16_t* const drow = dqkv + (row0 + kw) * W3 + h * AD + c * 8;
 #pragma unroll
-  for (int jj = 0; jj < 3; jj++) {
-    float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int jj = 0; jj < 3; jj++)
 #pragma unroll
     for (int it = 0; it < 4; it++) {
       const int r = it * 8 + (lane >> 3);
-      const uint4 v = *reinterpret_cast<const uint4*>(st + jj * 4096 + off64(r, c * 8));
-      *reinterpret_cast<uint4*>(dqkv + (row0 + kw + r) * W3 + jj * H + h * AD + c * 8) = v;
-      float f[8];
-      unpack8(v, f);
-#pragma unroll
-      for (int e = 0; e < 8; e++) cs[e] += f[e];
+      *reinterpret_cast<uint4*>(drow + r * W3 + jj * H) = *reinterpret_cast<const uint4*>(st + jj * 4096 + off64(r, c * 8));
     }
-    if (dbqkv) {
+  if (dbqkv) {  // bias-gradient column sums (the encoder layer sums dqkv in a separate pass instead)
+#pragma unroll
+    for (int jj = 0; jj < 3; jj++) {
+      float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int it = 0; it < 4; it++) {
+        float f[8];
+        unpack8(*reinterpret_cast<const uint4*>(st + jj * 4096 + off64(it * 8 + (lane >> 3), c * 8)), f);
+#pragma unroll
+        for (int e = 0; e < 8; e++) cs[e] += f[e];
+      }
 #pragma unroll
       for (int o = 8; o < 64; o <<= 1)
 #pragma unroll
@@ -633,17 +747,23 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_long_kernel(const bf16_t* __r
 #pragma unroll
         for (int r = 0; r < 4; r++) o[dt][qt][r] *= alpha;
 #pragma unroll
-      for (int kt = 0; kt < 8; kt++) {
-        float pp[4];
+      for (int kp = 0; kp < 4; kp++) {
+        float pp[2][4];
 #pragma unroll
         for (int r = 0; r < 4; r++) {
-          float v = s[kt][qt][r];
-          if (thresh)
-            v = drop_hash(seed, ((uint64_t)bh * S + q) * S + j * BLK + kt * 16 + 4 * fq + r) >= thresh ? v * dscale
-                                                                                                       : 0.f;
-          pp[r] = v;
+          float v0 = s[2 * kp][qt][r], v1 = s[2 * kp + 1][qt][r];
+          if (thresh) {
+            const uint32_t hh = attn_pair_hash(seed, (uint64_t)bh * S + q, S, j * BLK + 32 * kp + 4 * fq + r);
+            v0 = keep_lo(hh, thresh) ? v0 * dscale : 0.f;
+            v1 = keep_hi(hh, thresh) ? v1 * dscale : 0.f;
+          }
+          pp[0][r] = v0;
+          pp[1][r] = v1;
         }
-        *reinterpret_cast<uint2*>(Pw + off128(qt * 16 + fr, kt * 16 + 4 * fq)) = pack4(pp[0], pp[1], pp[2], pp[3]);
+#pragma unroll
+        for (int u = 0; u < 2; u++)
+          *reinterpret_cast<uint2*>(Pw + off128(qt * 16 + fr, (2 * kp + u) * 16 + 4 * fq)) =
+              pack4(pp[u][0], pp[u][1], pp[u][2], pp[u][3]);
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // only this wave reads its P rows
@@ -835,13 +955,14 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_long_kernel(
         for (int r = 0; r < 4; r++) {
           const float D = __shfl(r & 1 ? dd2.y : dd2.x, (qb4 + r) >> 1, 64);
           const float lq = __shfl(r & 1 ? lse2.y : lse2.x, (qb4 + r) >> 1, 64);
+          const uint32_t hh =
+              thresh ? attn_pair_hash(seed, (uint64_t)bh * S + i * BLK + qb4 + r, S, kblk * BLK + kw + fr) : 0u;
 #pragma unroll
           for (int kt = 0; kt < 2; kt++) {
             const float p = __expf(s[qt][kt][r] + kbv[kt] - lq);
             float g = dp[qt][kt][r], pv = p;
             if (thresh) {
-              const bool keep = drop_hash(seed, ((uint64_t)bh * S + i * BLK + qb4 + r) * S + kblk * BLK + kw +
-                                                    kt * 16 + fr) >= thresh;
+              const bool keep = kt ? keep_hi(hh, thresh) : keep_lo(hh, thresh);
               pv = keep ? p * dscale : 0.f;
               g = keep ? g * dscale : 0.f;
             }
@@ -937,15 +1058,19 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_long_kernel(
     for (int qt = 0; qt < 2; qt++) {
       const int q = qblk * BLK + qb + qt * 16 + fr;
 #pragma unroll
-      for (int kt = 0; kt < 8; kt++)
+      for (int kp = 0; kp < 4; kp++)
 #pragma unroll
         for (int r = 0; r < 4; r++) {
-          const float p = __expf(s[kt][qt][r] + kb[kt][r] - lq[qt]);
-          float g = dp[kt][qt][r];
-          if (thresh)
-            g = drop_hash(seed, ((uint64_t)bh * S + q) * S + j * BLK + kt * 16 + 4 * fq + r) >= thresh ? g * dscale
-                                                                                                       : 0.f;
-          s[kt][qt][r] = p * (g - Dv[qt]);  // dS
+          const uint32_t hh =
+              thresh ? attn_pair_hash(seed, (uint64_t)bh * S + q, S, j * BLK + 32 * kp + 4 * fq + r) : 0u;
+#pragma unroll
+          for (int u = 0; u < 2; u++) {
+            const int kt = 2 * kp + u;
+            const float p = __expf(s[kt][qt][r] + kb[kt][r] - lq[qt]);
+            float g = dp[kt][qt][r];
+            if (thresh) g = (u ? keep_hi(hh, thresh) : keep_lo(hh, thresh)) ? g * dscale : 0.f;
+            s[kt][qt][r] = p * (g - Dv[qt]);  // dS
+          }
         }
     }
 #pragma unroll
@@ -969,23 +1094,25 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_long_kernel(
   store_tile(st, dqkv, q0 + qb, W3, h * AD, dbqkv, lane);
 }
 
-uint32_t attn_drop_thresh(float p) {
-  if (p <= 0.f) return 0u;
-  const double t = (double)p * 4294967296.0;
-  return t >= 4294967295.0 ? 4294967295u : (uint32_t)t;
+// t16 = round(p·2^16) (0: no dropout) and the keep scale 2^16 / (2^16 − t16)
+uint32_t attn_drop_t16(float p) {
+  if (!(p > 0.f)) return 0u;
+  const double t = (double)p * 65536.0 + 0.5;
+  return t >= 65536.0 ? 65536u : (uint32_t)t;
 }
+float attn_drop_scale(uint32_t t16) { return t16 >= 65536u ? 0.f : 65536.f / (float)(65536u - t16); }
 
 }  // namespace
 
-// KFA_ATTN_PF=0: the S = 128 backward exchanges D through global scratch (the
-// pre-round-4 form) instead of LDS.  (A persistent forward that prefetched the
-// next (sequence, head)'s Q / K / V into registers measured 96.5 vs 80 us per
-// BERT-base layer: its 72 prefetch VGPRs cost the third workgroup per CU and
-// spilled — not kept.)
-static bool attn_pf() {
+// (A persistent forward that prefetched the next (sequence, head)'s Q / K / V into
+// registers measured 96.5 vs 80 us per BERT-base layer: its 72 prefetch VGPRs cost
+// the third workgroup per CU and spilled — not kept.)
+// KFA_ATTN_MASK_LDS=0: the backward reads the forward's keep mask from memory per
+// step instead of parking it in LDS (A/B)
+static bool attn_mask_lds() {
   static int v = -1;
   if (v < 0) {
-    const char* e = getenv("KFA_ATTN_PF");
+    const char* e = getenv("KFA_ATTN_MASK_LDS");
     v = (e && e[0] == '0') ? 0 : 1;
   }
   return v == 1;
@@ -1000,44 +1127,69 @@ static bool attn_long_forced() {
   return v == 1;
 }
 
+// words of the packed keep mask the S = 128 forward can write (0 when it writes none)
+KFA_API long kfa_attn_mask_words(int B, int S, int heads) {
+  return (S == AS && !attn_long_forced()) ? (long)B * heads * 4 * AS : 0L;
+}
+
 // ctx [B*S, heads*64] = attention(qkv [B*S, 3*heads*64] (+ bqkv), key_bias [B, S]); lse [B*heads, S]
 // S = 128: one workgroup per (sequence, head); S = 128·n: per 128-query block, online softmax.
+// mask (nullable; kfa_attn_mask_words words): the S = 128 kernel stores its dropout keep bits there.
 KFA_API int kfa_attn_fwd(const void* qkv, const float* bqkv, const float* key_bias, void* out, float* lse, int B, int S,
-                         int heads, int d, float qscale, float p, unsigned long long seed, hipStream_t st) {
+                         int heads, int d, float qscale, float p, unsigned long long seed, unsigned* mask,
+                         hipStream_t st) {
   if (!bqkv || !key_bias) return -1;  // the caller passes zeros: no branches around the prologue loads
   if (B <= 0 || heads <= 0 || S <= 0 || S % BLK || S > 8192 || d != AD || (long)B * heads * (S / BLK) >= (1L << 31))
     return -1;
-  const uint32_t th = attn_drop_thresh(p);
-  const float ds = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  if (S == AS && !attn_long_forced())
-    hipLaunchKernelGGL(attn_fwd_kernel, dim3((unsigned)(B * heads)), dim3(256), 0, st, (const bf16_t*)qkv, bqkv,
-                       key_bias, (bf16_t*)out, lse, heads, qscale, th, ds, (uint64_t)seed);
-  else
+  const uint32_t th = attn_drop_t16(p);
+  const float ds = attn_drop_scale(th);
+  if (S == AS && !attn_long_forced()) {
+    const dim3 grid((unsigned)(B * heads));
+    if (!th)
+      hipLaunchKernelGGL(attn_fwd_kernel<0>, grid, dim3(256), 0, st, (const bf16_t*)qkv, bqkv, key_bias, (bf16_t*)out,
+                         lse, (uint32_t*)nullptr, heads, qscale, th, ds, (uint64_t)seed);
+    else if (!mask)
+      hipLaunchKernelGGL(attn_fwd_kernel<1>, grid, dim3(256), 0, st, (const bf16_t*)qkv, bqkv, key_bias, (bf16_t*)out,
+                         lse, (uint32_t*)nullptr, heads, qscale, th, ds, (uint64_t)seed);
+    else
+      hipLaunchKernelGGL(attn_fwd_kernel<2>, grid, dim3(256), 0, st, (const bf16_t*)qkv, bqkv, key_bias, (bf16_t*)out,
+                         lse, (uint32_t*)mask, heads, qscale, th, ds, (uint64_t)seed);
+  } else {
     hipLaunchKernelGGL(attn_fwd_long_kernel, dim3((unsigned)((long)B * heads * (S / BLK))), dim3(256), 0, st,
                        (const bf16_t*)qkv, bqkv, key_bias, (bf16_t*)out, lse, heads, S, qscale, th, ds, (uint64_t)seed);
+  }
   return kfa_status();
 }
 
 // dqkv [B*S, 3H] (overwritten); dbqkv [3H] fp32 (+)= bias gradient (nullable)
-// (out = the forward's ctx: D = rowsum(dO∘O) is formed from it).  work: B*heads*S floats (D of every query)
+// (out = the forward's ctx: D = rowsum(dO∘O) is formed from it).  work: B*heads*S floats (D of every query,
+// S > 128).  mask: the S = 128 forward's keep bits (nullable: the kernel re-hashes).
 KFA_API int kfa_attn_bwd(const void* qkv, const float* bqkv, const float* key_bias, const void* out, const float* lse,
                          const void* dout, void* dqkv, float* dbqkv, int B, int S, int heads, int d, float qscale,
-                         float p, unsigned long long seed, float* work, hipStream_t st) {
+                         float p, unsigned long long seed, const unsigned* mask, float* work, hipStream_t st) {
   if (!bqkv || !key_bias) return -1;
   if (B <= 0 || heads <= 0 || S <= 0 || S % BLK || S > 8192 || d != AD || (long)B * heads * (S / BLK) >= (1L << 31))
     return -1;
-  const uint32_t th = attn_drop_thresh(p);
-  const float ds = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const uint32_t th = attn_drop_t16(p);
+  const float ds = attn_drop_scale(th);
   if (S == AS && !attn_long_forced()) {
-    if (!work) return -3;
-    if (attn_pf())
-      hipLaunchKernelGGL(attn_bwd_kernel<true>, dim3((unsigned)(B * heads)), dim3(256), 0, st, (const bf16_t*)qkv,
-                         bqkv, key_bias, (const bf16_t*)out, lse, (const bf16_t*)dout, (bf16_t*)dqkv, dbqkv, work, heads,
-                         qscale, th, ds, (uint64_t)seed);
+    const dim3 grid((unsigned)(B * heads));
+    if (!th)
+      hipLaunchKernelGGL(attn_bwd_kernel<0>, grid, dim3(256), 0, st, (const bf16_t*)qkv, bqkv, key_bias,
+                         (const bf16_t*)out, lse, (const bf16_t*)dout, (bf16_t*)dqkv, dbqkv, (const uint32_t*)nullptr,
+                         heads, qscale, th, ds, (uint64_t)seed);
+    else if (!mask)
+      hipLaunchKernelGGL(attn_bwd_kernel<1>, grid, dim3(256), 0, st, (const bf16_t*)qkv, bqkv, key_bias,
+                         (const bf16_t*)out, lse, (const bf16_t*)dout, (bf16_t*)dqkv, dbqkv, (const uint32_t*)nullptr,
+                         heads, qscale, th, ds, (uint64_t)seed);
+    else if (attn_mask_lds())
+      hipLaunchKernelGGL(attn_bwd_kernel<2>, grid, dim3(256), 0, st, (const bf16_t*)qkv, bqkv, key_bias,
+                         (const bf16_t*)out, lse, (const bf16_t*)dout, (bf16_t*)dqkv, dbqkv, (const uint32_t*)mask,
+                         heads, qscale, th, ds, (uint64_t)seed);
     else
-      hipLaunchKernelGGL(attn_bwd_kernel<false>, dim3((unsigned)(B * heads)), dim3(256), 0, st, (const bf16_t*)qkv,
-                         bqkv, key_bias, (const bf16_t*)out, lse, (const bf16_t*)dout, (bf16_t*)dqkv, dbqkv, work, heads,
-                         qscale, th, ds, (uint64_t)seed);
+      hipLaunchKernelGGL(attn_bwd_kernel<3>, grid, dim3(256), 0, st, (const bf16_t*)qkv, bqkv, key_bias,
+                         (const bf16_t*)out, lse, (const bf16_t*)dout, (bf16_t*)dqkv, dbqkv, (const uint32_t*)mask,
+                         heads, qscale, th, ds, (uint64_t)seed);
     return kfa_status();
   }
   if (!work) return -3;

@@ -55,8 +55,9 @@ _lib.register("kfa_embed_bwd", [P, P, L, P, P, I, L, I, I, P])
 _lib.register("kfa_colsum", [P, P, P, L, I, I, P])
 _lib.register("kfa_embed_small_ws_floats", [I, I], restype=_lib.L)
 _lib.register("kfa_embed_small_bwd", [P, P, _lib.L, P, I, _lib.L, I, I, P, P])
-_lib.register("kfa_attn_fwd", [P, P, P, P, P, I, I, I, I, Fl, Fl, U64, P])
-_lib.register("kfa_attn_bwd", [P, P, P, P, P, P, P, P, I, I, I, I, Fl, Fl, U64, P, P])
+_lib.register("kfa_attn_fwd", [P, P, P, P, P, I, I, I, I, Fl, Fl, U64, P, P])
+_lib.register("kfa_attn_bwd", [P, P, P, P, P, P, P, P, I, I, I, I, Fl, Fl, U64, P, P, P])
+_lib.register("kfa_attn_mask_words", [I, I, I], _lib.L)
 
 # env KFA_FUSED_ATTN=0 falls back to the split kernels + batched library GEMMs
 FUSED_ATTN = os.environ.get("KFA_FUSED_ATTN", "1") != "0"
@@ -449,8 +450,14 @@ def _zeros_f32(n: int, dev) -> torch.Tensor:
     return _lib.workspace(4 * n, dev, "const_zeros_f32").view(torch.float32)[:n]
 
 
-def attn_fwd(qkv, bqkv, key_bias, B, S, heads, p=0.0, seed=0):
-    """(ctx [B*S, H], lse [B*heads, S]) of softmax((q+b)(k+b)ᵀ/√d + key_bias)·(v+b), dropout p."""
+def attn_fwd(qkv, bqkv, key_bias, B, S, heads, p=0.0, seed=0, want_mask=False):
+    """(ctx [B*S, H], lse [B*heads, S]) of softmax((q+b)(k+b)ᵀ/√d + key_bias)·(v+b), dropout p.
+
+    ``want_mask``: also return the packed dropout keep mask the S = 128 kernel
+    writes (int32 [B*heads, 4, S], 2 KiB per head; None when there is no dropout or
+    another kernel runs) — :func:`attn_bwd` reads it instead of re-hashing every
+    score.  Dropout: one counter hash per score pair, 16-bit thresholds
+    (``csrc/kernels/attention.hip``: attn_pair_hash)."""
     T_, W3 = qkv.shape
     H = W3 // 3
     d = H // heads
@@ -462,14 +469,21 @@ def attn_fwd(qkv, bqkv, key_bias, B, S, heads, p=0.0, seed=0):
     bqkv, key_bias = _attn_biases(bqkv, key_bias, W3, B * S, qkv.device)
     out = torch.empty(T_, H, dtype=qkv.dtype, device=qkv.device)
     lse = torch.empty(B * heads, S, dtype=torch.float32, device=qkv.device)
+    mask = None
+    if want_mask and p > 0:
+        words = _lib.lib().kfa_attn_mask_words(B, S, heads)
+        if words:
+            mask = torch.empty(B * heads, 4, S, dtype=torch.int32, device=qkv.device)
+            assert mask.numel() == words
     _lib.call("kfa_attn_fwd", _lib.ptr(qkv), _lib.ptr(bqkv), _lib.ptr(key_bias), _lib.ptr(out), _lib.ptr(lse), B, S,
-              heads, d, 1.0 / math.sqrt(d), float(p), hash_key(seed), _lib.stream())
-    return out, lse
+              heads, d, 1.0 / math.sqrt(d), float(p), hash_key(seed), _lib.ptr(mask), _lib.stream())
+    return (out, lse, mask) if want_mask else (out, lse)
 
 
-def attn_bwd(qkv, bqkv, key_bias, out, lse, dout, dbqkv, B, S, heads, p=0.0, seed=0):
-    """dqkv [B*S, 3H] of :func:`attn_fwd` (``out``, ``lse``: its outputs); the bias
-    gradient is added into ``dbqkv`` (fp32, nullable)."""
+def attn_bwd(qkv, bqkv, key_bias, out, lse, dout, dbqkv, B, S, heads, p=0.0, seed=0, mask=None):
+    """dqkv [B*S, 3H] of :func:`attn_fwd` (``out``, ``lse``, ``mask``: its outputs); the
+    bias gradient is added into ``dbqkv`` (fp32, nullable).  Without ``mask`` the
+    kernel regenerates the dropout decisions from the hash (same values)."""
     T_, W3 = qkv.shape
     H = W3 // 3
     d = H // heads
@@ -479,11 +493,14 @@ def attn_bwd(qkv, bqkv, key_bias, out, lse, dout, dbqkv, B, S, heads, p=0.0, see
     if tuple(out.shape) != (T_, H) or out.dtype != qkv.dtype or not out.is_contiguous():
         raise ValueError("attn_bwd: out must be the contiguous bf16 [B*S, H] forward output")
     bqkv, key_bias = _attn_biases(bqkv, key_bias, W3, B * S, qkv.device)
+    if mask is not None and (mask.dtype != torch.int32 or mask.numel() != _lib.lib().kfa_attn_mask_words(B, S, heads)
+                             or not mask.is_contiguous()):
+        raise ValueError("attn_bwd: mask must be the forward's int32 [B*heads, 4, S] keep mask")
     dqkv = torch.empty_like(qkv)
     work = _lib.workspace(B * heads * S * 4, qkv.device, "attn_rowdot")  # D = rowsum(dO∘O) (S > 128)
     _lib.call("kfa_attn_bwd", _lib.ptr(qkv), _lib.ptr(bqkv), _lib.ptr(key_bias), _lib.ptr(out), _lib.ptr(lse),
               _lib.ptr(dout), _lib.ptr(dqkv), _lib.ptr(dbqkv), B, S, heads, d, 1.0 / math.sqrt(d), float(p),
-              hash_key(seed), _lib.ptr(work), _lib.stream())
+              hash_key(seed), _lib.ptr(mask if p > 0 else None), _lib.ptr(work), _lib.stream())
     return dqkv
 
 
@@ -565,8 +582,8 @@ class EncoderLayerFn(torch.autograd.Function):
         # attention
         qkv = mm(x, wqkv)                                                 # [T, 3H]
         if fused:
-            ctxr, lse = attn_fwd(qkv, bqkv, key_bias, B, S, heads, pa, s_attn)
-            att = (qkv, lse)
+            ctxr, lse, amask = attn_fwd(qkv, bqkv, key_bias, B, S, heads, pa, s_attn, want_mask=True)
+            att = (qkv, lse, amask)
         else:
             q = torch.empty(B * heads, S, d, dtype=x.dtype, device=dev)
             k = torch.empty_like(q)
@@ -638,10 +655,10 @@ class EncoderLayerFn(torch.autograd.Function):
         res_shared = dao is dx_res  # no hidden dropout: one tensor, also the side stream's wgrad operand
         del dao
         if fused:
-            qkv, lse = att
+            qkv, lse, amask = att
             # QKV-bias gradient as a column-sum pass (27 us) rather than the kernel's
             # per-wave atomics: 1024 adds per bias element serialise at L2 (+160 us / layer)
-            dqkv = attn_bwd(qkv, bqkv, key_bias, ctxr, lse, dctxr, None, B, S, heads, pa, s_attn)
+            dqkv = attn_bwd(qkv, bqkv, key_bias, ctxr, lse, dctxr, None, B, S, heads, pa, s_attn, mask=amask)
             colsum_(dqkv, G(bqkv))
             del dctxr
         else:

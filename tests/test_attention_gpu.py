@@ -1,8 +1,10 @@
 """Fused attention (csrc/kernels/attention.hip) vs a plain PyTorch fp32 reference.
 
 The dropout case rebuilds the kernels' counter-hash keep mask in numpy (numpy copy
-of drop_hash in csrc/kernels/common.h) so forward AND backward are checked
-element-wise against the reference with the identical mask."""
+of drop_hash in csrc/kernels/common.h, one hash per (q, k) / (q, k + 16) score pair,
+16-bit halves against round(p·2^16) — attention.hip attn_pair_hash) so forward AND
+backward are checked element-wise against the reference with the identical mask;
+the S = 128 backward runs both from the forward's packed mask and re-hashing."""
 import math
 
 import numpy as np
@@ -38,11 +40,20 @@ def _drop_hash(seed, i):
     return x
 
 
+def _t16(p):
+    return min(int(p * 65536.0 + 0.5), 65536)
+
+
 def _keep_mask(seed, B, heads, S, p):
+    """[B, heads, S, S] keep mask: pair (row, k) / (row, k + 16) (k with bit 4 clear)
+    shares the hash of index row·S + k; low half decides k, high half k + 16."""
     from kubeflow_controller_amd.ops.transformer import hash_key  # the launch key the wrapper passes
-    h = _drop_hash(hash_key(seed), np.arange(B * heads * S * S, dtype=np.uint64))
-    thresh = min(int(p * 4294967296.0), 4294967295)
-    return torch.from_numpy((h >= thresh).reshape(B, heads, S, S).astype(np.float32))
+    key = np.arange(S, dtype=np.uint64)
+    rows = np.arange(B * heads * S, dtype=np.uint64)
+    idx = rows[:, None] * np.uint64(S) + (key & ~np.uint64(16))[None, :]
+    h = _drop_hash(hash_key(seed), idx)
+    half = np.where((key & np.uint64(16)) != 0, h >> np.uint32(16), h & np.uint32(0xFFFF))
+    return torch.from_numpy((half >= _t16(p)).reshape(B, heads, S, S).astype(np.float32))
 
 
 def _reference(qkv, bqkv, kb, B, S, heads, d, mask, p):
@@ -53,7 +64,7 @@ def _reference(qkv, bqkv, kb, B, S, heads, d, mask, p):
         sc = sc + kb.view(B, 1, 1, S)
     pr = torch.softmax(sc, -1)
     if mask is not None:
-        pr = pr * mask / (1.0 - p)
+        pr = pr * mask / (1.0 - _t16(p) / 65536.0)
     return (pr @ v).permute(0, 2, 1, 3).reshape(B * S, heads * d)
 
 
@@ -72,7 +83,8 @@ def test_fused_attention_fwd_bwd(p, S):
     m[1, S - 38:] = 0   # masked tail, crossing a 128-key block boundary for S > 128
     kb = ((1 - m) * -10000.0).contiguous()
     seed = 987654321
-    out, lse = T.attn_fwd(qkv, bqkv, kb, B, S, heads, p, seed)
+    out, lse, kmask = T.attn_fwd(qkv, bqkv, kb, B, S, heads, p, seed, want_mask=True)
+    assert (kmask is not None) == (p > 0 and S == 128)
     mask = _keep_mask(seed, B, heads, S, p).to(D) if p > 0 else None
     xr = qkv.float().requires_grad_()
     br = bqkv.clone().requires_grad_()
@@ -81,9 +93,21 @@ def test_fused_attention_fwd_bwd(p, S):
     dout = torch.randn(B * S, H, device=D)
     ref.backward(dout)
     db = torch.zeros(3 * H, device=D)
-    dqkv = T.attn_bwd(qkv, bqkv, kb, out, lse, dout.to(torch.bfloat16), db, B, S, heads, p, seed)
+    dqkv = T.attn_bwd(qkv, bqkv, kb, out, lse, dout.to(torch.bfloat16), db, B, S, heads, p, seed, mask=kmask)
     _close(dqkv, xr.grad, 3e-2, "dqkv")
     _close(db, br.grad, 3e-2, "dbqkv")
+    if kmask is not None:  # the re-hashing backward: the same decisions, bit for bit the same result
+        dqkv_h = T.attn_bwd(qkv, bqkv, kb, out, lse, dout.to(torch.bfloat16), None, B, S, heads, p, seed)
+        assert torch.equal(dqkv_h, dqkv)
+        # the packed words: word [bh][c][q] bit (k >> 4)·4 + (k & 3) for the keys with (k >> 2) & 3 == c
+        m = mask.view(B * heads, S, S).to(torch.int64).cpu()
+        k = torch.arange(S)
+        bit = (k >> 4) * 4 + (k & 3)
+        words = torch.zeros(B * heads, 4, S, dtype=torch.int64)
+        for c in range(4):
+            sel = ((k >> 2) & 3) == c
+            words[:, c, :] = (m[:, :, sel] << bit[sel]).sum(-1)
+        assert torch.equal(kmask.cpu().to(torch.int64) & 0xFFFFFFFF, words)
 
 
 def test_fused_attention_lse_matches():

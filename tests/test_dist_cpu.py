@@ -226,8 +226,8 @@ def _agree_worker(rank, world, port, lockstep, out):
     # rank 1 would pick differently; only a lockstep job takes rank 0's decision
     got = conv._agree(rank == 0, torch.device("cpu"))
     # the GEMM tuner's multi-way choice (index of the fastest candidate) follows the same rule
-    from kubeflow_controller_amd.ops import gemm
-    pick = gemm._agree_int(3 if rank == 0 else 1, torch.device("cpu"))
+    from kubeflow_controller_amd.ops import routes  # every per-shape routing decision (ops/routes.decide)
+    pick = routes._agree_index(3 if rank == 0 else 1, torch.device("cpu"))
     out[rank] = (bool(got), pick)
     dist.barrier()
     dist.destroy_process_group()
