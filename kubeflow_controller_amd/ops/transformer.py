@@ -78,6 +78,11 @@ FFN_GELU_EPI = os.environ.get("KFA_FFN_GELU_EPI", "0") == "1"
 # GELU' arithmetic (~25 VALU ops per element) lands on the store waves' share of the MFMA
 # pipeline at the tile boundary, and the extra operand registers spill (docs/kernels.md).
 DACT_EPI = os.environ.get("KFA_DACT_EPI", "0") == "1"
+# KFA_ATTN_MASK=1: the encoder's attention forward stores its packed dropout keep mask
+# and the backward reads it instead of re-hashing.  Off: the backward is HBM-bound
+# once the hash is paired (BERT-base layer bwd 86 us re-hashing, 88 us without
+# dropout, 96 us reading the mask — tools/bench_attn.py, docs/kernels.md).
+ATTN_MASK = os.environ.get("KFA_ATTN_MASK", "0") == "1"
 _MASK64 = (1 << 64) - 1
 
 
@@ -582,7 +587,8 @@ class EncoderLayerFn(torch.autograd.Function):
         # attention
         qkv = mm(x, wqkv)                                                 # [T, 3H]
         if fused:
-            ctxr, lse, amask = attn_fwd(qkv, bqkv, key_bias, B, S, heads, pa, s_attn, want_mask=True)
+            ctxr, lse, amask = attn_fwd(qkv, bqkv, key_bias, B, S, heads, pa, s_attn, want_mask=True) if ATTN_MASK \
+                else attn_fwd(qkv, bqkv, key_bias, B, S, heads, pa, s_attn) + (None,)
             att = (qkv, lse, amask)
         else:
             q = torch.empty(B * heads, S, d, dtype=x.dtype, device=dev)

@@ -367,5 +367,28 @@ def make_comm(device: torch.device, process_group=None, store=None, mode: Option
     if process_group is not None and process_group is not dist.group.WORLD:
         raise CommError("the native communicator spans the default group's ranks only")
     t = float(os.environ.get("KFA_DIST_INIT_TIMEOUT", "300"))
-    return Communicator.create(store or default_store(), dist.get_rank(), dist.get_world_size(), device,
-                               timeout_s=t)
+    world = dist.get_world_size()
+    comm, err = None, ""
+    try:
+        comm = Communicator.create(store or default_store(), dist.get_rank(), world, device, timeout_s=t)
+        probe = torch.ones(1, device=device)  # one collective end to end before any training traffic
+        comm.all_reduce(probe, "sum")
+        ok = int(probe.item()) == world
+        err = "" if ok else f"probe all-reduce gave {probe.item()} (world {world})"
+    except Exception as e:  # noqa: BLE001 - decided collectively below
+        ok, err = False, str(e)
+    # every rank keeps the native layer or none does (a rank that fell back alone would
+    # leave its peers waiting in collectives it never joins)
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32,
+                        device=device if dist.get_backend() == "nccl" else torch.device("cpu"))
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if int(flag.item()) == 1:
+        return comm
+    if comm is not None:
+        comm.destroy()
+    if mode == "native" and os.environ.get("KFA_COMM", "").lower() == "native":
+        raise CommError(f"native communicator unavailable: {err or 'another rank failed'}")
+    import sys
+    print(f"[kfc comm] native communicator unavailable ({err or 'another rank failed'}): torch.distributed",
+          file=sys.stderr, flush=True)
+    return TorchComm(process_group)

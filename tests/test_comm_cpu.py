@@ -215,3 +215,43 @@ def test_comm_mode_selection(monkeypatch):
     assert C.comm_mode(torch.device("cuda", 0)) == "torch"
     monkeypatch.setenv("KFA_COMM", "native")
     assert C.comm_mode(torch.device("cpu")) == "native"
+
+
+def _fallback_worker(rank, world, port, out):
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    # the healthy ranks wait this long for the failed one's connection
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), KFA_DIST_INIT_TIMEOUT="5")
+    os.environ.pop("KFA_COMM", None)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from kubeflow_controller_amd.parallel import comm as C
+    res = {}
+    c = C.make_comm(torch.device("cpu"), mode="native")  # every rank comes up: the native layer is kept
+    res["ok"] = repr(c)
+    t = torch.full((4,), float(rank + 1))
+    c.all_reduce(t, "sum")
+    res["ok_sum"] = t.tolist()
+    if rank == 1:  # this rank's native bring-up fails: every rank must fall back together
+        def broken(*a, **k):
+            raise C.CommError("simulated bring-up failure")
+        C.Communicator.create = classmethod(lambda cls, *a, **k: broken())
+    c2 = C.make_comm(torch.device("cpu"), mode="native")
+    res["fallback"] = repr(c2)
+    t = torch.full((4,), float(rank + 1))
+    c2.all_reduce(t, "sum")
+    res["fb_sum"] = t.tolist()
+    torch.save(res, f"{out}.{rank}")
+    dist.destroy_process_group()
+
+
+def test_make_comm_falls_back_on_every_rank_together(tmp_path):
+    """A rank whose native communicator cannot come up makes EVERY rank use
+    torch.distributed (decided by one MIN all-reduce over the process group):
+    a lone fallback would leave its peers blocked in collectives it never joins."""
+    out = str(tmp_path / "f")
+    mp.start_processes(_fallback_worker, args=(3, _free_port(), out), nprocs=3, join=True, start_method="spawn")
+    for r in range(3):
+        res = torch.load(f"{out}.{r}", weights_only=True)
+        assert res["ok"].startswith("Communicator(host"), res
+        assert res["fallback"].startswith("TorchComm"), res
+        assert res["ok_sum"] == [6.0] * 4 and res["fb_sum"] == [6.0] * 4

@@ -70,5 +70,28 @@ def main(paths, keep=("gemm", "wgrad", "conv", "seg_", "radix", "scan_max", "bn_
               f"{fmt(wr, '.1f')} | {fmt(tbs, '.2f')} |")
 
 
+def issue(paths, keep=("attn", "gemm", "wgrad", "conv", "ln_", "bias_act")):
+    """Per-wave issue mix (passes with SQ_INSTS_* and SQ_WAVES): instructions per wave
+    and the share of wave cycles spent issuing VALU / waiting."""
+    rows = load(paths)
+    print("| kernel | dispatches | mean us | VALU / wave | SALU / wave | MFMA / wave | LDS / wave | "
+          "VALU-active share | wait-any share |")
+    print("|---|---:|---:|---:|---:|---:|---:|---:|---:|")
+    for k, m in sorted(rows.items(), key=lambda kv: -kv[1]["_us"] * kv[1]["_n"]):
+        w = m.get("SQ_WAVES")
+        if not any(s in k for s in keep) or not w or "SQ_INSTS_VALU" not in m:
+            continue
+        per = lambda c: fmt(m[c] / w if c in m else None, ".0f")  # noqa: E731
+        wc = m.get("SQ_WAVE_CYCLES")
+        va = m["SQ_ACTIVE_INST_VALU"] / wc if wc and "SQ_ACTIVE_INST_VALU" in m else None
+        wa = m["SQ_WAIT_ANY"] / wc if wc and "SQ_WAIT_ANY" in m else None
+        print(f"| `{k}` | {m['_n']} | {m['_us']:.1f} | {per('SQ_INSTS_VALU')} | {per('SQ_INSTS_SALU')} | "
+              f"{per('SQ_INSTS_MFMA')} | {per('SQ_INSTS_LDS')} | {fmt(va and va * 100, '.0f')}% | "
+              f"{fmt(wa and wa * 100, '.0f')}% |")
+
+
 if __name__ == "__main__":
-    main(sys.argv[1:])
+    if sys.argv[1:2] == ["--issue"]:
+        issue(sys.argv[2:])
+    else:
+        main(sys.argv[1:])
