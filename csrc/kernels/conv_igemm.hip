@@ -353,7 +353,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
   // pointwise fast paths: A row m is T[m] (1x1 / stride 1 / no pad) and/or D row m is D[m]
   const bool lin_a = g.R == 1 && g.S == 1 && g.sa == 1 && g.oa == 0 && g.ob == 0 && g.H == g.P && g.W == g.Q;
   const bool lin_d = g.os == 1 && g.oph == 0 && g.opw == 0 && g.OH == g.P && g.OW == g.Q;
-  int a_hb[AR], a_wb[AR], a_vo[AR];  // a_vo: byte offset of the row's image + swizzled chunk (< 2^31, host-checked)
+  int a_hb[AR], a_wb[AR], a_vo[AR];  // a_vo: byte offset of the row at tap (0, 0) + swizzled chunk (< 2^31, host-checked)
   unsigned b_off[BR];
   const __amdgpu_buffer_rsrc_t rT = rsrc(T, g.t_bytes), rB = rsrc(B, g.b_bytes), rD = rsrc(D, g.d_bytes);
   const __amdgpu_buffer_rsrc_t rE = rsrc(E ? E : D, E ? g.d_bytes : 0u);
@@ -369,12 +369,12 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
         a_hb[i] = 0;
         a_wb[i] = 0;
         a_vo[i] = (m * g.C + cs) * 2;
-      } else if (m < g.M) {
+      } else if (m < g.M) {  // a_vo: the row's offset at tap (0, 0) (may lie outside the image)
         const int nb = fdiv(m, PQ, rPQ), rem = m - nb * PQ;
         const int p = fdiv(rem, g.Q, rQ), q = rem - p * g.Q;
         a_hb[i] = p * g.sa + g.oa;
         a_wb[i] = q * g.sa + g.ob;
-        a_vo[i] = (nb * g.H * g.W * g.C + cs) * 2;
+        a_vo[i] = ((nb * g.H * g.W + a_hb[i] * g.W + a_wb[i]) * g.C + cs) * 2;
       } else {
         a_hb[i] = -(1 << 28);  // forces out-of-range
         a_wb[i] = 0;
@@ -421,6 +421,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
     const int ti = nx_ti, k0 = nx_kt * BK, c0 = nx_c0;
     if (ti != setup_tile) { setup(tile_of(ti)); setup_tile = ti; }
     const int dh = nx_r * g.ra, dw = nx_s * g.ra;
+    const int ta_off = (dh * g.W + dw) * g.C * 2;  // the tap's offset: one scalar add per DMA, no per-lane multiply
     nx_c0 += BK;  // advance to the next slice: BK channels of one tap, or BK / C whole taps (C < BK)
     while (nx_c0 >= g.C) {
       nx_c0 -= g.C;
@@ -438,7 +439,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
         if (!lin_a) {
           const int ih = a_hb[i] + dh, iw = a_wb[i] + dw;
           const bool ok = (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
-          vo = ok ? a_vo[i] + (ih * g.W + iw) * g.C * 2 : (int)kOOB;
+          vo = ok ? a_vo[i] + ta_off : (int)kOOB;
           pr_ok |= ok ? (1u << i) : 0u;
         } else {
           pr_ok |= 1u << i;
@@ -456,7 +457,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
       for (int i = 0; i < AR; i++) {
         const int ih = a_hb[i] + dh, iw = a_wb[i] + dw;
         const bool ok = (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
-        const int vo = ok ? a_vo[i] + (ih * g.W + iw) * g.C * 2 : (int)kOOB;
+        const int vo = ok ? a_vo[i] + ta_off : (int)kOOB;  // selects, no branch
         buf_dma16_act(rT, As + buf * BM * BK + (i * RPP + wave * 8) * BK, vo, c0 * 2);
       }
     }
