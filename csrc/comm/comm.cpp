@@ -204,6 +204,12 @@ struct Backend {
   virtual int recv(void* r, size_t n, int dt, int peer, void* st) = 0;
   virtual int group_start() = 0;
   virtual int group_end() = 0;
+  // receive ONE message from whichever peer sends first (host backend: the async
+  // parameter server's request loop); *src = that peer
+  virtual int recv_any(void*, size_t, int, int* src, int64_t) {
+    *src = -1;
+    return fail(E_ARG, std::string("recv_any: not supported by the ") + name() + " backend");
+  }
   virtual int async_error() { return OK; }
   virtual void abort() {}
 };
@@ -436,6 +442,8 @@ struct Host : Backend {
   };
   std::vector<XOp> queued;  // grouped point-to-point ops
   int depth = 0;
+  int rr = 0;                 // recv_any: last peer served
+  std::vector<char> closed;   // recv_any: peers whose connection ended
   ~Host() override {
     for (int fd : fds)
       if (fd >= 0) ::close(fd);
@@ -608,6 +616,44 @@ struct Host : Backend {
     if (depth > 0) { queued.push_back(o); return OK; }
     std::vector<XOp> ops{o};
     return run(ops);
+  }
+  // Wait until a peer's socket is readable and receive its next message with the
+  // normal directed path.  Peers are scanned round-robin from the last one served
+  // (no starvation); a peer whose connection closed with nothing left to read
+  // (a finished worker) is skipped from then on.
+  int recv_any(void* r, size_t n, int dt, int* src, int64_t tmo_ms) override {
+    *src = -1;
+    if (depth > 0) return fail(E_STATE, "recv_any inside a group");
+    const auto deadline = Clock::now() + std::chrono::milliseconds(tmo_ms > 0 ? tmo_ms : timeout_ms);
+    if (closed.size() != (size_t)world) closed.assign(world, 0);
+    for (;;) {
+      std::vector<pollfd> pf;
+      std::vector<int> who;
+      for (int k = 1; k <= world; k++) {
+        const int p = (rr + k) % world;
+        if (p == rank || closed[p]) continue;
+        pf.push_back(pollfd{fds[p], POLLIN, 0});
+        who.push_back(p);
+      }
+      if (pf.empty()) return fail(E_PROTO, "recv_any: every peer closed its connection");
+      const int64_t left = ms_left(deadline);
+      if (left <= 0) return fail(E_TIMEOUT, "recv_any timed out (no peer sent a message)");
+      const int rc = poll(pf.data(), pf.size(), (int)std::min<int64_t>(left, 1000));
+      if (rc < 0 && errno != EINTR) return fail(E_SYS, std::string("poll: ") + strerror(errno));
+      for (size_t k = 0; k < pf.size(); k++) {
+        if (!(pf[k].revents & (POLLIN | POLLHUP | POLLERR))) continue;
+        char b;
+        const ssize_t g = ::recv(pf[k].fd, &b, 1, MSG_PEEK | MSG_DONTWAIT);
+        if (g == 0) { closed[who[k]] = 1; continue; }  // orderly close, nothing pending
+        if (g < 0 && (errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR)) continue;
+        if (g < 0) return fail(E_SYS, std::string("recv: ") + strerror(errno));
+        rr = who[k];
+        *src = who[k];
+        XOp o{who[k], false, static_cast<char*>(r), n * dsize(dt)};
+        std::vector<XOp> ops{o};
+        return run(ops);
+      }
+    }
   }
   int group_start() override {
     depth++;
@@ -855,6 +901,14 @@ KFC_API int kfc_recv(void* h, void* r, size_t n, int dt, int peer, void* stream)
   KFC_COMM(h);
   if (int e = chk_args(dt, SUM)) return e;
   return c->be->recv(r, n, dt, peer, stream);
+}
+
+// one message from whichever peer sends first (host backend); *src = its rank;
+// timeout_ms <= 0: the communicator's timeout
+KFC_API int kfc_recv_any(void* h, void* r, size_t n, int dt, int* src, int timeout_ms) {
+  KFC_COMM(h);
+  if (int e = chk_args(dt, SUM)) return e;
+  return c->be->recv_any(r, n, dt, src, timeout_ms);
 }
 
 // All-to-all with per-peer element counts / offsets (the embedding exchange): one

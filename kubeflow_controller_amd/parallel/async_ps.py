@@ -30,10 +30,14 @@ e.g. at the end of training) the partial sum is applied so no one blocks
 forever.  ``aggregate = 0``: every push applies at once (async).
 
 Headers and payloads use distinct tags, and every request from one worker is
-sequential, so a PS never interleaves two workers' payloads.  Two transports:
+sequential, so a PS never interleaves two workers' payloads.  The request channel
+(``parallel/comm.py:P2P``) is the first-party host transport by default —
+``csrc/comm`` TCP streams per rank pair with an any-source receive for the PS
+loop (``kfc_recv_any``), where the per-pair message order stands in for the tags
+— or gloo (``KFA_PS_P2P=torch``).  Two payload transports:
 
 * **host** (:class:`AsyncPSServer` / :class:`AsyncPSClient`): payloads are CPU
-  tensors over gloo — TF's gRPC PS in spirit, for CPU replicas;
+  tensors on the request channel — TF's gRPC PS in spirit, for CPU replicas;
 * **device** (:class:`DeviceAsyncPSServer` / :class:`DeviceAsyncPSClient`): the
   PS task keeps its variables, Adam slots and one gradient mailbox per worker
   in the HBM of the GPU it is co-located with and exports them by HIP IPC
@@ -62,6 +66,7 @@ from typing import Callable, Dict, List, Optional, Sequence, Tuple
 import torch
 import torch.distributed as dist
 
+from .comm import make_p2p
 from .ps import ps_assignment
 
 PULL, PUSH, DONE, PUSH_DEV = 1, 2, 3, 4
@@ -135,8 +140,11 @@ class _Service:
     def _acc_add(self, g: torch.Tensor) -> None: ...
     def _acc(self) -> torch.Tensor: ...
     def _reply(self, dst: int, applied: int) -> None:
-        dist.send(torch.tensor([self.global_step, applied], dtype=torch.int64), dst, group=self.group,
-                  tag=TAG_REPLY)
+        self.p2p.send(torch.tensor([self.global_step, applied], dtype=torch.int64), dst, tag=TAG_REPLY)
+
+    def close(self) -> None:
+        """Release the request channel (after :meth:`serve`)."""
+        self.p2p.destroy()
 
     def serve(self, log: Optional[Callable[[str], None]] = None) -> int:
         """Run until every worker sent DONE; returns the number of pushes applied."""
@@ -159,7 +167,7 @@ class _Service:
             self._acc_reset()
 
         while active > 0:
-            src = dist.recv(hdr, src=None, group=self.group, tag=TAG_HDR)
+            src = self.p2p.recv_any(hdr, tag=TAG_HDR)
             op, tag = int(hdr[0]), int(hdr[1])
             if op == PULL:
                 self._send_vars(src)
@@ -196,7 +204,7 @@ class AsyncPSServer(_Service):
 
     def __init__(self, init_params: Sequence[Tuple[str, torch.Tensor]], num_workers: int, num_ps: int, ps_index: int,
                  lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, optimizer: str = "adam", group=None,
-                 aggregate: int = 0):
+                 aggregate: int = 0, p2p=None):
         self.W, self.P, self.idx = num_workers, num_ps, ps_index
         shapes = [(n, p.shape) for n, p in init_params]
         self.assignment = ps_assignment(list(init_params), num_ps)
@@ -210,6 +218,7 @@ class AsyncPSServer(_Service):
         self.lr, self.betas, self.eps, self.opt = lr, betas, eps, optimizer
         self.group = group
         self._init_service(aggregate)
+        self.p2p = p2p if p2p is not None else make_p2p(group=group)
 
     def _apply(self, g: torch.Tensor, scale: float = 1.0) -> None:
         self.t += 1
@@ -225,12 +234,12 @@ class AsyncPSServer(_Service):
         self.w.addcdiv_(self.m, self.v.sqrt().add_(self.eps), value=-step)
 
     def _send_vars(self, src: int) -> None:
-        dist.send(self.w, src, group=self.group, tag=TAG_DATA)
+        self.p2p.send(self.w, src, tag=TAG_DATA)
 
     def _recv_grad(self, src: int, op: int) -> torch.Tensor:
         if op != PUSH:
             raise RuntimeError(f"PS {self.idx}: host server got a device push from rank {src}")
-        dist.recv(self.grad, src, group=self.group, tag=TAG_DATA)
+        self.p2p.recv(self.grad, src, tag=TAG_DATA)
         return self.grad
 
     def _acc_reset(self) -> None:
@@ -252,12 +261,16 @@ class _ClientSteps:
         self._hdr = torch.zeros(2, dtype=torch.int64)
         self._reply = torch.zeros(2, dtype=torch.int64)
 
+    def close(self) -> None:
+        """Release the request channel (after :meth:`done`)."""
+        self.p2p.destroy()
+
     def _header(self, rank: int, op: int, tag: int = 0) -> None:
         self._hdr[0], self._hdr[1] = op, tag
-        dist.send(self._hdr, rank, group=self.group, tag=TAG_HDR)
+        self.p2p.send(self._hdr, rank, tag=TAG_HDR)
 
     def _await_reply(self, k: int, rank: int) -> int:
-        dist.recv(self._reply, rank, group=self.group, tag=TAG_REPLY)
+        self.p2p.recv(self._reply, rank, tag=TAG_REPLY)
         step, applied = int(self._reply[0]), int(self._reply[1])
         self.tags[k] = step
         if not applied:
@@ -268,7 +281,8 @@ class _ClientSteps:
 class AsyncPSClient(_ClientSteps):
     """Worker side: pull variables from / push gradients to every PS task (host transport)."""
 
-    def __init__(self, params: Sequence[Tuple[str, torch.nn.Parameter]], num_workers: int, num_ps: int, group=None):
+    def __init__(self, params: Sequence[Tuple[str, torch.nn.Parameter]], num_workers: int, num_ps: int, group=None,
+                 p2p=None):
         self.W, self.P, self.group = num_workers, num_ps, group
         self.params = list(params)
         self.assignment = ps_assignment(self.params, num_ps)
@@ -279,13 +293,14 @@ class AsyncPSClient(_ClientSteps):
             names, n = _layout(shapes, self.assignment, k)
             self.plan.append((num_workers + k, [by_name[x] for x in names], torch.zeros(n)))
         self._init_steps(num_ps)
+        self.p2p = p2p if p2p is not None else make_p2p(group=group)
 
     def pull(self) -> None:
         for rank, ps, buf in self.plan:
             if not ps:
                 continue
             self._header(rank, PULL)
-            dist.recv(buf, rank, group=self.group, tag=TAG_DATA)
+            self.p2p.recv(buf, rank, tag=TAG_DATA)
             off = 0
             with torch.no_grad():
                 for p in ps:
@@ -309,7 +324,7 @@ class AsyncPSClient(_ClientSteps):
                     buf[off:off + n].copy_(p.grad.reshape(-1))
                 off += n
             self._header(rank, PUSH, self.tags[k])
-            dist.send(buf, rank, group=self.group, tag=TAG_DATA)
+            self.p2p.send(buf, rank, tag=TAG_DATA)
             live.append((k, rank))
         step = -1
         for k, rank in live:
@@ -416,7 +431,7 @@ class DeviceAsyncPSServer(_Service):
 
     def __init__(self, init_params: Sequence[Tuple[str, torch.Tensor]], num_workers: int, num_ps: int, ps_index: int,
                  store, device, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, optimizer: str = "adam",
-                 group=None, aggregate: int = 0, channels_last: bool = False):
+                 group=None, aggregate: int = 0, channels_last: bool = False, p2p=None):
         self.W, self.P, self.idx = num_workers, num_ps, ps_index
         shapes = [(n, p.shape) for n, p in init_params]
         self.assignment = ps_assignment(list(init_params), num_ps)
@@ -448,6 +463,8 @@ class DeviceAsyncPSServer(_Service):
         store.set(_ipc_key(ps_index, "gpu"), physical_gpu())
         self._done = torch.cuda.Event()
         store.set(_ipc_key(ps_index, "ready"), "1")
+        # after the buffers are published: the workers join the channel once they mapped them
+        self.p2p = p2p if p2p is not None else make_p2p(store, group=group)
 
     def _apply(self, g: torch.Tensor, scale: float = 1.0) -> None:
         from ..ops import _lib, optim  # noqa: F401  (optim registers kfa_adam_step)
@@ -468,12 +485,12 @@ class DeviceAsyncPSServer(_Service):
 
     def _send_vars(self, src: int) -> None:  # a host-transport client (IPC mapping failed on its side)
         self.stage.copy_(self.w)
-        dist.send(self.stage, src, group=self.group, tag=TAG_DATA)
+        self.p2p.send(self.stage, src, tag=TAG_DATA)
 
     def _recv_grad(self, src: int, op: int) -> torch.Tensor:
         if op == PUSH_DEV:
             return self.mail[src]
-        dist.recv(self.stage, src, group=self.group, tag=TAG_DATA)
+        self.p2p.recv(self.stage, src, tag=TAG_DATA)
         self.mail[src].copy_(self.stage, non_blocking=False)
         return self.mail[src]
 
@@ -514,7 +531,8 @@ class DeviceAsyncPSClient(_ClientSteps):
     served over the host transport (``transports[k] == "host"``)."""
 
     def __init__(self, params: Sequence[Tuple[str, torch.nn.Parameter]], num_workers: int, num_ps: int, rank: int,
-                 store, group=None, timeout: float = 300.0, log: Optional[Callable[[str], None]] = None):
+                 store, group=None, timeout: float = 300.0, log: Optional[Callable[[str], None]] = None,
+                 p2p=None):
         import time
 
         from .flat import FlatGroup
@@ -563,7 +581,7 @@ class DeviceAsyncPSClient(_ClientSteps):
                 self.transport_desc.append(f"PS {k}: device ({where})")
             except Exception as e:  # noqa: BLE001 — any mapping failure: fall back, loudly
                 log(f"Worker {rank}: WARNING: HIP IPC mapping of PS {k}'s device buffers failed ({e}); "
-                    f"using the HOST transport for PS {k} (gloo, slower)")
+                    f"using the HOST transport for PS {k} (payloads over the request channel, slower)")
                 self.transports.append("host")
                 self.transport_desc.append(f"PS {k}: host ({e})")
                 w = mail = None
@@ -572,6 +590,7 @@ class DeviceAsyncPSClient(_ClientSteps):
             self.plan.append((num_workers + k, groups, w, mail, stage))
         self._ev: Dict[torch.device, torch.cuda.Event] = {}
         self._init_steps(num_ps)
+        self.p2p = p2p if p2p is not None else make_p2p(store, group=group)
 
     def zero_grad(self) -> None:
         for _, groups, *_ in self.plan:
@@ -585,7 +604,7 @@ class DeviceAsyncPSClient(_ClientSteps):
                 continue
             if stage is not None:
                 self._header(rank, PULL)
-                dist.recv(stage, rank, group=self.group, tag=TAG_DATA)
+                self.p2p.recv(stage, rank, tag=TAG_DATA)
                 src = stage
             else:
                 src = w
@@ -620,7 +639,7 @@ class DeviceAsyncPSClient(_ClientSteps):
                 self._header(rank, PUSH_DEV, self.tags[k])
             else:
                 self._header(rank, PUSH, self.tags[k])
-                dist.send(stage, rank, group=self.group, tag=TAG_DATA)
+                self.p2p.send(stage, rank, tag=TAG_DATA)
         step = -1
         for k, rank, *_ in live:
             s = self._await_reply(k, rank)

@@ -75,6 +75,7 @@ def lib() -> ctypes.CDLL:
         "kfc_broadcast": ([_P, _P, _P, _S, _I, _I, _P], _I),
         "kfc_reduce": ([_P, _P, _P, _S, _I, _I, _I, _P], _I),
         "kfc_send": ([_P, _P, _S, _I, _I, _P], _I), "kfc_recv": ([_P, _P, _S, _I, _I, _P], _I),
+        "kfc_recv_any": ([_P, _P, _S, _I, ctypes.POINTER(_I), _I], _I),
         "kfc_all_to_all_v": ([_P, _P, _P, _P, _P, _P, _P, _I, _P], _I),
         "kfc_group_start": ([_P], _I), "kfc_group_end": ([_P], _I), "kfc_async_error": ([_P], _I),
         "kfc_comm_abort": ([_P], None), "kfc_comm_destroy": ([_P], None),
@@ -224,6 +225,17 @@ class Communicator:
         dt = self._dt(t)
         return self._run([t], lambda s: lib().kfc_recv(self._h, _ptr(t), t.numel(), dt, src, s), "recv", async_op)
 
+    def recv_any(self, t: torch.Tensor, timeout_s: Optional[float] = None) -> int:
+        """Receive one message from whichever rank sends first (host backend, CPU
+        tensors); returns that rank.  Every rank's messages to this one arrive in
+        the order it sent them."""
+        if self.device.type != "cpu":
+            raise CommError("recv_any: host-memory tensors only")
+        src = ctypes.c_int(-1)
+        _check(lib().kfc_recv_any(self._h, _ptr(t), t.numel(), self._dt(t), ctypes.byref(src),
+                                  int((timeout_s or 0) * 1000)), "recv_any")
+        return src.value
+
     def all_to_all_single(self, out: torch.Tensor, inp: torch.Tensor, out_splits: Sequence[int],
                           in_splits: Sequence[int], async_op: bool = False) -> Work:
         """Rows of ``inp`` (``in_splits[p]`` of them to rank p) -> rows of ``out``
@@ -318,6 +330,9 @@ class TorchComm:
         dist.recv(t, src, group=self.pg)
         return Work()
 
+    def recv_any(self, t, timeout_s=None, tag: int = 0) -> int:
+        return dist.recv(t, src=None, group=self.pg, tag=tag)
+
     def all_to_all_single(self, out, inp, out_splits, in_splits, async_op=False):
         return dist.all_to_all_single(out, inp, list(out_splits), list(in_splits), group=self.pg,
                                       async_op=async_op) or Work()
@@ -333,6 +348,59 @@ class TorchComm:
 
     def __repr__(self) -> str:
         return f"TorchComm({dist.get_backend(self.pg) if dist.is_initialized() else 'none'}, {self.world} ranks)"
+
+
+class P2P:
+    """Point-to-point channel of the asynchronous parameter server
+    (``parallel/async_ps.py``): ``send`` / ``recv`` to one rank, ``recv_any`` from
+    whichever rank sends first.  ``native``: the first-party host transport
+    (:class:`Communicator`, ``backend="host"``: per-pair ordered TCP streams, so
+    the protocol's tags are implied by the order of its messages); else
+    ``torch.distributed`` on the default group with the tags (gloo)."""
+
+    def __init__(self, comm=None, group=None):
+        self.comm, self.group = comm, group
+
+    @property
+    def native(self) -> bool:
+        return self.comm is not None
+
+    def send(self, t: torch.Tensor, dst: int, tag: int = 0) -> None:
+        if self.comm is not None:
+            self.comm.send(t, dst)
+        else:
+            dist.send(t, dst, group=self.group, tag=tag)
+
+    def recv(self, t: torch.Tensor, src: int, tag: int = 0) -> None:
+        if self.comm is not None:
+            self.comm.recv(t, src)
+        else:
+            dist.recv(t, src, group=self.group, tag=tag)
+
+    def recv_any(self, t: torch.Tensor, tag: int = 0) -> int:
+        if self.comm is not None:
+            return self.comm.recv_any(t)
+        return dist.recv(t, src=None, group=self.group, tag=tag)
+
+    def destroy(self) -> None:
+        if self.comm is not None:
+            self.comm.destroy()
+            self.comm = None
+
+    def __repr__(self) -> str:
+        return f"P2P({self.comm!r})" if self.comm is not None else "P2P(torch.distributed)"
+
+
+def make_p2p(store=None, mode: Optional[str] = None, timeout_s: Optional[float] = None, group=None) -> P2P:
+    """The async PS control / host-data channel over the default group's ranks:
+    ``KFA_PS_P2P`` = ``native`` (default: the first-party host transport) | ``torch``
+    (gloo; also for a sub-group).  Collective over every rank of the default group."""
+    mode = (mode or os.environ.get("KFA_PS_P2P", "native")).lower()
+    if mode == "torch" or not dist.is_initialized() or (group is not None and group is not dist.group.WORLD):
+        return P2P(None, group)
+    t = timeout_s if timeout_s is not None else float(os.environ.get("KFA_PS_P2P_TIMEOUT", "1800"))
+    return P2P(Communicator.create(store or default_store(), dist.get_rank(), dist.get_world_size(),
+                                   torch.device("cpu"), backend="host", key="kfc/ps_p2p", timeout_s=t))
 
 
 def comm_mode(device: torch.device) -> str:

@@ -254,10 +254,12 @@ def run_ps_async(spec: ClusterSpec, args) -> int:
         server = AsyncPSServer(list(model.named_parameters()), W, P, spec.task_index, lr=args.learning_rate,
                                optimizer=args.optimizer, aggregate=agg)
     _log(f"PS {spec.task_index}: serving {len(server.names)} variables ({server.w.numel()} values), "
-         f"{transport}-resident ({'GPU HBM, HIP IPC pull/push' if transport == 'device' else 'host memory, gloo'}), "
+         f"{transport}-resident ({'GPU HBM, HIP IPC pull/push' if transport == 'device' else 'host memory'}; "
+         f"requests over {server.p2p!r}), "
          + (f"sync replicas: mean of {agg} of {W} workers' gradients per update, stale ones dropped" if agg
             else "async updates"))
     pushes = server.serve(log=_log)
+    server.close()
     _log(f"PS {spec.task_index}: all {W} workers done; {pushes} gradients applied in {server.global_step} updates, "
          f"{server.dropped} stale dropped; exiting")
     dist.destroy_process_group()
@@ -335,6 +337,7 @@ def run_worker_async(spec: ClusterSpec, args) -> int:
         _log(f"Worker {spec.task_index}: {local_step} pushes, {client.pushes_dropped} dropped as stale")
     client.pull()  # evaluate the PS's current variables, as the reference's session does
     client.done()
+    client.close()
     if data is not None:
         with torch.no_grad():
             model.eval()

@@ -255,3 +255,42 @@ def test_make_comm_falls_back_on_every_rank_together(tmp_path):
         assert res["ok"].startswith("Communicator(host"), res
         assert res["fallback"].startswith("TorchComm"), res
         assert res["ok_sum"] == [6.0] * 4 and res["fb_sum"] == [6.0] * 4
+
+
+def _any_worker(rank, world, port, out):
+    sys.path.insert(0, ROOT)
+    import time
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from kubeflow_controller_amd.parallel.comm import make_p2p
+    p2p = make_p2p(mode="native", timeout_s=60)
+    res = {}
+    if rank == 0:
+        got = []
+        buf = torch.zeros(4, dtype=torch.int64)
+        for _ in range(2 * (world - 1)):  # two messages from every peer, in whatever order they arrive
+            src = p2p.recv_any(buf)
+            got.append((src, buf.tolist()))
+        res["got"] = got
+    else:
+        if rank == 1:
+            time.sleep(0.3)  # rank 2's messages first
+        for k in range(2):
+            p2p.send(torch.tensor([rank, k, rank * 10 + k, 7], dtype=torch.int64), 0)
+        p2p.destroy()  # a finished peer closes its connections: rank 0 keeps serving the others
+    torch.save(res, f"{out}.{rank}")
+    dist.destroy_process_group()
+
+
+def test_recv_any_serves_every_peer_in_per_peer_order(tmp_path):
+    """kfc_recv_any (the async PS request loop's receive): messages from whichever
+    rank sends first, each rank's in its send order, peers that closed skipped."""
+    out = str(tmp_path / "any")
+    mp.start_processes(_any_worker, args=(3, _free_port(), out), nprocs=3, join=True, start_method="spawn")
+    got = torch.load(f"{out}.0", weights_only=True)["got"]
+    assert sorted(s for s, _ in got) == [1, 1, 2, 2]
+    for r in (1, 2):
+        mine = [v for s, v in got if s == r]
+        assert mine == [[r, 0, r * 10, 7], [r, 1, r * 10 + 1, 7]]
+    assert got[0][0] == 2  # rank 1 started late

@@ -210,12 +210,12 @@ def test_bert_tiny_cpu_trains():
     assert losses[-1] < losses[0] - 0.5, losses
 
 
-def _async_ps_worker(rank, W, P, port, out):
+def _async_ps_worker(rank, W, P, port, out, p2p="native"):
     sys.path.insert(0, ROOT)
     import torch.distributed as dist
     from kubeflow_controller_amd.parallel.async_ps import AsyncPSClient, AsyncPSServer
     torch.set_num_threads(1)
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), KFA_PS_P2P=p2p)
     dist.init_process_group("gloo", rank=rank, world_size=W + P)
     m = torch.nn.Sequential(torch.nn.Linear(300, 20), torch.nn.Linear(20, 4))
     for p in m.parameters():
@@ -223,7 +223,9 @@ def _async_ps_worker(rank, W, P, port, out):
     if rank >= W:
         s = AsyncPSServer(list(m.named_parameters()), W, P, rank - W, lr=0.25, optimizer="sgd")
         pushes = s.serve()
-        torch.save({"w": s.w, "names": s.names, "pushes": pushes, "step": s.global_step}, f"{out}.ps{rank - W}")
+        torch.save({"w": s.w, "names": s.names, "pushes": pushes, "step": s.global_step, "p2p": repr(s.p2p)},
+                   f"{out}.ps{rank - W}")
+        s.close()
     else:
         c = AsyncPSClient(list(m.named_parameters()), W, P)
         steps = []
@@ -234,18 +236,24 @@ def _async_ps_worker(rank, W, P, port, out):
             steps.append(c.push())
         c.pull()
         c.done()
-        torch.save({"steps": steps, "final": {n: p.detach().clone() for n, p in m.named_parameters()}},
-                   f"{out}.w{rank}")
+        torch.save({"steps": steps, "final": {n: p.detach().clone() for n, p in m.named_parameters()},
+                    "p2p": repr(c.p2p)}, f"{out}.w{rank}")
+        c.close()
     dist.destroy_process_group()
 
 
-def test_async_ps_applies_every_push_exactly_once(tmp_path):
+@pytest.mark.parametrize("p2p", ["native", "torch"])
+def test_async_ps_applies_every_push_exactly_once(tmp_path, p2p):
     """Async PS (reference default mode): any-source service loop, round-robin
-    placement over 2 PS tasks, every worker push applied once; global step from PS 0."""
+    placement over 2 PS tasks, every worker push applied once; global step from PS 0.
+    Request channel: the first-party host transport (csrc/comm, kfc_recv_any) or gloo."""
     W, P = 3, 2
     out = str(tmp_path / "aps")
-    mp.start_processes(_async_ps_worker, args=(W, P, _free_port(), out), nprocs=W + P, join=True,
+    mp.start_processes(_async_ps_worker, args=(W, P, _free_port(), out, p2p), nprocs=W + P, join=True,
                        start_method="spawn")
+    want = "P2P(Communicator(host" if p2p == "native" else "P2P(torch.distributed)"
+    assert all(torch.load(f"{out}.{r}", weights_only=True)["p2p"].startswith(want)
+               for r in ["ps0", "ps1", "w0", "w1", "w2"])
     total = 0.25 * 7 * sum(range(1, W + 1))       # lr * steps * sum of the constant grads
     names = ["0.weight", "0.bias", "1.weight", "1.bias"]
     for k in range(P):
