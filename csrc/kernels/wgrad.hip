@@ -97,6 +97,19 @@ __device__ __forceinline__ short8 tr_operand(const bf16_t* tile, int kb, int cb,
   return short8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 }
 
+// The same transposed read as inline asm, for the hand-counted ping-pong kernel:
+// hipcc puts an s_waitcnt vmcnt(0) in front of every compiler-visible
+// ds_read_b64_tr_b16 that follows an LDS-DMA into the same array (it cannot tell
+// the pieces apart), draining the whole DMA pipeline once per phase; the asm form
+// is ordered by the kernel's own counted vmcnt + s_barrier + lgkmcnt(0) instead.
+// OFF: the read's constant byte offset (piece and k-half), folded into the instruction.
+template <int OFF>
+__device__ __forceinline__ v4i16 ds_tr16(unsigned addr) {
+  v4i16 v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF) : "memory");
+  return v;
+}
+
 // WM x WN waves, each TM x TN MFMA 16x16 tiles: block tile BM = 16*WM*TM output
 // channels x BN = 16*WN*TN (r,s,ci) columns.  OUT_PART: fp32 split-K partials;
 // otherwise the epilogue accumulates straight into the (bf16/fp32) gradient.
@@ -348,6 +361,35 @@ __device__ __forceinline__ void wp_retire(int younger) {  // all but the pieces 
   else wp_vmcnt<0>();
 }
 
+// Diagnostic build only (KFA_WP_STAMP=1: three segments per phase, 2: five):
+// per-segment s_memtime cycle sums of the k-loop of blocks 0..255, waves 0 and 4
+// (one per wave group), read back by kfa_wp_stamps (tools/wgrad_stamps.py).  The
+// stamp's lgkmcnt(0) drains LDS reads in flight, so read shares, not run times.
+#ifndef KFA_WP_STAMP
+#define KFA_WP_STAMP 0
+#endif
+#if KFA_WP_STAMP
+constexpr int kWpSeg = 24;  // [phase 0..3][segment 0..4], prologue, epilogue, k-tiles, spare
+__device__ unsigned g_wp_stamps[256 * 2 * kWpSeg];
+__device__ __forceinline__ unsigned long long wp_now() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define WP_ST(i)                          \
+  do {                                    \
+    const unsigned long long t_ = wp_now(); \
+    wsum[i] += (unsigned)(t_ - wlast);    \
+    wlast = t_;                           \
+  } while (0)
+#else
+#define WP_ST(i) \
+  do {           \
+  } while (0)
+#endif
+
 // GATHER: X is the implicit im2col of an NHWC activation (3x3 / strided / padded
 // convs): an X column n is a fixed (r, s, ci) per lane and piece, its row a pixel k
 // whose (image, p, q) each lane carries per DMA row across k-tiles (the B0 / B1
@@ -372,6 +414,10 @@ __global__ __launch_bounds__(512, 1) void wgrad_pp_kernel(const bf16_t* __restri
   const int ke = min(g.K, kb + g.kchunk);
   if (kb >= ke) return;
   const int nk = (ke - kb + WP_BK - 1) / WP_BK;
+#if KFA_WP_STAMP
+  unsigned wsum[kWpSeg] = {};
+  unsigned long long wlast = wp_now();
+#endif
 
   const __amdgpu_buffer_rsrc_t rA = wrsrc(dY, (unsigned)g.K * (unsigned)g.Co * 2u);
   const __amdgpu_buffer_rsrc_t rB = wrsrc(X, GATHER ? g.x_bytes : (unsigned)g.K * (unsigned)g.Ci * 2u);
@@ -456,9 +502,22 @@ __global__ __launch_bounds__(512, 1) void wgrad_pp_kernel(const bf16_t* __restri
 #pragma unroll
     for (int j = 0; j < TM; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
   short8 a[4][2], b0[2][2], b1[2][2];
-  auto rd = [&](const char* piece, int cb, int ks) -> short8 {
-    return tr_operand<128>(reinterpret_cast<const bf16_t*>(piece), ks * 32, cb, lane);
+  // operand (8 consecutive k of column cb + 4 (lane & 3)) of piece PC, k-half KS of the
+  // k-tile image at `buf`: tr_operand<128>'s two reads with the piece / k-half offsets
+  // as immediates (a k-half is 32 rows: the swizzle repeats every 16)
+  const int tq = (lane & 15) >> 2, tp = lane & 3, tg = lane >> 4;
+  auto rd = [&](const char* buf, auto pc, int cb, auto kc) __attribute__((always_inline)) -> short8 {
+    constexpr int OFF = decltype(pc)::value * WP_PIECE + decltype(kc)::value * 32 * 256;
+    const unsigned b = (unsigned)(uintptr_t)(__attribute__((address_space(3))) const char*)buf;
+    const int col = cb + 4 * tp, r0 = 8 * tg + tq;
+    const v4i16 x = ds_tr16<OFF>(b + (unsigned)img_off<128>(r0, col));
+    const v4i16 y = ds_tr16<OFF>(b + (unsigned)img_off<128>(r0 + 4, col));
+    return short8{x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
   };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
 
   issue(-6, std::integral_constant<int, 0>{}, std::false_type{});
   issue(-5, std::integral_constant<int, 1>{}, std::false_type{});
@@ -469,6 +528,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_pp_kernel(const bf16_t* __restri
   retire(-1, std::false_type{});
   asm volatile("s_barrier" ::: "memory");
   if (wr) asm volatile("s_barrier" ::: "memory");  // group 1 runs one barrier behind
+  WP_ST(20);
 
   auto mfma_q = [&](short8 (&bb)[2][2], int mh, int nh) __attribute__((always_inline)) {
     __builtin_amdgcn_s_setprio(1);
@@ -486,57 +546,77 @@ __global__ __launch_bounds__(512, 1) void wgrad_pp_kernel(const bf16_t* __restri
   auto ktile = [&](int u, auto st) __attribute__((always_inline)) {
     const char* buf = smem + (u & 1) * (4 * WP_PIECE);
     const int P = 4 * u;
-    {  // s0: A0 + B0
-      const char* pa = buf;
-      const char* pb = buf + WP_PIECE;
+    {  // s0: A0 (piece 0) + B0 (piece 1)
 #pragma unroll
       for (int ni = 0; ni < 2; ni++) {
-        b0[ni][0] = rd(pb, wc * 32 + ni * 16, 0);
-        b0[ni][1] = rd(pb, wc * 32 + ni * 16, 1);
+        b0[ni][0] = rd(buf, I1{}, wc * 32 + ni * 16, I0{});
+        b0[ni][1] = rd(buf, I1{}, wc * 32 + ni * 16, I1{});
       }
 #pragma unroll
       for (int mi = 0; mi < 4; mi++) {
-        a[mi][0] = rd(pa, wr * 64 + mi * 16, 0);
-        a[mi][1] = rd(pa, wr * 64 + mi * 16, 1);
+        a[mi][0] = rd(buf, I0{}, wr * 64 + mi * 16, I0{});
+        a[mi][1] = rd(buf, I0{}, wr * 64 + mi * 16, I1{});
       }
-      issue(P, std::integral_constant<int, 2>{}, st);
+      issue(P, I2{}, st);
+      if (KFA_WP_STAMP >= 2) WP_ST(3);
       retire(P, st);
+      if (KFA_WP_STAMP >= 2) WP_ST(4);
       asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);  // the MFMAs read the asm reads' registers: keep them behind the wait
+      WP_ST(0);
       mfma_q(b0, 0, 0);
+      WP_ST(1);
       asm volatile("s_barrier" ::: "memory");
+      WP_ST(2);
     }
-    {  // s1: B1
-      const char* pb = buf + 2 * WP_PIECE;
+    {  // s1: B1 (piece 2)
 #pragma unroll
       for (int ni = 0; ni < 2; ni++) {
-        b1[ni][0] = rd(pb, wc * 32 + ni * 16, 0);
-        b1[ni][1] = rd(pb, wc * 32 + ni * 16, 1);
+        b1[ni][0] = rd(buf, I2{}, wc * 32 + ni * 16, I0{});
+        b1[ni][1] = rd(buf, I2{}, wc * 32 + ni * 16, I1{});
       }
-      issue(P + 1, std::integral_constant<int, 3>{}, st);
+      issue(P + 1, I3{}, st);
+      if (KFA_WP_STAMP >= 2) WP_ST(8);
       retire(P + 1, st);
+      if (KFA_WP_STAMP >= 2) WP_ST(9);
       asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      WP_ST(5);
       mfma_q(b1, 0, 1);
+      WP_ST(6);
       asm volatile("s_barrier" ::: "memory");
+      WP_ST(7);
     }
-    {  // s2: A1
-      const char* pa = buf + 3 * WP_PIECE;
+    {  // s2: A1 (piece 3)
 #pragma unroll
       for (int mi = 0; mi < 4; mi++) {
-        a[mi][0] = rd(pa, wr * 64 + mi * 16, 0);
-        a[mi][1] = rd(pa, wr * 64 + mi * 16, 1);
+        a[mi][0] = rd(buf, I3{}, wr * 64 + mi * 16, I0{});
+        a[mi][1] = rd(buf, I3{}, wr * 64 + mi * 16, I1{});
       }
-      issue(P + 2, std::integral_constant<int, 0>{}, st);
+      issue(P + 2, I0{}, st);
+      if (KFA_WP_STAMP >= 2) WP_ST(13);
       retire(P + 2, st);
+      if (KFA_WP_STAMP >= 2) WP_ST(14);
       asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      WP_ST(10);
       mfma_q(b1, 1, 1);
+      WP_ST(11);
       asm volatile("s_barrier" ::: "memory");
+      WP_ST(12);
     }
     {  // s3: registers only
-      issue(P + 3, std::integral_constant<int, 1>{}, st);
+      issue(P + 3, I1{}, st);
+      if (KFA_WP_STAMP >= 2) WP_ST(18);
       retire(P + 3, st);
+      if (KFA_WP_STAMP >= 2) WP_ST(19);
       asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      WP_ST(15);
       mfma_q(b0, 1, 0);
+      WP_ST(16);
       asm volatile("s_barrier" ::: "memory");
+      WP_ST(17);
     }
   };
   int u = 0;
@@ -570,7 +650,23 @@ __global__ __launch_bounds__(512, 1) void wgrad_pp_kernel(const bf16_t* __restri
       }
     }
   }
+#if KFA_WP_STAMP
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the partial tile's stores drained
+  WP_ST(21);
+  wsum[22] = (unsigned)nk;
+  if (lane == 0 && bid < 256 && (wave & 3) == 0) {
+#pragma unroll
+    for (int i = 0; i < kWpSeg; i++) g_wp_stamps[(bid * 2 + wr) * kWpSeg + i] = wsum[i];
+  }
+#endif
 }
+
+#if KFA_WP_STAMP
+KFA_API int kfa_wp_stamps(unsigned* out, int n) {
+  if (n > 256 * 2 * kWpSeg) n = 256 * 2 * kWpSeg;
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wp_stamps), (size_t)n * sizeof(unsigned), 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 // grad[i] (+)= sum_s part[s][i].  Block = 64 element-lanes (4 elements each)
 // x 4 split-lanes; each thread keeps 8 independent loads in flight (the split
