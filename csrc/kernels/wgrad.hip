@@ -501,7 +501,19 @@ __global__ __launch_bounds__(512, 1) void wgrad_pp_kernel(const bf16_t* __restri
   for (int i = 0; i < TN; i++)
 #pragma unroll
     for (int j = 0; j < TM; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-  short8 a[4][2], b0[2][2], b1[2][2];
+  // Operand registers: ah = A rows 32-63 of the wave's current 64-row half (MFMA rows
+  // mi 2-3), b0 = B0, and two slots sx / sy that alternate, k-tile by k-tile, between
+  // A rows 0-31 (mi 0-1) and B1.  The next k-tile's A0 rows 0-31 go into the slot B1
+  // vacates after phase 2, in phase 3 (whose reads were empty), so the four phases
+  // read 16 / 8 / 16 / 8 operands instead of 24 / 8 / 16 / 0: the 24-read phase ran
+  // 600+ cycles against the partner group's ~300 of MFMAs (tools/wgrad_stamps.py).
+  // A0 (piece 0) of k-tile u + 1 was DMA'd at phase 4u - 2, five phases before that
+  // read (retired by phase 4u + 2's vmcnt, published by its barrier) — the same
+  // distance as every other piece.
+  // (BAL; the gathered variant keeps the 24 / 8 / 16 / 0 order: with its per-lane pixel
+  // state the next image's addresses spill)
+  constexpr bool BAL = !GATHER;
+  short8 ah[2][2], b0[2][2], sx[2][2], sy[2][2];
   // operand (8 consecutive k of column cb + 4 (lane & 3)) of piece PC, k-half KS of the
   // k-tile image at `buf`: tr_operand<128>'s two reads with the piece / k-half offsets
   // as immediates (a k-half is 32 rows: the swizzle repeats every 16)
@@ -518,6 +530,22 @@ __global__ __launch_bounds__(512, 1) void wgrad_pp_kernel(const bf16_t* __restri
   using I1 = std::integral_constant<int, 1>;
   using I2 = std::integral_constant<int, 2>;
   using I3 = std::integral_constant<int, 3>;
+  // A rows 16 h .. 16 h + 31 of the wave's 64-row half (piece PC) into `dst`; B columns
+  // (piece PC) of the wave into `dst`
+  auto rd_a = [&](short8 (&dst)[2][2], const char* buf, auto pc, int h) __attribute__((always_inline)) {
+#pragma unroll
+    for (int mi = 0; mi < 2; mi++) {
+      dst[mi][0] = rd(buf, pc, wr * 64 + (h + mi) * 16, I0{});
+      dst[mi][1] = rd(buf, pc, wr * 64 + (h + mi) * 16, I1{});
+    }
+  };
+  auto rd_b = [&](short8 (&dst)[2][2], const char* buf, auto pc) __attribute__((always_inline)) {
+#pragma unroll
+    for (int ni = 0; ni < 2; ni++) {
+      dst[ni][0] = rd(buf, pc, wc * 32 + ni * 16, I0{});
+      dst[ni][1] = rd(buf, pc, wc * 32 + ni * 16, I1{});
+    }
+  };
 
   issue(-6, std::integral_constant<int, 0>{}, std::false_type{});
   issue(-5, std::integral_constant<int, 1>{}, std::false_type{});
@@ -528,9 +556,11 @@ __global__ __launch_bounds__(512, 1) void wgrad_pp_kernel(const bf16_t* __restri
   retire(-1, std::false_type{});
   asm volatile("s_barrier" ::: "memory");
   if (wr) asm volatile("s_barrier" ::: "memory");  // group 1 runs one barrier behind
+  if constexpr (BAL) rd_a(sx, smem, I0{}, 0);  // k-tile 0's A0 rows 0-31 (retired and published above)
   WP_ST(20);
 
-  auto mfma_q = [&](short8 (&bb)[2][2], int mh, int nh) __attribute__((always_inline)) {
+  // quadrant (mh, nh) of the wave tile: A rows mi 0-1 from `alo`, 2-3 from ah
+  auto mfma_q = [&](short8 (&alo)[2][2], short8 (&bb)[2][2], int mh, int nh) __attribute__((always_inline)) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int ks = 0; ks < 2; ks++)
@@ -538,25 +568,20 @@ __global__ __launch_bounds__(512, 1) void wgrad_pp_kernel(const bf16_t* __restri
       for (int ni = 0; ni < 2; ni++)
 #pragma unroll
         for (int mi = 0; mi < 4; mi++)
-          acc[nh * 2 + ni][mh * 4 + mi] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[ni][ks], a[mi][ks], acc[nh * 2 + ni][mh * 4 + mi], 0, 0, 0);
+          acc[nh * 2 + ni][mh * 4 + mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              bb[ni][ks], mi < 2 ? alo[mi][ks] : ah[mi - 2][ks], acc[nh * 2 + ni][mh * 4 + mi], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
 
-  auto ktile = [&](int u, auto st) __attribute__((always_inline)) {
+  // k-tile u; sp holds its A0 rows 0-31 on entry, sq is free (and holds the next
+  // k-tile's A0 rows 0-31 on exit)
+  auto ktile = [&](int u, auto st, short8 (&sp)[2][2], short8 (&sq)[2][2]) __attribute__((always_inline)) {
     const char* buf = smem + (u & 1) * (4 * WP_PIECE);
     const int P = 4 * u;
-    {  // s0: A0 (piece 0) + B0 (piece 1)
-#pragma unroll
-      for (int ni = 0; ni < 2; ni++) {
-        b0[ni][0] = rd(buf, I1{}, wc * 32 + ni * 16, I0{});
-        b0[ni][1] = rd(buf, I1{}, wc * 32 + ni * 16, I1{});
-      }
-#pragma unroll
-      for (int mi = 0; mi < 4; mi++) {
-        a[mi][0] = rd(buf, I0{}, wr * 64 + mi * 16, I0{});
-        a[mi][1] = rd(buf, I0{}, wr * 64 + mi * 16, I1{});
-      }
+    {  // s0: A0 rows 32-63 (piece 0) + B0 (piece 1)
+      if constexpr (!BAL) rd_a(sp, buf, I0{}, 0);
+      rd_a(ah, buf, I0{}, 2);
+      rd_b(b0, buf, I1{});
       issue(P, I2{}, st);
       if (KFA_WP_STAMP >= 2) WP_ST(3);
       retire(P, st);
@@ -564,17 +589,13 @@ __global__ __launch_bounds__(512, 1) void wgrad_pp_kernel(const bf16_t* __restri
       asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);  // the MFMAs read the asm reads' registers: keep them behind the wait
       WP_ST(0);
-      mfma_q(b0, 0, 0);
+      mfma_q(sp, b0, 0, 0);
       WP_ST(1);
       asm volatile("s_barrier" ::: "memory");
       WP_ST(2);
     }
-    {  // s1: B1 (piece 2)
-#pragma unroll
-      for (int ni = 0; ni < 2; ni++) {
-        b1[ni][0] = rd(buf, I2{}, wc * 32 + ni * 16, I0{});
-        b1[ni][1] = rd(buf, I2{}, wc * 32 + ni * 16, I1{});
-      }
+    {  // s1: B1 (piece 2) into the free slot
+      rd_b(sq, buf, I2{});
       issue(P + 1, I3{}, st);
       if (KFA_WP_STAMP >= 2) WP_ST(8);
       retire(P + 1, st);
@@ -582,17 +603,14 @@ __global__ __launch_bounds__(512, 1) void wgrad_pp_kernel(const bf16_t* __restri
       asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       WP_ST(5);
-      mfma_q(b1, 0, 1);
+      mfma_q(sp, sq, 0, 1);
       WP_ST(6);
       asm volatile("s_barrier" ::: "memory");
       WP_ST(7);
     }
-    {  // s2: A1 (piece 3)
-#pragma unroll
-      for (int mi = 0; mi < 4; mi++) {
-        a[mi][0] = rd(buf, I3{}, wr * 64 + mi * 16, I0{});
-        a[mi][1] = rd(buf, I3{}, wr * 64 + mi * 16, I1{});
-      }
+    {  // s2: A1 (piece 3): rows 0-31 into sp (A0's are done), 32-63 into ah
+      rd_a(sp, buf, I3{}, 0);
+      rd_a(ah, buf, I3{}, 2);
       issue(P + 2, I0{}, st);
       if (KFA_WP_STAMP >= 2) WP_ST(13);
       retire(P + 2, st);
@@ -600,12 +618,14 @@ __global__ __launch_bounds__(512, 1) void wgrad_pp_kernel(const bf16_t* __restri
       asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       WP_ST(10);
-      mfma_q(b1, 1, 1);
+      mfma_q(sp, sq, 1, 1);
       WP_ST(11);
       asm volatile("s_barrier" ::: "memory");
       WP_ST(12);
     }
-    {  // s3: registers only
+    {  // s3: the next k-tile's A0 rows 0-31 into sq (B1 is done)
+      if constexpr (BAL)
+        if (decltype(st)::value || u + 1 < nk) rd_a(sq, smem + ((u + 1) & 1) * (4 * WP_PIECE), I0{}, 0);
       issue(P + 3, I1{}, st);
       if (KFA_WP_STAMP >= 2) WP_ST(18);
       retire(P + 3, st);
@@ -613,15 +633,26 @@ __global__ __launch_bounds__(512, 1) void wgrad_pp_kernel(const bf16_t* __restri
       asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       WP_ST(15);
-      mfma_q(b0, 1, 0);
+      mfma_q(sp, b0, 1, 0);
       WP_ST(16);
       asm volatile("s_barrier" ::: "memory");
       WP_ST(17);
     }
   };
   int u = 0;
-  for (; u + 2 < nk; u++) ktile(u, std::true_type{});
-  for (; u < nk; u++) ktile(u, std::false_type{});
+  if constexpr (BAL) {
+    for (; u + 3 < nk; u += 2) {  // steady (u + 2 < nk) pairs: the slots swap roles every k-tile
+      ktile(u, std::true_type{}, sx, sy);
+      ktile(u + 1, std::true_type{}, sy, sx);
+    }
+    // the last 1-3 k-tiles (u even here)
+    if (u < nk) ktile(u, std::false_type{}, sx, sy);
+    if (u + 1 < nk) ktile(u + 1, std::false_type{}, sy, sx);
+    if (u + 2 < nk) ktile(u + 2, std::false_type{}, sx, sy);
+  } else {
+    for (; u + 2 < nk; u++) ktile(u, std::true_type{}, sx, sy);
+    for (; u < nk; u++) ktile(u, std::false_type{}, sx, sy);
+  }
   if (!wr) asm volatile("s_barrier" ::: "memory");  // both groups at the same barrier count
 
   // acc[ni][mi] = D[m = m0 + 128 wr + 16 mi + fr][n = n0 + 64 wc + 16 ni + 4 fq + r]

@@ -14,11 +14,11 @@ done
 paste $O/wg_ab.txt $O/wg_new.txt | awk '{print $2, $3, $6, "->", $10, $13}'
 KFA_KERNELS_SO=_hip_kernels_st1.so timeout -k 10 180 python3 -u tools/wgrad_stamps.py 32768x2304x768 32768x768x768 > $O/st1.txt 2>&1 || { tail -20 $O/st1.txt; exit 1; }
 cat $O/st1.txt
-for i in 1 2; do
+for i in 1 2 3; do
   for v in ab new; do
     so=_hip_kernels.so; [[ $v == ab ]] && so=_hip_kernels_ab.so
     r=$(KFA_KERNELS_SO=$so timeout -k 10 300 python3 -u tools/bench_model.py --model bert_base --batch 256 --seq 128 --steps 20 --warmup 5 2>$O/bert_$v.err | tail -1) || { tail -20 $O/bert_$v.err; exit 1; }
     echo "bert $v $(echo "$r" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'])")"
   done
 done
-ABSO=_hip_kernels_ab.so timeout -k 10 900 bash tools/gpu_ab_so.sh
+[[ -n "$WG_R50" ]] && ABSO=_hip_kernels_ab.so timeout -k 10 900 bash tools/gpu_ab_so.sh
