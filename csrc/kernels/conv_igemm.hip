@@ -492,13 +492,13 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
         for (int mi = 0; mi < TM; mi++)
           acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[ks][ni], af[ks][mi], acc[ni][mi], 0, 0, 0);
     };
+    auto rd = [&](const bf16_t* p) {
+      short8 v;
+      const unsigned la = (unsigned)(uintptr_t)(__attribute__((address_space(3))) const bf16_t*)p;
+      asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(la) : "memory");
+      return v;
+    };
     if constexpr (TM + 2 * TN <= 15) {
-      auto rd = [&](const bf16_t* p) {
-        short8 v;
-        const unsigned la = (unsigned)(uintptr_t)(__attribute__((address_space(3))) const bf16_t*)p;
-        asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(la) : "memory");
-        return v;
-      };
 #pragma unroll
       for (int i = 0; i < TN; i++) bf[0][i] = rd(Bb + swz(wn * TN * 16 + i * 16 + fr, fq));
 #pragma unroll
@@ -514,6 +514,23 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
       lgkm_wait<0>();
       __builtin_amdgcn_sched_barrier(0);
       mfma(1);
+    } else if constexpr (PRO) {
+      // 8-wave 256x256 tiles with the BatchNorm prologue: one k-half's 12 reads, wait,
+      // its MFMAs.  Inline asm: with compiler-visible reads hipcc waited vmcnt(0) — the
+      // NEXT slice's register loads and DMAs, issued at the top of the step — before
+      // every step's first read (the plain variants keep the compiler's form below: no
+      // such wait there, and its counted lgkmcnt interleave)
+#pragma unroll
+      for (int ks = 0; ks < 2; ks++) {
+#pragma unroll
+        for (int i = 0; i < TM; i++) af[ks][i] = rd(Ab + swz(wm * TM * 16 + i * 16 + fr, ks * 4 + fq));
+#pragma unroll
+        for (int i = 0; i < TN; i++) bf[ks][i] = rd(Bb + swz(wn * TN * 16 + i * 16 + fr, ks * 4 + fq));
+        lgkm_wait<0>();
+        __builtin_amdgcn_sched_barrier(0);
+        mfma(ks);
+        __builtin_amdgcn_sched_barrier(0);
+      }
     } else {
 #pragma unroll
       for (int ks = 0; ks < 2; ks++) {
@@ -549,9 +566,19 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
       const int c = pr_ch + pr_cs;
       float sc[8], sh[8];
       {
-        const float4 a0 = *reinterpret_cast<const float4*>(ssl + c), a1 = *reinterpret_cast<const float4*>(ssl + c + 4);
-        const float4 b0 = *reinterpret_cast<const float4*>(ssl + g.C + c);
-        const float4 b1 = *reinterpret_cast<const float4*>(ssl + g.C + c + 4);
+        // inline-asm reads: compiler-visible ones got an s_waitcnt vmcnt(0) (draining the
+        // next slice's B DMAs) in front of them
+        typedef __attribute__((ext_vector_type(4))) float f32x4;
+        f32x4 v[4];
+        const unsigned la = (unsigned)(uintptr_t)(__attribute__((address_space(3))) const float*)(ssl + c);
+        const unsigned lb = (unsigned)(uintptr_t)(__attribute__((address_space(3))) const float*)(ssl + g.C + c);
+        asm volatile("ds_read_b128 %0, %1" : "=v"(v[0]) : "v"(la) : "memory");
+        asm volatile("ds_read_b128 %0, %1 offset:16" : "=v"(v[1]) : "v"(la) : "memory");
+        asm volatile("ds_read_b128 %0, %1" : "=v"(v[2]) : "v"(lb) : "memory");
+        asm volatile("ds_read_b128 %0, %1 offset:16" : "=v"(v[3]) : "v"(lb) : "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]) :: "memory");
+        const float4 a0 = make_float4(v[0][0], v[0][1], v[0][2], v[0][3]), a1 = make_float4(v[1][0], v[1][1], v[1][2], v[1][3]);
+        const float4 b0 = make_float4(v[2][0], v[2][1], v[2][2], v[2][3]), b1 = make_float4(v[3][0], v[3][1], v[3][2], v[3][3]);
         sc[0] = a0.x; sc[1] = a0.y; sc[2] = a0.z; sc[3] = a0.w; sc[4] = a1.x; sc[5] = a1.y; sc[6] = a1.z; sc[7] = a1.w;
         sh[0] = b0.x; sh[1] = b0.y; sh[2] = b0.z; sh[3] = b0.w; sh[4] = b1.x; sh[5] = b1.y; sh[6] = b1.z; sh[7] = b1.w;
       }
@@ -563,7 +590,13 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(const bf16_
 #pragma unroll
         for (int j = 0; j < 8; j++) f[j] = ok ? fmaxf(fmaf(f[j], sc[j], sh[j]), 0.f) : 0.f;
         uint4 o = pack8(f);
-        *reinterpret_cast<uint4*>(As + buf * BM * BK + (i * RPP + wave * 8) * BK + lane * 8) = o;
+        {  // inline asm: a compiler-visible LDS store got an s_waitcnt vmcnt(0) for the DMAs in flight
+          typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+          const u32x4 w = {o.x, o.y, o.z, o.w};
+          const unsigned la = (unsigned)(uintptr_t)(__attribute__((address_space(3))) bf16_t*)(
+              As + buf * BM * BK + (i * RPP + wave * 8) * BK + lane * 8);
+          asm volatile("ds_write_b128 %0, %1" ::"v"(la), "v"(w) : "memory");
+        }
         if (pr_y) {
           __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<decltype(__builtin_amdgcn_raw_buffer_load_b128(rY, 0, 0, 0))*>(&o),
                                                  rY, (unsigned)pr_vo[i], (unsigned)pr_soff, 0);

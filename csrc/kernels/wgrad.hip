@@ -110,6 +110,18 @@ __device__ __forceinline__ v4i16 ds_tr16(unsigned addr) {
   return v;
 }
 
+// tr_operand through ds_tr16: k-half KS's row offset (32 rows; the swizzle repeats
+// every 16) as the immediate
+template <int WIDTH, int KS>
+__device__ __forceinline__ short8 tr_operand_asm(const bf16_t* tile, int cb, int lane) {
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const int col = cb + 4 * p, r0 = 8 * g + q;
+  const unsigned b = (unsigned)(uintptr_t)(__attribute__((address_space(3))) const bf16_t*)tile;
+  const v4i16 a = ds_tr16<KS * 32 * WIDTH * 2>(b + (unsigned)img_off<WIDTH>(r0, col));
+  const v4i16 c = ds_tr16<KS * 32 * WIDTH * 2>(b + (unsigned)img_off<WIDTH>(r0 + 4, col));
+  return short8{a[0], a[1], a[2], a[3], c[0], c[1], c[2], c[3]};
+}
+
 // WM x WN waves, each TM x TN MFMA 16x16 tiles: block tile BM = 16*WM*TM output
 // channels x BN = 16*WN*TN (r,s,ci) columns.  OUT_PART: fp32 split-K partials;
 // otherwise the epilogue accumulates straight into the (bf16/fp32) gradient.
@@ -272,25 +284,55 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_kernel(const bf16_t* __
     }
     const bf16_t* At = As + buf * BKW * BM;
     const bf16_t* Bt = Bs + buf * BKW * BN;
-#pragma unroll
-    for (int ks = 0; ks < 2; ks++) {
-      short8 af[TM], bf[TN];
+    // Operand reads as inline asm (tr_operand_asm): hipcc waited vmcnt(0) in front of
+    // the builtin reads — for the NEXT step's DMAs issued just above — so no step's
+    // loads overlapped its own MFMAs.  The waits are explicit: both k-halves' reads,
+    // a counted wait for k-half 0's, its MFMAs (k-half 1's reads still landing), a
+    // wait, k-half 1's MFMAs; the 8-wave variant (at the VGPR limit) reads, waits and
+    // multiplies one k-half at a time.
+    constexpr bool PIPE = NW < 8;
+    short8 af[2][TM], bf[2][TN];
+    auto rd_ks = [&](auto kc) __attribute__((always_inline)) {
+      constexpr int ks = decltype(kc)::value;
 #pragma unroll
       for (int i = 0; i < TM; i++) {
         const int c = wm * TM * 16 + i * 16;  // within one sub-image (TM * 16 <= 128, aligned)
-        af[i] = tr_operand<WA>(At + (c / WA) * BKW * WA, ks * 32, c % WA, lane);
+        af[ks][i] = tr_operand_asm<WA, ks>(At + (c / WA) * BKW * WA, c % WA, lane);
       }
 #pragma unroll
       for (int i = 0; i < TN; i++) {
         const int c = wn * TN * 16 + i * 16;
-        bf[i] = tr_operand<WB>(Bt + (c / WB) * BKW * WB, ks * 32, c % WB, lane);
+        bf[ks][i] = tr_operand_asm<WB, ks>(Bt + (c / WB) * BKW * WB, c % WB, lane);
       }
+    };
+    auto mfma_ks = [&](int ks) __attribute__((always_inline)) {
 #pragma unroll
       for (int ni = 0; ni < TN; ni++)
 #pragma unroll
         for (int mi = 0; mi < TM; mi++)
-          acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[ni], af[mi], acc[ni][mi], 0, 0, 0);
+          acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[ks][ni], af[ks][mi], acc[ni][mi], 0, 0, 0);
+    };
+    rd_ks(std::integral_constant<int, 0>{});
+    if constexpr (PIPE) {
+      // both k-halves' reads in flight; k-half 0's retired = at most RH younger ones
+      // outstanding (the 4-bit counter caps the count at 15: a read more is waited for)
+      constexpr int RH = 2 * (TM + TN) < 15 ? 2 * (TM + TN) : 15;
+      rd_ks(std::integral_constant<int, 1>{});
+      asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(RH) : "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_ks(0);
+      __builtin_amdgcn_sched_barrier(0);
+    } else {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_ks(0);
+      __builtin_amdgcn_sched_barrier(0);
+      rd_ks(std::integral_constant<int, 1>{});
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_ks(1);
+    __builtin_amdgcn_sched_barrier(0);
     lds_barrier();
   }
   // lane holds D[n = .. + (lane>>4)*4 + i][m = .. + (lane&15)]: 4 consecutive n per store
