@@ -674,6 +674,35 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
 // DMA retire behind it (profiles/r3_gemm_ppp.txt); here the burst drains from
 // group 1's counter while group 0's pipeline keeps running.  LDS: 128 KB ring +
 // 32 KB hand-off = the CU's whole 160 KB.  No split remainder (data-parallel tiles).
+// Diagnostic build only (KFA_PW_STAMP=1: three segments per phase, 2: five): per-
+// segment s_memtime cycle sums of gemm_ppw_kernel's k-loop for blocks 0..255, waves 0
+// (DMA group) and 4 (store group), read back by kfa_pw_stamps (tools/ppw_stamps.py).
+// The stamp's lgkmcnt(0) drains LDS reads in flight: read shares, not run times.
+#ifndef KFA_PW_STAMP
+#define KFA_PW_STAMP 0
+#endif
+#if KFA_PW_STAMP
+constexpr int kPwSeg = 24;  // [phase 0..3][segment 0..4], prologue, epilogue, k-tiles, spare
+__device__ unsigned g_pw_stamps[256 * 2 * kPwSeg];
+__device__ __forceinline__ unsigned long long pw_now() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define PW_ST(i)                            \
+  do {                                      \
+    const unsigned long long t_ = pw_now(); \
+    psum[i] += (unsigned)(t_ - plast_t);    \
+    plast_t = t_;                           \
+  } while (0)
+#else
+#define PW_ST(i) \
+  do {           \
+  } while (0)
+#endif
+
 constexpr int HANDOFF = 16384;  // bytes per hand-off half: 4 waves x 64 rows x 32 cols x bf16
 
 // DACT: the GELU-backward epilogue (the BERT FFN-down data gradient dz = (df2 · W2) *
@@ -698,6 +727,10 @@ __global__ __launch_bounds__(512, 1) void gemm_ppw_kernel(PppArgs g) {
   const int my_tiles = lc < ntiles ? (ntiles - 1 - lc) / nwg + 1 : 0;
   const int J = my_tiles * nk;
   if (J == 0) return;
+#if KFA_PW_STAMP
+  unsigned psum[kPwSeg] = {};
+  unsigned long long plast_t = pw_now();
+#endif
   constexpr int GM = 4;
   auto tile_mn = [&](int i, int& m0, int& n0) __attribute__((always_inline)) {
     const int wg = lc + i * nwg;
@@ -924,6 +957,20 @@ __global__ __launch_bounds__(512, 1) void gemm_ppw_kernel(PppArgs g) {
   if (loader) vm_wait<4 * DW>();
   asm volatile("s_barrier" ::: "memory");
   if (wr) asm volatile("s_barrier" ::: "memory");
+  // B0 of k-tile u is read at the end of k-tile u - 1 (after its last MFMAs, which were
+  // the last use of b0) instead of with A0 in phase 0: the 12-read phase ran ~800
+  // cycles against ~450 for the others (tools/ppw_stamps.py).  Not in the DACT variant
+  // (register-bound: b0 live across the boundary phase spills)
+  auto rd_b0 = [&](int u) __attribute__((always_inline)) {
+    const char* pb = smem + (u & 1) * (4 * PIECE) + PIECE + wc * 32 * 128;
+#pragma unroll
+    for (int ni = 0; ni < 2; ni++) {
+      b0[ni][0] = *reinterpret_cast<const short8*>(pb + ni * 16 * 128 + ro0);
+      b0[ni][1] = *reinterpret_cast<const short8*>(pb + ni * 16 * 128 + ro1);
+    }
+  };
+  if constexpr (!DACT) rd_b0(0);
+  PW_ST(20);
 
   int cm0, cn0, pm0 = 0, pn0 = 0;
   tile_mn(0, cm0, cn0);
@@ -937,15 +984,11 @@ __global__ __launch_bounds__(512, 1) void gemm_ppw_kernel(PppArgs g) {
   };
   auto ktile = [&](int u, auto mode, bool pre = false) __attribute__((always_inline)) {
     constexpr bool EPI = decltype(mode)::value;
+    if (KFA_PW_STAMP == 3) PW_ST(19);  // k-tile entry: the previous k-tile's tail (advance, loop branch)
     const char* buf = smem + (u & 1) * (4 * PIECE);
-    {  // s0: A0 + B0 -> quadrant (0, 0)
+    {  // s0: A0 (B0 was read at the end of the previous k-tile; DACT: here) -> quadrant (0, 0)
       const char* pa = buf + wr * 64 * 128;
-      const char* pb = buf + PIECE + wc * 32 * 128;
-#pragma unroll
-      for (int ni = 0; ni < 2; ni++) {
-        b0[ni][0] = rd(pb + ni * 16 * 128 + ro0);
-        b0[ni][1] = rd(pb + ni * 16 * 128 + ro1);
-      }
+      if constexpr (DACT) rd_b0(u);
 #pragma unroll
       for (int mi = 0; mi < 4; mi++) {
         a[mi][0] = rd(pa + mi * 16 * 128 + ro0);
@@ -953,10 +996,15 @@ __global__ __launch_bounds__(512, 1) void gemm_ppw_kernel(PppArgs g) {
       }
       if constexpr (EPI) epi(0, 0, 0, pm0, pn0);
       issue(std::integral_constant<int, 2>{}, u + 1);
+      if (KFA_PW_STAMP == 2) PW_ST(3);
       retire(EPI);
+      if (KFA_PW_STAMP == 2) PW_ST(4);
       asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      PW_ST(0);
       mfma_q(b0, 0, 0);
+      PW_ST(1);
       asm volatile("s_barrier" ::: "memory");
+      PW_ST(2);
     }
     {  // s1: B1 -> quadrant (0, 1)
       const char* pb = buf + 2 * PIECE + wc * 32 * 128;
@@ -967,10 +1015,15 @@ __global__ __launch_bounds__(512, 1) void gemm_ppw_kernel(PppArgs g) {
       }
       if constexpr (EPI) epi(0, 1, 1, pm0, pn0);
       issue(std::integral_constant<int, 3>{}, u + 1);
+      if (KFA_PW_STAMP == 2) PW_ST(8);
       retire(EPI);
+      if (KFA_PW_STAMP == 2) PW_ST(9);
       asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      PW_ST(5);
       mfma_q(b1, 0, 1);
+      PW_ST(6);
       asm volatile("s_barrier" ::: "memory");
+      PW_ST(7);
     }
     {  // s2: A1 -> quadrant (1, 1)
       const char* pa = buf + 3 * PIECE + wr * 64 * 128;
@@ -981,19 +1034,30 @@ __global__ __launch_bounds__(512, 1) void gemm_ppw_kernel(PppArgs g) {
       }
       if constexpr (EPI) epi(1, 1, 0, pm0, pn0);
       issue(std::integral_constant<int, 0>{}, u + 2);
+      if (KFA_PW_STAMP == 2) PW_ST(13);
       retire(EPI);
+      if (KFA_PW_STAMP == 2) PW_ST(14);
       asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      PW_ST(10);
       mfma_q(b1, 1, 1);
+      PW_ST(11);
       asm volatile("s_barrier" ::: "memory");
+      PW_ST(12);
     }
     {  // s3: registers only -> quadrant (1, 0)
       if constexpr (EPI) epi(1, 0, 1, pm0, pn0);
       (void)pre;
       issue(std::integral_constant<int, 1>{}, u + 2);
+      if (KFA_PW_STAMP == 2) PW_ST(18);
       retire(EPI);
+      if (KFA_PW_STAMP == 2) PW_ST(19);
       asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      PW_ST(15);
       mfma_q(b0, 1, 0);
+      PW_ST(16);
+      if constexpr (!DACT) rd_b0(u + 1);  // the next k-tile's B0 (retired by this phase's vmcnt, published by its first barrier)
       asm volatile("s_barrier" ::: "memory");
+      PW_ST(17);
     }
     advance(true);
     advance(false);
@@ -1030,6 +1094,14 @@ __global__ __launch_bounds__(512, 1) void gemm_ppw_kernel(PppArgs g) {
     tail(1, 0);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail's zero-fill DMAs land before the LDS is released
+#if KFA_PW_STAMP
+  PW_ST(21);
+  psum[22] = (unsigned)J;
+  if (lane == 0 && bid < 256 && (wave & 3) == 0) {
+#pragma unroll
+    for (int i = 0; i < kPwSeg; i++) g_pw_stamps[(bid * 2 + wr) * kPwSeg + i] = psum[i];
+  }
+#endif
 }
 
 // out[c] (+)= sum over rows of part[r][c] (the DACT epilogue's column-sum bands):
@@ -1048,6 +1120,13 @@ __global__ __launch_bounds__(256) void colpart_reduce(const float* __restrict__ 
     out[c] = accumulate ? out[c] + t : t;
   }
 }
+
+#if KFA_PW_STAMP
+KFA_API int kfa_pw_stamps(unsigned* out, int n) {
+  if (n > 256 * 2 * kPwSeg) n = 256 * 2 * kPwSeg;
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pw_stamps), (size_t)n * sizeof(unsigned), 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 int ppp_cus() {
   static int c = 0;

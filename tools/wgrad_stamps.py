@@ -37,15 +37,25 @@ def run(rows: int, co: int, ci: int) -> None:
     for _ in range(20):
         wgrad_into(x, dy, out, 1, 1, rows, ci, 1, rows, co, 1, 1, 1, 0, accumulate=True)
     torch.cuda.synchronize()
+    report(read_stamps("kfa_wp_stamps"), f"{rows}x{co}x{ci}")
+
+
+def read_stamps(sym: str) -> np.ndarray:
     buf = np.zeros(256 * 2 * SEG, dtype=np.uint32)
-    fn = _lib.lib().kfa_wp_stamps
+    fn = getattr(_lib.lib(), sym)
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
     rc = fn(buf.ctypes.data, buf.size)
     assert rc == 0, rc
+    return buf
+
+
+def report(buf: np.ndarray, label: str) -> None:
+    """Per wave group: shares of prologue / k-loop / epilogue and the mean cycles
+    of each phase segment per k-tile (blocks whose stamp record is non-empty)."""
     s = buf.reshape(256, 2, SEG).astype(np.float64)
     live = s[:, 0, 22] > 0
     s = s[live]
-    print(f"{rows}x{co}x{ci}: {live.sum()} blocks, {s[:, 0, 22].mean():.0f} k-tiles per block")
+    print(f"{label}: {live.sum()} blocks, {s[:, 0, 22].mean():.0f} k-tiles per block")
     for grp in range(2):
         g = s[:, grp, :].mean(axis=0)
         loop = g[:20].sum()
@@ -56,10 +66,14 @@ def run(rows: int, co: int, ci: int) -> None:
         for ph in range(4):
             cells = []
             for k in (3, 4, 0, 1, 2):
+                if ph == 3 and k == 4 and not (g[3] > 0):  # stamp build 3: slot 19 = k-tile entry
+                    continue
                 v = g[ph * 5 + k]
                 if v > 0:
                     cells.append(f"{NAMES[k]} {v / kt:6.0f}")
             print(f"    phase {ph}: " + "  ".join(cells) + "   (cycles per k-tile)")
+        if g[19] > 0 and not g[3] > 0:
+            print(f"    k-tile entry (tail of the previous k-tile: advance, loop branch): {g[19] / kt:6.0f}")
 
 
 if __name__ == "__main__":
