@@ -334,7 +334,7 @@ __global__ __launch_bounds__(256) void bias_act_bwd_kernel(const bf16_t* __restr
                                                            const float* __restrict__ b, bf16_t* __restrict__ dx,
                                                            float* __restrict__ dbias, long rows, int N, int act,
                                                            long rows_per_block, uint32_t thresh, float dscale,
-                                                           uint64_t seed) {
+                                                           uint64_t seed, const float* __restrict__ gscale) {
   constexpr int RL = 256 / CL, W = CL * 8;
   __shared__ float red[RL][W];
   const int cl = threadIdx.x % CL, rl = threadIdx.x / CL;
@@ -342,6 +342,7 @@ __global__ __launch_bounds__(256) void bias_act_bwd_kernel(const bf16_t* __restr
   const long r0 = (long)blockIdx.y * rows_per_block;
   const long r1 = min(rows, r0 + rows_per_block);
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const float gs = gscale ? *gscale : 1.f;  // upstream gradient scalar (device-resident)
   if (c < N) {
     float bb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (b) load8f(b + c, bb);
@@ -349,6 +350,9 @@ __global__ __launch_bounds__(256) void bias_act_bwd_kernel(const bf16_t* __restr
     for (long r = r0 + rl; r < r1; r += RL) {
       float d[8], z[8];
       load8(dy + r * N + c, d);
+      if (gscale)
+#pragma unroll
+        for (int e = 0; e < 8; e++) d[e] *= gs;
       if (thresh)
 #pragma unroll
         for (int e = 0; e < 8; e++) d[e] = keep(seed, r * N + c + e, thresh) ? d[e] * dscale : 0.f;
@@ -857,10 +861,28 @@ KFA_API long kfa_colsum_part_floats(long rows, int N) {  // no scratch needed an
 
 // dx = dropout_mask(dy) * act'(x + b) (dx nullable: then only dbias is produced);
 // dbias (+)= column sums of dx (fp32 atomics, one per column per block).
+static int bias_act_bwd_launch(const void* dy, const void* x, const float* b, void* dx, float* dbias, long rows,
+                               int N, int act, float p, unsigned long long seed, int accumulate, const float* gscale,
+                               hipStream_t s);
+
 KFA_API int kfa_bias_act_bwd(const void* dy, const void* x, const float* b, void* dx, float* part, float* dbias,
                              long rows, int N, int act, float p, unsigned long long seed, int accumulate,
                              hipStream_t s) {
   (void)part;
+  return bias_act_bwd_launch(dy, x, b, dx, dbias, rows, N, act, p, seed, accumulate, nullptr, s);
+}
+
+// dx = dy * (*gscale) (dx must not alias dy) and dbias (+)= its column sums, one pass: the tied
+// MLM decoder's backward scales the loss kernel's dlogits by the upstream gradient and
+// takes the decoder-bias gradient in the same read (was a torch mul_ + a column-sum pass)
+KFA_API int kfa_scale_colsum(const void* dy, void* dx, float* dbias, long rows, int N, const float* gscale,
+                             int accumulate, hipStream_t s) {
+  return bias_act_bwd_launch(dy, nullptr, nullptr, dx, dbias, rows, N, kNone, 0.f, 0ull, accumulate, gscale, s);
+}
+
+static int bias_act_bwd_launch(const void* dy, const void* x, const float* b, void* dx, float* dbias, long rows,
+                               int N, int act, float p, unsigned long long seed, int accumulate, const float* gscale,
+                               hipStream_t s) {
   if (rows <= 0 || N % 8) return -1;
   const long chunks = colsum_chunks(rows);
   const long rpb = (rows + chunks - 1) / chunks;
@@ -876,12 +898,12 @@ KFA_API int kfa_bias_act_bwd(const void* dy, const void* x, const float* b, void
     const long rp = (rows + ch - 1) / ch;
     hipLaunchKernelGGL(bias_act_bwd_kernel<16>, dim3((unsigned)bx, (unsigned)ch), dim3(256), 0, s,
                        (const bf16_t*)dy, (const bf16_t*)x, b, (bf16_t*)dx, dbias, rows, N, act, rp, th, ds,
-                       (uint64_t)seed);
+                       (uint64_t)seed, gscale);
     return kfa_status();
   }
   hipLaunchKernelGGL(bias_act_bwd_kernel<64>, dim3((N + 511) / 512, (unsigned)chunks), dim3(256), 0, s,
                      (const bf16_t*)dy, (const bf16_t*)x, b, (bf16_t*)dx, dbias, rows, N, act, rpb, th, ds,
-                     (uint64_t)seed);
+                     (uint64_t)seed, gscale);
   return kfa_status();
 }
 

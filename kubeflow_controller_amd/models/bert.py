@@ -164,7 +164,7 @@ class BertForPreTraining(nn.Module):
         join_in = None
         for i, layer in enumerate(self.layers):
             join_out = T.ResidualJoin() if (self.training and i + 1 < len(self.layers)) else None
-            lcfg = (B, S, cfg.heads, ph, pa, T.mix_seed(step_seed, i), cfg.ln_eps, join_in, join_out)
+            lcfg = (B, S, cfg.heads, ph, pa, T.s64(T.mix_seed(step_seed, i)), cfg.ln_eps, join_in, join_out)
             h = T.EncoderLayerFn.apply(h, kb, lcfg, *layer.params())
             join_in = join_out
         # MLM on the masked positions only

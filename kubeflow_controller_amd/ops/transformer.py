@@ -45,6 +45,7 @@ _lib.register("kfa_ln_bwd", [P, P, P, P, P, P, P, P, P, P, P, L, I, Fl, U64, I, 
 _lib.register("kfa_ln_bwd2", [P, P, P, P, P, P, P, P, P, P, P, P, L, I, Fl, U64, I, P])
 _lib.register("kfa_bias_act_fwd", [P, P, P, L, I, I, Fl, U64, P])
 _lib.register("kfa_bias_act_bwd", [P, P, P, P, P, P, L, I, I, Fl, U64, I, P])
+_lib.register("kfa_scale_colsum", [P, P, P, L, I, P, I, P])
 _lib.register("kfa_qkv_split", [P, P, P, P, P, L, I, I, I, Fl, P])
 _lib.register("kfa_qkv_merge_bwd", [P, P, P, P, P, P, L, I, I, I, Fl, I, P])
 _lib.register("kfa_heads_permute", [P, P, L, I, I, I, I, P])
@@ -93,6 +94,16 @@ def mix_seed(*parts: int) -> int:
         h ^= (int(p) + 0x9E3779B97F4A7C15 + (h << 6) + (h >> 2)) & _MASK64
         h = (h * 0xBF58476D1CE4E5B9) & _MASK64
     return h
+
+
+def s64(seed: int) -> int:
+    """A 64-bit seed as the signed int64 with the same bits.  Seeds cross
+    ``torch.autograd.Function.apply`` in this form: torch's profiler (record_shapes)
+    converts Function arguments to int64 and rejects values >= 2^63.  Every consumer
+    masks back to 64 bits (:func:`hash_key`, :func:`mix_seed`), so both forms give
+    the same masks."""
+    s = int(seed) & _MASK64
+    return s - (1 << 64) if s >= (1 << 63) else s
 
 
 def hash_key(seed: int) -> int:
@@ -345,7 +356,7 @@ class DenseFn(torch.autograd.Function):
 def dense(x, weight, bias=None, act=None, p=0.0, seed=0):
     if not x.is_cuda:
         return dense_reference(x, weight, bias, act)
-    return DenseFn.apply(x, weight, bias, act, float(p), int(seed))
+    return DenseFn.apply(x, weight, bias, act, float(p), s64(seed))
 
 
 def _act_ref(z, act):
@@ -740,7 +751,10 @@ def dense_dropout(x, p, seed):
         return x
     if not x.is_cuda:
         return F.dropout(x, p)
-    return DropoutFn.apply(x, float(p), int(seed))
+    return DropoutFn.apply(x, float(p), s64(seed))
+
+
+DEC_SCALE_COLSUM = os.environ.get("KFA_DEC_SCALE_COLSUM", "1") != "0"
 
 
 class DecoderXentFn(torch.autograd.Function):
@@ -766,12 +780,24 @@ class DecoderXentFn(torch.autograd.Function):
     def backward(ctx, g):
         t, w, dlog = ctx.saved_tensors
         wp, bp = ctx.params
-        dlog.mul_(g.to(dlog.dtype))
-        dt = _gemm.dgrad_auto(dlog, w, "decoder_dgrad")
-        gw, _, dw = _grad_target(wp)
-        _wgrad_(gw, dlog, t)
+        # dlogits * g and the decoder-bias gradient in one pass over the logits-sized
+        # tensor (g stays on the device: no host sync)
+        n, V = dlog.shape
         gb, _, db = _grad_target(bp)
-        colsum_(dlog, gb)
+        if not DEC_SCALE_COLSUM:  # A/B: torch mul_ + a separate column-sum pass
+            dlog.mul_(g.to(dlog.dtype))
+            dt = _gemm.dgrad_auto(dlog, w, "decoder_dgrad")
+            gw, _, dw = _grad_target(wp)
+            _wgrad_(gw, dlog, t)
+            colsum_(dlog, gb)
+            return dt, _finish(wp, gw, dw), _finish(bp, gb, db), None
+        gs = g.detach().to(torch.float32).reshape(1).contiguous()
+        dls = torch.empty_like(dlog)
+        _lib.call("kfa_scale_colsum", _lib.ptr(dlog), _lib.ptr(dls), _lib.ptr(gb), n, V, _lib.ptr(gs), 1, _lib.stream())
+        del dlog
+        dt = _gemm.dgrad_auto(dls, w, "decoder_dgrad")
+        gw, _, dw = _grad_target(wp)
+        _wgrad_(gw, dls, t)
         return dt, _finish(wp, gw, dw), _finish(bp, gb, db), None
 
 

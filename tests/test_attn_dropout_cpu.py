@@ -48,3 +48,14 @@ def test_pair_hash_seeds_differ():
     b, _ = _keeps(2, 256, 128, 0.1)
     agree = (a == b).mean()
     assert abs(agree - (0.9 * 0.9 + 0.1 * 0.1)) < 0.01
+
+
+def test_seed_crosses_autograd_as_signed_int64_with_the_same_masks():
+    """Seeds reach torch.autograd.Function.apply as signed int64 (torch's profiler
+    rejects Python ints >= 2^63 there); the mask keys must not change."""
+    from kubeflow_controller_amd.ops import transformer as T
+    for s in (0, 5, 2**63 - 1, 2**63, 2**63 + 12345, 2**64 - 1):
+        v = T.s64(s)
+        assert -(2**63) <= v < 2**63
+        assert T.hash_key(v) == T.hash_key(s)
+        assert T.mix_seed(v, 3) == T.mix_seed(s, 3)
