@@ -133,6 +133,14 @@ class BertForPreTraining(nn.Module):
             self._pos_cache[key] = t
         return t
 
+    def _cls_rows(self, B, S, device):
+        key = ("cls", B, S, str(device))
+        t = self._pos_cache.get(key)
+        if t is None:
+            t = torch.arange(B, device=device, dtype=torch.int64) * S
+            self._pos_cache[key] = t
+        return t
+
     @staticmethod
     def key_bias(attention_mask):
         if attention_mask is None:
@@ -167,14 +175,17 @@ class BertForPreTraining(nn.Module):
             lcfg = (B, S, cfg.heads, ph, pa, T.s64(T.mix_seed(step_seed, i)), cfg.ln_eps, join_in, join_out)
             h = T.EncoderLayerFn.apply(h, kb, lcfg, *layer.params())
             join_in = join_out
-        # MLM on the masked positions only
-        hm = h.index_select(0, mlm_positions.reshape(-1))
+        # the masked positions (MLM) and the [CLS] rows (NSP) in ONE gather: its backward
+        # is one zero-fill + one index_add into [T, H] instead of two and a sum of them
+        pos = mlm_positions.reshape(-1)
+        rows = torch.cat([pos.to(torch.int64), self._cls_rows(B, S, dev)])
+        g = h.index_select(0, rows)
+        hm, hc = g[:pos.numel()], g[pos.numel():]
         t = T.dense(hm, self.mlm_w, self.mlm_b, "gelu")
         t = T.layer_norm(t, self.mlm_ln_g, self.mlm_ln_b, cfg.ln_eps)
         mlm = T.decoder_xent(t, self.word_emb, self.dec_b, mlm_labels.reshape(-1))
         # NSP on [CLS]
-        cls_rows = torch.arange(B, device=dev) * S
-        pooled = T.dense(h.index_select(0, cls_rows), self.pool_w, self.pool_b, "tanh")
+        pooled = T.dense(hc, self.pool_w, self.pool_b, "tanh")
         nsp = classifier_xent(pooled.contiguous(), self.nsp_w, self.nsp_b, nsp_labels)  # fused 2-way head + loss
         return mlm + nsp
 
