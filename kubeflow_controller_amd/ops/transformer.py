@@ -57,7 +57,8 @@ _lib.register("kfa_colsum", [P, P, P, L, I, I, P])
 _lib.register("kfa_embed_small_ws_floats", [I, I], restype=_lib.L)
 _lib.register("kfa_embed_small_bwd", [P, P, _lib.L, P, I, _lib.L, I, I, P, P])
 _lib.register("kfa_attn_fwd", [P, P, P, P, P, I, I, I, I, Fl, Fl, U64, P, P])
-_lib.register("kfa_attn_bwd", [P, P, P, P, P, P, P, P, I, I, I, I, Fl, Fl, U64, P, P, P])
+_lib.register("kfa_attn_bwd", [P, P, P, P, P, P, P, P, I, I, I, I, Fl, Fl, U64, P, P, P, P])
+_lib.register("kfa_attn_dbias_part_floats", [I, I], L)
 _lib.register("kfa_attn_mask_words", [I, I, I], _lib.L)
 
 # env KFA_FUSED_ATTN=0 falls back to the split kernels + batched library GEMMs
@@ -514,9 +515,12 @@ def attn_bwd(qkv, bqkv, key_bias, out, lse, dout, dbqkv, B, S, heads, p=0.0, see
         raise ValueError("attn_bwd: mask must be the forward's int32 [B*heads, 4, S] keep mask")
     dqkv = torch.empty_like(qkv)
     work = _lib.workspace(B * heads * S * 4, qkv.device, "attn_rowdot")  # D = rowsum(dO∘O) (S > 128)
+    # the S = 128 kernel's bias gradient: per-(sequence, wave) partial rows, then one sum
+    dbpart = (_lib.workspace(_lib.lib().kfa_attn_dbias_part_floats(B, heads) * 4, qkv.device, "attn_dbias")
+              if dbqkv is not None else None)
     _lib.call("kfa_attn_bwd", _lib.ptr(qkv), _lib.ptr(bqkv), _lib.ptr(key_bias), _lib.ptr(out), _lib.ptr(lse),
               _lib.ptr(dout), _lib.ptr(dqkv), _lib.ptr(dbqkv), B, S, heads, d, 1.0 / math.sqrt(d), float(p),
-              hash_key(seed), _lib.ptr(mask if p > 0 else None), _lib.ptr(work), _lib.stream())
+              hash_key(seed), _lib.ptr(mask if p > 0 else None), _lib.ptr(work), _lib.ptr(dbpart), _lib.stream())
     return dqkv
 
 
@@ -673,10 +677,14 @@ class EncoderLayerFn(torch.autograd.Function):
         del dao
         if fused:
             qkv, lse, amask = att
-            # QKV-bias gradient as a column-sum pass (27 us) rather than the kernel's
-            # per-wave atomics: 1024 adds per bias element serialise at L2 (+160 us / layer)
-            dqkv = attn_bwd(qkv, bqkv, key_bias, ctxr, lse, dctxr, None, B, S, heads, pa, s_attn, mask=amask)
-            colsum_(dqkv, G(bqkv))
+            # QKV-bias gradient: a column-sum pass over dqkv (it is still in the Infinity
+            # Cache); KFA_ATTN_DBIAS=1: the kernel's per-(sequence, wave) column sums of the
+            # tile it stores (partial rows + one small sum) — +10 us in the kernel, no net gain
+            if ATTN_DBIAS:
+                dqkv = attn_bwd(qkv, bqkv, key_bias, ctxr, lse, dctxr, G(bqkv), B, S, heads, pa, s_attn, mask=amask)
+            else:
+                dqkv = attn_bwd(qkv, bqkv, key_bias, ctxr, lse, dctxr, None, B, S, heads, pa, s_attn, mask=amask)
+                colsum_(dqkv, G(bqkv))
             del dctxr
         else:
             q, k, v, probs, pdrop = att
@@ -755,6 +763,7 @@ def dense_dropout(x, p, seed):
 
 
 DEC_SCALE_COLSUM = os.environ.get("KFA_DEC_SCALE_COLSUM", "1") != "0"
+ATTN_DBIAS = os.environ.get("KFA_ATTN_DBIAS", "0") == "1"  # measured equal / slower than the pass (docs/kernels.md)
 
 
 class DecoderXentFn(torch.autograd.Function):
