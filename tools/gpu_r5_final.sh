@@ -18,9 +18,9 @@ timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_WA
   -- python3 $R/tools/bench_model.py --model bert_base --batch 256 --seq 128 --steps 2 --warmup 2 > $R/$O/bert_pmc.log 2>&1 || { tail -5 $R/$O/bert_pmc.log; exit 1; }
 cd $R
 ms=$(python3 -c "import json;print([json.loads(l) for l in open('$O/bert_trace.log') if l.startswith('{')][-1]['ms_per_step'])")
-python3 tools/profile_summary.py $(ls $O/bt/*kernel_trace.csv | head -1) 5 "$ms" "BERT-base 256x128 1x MI355X (round-5 HEAD, after the wgrad asm reads)" adam_kernel > $O/bert.md
+python3 tools/profile_summary.py $(ls $O/bt/*kernel_trace.csv | head -1) 5 "$ms" "BERT-base 256x128 1x MI355X (round-5 late HEAD)" adam_kernel > $O/bert.md
 ms=$(python3 -c "import json;print([json.loads(l) for l in open('$O/r50_trace.log') if l.startswith('{')][-1]['ms_per_step'])")
-python3 tools/profile_summary.py $(ls $O/rt/*kernel_trace.csv | head -1) 10 "$ms" "ResNet-50 bs256 1x MI355X (round-5 HEAD, after the wgrad asm reads)" > $O/r50.md
+python3 tools/profile_summary.py $(ls $O/rt/*kernel_trace.csv | head -1) 10 "$ms" "ResNet-50 bs256 1x MI355X (round-5 late HEAD)" > $O/r50.md
 python3 tools/pmc_derived.py $(ls $O/bp/*counter_collection.csv) > $O/bert_pmc.md || true
 python3 tools/kernel_list.py $(ls $O/rt/*kernel_trace.csv | head -1) 15 > $O/r50_klist.txt
 python3 tools/kernel_list.py $(ls $O/bt/*kernel_trace.csv | head -1) 8 > $O/bert_klist.txt
