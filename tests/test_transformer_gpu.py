@@ -230,7 +230,10 @@ def test_embedding_small_table_grad(R, Dm, pattern, monkeypatch):
     _close(g_new, t.grad, 2e-2, "vs one-hot path")
 
 
-def test_decoder_xent():
+@pytest.mark.parametrize("gscale", [1.0, -2.5], ids=["unit_grad", "scaled_grad"])
+def test_decoder_xent(gscale):
+    """The backward scales dlogits by the upstream gradient (a device scalar) in the
+    same pass as the decoder-bias column sums (kfa_scale_colsum)."""
     from kubeflow_controller_amd.ops import transformer as T
     torch.manual_seed(0)
     n, H, V = 300, 256, 30528
@@ -242,8 +245,8 @@ def test_decoder_xent():
     tr, wr, br = (z.detach().float().requires_grad_() for z in (t, w, b))
     lr = F.cross_entropy(tr @ wr.t() + br, lab)
     assert abs(loss.item() - lr.item()) < 2e-2 * max(1, lr.item())
-    loss.backward()
-    lr.backward()
+    (loss * gscale).backward()
+    (lr * gscale).backward()
     _close(t.grad, tr.grad, 3e-2, "dt")
     _close(w.grad, wr.grad, 3e-2, "dw")
     _close(b.grad, br.grad, 3e-2, "db")
