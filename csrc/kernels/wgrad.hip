@@ -874,7 +874,11 @@ static bool pp_shape(long K, int Co, int N, bool pointwise, int Ci = 0, int H = 
   if (!pointwise) return wgrad_pp_gather() && Ci % 64 == 0 && Co % 256 == 0 && N % 256 == 0 && K >= 8192 && H < 16384 && W < 16384;
   // per-shape table (tools/bench_wgrad_pp.py, 1x MI355X): wins from 256 x 256 channels up (BERT dW -4..-9 %,
   // ResNet-50 1x1s at 50176 / 200704 pixels -2..-5 %); the 128-channel ResNet shapes lose 10-24 %
-  return wgrad_pp_mode() == 2 ? (Co >= 128 && N >= 128) : (K >= 8192 && Co >= 256 && N >= 256);
+  // a short reduction takes the ping-pong kernel too when its 256 x 256 tiles alone fill the
+  // chip (no split-K): the BERT MLM decoder, 5120 x 30528 x 768, 320.6 -> 286.8 us
+  const long tiles = (long)((Co + 255) / 256) * ((N + 255) / 256);
+  return wgrad_pp_mode() == 2 ? (Co >= 128 && N >= 128)
+                              : (Co >= 256 && N >= 256 && (K >= 8192 || tiles >= num_cus()));
 }
 
 WPlan plan(long K, int Co, int N, bool pointwise = false) {
