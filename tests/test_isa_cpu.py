@@ -73,3 +73,33 @@ def test_pp_kernels_do_not_spill_in_the_loop(wgrad_s):
         assert _meta(wgrad_s, name, "vgpr_count") <= 256
         # the pointwise variant parks two values across its k-loop (4 scratch ops per wave in total)
         assert _meta(wgrad_s, name, "vgpr_spill_count") <= 2, name
+
+
+@pytest.fixture(scope="module")
+def conv_s(tmp_path_factory):
+    out = tmp_path_factory.mktemp("isa") / "conv_igemm.s"
+    subprocess.run([HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "-munsafe-fp-atomics",
+                    f"-I{ROOT}/csrc/kernels", "--cuda-device-only", "-S", f"{ROOT}/csrc/kernels/conv_igemm.hip",
+                    "-o", str(out)], check=True, capture_output=True, timeout=900)
+    return out.read_text()
+
+
+def test_conv_asm_fragment_reads_have_no_hazards(conv_s):
+    """conv_igemm_kernel's 4-wave tiles (and the BatchNorm-prologue forms) read their
+    MFMA fragments with inline-asm ds_read_b128 and counted lgkmcnt waits
+    (csrc/kernels/conv_igemm.hip, `compute`)."""
+    import asm_read_hazards
+    found = 0
+    for name, body in _bodies(conv_s, "conv_igemm_kernel"):
+        if not any(l.strip() == ";;#ASMSTART" and "ds_read" in nxt for l, nxt in zip(body, body[1:])):
+            continue
+        found += 1
+        assert asm_read_hazards.check(body) == [], name
+    assert found >= 32  # 128x128, 128x64, 256x64 x 8 epilogues + the 8 prologue forms
+
+
+def test_conv_kernels_do_not_spill(conv_s):
+    for name, _ in _bodies(conv_s, "conv_"):
+        if "Lj31E" in name:  # kEpiAll (pick_epi's catch-all, the ReLU mask read from y): off the ResNet step
+            continue
+        assert _meta(conv_s, name, "vgpr_spill_count") == 0, name
