@@ -112,8 +112,11 @@ class BertForPreTraining(nn.Module):
         self.nsp_b = nn.Parameter(torch.zeros(2))
         for w in (self.mlm_w, self.pool_w, self.nsp_w):
             nn.init.normal_(w, 0.0, cfg.init_range)
-        # the word embedding is written by two direct-gradient kernels per step
+        # the word embedding is written by two direct-gradient kernels per step; the
+        # module-level map survives copy.deepcopy (a Parameter's own attributes do
+        # not), the Engine re-applies it (trainer/engine.py)
         self.word_emb._kfa_uses = 2
+        self._kfa_param_uses = {"word_emb": 2}
         self.seed = seed
         self._step = 0
         self._pos_cache = {}

@@ -103,31 +103,42 @@ class FusedSGD(_FusedBase):
         self.mom = [torch.zeros(s.numel, dtype=torch.float32, device=s.device) if momentum else None
                     for s in self.spaces]
 
+    def begin_step(self) -> None:
+        """Open one optimizer step whose updates are issued per range (``update``)."""
+        self._first = int(self.step_count == 0)
+        self.step_count += 1
+
+    @torch.no_grad()
+    def update(self, si: int, a: int, b: int, grad_scale: float = 1.0, lr: Optional[float] = None) -> None:
+        """Elements [a, b) of space ``si`` in the step opened by ``begin_step`` (the
+        update is elementwise, so any cut of a space into ranges gives the whole-space result)."""
+        if b <= a:
+            return
+        lr = self.lr if lr is None else lr
+        s, mom = self.spaces[si], self.mom[si]
+        w, wb, gr = s.w[a:b], (s.wb[a:b] if s.wb is not None else None), s.grad[a:b]
+        mom = mom[a:b] if mom is not None else None
+        if self._cpu(s):
+            d = gr.float() * grad_scale + self._wd(s) * w
+            if mom is not None:
+                if self._first:
+                    mom.copy_(d)
+                else:
+                    mom.mul_(self.momentum).add_(d, alpha=1 - self.dampening)
+                d = d + self.momentum * mom if self.nesterov else mom
+            w.add_(d, alpha=-lr)
+            if wb is not None:
+                wb.copy_(w)
+            return
+        _lib.call("kfa_sgd_step", _lib.ptr(w), _lib.ptr(wb), _lib.ptr(gr), int(gr.dtype == torch.bfloat16),
+                  _lib.ptr(mom), b - a, lr, self.momentum, self.dampening, self._wd(s), int(self.nesterov),
+                  grad_scale, self._first, _lib.stream())
+
     @torch.no_grad()
     def step(self, grad_scale: float = 1.0, lr: Optional[float] = None) -> None:
-        lr = self.lr if lr is None else lr
-        first = int(self.step_count == 0)
+        self.begin_step()
         for si, s in enumerate(self.spaces):
-            w, wb, gr, mom = s.w, s.wb, s.grad, self.mom[si]
-            n = w.numel()
-            if n == 0:
-                continue
-            if self._cpu(s):
-                d = gr.float() * grad_scale + self._wd(s) * w
-                if mom is not None:
-                    if first:
-                        mom.copy_(d)
-                    else:
-                        mom.mul_(self.momentum).add_(d, alpha=1 - self.dampening)
-                    d = d + self.momentum * mom if self.nesterov else mom
-                w.add_(d, alpha=-lr)
-                if wb is not None:
-                    wb.copy_(w)
-                continue
-            _lib.call("kfa_sgd_step", _lib.ptr(w), _lib.ptr(wb), _lib.ptr(gr), int(gr.dtype == torch.bfloat16),
-                      _lib.ptr(mom), n, lr, self.momentum, self.dampening, self._wd(s), int(self.nesterov),
-                      grad_scale, first, _lib.stream())
-        self.step_count += 1
+            self.update(si, 0, s.numel, grad_scale, lr)
 
 
 class FusedAdam(_FusedBase):
@@ -143,33 +154,44 @@ class FusedAdam(_FusedBase):
         self._t = torch.zeros(1, dtype=torch.int32, device=dev) if dev.type == "cuda" else None
         self._bc = torch.ones(2, dtype=torch.float32, device=dev) if dev.type == "cuda" else None
 
-    @torch.no_grad()
-    def step(self, grad_scale: float = 1.0, lr: Optional[float] = None) -> None:
-        lr = self.lr if lr is None else lr
+    def begin_step(self) -> None:
+        """Open one optimizer step whose updates are issued per range (``update``):
+        the step count and the bias corrections advance once, here."""
         if self._t is not None:
             if not torch.cuda.is_current_stream_capturing():
                 self._t.fill_(self.step_count)  # eager steps (and resumes) re-seed the device count
             _lib.call("kfa_adam_bc", _lib.ptr(self._t), _lib.ptr(self._bc), self.b1, self.b2, _lib.stream())
         self.step_count += 1
+
+    @torch.no_grad()
+    def update(self, si: int, a: int, b: int, grad_scale: float = 1.0, lr: Optional[float] = None) -> None:
+        """Elements [a, b) of space ``si`` in the step opened by ``begin_step`` (elementwise:
+        any cut of a space into ranges gives the whole-space result bit for bit)."""
+        if b <= a:
+            return
+        lr = self.lr if lr is None else lr
         t = self.step_count
         bc1 = 1.0 - self.b1 ** t
         bc2 = 1.0 - self.b2 ** t
+        s = self.spaces[si]
+        w, wb, gr = s.w[a:b], (s.wb[a:b] if s.wb is not None else None), s.grad[a:b]
+        m, v = self.m[si][a:b], self.v[si][a:b]
+        wd = self._wd(s)
+        if self._cpu(s):
+            d = gr.float() * grad_scale
+            m.mul_(self.b1).add_(d, alpha=1 - self.b1)
+            v.mul_(self.b2).addcmul_(d, d, value=1 - self.b2)
+            denom = (v.sqrt() / math.sqrt(bc2)).add_(self.eps)
+            w.mul_(1 - lr * wd).addcdiv_(m, denom, value=-lr / bc1)
+            if wb is not None:
+                wb.copy_(w)
+            return
+        _lib.call("kfa_adam_step", _lib.ptr(w), _lib.ptr(wb), _lib.ptr(gr), int(gr.dtype == torch.bfloat16),
+                  _lib.ptr(m), _lib.ptr(v), b - a, lr, self.b1, self.b2, self.eps, wd, bc1, bc2, grad_scale,
+                  _lib.ptr(self._bc), _lib.stream())
+
+    @torch.no_grad()
+    def step(self, grad_scale: float = 1.0, lr: Optional[float] = None) -> None:
+        self.begin_step()
         for si, s in enumerate(self.spaces):
-            w, wb, gr = s.w, s.wb, s.grad
-            m, v = self.m[si], self.v[si]
-            n = w.numel()
-            if n == 0:
-                continue
-            wd = self._wd(s)
-            if self._cpu(s):
-                d = gr.float() * grad_scale
-                m.mul_(self.b1).add_(d, alpha=1 - self.b1)
-                v.mul_(self.b2).addcmul_(d, d, value=1 - self.b2)
-                denom = (v.sqrt() / math.sqrt(bc2)).add_(self.eps)
-                w.mul_(1 - lr * wd).addcdiv_(m, denom, value=-lr / bc1)
-                if wb is not None:
-                    wb.copy_(w)
-                continue
-            _lib.call("kfa_adam_step", _lib.ptr(w), _lib.ptr(wb), _lib.ptr(gr), int(gr.dtype == torch.bfloat16),
-                      _lib.ptr(m), _lib.ptr(v), n, lr, self.b1, self.b2, self.eps, wd, bc1, bc2, grad_scale,
-                      _lib.ptr(self._bc), _lib.stream())
+            self.update(si, 0, s.numel, grad_scale, lr)

@@ -31,7 +31,7 @@ import torch
 import torch.distributed as dist
 
 from .buckets import Bucket, plan_buckets
-from .flat import ALIGN, FlatGroup, set_ready_callback
+from .flat import ALIGN, FlatGroup, register_ready_hook
 
 
 def _join_side_streams(t: torch.Tensor) -> None:
@@ -60,15 +60,29 @@ class GradSync:
         eb = [(g.grad32 if g.grad32 is not None else g.grad).element_size() for g in self.groups]
         self.buckets, self._of_param = plan_buckets(self.groups, bucket_mb, ALIGN, eb)
         self._hooks = []
+        self._on_ready = None  # single process: per-bucket callback (Engine's overlapped optimizer)
         if self.overlap:
-            for (gi, pi), bs in self._of_param.items():
-                p = self.groups[gi].params[pi]
-                hook = self._make_hook(bs)
-                # fired either by autograd's AccumulateGrad or by a kernel that wrote
-                # the gradient straight into the flat buffer (flat.notify_grad_ready)
-                self._hooks.append(p.register_post_accumulate_grad_hook(hook))
-                set_ready_callback(p, hook)
+            self._install_hooks()
         self.reset()
+
+    def _install_hooks(self) -> None:
+        for (gi, pi), bs in self._of_param.items():
+            p = self.groups[gi].params[pi]
+            hook = self._make_hook(bs)
+            # fired either by autograd's AccumulateGrad or by a kernel that wrote
+            # the gradient straight into the flat buffer (flat.notify_grad_ready)
+            self._hooks.append(register_ready_hook(p, hook))
+
+    def on_bucket_ready(self, cb) -> None:
+        """Single process (world == 1, no collective): call ``cb(bucket)`` the moment a
+        bucket's last gradient lands during backward, and from ``finish`` for any bucket
+        that did not complete (parameters without a gradient this step).  The Engine
+        issues that bucket's optimizer update from it (``trainer/engine.py``)."""
+        if self.world != 1:
+            raise ValueError("on_bucket_ready: world > 1 buckets run their all-reduce")
+        self._on_ready = cb
+        if not self._hooks:
+            self._install_hooks()
 
     def spaces(self):
         """What the fused optimizer updates: each whole flat group."""
@@ -89,6 +103,11 @@ class GradSync:
             b.work = None
 
     def _launch(self, b: Bucket) -> None:
+        if self.world == 1:
+            if self._on_ready is not None and b.work is None:
+                b.work = True
+                self._on_ready(b)
+            return
         g = self.groups[b.group]
         view = g.grad[b.start:b.end]
         _join_side_streams(view)
@@ -105,6 +124,9 @@ class GradSync:
             from ..ops import streams
             streams.join(self.groups[0].grad.device)  # the optimizer reads every weight gradient
         if self.world == 1:
+            if self._on_ready is not None:
+                for b in self.buckets:
+                    self._launch(b)
             self.reset()
             return 1.0
         for b in self.buckets:

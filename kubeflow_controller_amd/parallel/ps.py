@@ -38,7 +38,7 @@ import torch
 import torch.distributed as dist
 
 from .buckets import Bucket, plan_buckets
-from .flat import ALIGN, FlatGroup, set_ready_callback
+from .flat import ALIGN, FlatGroup, register_ready_hook
 
 
 def ps_assignment(params: Sequence[Tuple[str, torch.Tensor]], num_ps: int, strategy: str = "round_robin"
@@ -146,8 +146,7 @@ class ShardedGradSync:
             for (gi, pi), bs in self._of_param.items():
                 p = self.groups[gi].params[pi]
                 hook = self._make_hook(bs)
-                self._hooks.append(p.register_post_accumulate_grad_hook(hook))
-                set_ready_callback(p, hook)
+                self._hooks.append(register_ready_hook(p, hook))
         self._pull_hooks = []
         self._stage: Dict[int, torch.Tensor] = {}  # per-bucket reduce-dtype staging (allocated once)
         self._static_mode = "wait-all"
