@@ -41,7 +41,7 @@ def test_overlapped_adam_matches_one_pass_bert():
         assert abs(a - b) <= 1e-3 * max(1.0, abs(a)), losses
 
 
-@pytest.mark.parametrize("which", ["bert", "resnet"])
+@pytest.mark.parametrize("which", ["bert", "resnet", "resnet50", "wide_deep"])
 def test_every_bucket_completes_once_in_backward(which):
     """Every gradient bucket's ready count reaches exactly 0 in one backward on the
     HIP paths (direct gradients reported once, the tied word embedding twice): a
@@ -56,13 +56,22 @@ def test_every_bucket_completes_once_in_backward(which):
         batch = tuple(t.to(d) if isinstance(t, torch.Tensor) else t
                       for t in synthetic_mlm_batch(cfg, 8, 128, generator=torch.Generator().manual_seed(0)))
         kw = dict(optimizer="adam", channels_last=False, bucket_mb=0.5)
+    elif which == "wide_deep":
+        from kubeflow_controller_amd.models.wide_deep import (WideDeep, WideDeepConfig, prepare_batch,
+                                                              synthetic_batch, wide_deep_loss)
+        cfg = WideDeepConfig.tiny()
+        m, loss = WideDeep(cfg, device=d), wide_deep_loss
+        batch = prepare_batch(m, *synthetic_batch(cfg, 512, torch.Generator().manual_seed(0)), d)
+        kw = dict(optimizer="adam", channels_last=False, bucket_mb=0.01)
     else:
-        from kubeflow_controller_amd.models.resnet import resnet_tiny
+        from kubeflow_controller_amd.models.resnet import resnet50, resnet_tiny
         from kubeflow_controller_amd.ops.loss import cross_entropy
-        m, loss = resnet_tiny(10), (lambda mm, x, y: cross_entropy(mm(x), y))
-        x = torch.randn(8, 3, 32, 32, device=d).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-        batch = (x, torch.randint(0, 10, (8,), device=d))
-        kw = dict(optimizer="sgd", channels_last=True, bucket_mb=0.05)
+        big = which == "resnet50"
+        m, loss = (resnet50(1000) if big else resnet_tiny(10)), (lambda mm, x, y: cross_entropy(mm(x), y))
+        hw, nc = (224, 1000) if big else (32, 10)
+        x = torch.randn(8, 3, hw, hw, device=d).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        batch = (x, torch.randint(0, nc, (8,), device=d))
+        kw = dict(optimizer="sgd", channels_last=True, bucket_mb=8.0 if big else 0.05)
     e = Engine(m, loss, compute_dtype=torch.bfloat16, dist_info=DistInfo(device=d), opt_overlap=True, **kw)
     fired = []
     e.sync._on_ready = lambda b: fired.append(b.index)
