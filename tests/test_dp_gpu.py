@@ -1,0 +1,100 @@
+"""Data-parallel training on the HIP kernels (GradSync buckets fired from the direct-
+gradient notifications) matches one process on the concatenated batch.
+
+Two ranks share the box's one GPU over gloo (RCCL refuses two ranks on one device;
+``KFA_COMM=torch``), so the bucket bookkeeping of the GPU path — HIP backwards that
+write the flat gradient and notify — drives real all-reduces.  A bucket that fired
+before its last gradient landed (the round-5 double count, ``docs/architecture.md``)
+all-reduces a partial gradient and the ranks' weights leave the single-process ones.
+SGD (linear in the gradient) keeps the comparison tight: the updates agree to the
+bf16 rounding of the gradient buffer (each rank rounds its half-sum, one process the
+whole sum), and the two ranks' weights agree exactly.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+B, S, STEPS = 4, 128, 2
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _cfg():
+    from kubeflow_controller_amd.models.bert import BertConfig
+    return BertConfig(vocab_size=1024, hidden=256, layers=2, heads=4, intermediate=1024, max_position=128,
+                      hidden_dropout=0.0, attn_dropout=0.0)
+
+
+def _batch(cfg, r, d):
+    from kubeflow_controller_amd.models.bert import synthetic_mlm_batch
+    return synthetic_mlm_batch(cfg, B, S, torch.Generator().manual_seed(100 + r))
+
+
+def _engine(model, d, info):
+    from kubeflow_controller_amd.models.bert import bert_loss
+    from kubeflow_controller_amd.trainer.engine import Engine
+    return Engine(model, bert_loss, optimizer="sgd", lr=0.1, momentum=0.0, weight_decay=0.0,
+                  compute_dtype=torch.bfloat16, channels_last=False, bucket_mb=0.5, dist_info=info)
+
+
+def _to(batch, d):
+    return tuple(t.to(d) if isinstance(t, torch.Tensor) else t for t in batch)
+
+
+def _worker(rank, world, port, out):
+    import torch.distributed as dist
+    from kubeflow_controller_amd.models.bert import BertForPreTraining
+    from kubeflow_controller_amd.trainer.engine import DistInfo
+    os.environ["KFA_COMM"] = "torch"
+    d = torch.device("cuda", 0)
+    torch.cuda.set_device(d)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    cfg = _cfg()
+    torch.manual_seed(5)
+    e = _engine(BertForPreTraining(cfg), d, DistInfo(rank=rank, world=world, device=d))
+    batch = _to(_batch(cfg, rank, d), d)
+    for _ in range(STEPS):
+        e.train_step(*batch)
+    torch.cuda.synchronize()
+    torch.save([g.fp32.cpu() for g in e.groups], f"{out}.{rank}")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_two_ranks_match_single_process(tmp_path):
+    from kubeflow_controller_amd.models.bert import BertForPreTraining
+    from kubeflow_controller_amd.trainer.engine import DistInfo
+    out = str(tmp_path / "w")
+    mp.start_processes(_worker, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    d = torch.device("cuda", 0)
+    cfg = _cfg()
+    torch.manual_seed(5)
+    e = _engine(BertForPreTraining(cfg), d, DistInfo(device=d))
+    init = [g.fp32.cpu().clone() for g in e.groups]
+    parts = [_batch(cfg, r, d) for r in range(2)]
+    ids, tt, _, flat, labels, nsp = (list(x) for x in zip(*parts))
+    flat = [f + r * B * S for r, f in enumerate(flat)]  # positions index the concatenated [B*S] rows
+    batch = _to((torch.cat(ids), torch.cat(tt), None, torch.cat(flat), torch.cat(labels), torch.cat(nsp)), d)
+    for _ in range(STEPS):
+        e.train_step(*batch)
+    torch.cuda.synchronize()
+    ref = [g.fp32.cpu() for g in e.groups]
+    w0, w1 = (torch.load(f"{out}.{r}", weights_only=True) for r in range(2))
+    for a, b in zip(w0, w1):  # every rank applied the same summed update
+        torch.testing.assert_close(a, b, rtol=0, atol=0)
+    for a, r, i in zip(w0, ref, init):
+        n = r.numel()  # world 2 pads each group to a multiple of 16 elements (reduce-scatter shards)
+        da, dr = a[:n] - i, r - i
+        tol = 2e-2 * dr.abs() + 1e-2 * float(dr.abs().max())
+        assert bool(((da - dr).abs() <= tol).all()), float((da - dr).abs().max())
