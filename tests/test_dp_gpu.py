@@ -41,18 +41,19 @@ def _batch(cfg, r, d):
     return synthetic_mlm_batch(cfg, B, S, torch.Generator().manual_seed(100 + r))
 
 
-def _engine(model, d, info):
+def _engine(model, d, info, ps=0):
     from kubeflow_controller_amd.models.bert import bert_loss
     from kubeflow_controller_amd.trainer.engine import Engine
     return Engine(model, bert_loss, optimizer="sgd", lr=0.1, momentum=0.0, weight_decay=0.0,
-                  compute_dtype=torch.bfloat16, channels_last=False, bucket_mb=0.5, dist_info=info)
+                  compute_dtype=torch.bfloat16, channels_last=False, bucket_mb=0.5, dist_info=info,
+                  ps=ps, ps_placement="sharded")
 
 
 def _to(batch, d):
     return tuple(t.to(d) if isinstance(t, torch.Tensor) else t for t in batch)
 
 
-def _worker(rank, world, port, out):
+def _worker(rank, world, port, out, ps=0):
     import torch.distributed as dist
     from kubeflow_controller_amd.models.bert import BertForPreTraining
     from kubeflow_controller_amd.trainer.engine import DistInfo
@@ -62,21 +63,25 @@ def _worker(rank, world, port, out):
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     cfg = _cfg()
     torch.manual_seed(5)
-    e = _engine(BertForPreTraining(cfg), d, DistInfo(rank=rank, world=world, device=d))
+    e = _engine(BertForPreTraining(cfg), d, DistInfo(rank=rank, world=world, device=d), ps)
     batch = _to(_batch(cfg, rank, d), d)
     for _ in range(STEPS):
         e.train_step(*batch)
+    e.wait()
     torch.cuda.synchronize()
     torch.save([g.fp32.cpu() for g in e.groups], f"{out}.{rank}")
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_dp_two_ranks_match_single_process(tmp_path):
+def test_dp_two_ranks_match_single_process(tmp_path, ps=0):
+    """Bucketed all-reduce (parallel/ddp.py).  (The parameter-server layouts keep the
+    fp32 masters in the owners' compact shards, ``ShardedGradSync.w32``, and pull only
+    the compute weights: ``g.fp32`` is not theirs to compare.)"""
     from kubeflow_controller_amd.models.bert import BertForPreTraining
     from kubeflow_controller_amd.trainer.engine import DistInfo
     out = str(tmp_path / "w")
-    mp.start_processes(_worker, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    mp.start_processes(_worker, args=(2, _free_port(), out, ps), nprocs=2, join=True, start_method="spawn")
     d = torch.device("cuda", 0)
     cfg = _cfg()
     torch.manual_seed(5)
