@@ -102,6 +102,7 @@ class FusedSGD(_FusedBase):
         self.nesterov = nesterov
         self.mom = [torch.zeros(s.numel, dtype=torch.float32, device=s.device) if momentum else None
                     for s in self.spaces]
+        self._first = 1  # set per step by begin_step
 
     def begin_step(self) -> None:
         """Open one optimizer step whose updates are issued per range (``update``)."""

@@ -171,6 +171,7 @@ class Engine:
         return self._eager_step(*batch)
 
     def _eager_step(self, *batch) -> torch.Tensor:
+        self._opt_open = False  # (a step whose backward raised never closed its optimizer step)
         self.zero_grad()
         loss = self.loss_fn(self.model, *batch)
         loss.backward()
