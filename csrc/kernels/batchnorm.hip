@@ -302,13 +302,14 @@ __global__ __launch_bounds__(NT) void bn_apply(const bf16_t* __restrict__ x, con
 // The apply passes keep no per-block partials, so their grid need not follow the
 // statistics passes' (max_row_blocks caps C >= 1024 at 512-1024 blocks: 2-4 per
 // CU, too few loads in flight to stream at HBM rate).  KFA_BN_APPLY_BLOCKS=0
-// restores the shared geometry.
+// restores the shared geometry.  Cap 16384 (round 5; was 4096): ResNet-50 13,107-13,130
+// vs 13,020-13,028 img/s on one box (tools/gpu_r5_bnblocks.sh), flat from 16384 up.
 static Geom apply_geom(long M, int C) {
   static int cap = -1;
   if (cap < 0) {
     const char* e = getenv("KFA_BN_APPLY_BLOCKS");
-    cap = e ? atoi(e) : 4096;
-    if (cap < 0) cap = 4096;
+    cap = e ? atoi(e) : 16384;
+    if (cap < 0) cap = 16384;
   }
   int shared = (1 << 20) / C;  // == max_row_blocks(C)
   shared = shared > 2048 ? 2048 : (shared < 64 ? 64 : shared);

@@ -36,7 +36,10 @@ def test_overlapped_adam_matches_one_pass_bert():
     def diff(a, b):
         return max(float((gb.fp32 - ga.fp32).abs().max()) for ga, gb in zip(a.groups, b.groups))
     d_ctl, d_ovl = diff(ref, ctl), diff(ref, ovl)
-    assert d_ovl <= max(4 * d_ctl, 1e-6), (d_ovl, d_ctl, losses)
+    # the one-pass runs differ by the embedding backward's fp32 atomic order (Adam turns
+    # near-zero gradient noise into up to ~lr of weight); an update that misses part of a
+    # bucket's gradient moved weights by 2e-3 .. 6e-3 here
+    assert d_ovl <= max(4 * d_ctl, 2e-4), (d_ovl, d_ctl, losses)
     for a, b in zip(losses["ref"], losses["ovl"]):
         assert abs(a - b) <= 1e-3 * max(1.0, abs(a)), losses
 
