@@ -33,13 +33,16 @@ def test_overlapped_adam_matches_one_pass_bert():
     torch.cuda.synchronize()
     assert ovl.opt.step_count == 3 and int(ovl.opt._t.item()) == 3
 
-    def diff(a, b):
-        return max(float((gb.fp32 - ga.fp32).abs().max()) for ga, gb in zip(a.groups, b.groups))
-    d_ctl, d_ovl = diff(ref, ctl), diff(ref, ovl)
-    # the one-pass runs differ by the embedding backward's fp32 atomic order (Adam turns
-    # near-zero gradient noise into up to ~lr of weight); an update that misses part of a
-    # bucket's gradient moved weights by 2e-3 .. 6e-3 here
-    assert d_ovl <= max(4 * d_ctl, 2e-4), (d_ovl, d_ctl, losses)
+    def frac(a, b):  # share of weights that moved apart by more than rounding
+        n = sum(g.fp32.numel() for g in a.groups)
+        return sum(int(((gb.fp32 - ga.fp32).abs() > 1e-5).sum()) for ga, gb in zip(a.groups, b.groups)) / n
+    # The one-pass runs already differ run to run: the embedding backward's fp32 atomics
+    # sum in a varying order, and Adam's first steps turn the sign of a near-zero gradient
+    # into a +-lr move, so a maximum difference cannot separate noise from a bug.  The
+    # share of weights that differ can: an update that missed part of a bucket's gradient
+    # moved whole tensors (19 of 41, ~15 % of the weights, before the bucket-count fix).
+    f_ctl, f_ovl = frac(ref, ctl), frac(ref, ovl)
+    assert f_ovl <= max(10 * f_ctl, 1e-3), (f_ovl, f_ctl, losses)
     for a, b in zip(losses["ref"], losses["ovl"]):
         assert abs(a - b) <= 1e-3 * max(1.0, abs(a)), losses
 
