@@ -295,7 +295,9 @@ def run_rank(args) -> int:
                        "grad_reduce": args.grad_reduce if info.world > 1 else None,
                        "backend": (torch.distributed.get_backend() if torch.distributed.is_initialized()
                                    else None),
-                       "comm": repr(engine.comm) if info.world > 1 else None,
+                       # layer / default group / RCCL transport per peer, and the per-step
+                       # compute-stream wait for the gradient collectives after backward
+                       "comm": dict(engine.comm_info(), comm_wait_ms=r["comm_wait_ms"]),
                        "routes": routes.summary(),
                        "optimizer": "SGD momentum 0.9 (fused HIP), fp32 master",
                        "hip_graph": engine._graph is not None,

@@ -9,9 +9,10 @@
   compiled by ``hipcc --offload-arch=gfx950`` into ONE shared object with a C
   ABI; Python binds it with ``ctypes`` (``ops/_lib.py``), so no torch headers
   are compiled and rebuilds take seconds.
-* ``build/sanitize/runtime_selftest_{asan,tsan}`` — the runtime core's native
-  self-test (``csrc/runtime/selftest.cpp``) under ASan+UBSan and TSan
-  (``--sanitize``; host code only).
+* ``build/sanitize/{runtime,comm}_selftest_{asan,tsan}`` — the runtime core's native
+  self-test (``csrc/runtime/selftest.cpp``) and the collective layer's
+  (``csrc/comm/comm_selftest.cpp``: 3 host-backend ranks as threads) under
+  ASan+UBSan and TSan (``--sanitize``; host code only).
 
 Everything lands inside the package directory so it travels with the repo
 snapshot to the GPU box (``gpurun``) and is visible as an in-tree ``.so``.
@@ -197,17 +198,25 @@ def sanitize_cxx() -> str:
     return os.environ.get("CXX", "g++")
 
 
-def sanitize_target(kind: str, canary: bool = False) -> str:
-    return os.path.join(ROOT, "build", "sanitize", f"runtime_selftest_{kind}" + ("_canary" if canary else ""))
+SELFTESTS = {
+    "runtime": [os.path.join(CSRC, "runtime", "selftest.cpp"), os.path.join(CSRC, "runtime", "runtime_core.h")],
+    "comm": [os.path.join(CSRC, "comm", "comm_selftest.cpp"), os.path.join(CSRC, "comm", "comm.cpp")],
+}
 
 
-def build_sanitized(kind: str, force: bool = False, canary: bool = False) -> str:
-    """Compile the runtime core's self-test under one sanitizer (host code only).
+def sanitize_target(kind: str, canary: bool = False, target: str = "runtime") -> str:
+    return os.path.join(ROOT, "build", "sanitize", f"{target}_selftest_{kind}" + ("_canary" if canary else ""))
+
+
+def build_sanitized(kind: str, force: bool = False, canary: bool = False, target: str = "runtime") -> str:
+    """Compile a native self-test under one sanitizer (host code only):
+    ``target`` = ``runtime`` (work queue, limiters, expectations, launcher) or
+    ``comm`` (the collective layer's host backend, 3 ranks as threads).
 
     ``canary=True`` also compiles in a deliberate defect (a data race under
     TSan, a heap overflow under ASan) so a test can prove the tool is live."""
-    srcs = [os.path.join(CSRC, "runtime", "selftest.cpp"), os.path.join(CSRC, "runtime", "runtime_core.h")]
-    tgt = sanitize_target(kind, canary)
+    srcs = SELFTESTS[target]
+    tgt = sanitize_target(kind, canary, target)
     with _lock:
         if not force and _up_to_date(tgt, srcs):
             return tgt
@@ -215,17 +224,18 @@ def build_sanitized(kind: str, force: bool = False, canary: bool = False) -> str
         tmp = tgt + f".tmp{os.getpid()}"
         cmd = [sanitize_cxx(), "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-Wall",
                "-Wno-unused-function", *SANITIZERS[kind], *(["-DKFA_SELFTEST_INJECT"] if canary else []),
-               srcs[0], "-o", tmp, "-lpthread"]
+               srcs[0], "-o", tmp, "-lpthread", *(["-ldl"] if target == "comm" else [])]
         _run(cmd, quiet=True)
         os.replace(tmp, tgt)
         _write_stamp(tgt, srcs)
     return tgt
 
 
-def run_sanitized(kind: str, timeout: float = 300.0, canary: bool = False) -> subprocess.CompletedProcess:
+def run_sanitized(kind: str, timeout: float = 300.0, canary: bool = False,
+                  target: str = "runtime") -> subprocess.CompletedProcess:
     """Build and run one sanitizer self-test; a sanitizer report makes it exit
     23 (ASan / UBSan build) or 25 (TSan build)."""
-    exe = build_sanitized(kind, canary=canary)
+    exe = build_sanitized(kind, canary=canary, target=target)
     env = dict(os.environ)
     env.pop("LD_PRELOAD", None)  # a preloaded runtime ahead of libasan/libtsan aborts the run
     if kind == "asan":  # UBSan shares the common flags (exitcode) of the ASan runtime
@@ -245,9 +255,9 @@ def build_all(force: bool = False) -> None:
 if __name__ == "__main__":
     if "--sanitize" in sys.argv:
         rc = 0
-        for kind in SANITIZERS:
-            r = run_sanitized(kind)
-            sys.stdout.write(f"[{kind}] " + r.stdout)
+        for target, kind in [(t, k) for t in SELFTESTS for k in SANITIZERS]:
+            r = run_sanitized(kind, target=target)
+            sys.stdout.write(f"[{target} {kind}] " + r.stdout)
             if r.returncode != 0:
                 sys.stderr.write(r.stderr[-8000:])
                 rc = r.returncode

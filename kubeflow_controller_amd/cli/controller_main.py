@@ -67,6 +67,9 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--root-dir", default=os.path.expanduser("~/.kfa/pods"), help="replica working/log dirs")
     ap.add_argument("--num-gpus", type=int, default=None, help="GPUs on this node (default: detect)")
     ap.add_argument("--gpu-policy", choices=["auto", "none", "share"], default="auto")
+    ap.add_argument("--gpu-binding", choices=["isolate", "visible"], default=None,
+                    help="isolate: HIP_VISIBLE_DEVICES=<the replica's GPU> (default, or KFA_GPU_BINDING); "
+                         "visible: every node GPU visible, the replica's ordinal in KFA_LOCAL_DEVICE / LOCAL_RANK")
     ap.add_argument("--threadiness", type=int, default=2)
     ap.add_argument("--resync", type=float, default=30.0)
     ap.add_argument("--url-file", default="", help="write the standalone apiserver URL to this file")
@@ -78,7 +81,7 @@ class Node:
 
     def __init__(self, store, *, threadiness: int = 2, resync: float = 30.0, kubelet: bool = True,
                  root_dir: str = "", num_gpus: Optional[int] = None, gpu_policy: str = "auto",
-                 kubelet_backoff: float = 1.0, extra_env=None):
+                 kubelet_backoff: float = 1.0, extra_env=None, gpu_binding: Optional[str] = None):
         from ..client.clientset import Clientset
         from ..client.informer import SharedInformerFactory
         from ..controller.controller import Controller
@@ -100,7 +103,7 @@ class Node:
             self.supervisor = Supervisor(self.kube_client, kinf.pods(), kinf.services(),
                                          root_dir or os.path.expanduser("~/.kfa/pods"), num_gpus=num_gpus,
                                          gpu_policy=gpu_policy, backoff_base=kubelet_backoff, extra_env=extra_env,
-                                         tfjob_informer=kinf.tfjobs())
+                                         tfjob_informer=kinf.tfjobs(), gpu_binding=gpu_binding)
         self.stop = threading.Event()
         self._threads: List[threading.Thread] = []
 
@@ -152,7 +155,8 @@ def main(argv: Optional[List[str]] = None) -> int:
                 f.write(server.url + "\n")
     run_kubelet = args.kubelet == "on" or (args.kubelet == "auto" and standalone)
     node = Node(store, threadiness=args.threadiness, resync=args.resync, kubelet=run_kubelet,
-                root_dir=args.root_dir, num_gpus=args.num_gpus, gpu_policy=args.gpu_policy)
+                root_dir=args.root_dir, num_gpus=args.num_gpus, gpu_policy=args.gpu_policy,
+                gpu_binding=args.gpu_binding)
     node.start()
     stop.wait()
     log.info("shutting down")

@@ -232,7 +232,8 @@ def cmd_kubelet(args) -> int:
     cs = Clientset(st)
     EndpointController(cs, inf.services())
     sup = Supervisor(cs, inf.pods(), inf.services(), args.root_dir, num_gpus=args.num_gpus,
-                     gpu_policy=args.gpu_policy, tfjob_informer=inf.tfjobs())
+                     gpu_policy=args.gpu_policy, tfjob_informer=inf.tfjobs(),
+                     gpu_binding=getattr(args, "gpu_binding", None))
     inf.start(stop)
     sup.run(stop)
     return 0
@@ -324,6 +325,7 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--root-dir", default=os.path.expanduser("~/.kfa/pods"))
     p.add_argument("--num-gpus", type=int, default=None)
     p.add_argument("--gpu-policy", default="auto", choices=["auto", "none", "share"])
+    p.add_argument("--gpu-binding", default=None, choices=["isolate", "visible"])
     p.set_defaults(fn=cmd_kubelet)
     p = sub.add_parser("up")
     p.add_argument("--listen", default="127.0.0.1:8443"); p.add_argument("--data-dir", default="")

@@ -7,7 +7,12 @@ and for each new one:
    the node policy (``gpu_policy="auto"``: every Worker / Local replica gets one
    GPU, round-robin over the free ones; PS replicas get none — parameter
    shards are owned by worker ranks); pins them with
-   ``HIP_VISIBLE_DEVICES``;
+   ``HIP_VISIBLE_DEVICES`` (``gpu_binding="isolate"``, the default) or — with
+   ``gpu_binding="visible"`` — keeps every node GPU visible and names the
+   replica's own ordinal in ``KFA_LOCAL_DEVICE`` / ``LOCAL_RANK`` (the
+   reference picks its device out of a fully visible set,
+   ``examples/workdir/mnist_replica.py:125-129``; the same device set as
+   ``bench.py`` under torchrun, so RCCL sees the same peers and transports);
 2. resolves the cluster spec: ``<svc>:2222`` endpoints in the args are served
    by the endpoint controller, the resolution map is exported as
    ``KFA_SERVICE_HOSTS`` (the kube-dns role) — the replica keeps the
@@ -95,7 +100,8 @@ class _Proc:
 class Supervisor:
     def __init__(self, clientset, pod_informer, service_informer, root_dir: str, *, num_gpus: Optional[int] = None,
                  gpu_policy: str = "auto", backoff_base: float = 1.0, backoff_max: float = 60.0,
-                 grace_period: float = 10.0, extra_env: Optional[Dict[str, str]] = None, tfjob_informer=None):
+                 grace_period: float = 10.0, extra_env: Optional[Dict[str, str]] = None, tfjob_informer=None,
+                 gpu_binding: Optional[str] = None):
         self.client = clientset
         self.pods = pod_informer.lister()
         self.services = service_informer.lister()
@@ -104,6 +110,9 @@ class Supervisor:
         os.makedirs(self.root, exist_ok=True)
         self.num_gpus = detect_gpus() if num_gpus is None else num_gpus
         self.gpu_policy = gpu_policy
+        self.gpu_binding = (gpu_binding or os.environ.get("KFA_GPU_BINDING", "isolate")).lower()
+        if self.gpu_binding not in ("isolate", "visible"):
+            raise ValueError(f"gpu_binding {self.gpu_binding!r}: isolate | visible")
         self.backoff_base = backoff_base
         self.backoff_max = backoff_max
         self.grace = grace_period
@@ -271,6 +280,11 @@ class Supervisor:
         if ps_gpus:  # the job's PS GPUs after the worker's own: IPC peer copies need them visible
             visible += [g for g in dict.fromkeys(ps_gpus) if g not in visible]
             env["KFA_PS_GPUS"] = ",".join(str(g) for g in ps_gpus)
+        env.pop("KFA_LOCAL_DEVICE", None)
+        if gpus and self.gpu_binding == "visible":
+            # every node GPU visible in physical order; the replica's own GPU by ordinal
+            visible = list(range(self.num_gpus))
+            env["KFA_LOCAL_DEVICE"] = str(gpus[0])
         env["HIP_VISIBLE_DEVICES"] = ",".join(str(g) for g in visible) if visible else ""
         env.pop("ROCR_VISIBLE_DEVICES", None)
         env.pop("CUDA_VISIBLE_DEVICES", None)

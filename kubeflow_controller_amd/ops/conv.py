@@ -111,8 +111,8 @@ def _agree(hit: bool, device) -> bool:
     import torch.distributed as dist
     if not _LOCKSTEP or not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return hit
-    dev = device if dist.get_backend() == "nccl" else torch.device("cpu")
-    t = torch.tensor([1 if hit else 0], dtype=torch.int32, device=dev)
+    from ..parallel.comm import control_device  # the CPU unless the default group is torch's RCCL
+    t = torch.tensor([1 if hit else 0], dtype=torch.int32, device=control_device(device))
     dist.broadcast(t, 0)
     return bool(t.item())
 

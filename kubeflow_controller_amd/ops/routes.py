@@ -37,7 +37,9 @@ ARCH = os.environ.get("KFA_ROUTES_ARCH", "gfx950")
 MODE = os.environ.get("KFA_ROUTES", "on").lower()     # on | off | retune
 TABLE_PATH = os.environ.get("KFA_ROUTES_FILE",
                             os.path.join(os.path.dirname(os.path.abspath(__file__)), f"routes_{ARCH}.json"))
-LIBRARY_NAMES = ("hipblaslt", "library", "vendor", "sep", "miopen")
+# candidate names that run a vendor library kernel; every other pick is an own HIP
+# kernel ("sep" = the separate own BatchNorm-apply pass, "igemm" / "pp" = own conv tiles)
+LIBRARY_NAMES = ("hipblaslt", "library", "vendor", "miopen")
 
 _table: Optional[Dict[str, str]] = None
 _made: Dict[str, dict] = {}      # key -> {"pick": name, "times": {...} | None, "from": "table" | "timed"}
@@ -80,8 +82,8 @@ def _agree_index(i: int, device) -> int:
     from . import conv as _c
     if not _c._LOCKSTEP or not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return i
-    dev = device if dist.get_backend() == "nccl" else torch.device("cpu")
-    t = torch.tensor([int(i)], dtype=torch.int32, device=dev)
+    from ..parallel.comm import control_device  # the CPU unless the default group is torch's RCCL
+    t = torch.tensor([int(i)], dtype=torch.int32, device=control_device(device))
     dist.broadcast(t, 0)
     return int(t.item())
 

@@ -401,11 +401,14 @@ CANARY_N = 64
 
 
 def physical_gpu() -> str:
-    """Physical index of this process's cuda:0 (the supervisor's ``KFA_GPUS`` /
-    ``HIP_VISIBLE_DEVICES`` list, first entry); "" when not pinned."""
-    vis = os.environ.get("KFA_GPUS") or os.environ.get("HIP_VISIBLE_DEVICES") or ""
-    first = vis.split(",")[0].strip()
-    return first
+    """Physical index of this process's own GPU (entry ``local_device()`` of the
+    supervisor's ``KFA_GPUS`` / ``HIP_VISIBLE_DEVICES`` list: the first one when the
+    replica is isolated, its ``KFA_LOCAL_DEVICE`` ordinal when every GPU is
+    visible); "" when not pinned."""
+    from ..trainer.cluster import local_device
+    vis = [v.strip() for v in (os.environ.get("KFA_GPUS") or os.environ.get("HIP_VISIBLE_DEVICES") or "").split(",")]
+    i = local_device()
+    return vis[i] if i < len(vis) else ""
 
 
 def local_ordinal(phys: str) -> Tuple[Optional[int], str]:

@@ -24,13 +24,28 @@ work object with ``wait()``):
 
 :func:`make_comm` picks one: ``KFA_COMM`` = ``native`` | ``torch``; default
 native on GPUs (RCCL), torch (gloo) on the CPU.
+
+ONE RCCL communicator per process: a GPU job whose gradient traffic runs on the
+native layer initialises ``torch.distributed`` with **gloo** (:func:`dist_backend`)
+and uses it for control scalars only — tuner agreement (``routes._agree_index``,
+``conv._agree``), the timing MAX, barriers, the native layer's keep/fall-back vote
+— always on CPU tensors (:func:`control_device`).  No torch RCCL communicator is
+created unless the native layer fails on some rank; then every rank falls back
+together to a torch ``nccl`` group created at that point.  ``KFA_COMM=torch``
+keeps the old layout (nccl default group, torch's communicator for everything)
+for A/B.  RCCL's transport choice per peer (P2P/IPC over xGMI vs SHM / NET) is
+read from its INIT/P2P log at bring-up (:attr:`Communicator.transport`) and
+reported in ``bench.py``'s ``config.comm``.
 """
 from __future__ import annotations
 
 import ctypes
 import itertools
 import os
-from typing import Optional, Sequence
+import re
+import sys
+import tempfile
+from typing import Dict, Optional, Sequence
 
 import torch
 import torch.distributed as dist
@@ -60,9 +75,9 @@ def lib() -> ctypes.CDLL:
     if _LIB is not None:
         return _LIB
     from .. import _build
-    path = _build.comm_target()
-    if not os.path.exists(path):
-        _build.build_comm()
+    # rebuilt when comm.cpp changed since the library was built (source stamp, under
+    # the build lock, atomic replace): a stale .so would bind a different ABI
+    path = _build.build_comm()
     L = ctypes.CDLL(path)
     sig = {
         "kfc_last_error": ([], ctypes.c_char_p), "kfc_listen": ([ctypes.c_char_p, _I, ctypes.POINTER(_I)], _I),
@@ -125,10 +140,13 @@ class Communicator:
 
     native = True
 
-    def __init__(self, handle, rank: int, world: int, device: torch.device, backend: str):
+    def __init__(self, handle, rank: int, world: int, device: torch.device, backend: str,
+                 debug_log: Optional[str] = None):
         self._h = handle
         self.rank, self.world, self.device, self.backend = rank, world, device, backend
         self.stream = torch.cuda.Stream(device=device) if device.type == "cuda" else None
+        self._debug_log = debug_log   # RCCL's INIT/P2P log of this process (transport capture)
+        self._transport: Optional[Dict] = None
 
     @classmethod
     def create(cls, store, rank: int, world: int, device: torch.device, backend: Optional[str] = None,
@@ -136,26 +154,54 @@ class Communicator:
                timeout_s: float = 300.0) -> "Communicator":
         """Collective over every rank: rank 0 listens and publishes its address under
         ``key`` in ``store`` (a ``torch.distributed`` Store); the others read it and
-        connect.  Every rank must create its communicators in the same order."""
+        connect.  Every rank must create its communicators in the same order.
+
+        Rank 0 publishes the key even when it fails before listening (``ERR:<why>``),
+        so the other ranks fail at once instead of waiting out the store timeout."""
         backend = backend or ("rccl" if device.type == "cuda" else "host")
         key = key or f"kfc/comm/{next(_KEYS)}"
-        L = lib()
         tmo = int(timeout_s * 1000)
         if rank == 0:
-            port = ctypes.c_int(0)
-            fd = L.kfc_listen(b"", 0, ctypes.byref(port))
-            if fd < 0:
-                _check(-fd, "kfc_listen")
+            try:
+                L = lib()
+                port = ctypes.c_int(0)
+                fd = L.kfc_listen(b"", 0, ctypes.byref(port))
+                if fd < 0:
+                    _check(-fd, "kfc_listen")
+            except Exception as e:  # noqa: BLE001 - tell the peers, then raise
+                store.set(key, f"ERR:{e}")
+                raise
             host = advertise_host or os.environ.get("MASTER_ADDR", "127.0.0.1")
             store.set(key, f"{host}:{port.value}")
+            log = _arm_rccl_log(key) if backend == "rccl" else None
             h = L.kfc_comm_init(backend.encode(), world, 0, None, 0, fd, tmo)
+            _disarm_rccl_log()
         else:
             addr = store.get(key).decode()
+            if addr.startswith("ERR:"):
+                raise CommError(f"rank 0 could not open the communicator: {addr[4:]}")
+            L = lib()
             host, _, port = addr.rpartition(":")
+            log = _arm_rccl_log(key) if backend == "rccl" else None
             h = L.kfc_comm_init(backend.encode(), world, rank, host.encode(), int(port), -1, tmo)
+            _disarm_rccl_log()
         if not h:
             raise CommError(f"kfc_comm_init({backend}, rank {rank}/{world}): {L.kfc_last_error().decode()}")
-        return cls(h, rank, world, device, backend)
+        return cls(h, rank, world, device, backend, debug_log=log)
+
+    @property
+    def transport(self) -> Dict:
+        """RCCL's transport per connection of this rank, from its INIT/P2P log:
+        ``{"via": {"P2P/IPC": n, ...}, "peers": {peer: transport}}`` (P2P/IPC =
+        direct xGMI peer access; SHM / NET = a fallback through host memory / sockets);
+        ``{"via": "unknown"}`` when the log was not available (``NCCL_DEBUG`` set by
+        the user, or RCCL's logging already initialised in this process)."""
+        if self._transport is None and self.backend == "rccl":
+            t = parse_rccl_transport(self._debug_log, self.rank)
+            if t.get("via") != "unknown":
+                self._transport = t
+            return t
+        return self._transport or {"via": self.backend}
 
     # -------------------------------------------------------------- plumbing
     def _stream_arg(self):
@@ -285,6 +331,54 @@ class Communicator:
         return f"Communicator({self.backend}, rank {self.rank}/{self.world}, {self.device})"
 
 
+_RCCL_LOG_VARS = ("NCCL_DEBUG", "NCCL_DEBUG_SUBSYS", "NCCL_DEBUG_FILE")
+
+
+def _arm_rccl_log(key: str) -> Optional[str]:
+    """Point RCCL's INFO log (INIT and P2P subsystems only) at a per-process file
+    for the transport capture, unless the user set ``NCCL_DEBUG`` (then theirs
+    stands) or ``KFA_RCCL_TRANSPORT_LOG=0``.  RCCL reads these variables once per
+    process, at its first call; the file keeps receiving the lazily-made
+    connections' lines (the first collectives)."""
+    if os.environ.get("KFA_RCCL_TRANSPORT_LOG", "1") != "1" or "NCCL_DEBUG" in os.environ:
+        return None
+    path = os.path.join(tempfile.gettempdir(),
+                        f"kfc_rccl_{os.getpid()}_{re.sub(r'[^A-Za-z0-9]', '_', key)}.log")
+    os.environ.update({"NCCL_DEBUG": "INFO", "NCCL_DEBUG_SUBSYS": "INIT,P2P", "NCCL_DEBUG_FILE": path})
+    return path
+
+
+def _disarm_rccl_log() -> None:
+    """Drop the logging variables from this process's environment again (children
+    must not inherit them); RCCL keeps the settings it already read."""
+    for v in _RCCL_LOG_VARS:
+        os.environ.pop(v, None)
+
+
+_VIA = re.compile(r"(\d+)\[[^\]]*\]\s*->\s*(\d+)\[[^\]]*\]\s*(?:\[\w+\]\s*)?via\s+(\S+)")
+
+
+def parse_rccl_transport(path: Optional[str], rank: int) -> Dict:
+    """Summarise RCCL's "Channel cc/r : a[d] -> b[e] via T" lines for ``rank``."""
+    if not path or not os.path.exists(path):
+        return {"via": "unknown"}
+    via: Dict[str, int] = {}
+    peers: Dict[int, str] = {}
+    with open(path, errors="replace") as f:
+        for line in f:
+            m = _VIA.search(line)
+            if not m:
+                continue
+            a, b, t = int(m.group(1)), int(m.group(2)), m.group(3)
+            if rank not in (a, b) or a == b:
+                continue
+            via[t] = via.get(t, 0) + 1
+            peers.setdefault(b if a == rank else a, t)
+    if not via:
+        return {"via": "unknown"}
+    return {"via": via, "peers": {str(k): v for k, v in sorted(peers.items())}}
+
+
 class TorchComm:
     """The same interface over ``torch.distributed`` (gloo on the CPU: the test double)."""
 
@@ -403,16 +497,61 @@ def make_p2p(store=None, mode: Optional[str] = None, timeout_s: Optional[float] 
                                    torch.device("cpu"), backend="host", key="kfc/ps_p2p", timeout_s=t))
 
 
+_CONTROL_ONLY = False  # the default group is gloo for control scalars; RCCL = the native layer
+
+
+def dist_backend(use_gpu: bool) -> str:
+    """Backend for a job's default ``torch.distributed`` group: ``KFA_DIST_BACKEND``
+    if set (gloo on GPUs = several ranks sharing one GPU, which RCCL refuses);
+    else on GPUs **gloo** when the gradient traffic will run on the native
+    communicator (control scalars only, see the module doc) and nccl under
+    ``KFA_COMM=torch``; gloo on the CPU."""
+    forced = os.environ.get("KFA_DIST_BACKEND")
+    if forced:
+        return forced
+    if not use_gpu:
+        return "gloo"
+    return "nccl" if os.environ.get("KFA_COMM", "").lower() == "torch" else "gloo"
+
+
+def init_default_group(rank: int, world: int, device: torch.device, timeout, store=None,
+                       backend: Optional[str] = None) -> str:
+    """``dist.init_process_group`` with :func:`dist_backend`; returns the backend.
+    An nccl group is bound to ``device`` (eager communicator); a control-only gloo
+    group on a GPU job marks this process for the native layer (:func:`comm_mode`)."""
+    global _CONTROL_ONLY
+    use_gpu = device.type == "cuda"
+    be = backend or dist_backend(use_gpu)
+    if be == "nccl":
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+    kw = {"device_id": device} if (be == "nccl" and use_gpu) else {}
+    if store is not None:
+        kw["store"] = store
+    dist.init_process_group(be, rank=rank, world_size=world, timeout=timeout, **kw)
+    _CONTROL_ONLY = use_gpu and be == "gloo" and not (backend or os.environ.get("KFA_DIST_BACKEND"))
+    return be
+
+
+def control_device(device) -> torch.device:
+    """Where a control scalar lives for a collective on the default group: the GPU
+    only when that group IS torch's RCCL (``KFA_COMM=torch``), else the CPU (gloo)."""
+    if device is not None and torch.device(device).type == "cuda" and dist.is_initialized() \
+            and dist.get_backend() == "nccl":
+        return torch.device(device)
+    return torch.device("cpu")
+
+
 def comm_mode(device: torch.device) -> str:
-    """``KFA_COMM`` if set; else native on GPUs whose process group runs RCCL — a job
-    that forced gloo on GPUs (``KFA_DIST_BACKEND=gloo``: several ranks sharing one
-    GPU, which RCCL refuses) keeps torch.distributed — and torch (gloo) on the CPU."""
+    """``KFA_COMM`` if set; else native on GPUs whose default group runs RCCL or is
+    the control-only gloo group of :func:`init_default_group` — a job that forced
+    gloo on GPUs (``KFA_DIST_BACKEND=gloo``: several ranks sharing one GPU, which
+    RCCL refuses) keeps torch.distributed — and torch (gloo) on the CPU."""
     m = os.environ.get("KFA_COMM", "").lower()
     if m in ("native", "torch"):
         return m
     if device.type != "cuda":
         return "torch"
-    if dist.is_initialized() and dist.get_backend() != "nccl":
+    if dist.is_initialized() and dist.get_backend() != "nccl" and not _CONTROL_ONLY:
         return "torch"
     return "native"
 
@@ -427,6 +566,31 @@ def default_store():
                              is_master=False)
 
 
+def _probe(comm, device, world: int, rank: int) -> str:
+    """One reduce-scatter and one all-gather over rank-distinct values, checked
+    element by element: catches a wrong offset, order or dtype, not only a dead
+    communicator ("" = good)."""
+    n = 4 * world + 3  # per-rank block, odd
+    base = torch.arange(n * world, dtype=torch.float32, device=device)
+    inp = base * (rank + 1) + 1000.0 * rank
+    out = torch.empty(n, dtype=torch.float32, device=device)
+    comm.reduce_scatter_tensor(out, inp, "sum")
+    tot = sum(r + 1 for r in range(world))
+    want = base[rank * n:(rank + 1) * n] * tot + 1000.0 * sum(range(world))
+    if not torch.equal(out, want):
+        return f"probe reduce-scatter mismatch on rank {rank}"
+    mine = torch.full((n,), float(rank * 7 + 1), device=device) + torch.arange(n, dtype=torch.float32, device=device)
+    g = torch.empty(n * world, dtype=torch.float32, device=device)
+    comm.all_gather_into_tensor(g, mine)
+    want = torch.cat([torch.full((n,), float(r * 7 + 1), device=device)
+                      + torch.arange(n, dtype=torch.float32, device=device) for r in range(world)])
+    if device.type == "cuda":
+        torch.cuda.current_stream(device).synchronize()
+    if not torch.equal(g, want):
+        return f"probe all-gather mismatch on rank {rank}"
+    return ""
+
+
 def make_comm(device: torch.device, process_group=None, store=None, mode: Optional[str] = None):
     """The communicator for a job's gradient / parameter traffic (see module doc)."""
     mode = mode or comm_mode(device)
@@ -435,20 +599,20 @@ def make_comm(device: torch.device, process_group=None, store=None, mode: Option
     if process_group is not None and process_group is not dist.group.WORLD:
         raise CommError("the native communicator spans the default group's ranks only")
     t = float(os.environ.get("KFA_DIST_INIT_TIMEOUT", "300"))
-    world = dist.get_world_size()
+    world, rank = dist.get_world_size(), dist.get_rank()
     comm, err = None, ""
     try:
-        comm = Communicator.create(store or default_store(), dist.get_rank(), world, device, timeout_s=t)
-        probe = torch.ones(1, device=device)  # one collective end to end before any training traffic
-        comm.all_reduce(probe, "sum")
-        ok = int(probe.item()) == world
-        err = "" if ok else f"probe all-reduce gave {probe.item()} (world {world})"
+        comm = Communicator.create(store or default_store(), rank, world, device, timeout_s=t)
+        err = _probe(comm, device, world, rank)  # before any training traffic
+        ok = not err
+        if ok and comm.backend == "rccl":
+            comm.transport  # noqa: B018 - read the log while the probe's connections are fresh
     except Exception as e:  # noqa: BLE001 - decided collectively below
         ok, err = False, str(e)
     # every rank keeps the native layer or none does (a rank that fell back alone would
-    # leave its peers waiting in collectives it never joins)
-    flag = torch.tensor([1 if ok else 0], dtype=torch.int32,
-                        device=device if dist.get_backend() == "nccl" else torch.device("cpu"))
+    # leave its peers waiting in collectives it never joins); the vote rides the
+    # default group on the CPU (gloo) unless that group is torch's RCCL
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=control_device(device))
     dist.all_reduce(flag, op=dist.ReduceOp.MIN)
     if int(flag.item()) == 1:
         return comm
@@ -456,7 +620,10 @@ def make_comm(device: torch.device, process_group=None, store=None, mode: Option
         comm.destroy()
     if mode == "native" and os.environ.get("KFA_COMM", "").lower() == "native":
         raise CommError(f"native communicator unavailable: {err or 'another rank failed'}")
-    import sys
     print(f"[kfc comm] native communicator unavailable ({err or 'another rank failed'}): torch.distributed",
           file=sys.stderr, flush=True)
+    if device.type == "cuda" and dist.get_backend() != "nccl":
+        # the control-only gloo default group cannot carry GPU tensors fast: torch's
+        # RCCL in a group of its own (created by every rank together, here)
+        return TorchComm(dist.new_group(backend="nccl"))
     return TorchComm(process_group)

@@ -61,6 +61,10 @@ class GradSync:
         self.buckets, self._of_param = plan_buckets(self.groups, bucket_mb, ALIGN, eb)
         self._hooks = []
         self._on_ready = None  # single process: per-bucket callback (Engine's overlapped optimizer)
+        # exposed communication per step: compute-stream time from the end of backward
+        # to the last bucket's collective (event pairs, read lazily: no host wait)
+        self._wait_ev: List[Tuple[torch.cuda.Event, torch.cuda.Event]] = []
+        self._wait_ms: List[float] = []
         if self.overlap:
             self._install_hooks()
         self.reset()
@@ -95,6 +99,12 @@ class GradSync:
                 b.pending -= 1
                 if b.pending == 0:
                     self._launch(b)
+                elif b.pending < 0:
+                    # a gradient reported ready more often than its bucket counts (an
+                    # undeclared tied parameter): the collective already ran without it
+                    raise RuntimeError(f"gradient bucket {b.group}:{b.start}-{b.end} got {b.total - b.pending} "
+                                       f"ready notifications for {b.total} tensors (declare tied parameters' "
+                                       "uses in _kfa_param_uses)")
         return hook
 
     def reset(self) -> None:
@@ -132,10 +142,40 @@ class GradSync:
         for b in self.buckets:
             if b.work is None:
                 self._launch(b)
+        timed = self.groups and self.groups[0].grad.is_cuda
+        if timed:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
         for b in self.buckets:
             b.work.wait()
+        if timed:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            self._wait_ev.append((e0, e1))
+            self._collect(block=False)
         self.reset()
         return 1.0 / self.world
+
+    def _collect(self, block: bool) -> None:
+        keep = []
+        for e0, e1 in self._wait_ev:
+            if block or e1.query():
+                if block:
+                    e1.synchronize()
+                self._wait_ms.append(e0.elapsed_time(e1))
+            else:
+                keep.append((e0, e1))
+        self._wait_ev = keep
+
+    def comm_wait_ms(self, reset: bool = False) -> Optional[float]:
+        """Mean per-step time the compute stream waited for the gradient collectives
+        after backward had issued its last kernel (the exposed, non-overlapped part of
+        the all-reduce), over the steps since the last reset; None at world 1 / CPU."""
+        self._collect(block=True)
+        v = sum(self._wait_ms) / len(self._wait_ms) if self._wait_ms else None
+        if reset:
+            self._wait_ms.clear()
+        return v
 
     def pull(self) -> None:
         """No-op: every rank applied the same update to the full weights."""

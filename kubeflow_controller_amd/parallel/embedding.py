@@ -369,8 +369,13 @@ class ShardedEmbedding(nn.Module):
         maxr = -(-self.num_rows // self.owners)  # equal-size pieces (gloo needs them)
         mine = torch.zeros(maxr, self.dim, device=self.weight.device)
         mine[:self.local_rows] = self.weight.detach()
-        parts = [torch.empty_like(mine) for _ in range(self.world)]
-        dist.all_gather(parts, mine, group=self.pg)
+        if self.comm is not None:  # the job's communicator (a gloo control group cannot take GPU tensors)
+            flat = torch.empty(self.world * maxr, self.dim, device=mine.device)
+            self.comm.all_gather_into_tensor(flat, mine)
+            parts = list(flat.split(maxr))
+        else:
+            parts = [torch.empty_like(mine) for _ in range(self.world)]
+            dist.all_gather(parts, mine, group=self.pg)
         parts = [p[:len(range(r, self.num_rows, self.owners))] for r, p in enumerate(parts[:self.owners])]
         full = torch.empty(self.num_rows, self.dim, device=self.weight.device)
         for r in range(self.owners):

@@ -202,6 +202,10 @@ class ShardedGradSync:
                 b.pending -= 1
                 if b.pending == 0:
                     self._push(b)
+                elif b.pending < 0:  # see ddp.GradSync._make_hook
+                    raise RuntimeError(f"gradient bucket {b.group}:{b.start}-{b.end} got {b.total - b.pending} "
+                                       f"ready notifications for {b.total} tensors (declare tied parameters' "
+                                       "uses in _kfa_param_uses)")
         return hook
 
     def reset(self) -> None:

@@ -65,7 +65,19 @@ class ClusterSpec:
         host, port = self.rendezvous()
         rank = 0 if self.is_local else self.task_index
         return {"RANK": str(rank), "WORLD_SIZE": str(1 if self.is_local else self.num_workers),
-                "LOCAL_RANK": "0", "MASTER_ADDR": host, "MASTER_PORT": str(port)}
+                "LOCAL_RANK": str(local_device()), "MASTER_ADDR": host, "MASTER_PORT": str(port)}
+
+
+def local_device(environ=None) -> int:
+    """This replica's own GPU as a device ordinal of this process: 0 when the
+    supervisor isolates it (``HIP_VISIBLE_DEVICES=<own>[,PS GPUs]``), its physical
+    index when every node GPU is visible (``gpu_binding="visible"``:
+    ``KFA_LOCAL_DEVICE``)."""
+    env = os.environ if environ is None else environ
+    try:
+        return max(0, int(env.get("KFA_LOCAL_DEVICE", "0") or 0))
+    except ValueError:
+        return 0
 
 
 def add_cluster_flags(ap: argparse.ArgumentParser) -> None:

@@ -36,7 +36,10 @@ def init_distributed(backend: Optional[str] = None, prefer_gpu: bool = True,
 
     ``KFA_DIST_BACKEND=gloo`` forces gloo even on GPUs: a rehearsal of the
     multi-rank path with several ranks sharing one GPU (RCCL refuses two ranks
-    on one device in a communicator).
+    on one device in a communicator).  Otherwise a GPU job's default group is gloo
+    for control scalars only and its gradient traffic runs on the first-party RCCL
+    communicator (``parallel/comm.py``), so the process holds ONE RCCL
+    communicator; ``KFA_COMM=torch`` makes the default group nccl instead.
 
     ``timeout_s`` (default ``KFA_DIST_INIT_TIMEOUT`` or 300 s) bounds the
     rendezvous and every collective: a rank that never arrives fails the job
@@ -57,13 +60,12 @@ def init_distributed(backend: Optional[str] = None, prefer_gpu: bool = True,
     else:
         dev = torch.device("cpu")
     if world > 1 and not dist.is_initialized():
-        be = backend or os.environ.get("KFA_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
-        kw = {"device_id": dev} if (be == "nccl" and use_gpu) else {}
-        if be == "nccl":
-            os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         import datetime
+        from ..parallel.comm import init_default_group
         t = float(timeout_s if timeout_s is not None else os.environ.get("KFA_DIST_INIT_TIMEOUT", "300"))
-        dist.init_process_group(be, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=t), **kw)
+        # GPU jobs: a control-only gloo group, the gradients on the native RCCL layer
+        # (parallel/comm.py: one RCCL communicator per process); KFA_COMM=torch: nccl
+        init_default_group(rank, world, dev, datetime.timedelta(seconds=t), backend=backend)
     return DistInfo(rank, world, local, dev)
 
 
@@ -291,11 +293,23 @@ class Engine:
         return checkpoint.restore(model_dir, self.info.rank, self.info.world, self.model, self.groups, self.opt,
                                   layout=self.layout(), sync=self.sync if self.sharded else None)
 
+    def comm_info(self) -> dict:
+        """What carries this job's gradient traffic (bench JSON ``config.comm``): the
+        layer, the default group's backend, RCCL's transport per peer (P2P/IPC =
+        xGMI peer access; SHM / NET = a fallback) — None at world 1."""
+        c = self.comm
+        return {"layer": repr(c) if self.info.world > 1 else None,
+                "default_group": dist.get_backend() if dist.is_initialized() else None,
+                "transport": c.transport if getattr(c, "native", False) else None}
+
     def layout(self) -> str:
         return self.sync.layout_signature() if self.sharded else f"allreduce|{self.info.world}"
 
 
 def synchronize(info: DistInfo) -> None:
+    """Device drained, then every rank at the same point (the default group's
+    barrier: gloo on the CPU for native-comm GPU jobs, torch's RCCL under
+    ``KFA_COMM=torch``)."""
     if info.device.type == "cuda":
         torch.cuda.synchronize()
     if dist.is_initialized():
@@ -316,13 +330,19 @@ def timed_steps(engine: Engine, batch, steps: int, warmup: int, graph: bool = Fa
         synchronize(engine.info)
         engine.capture(*batch)
     synchronize(engine.info)
+    cw = getattr(engine.sync, "comm_wait_ms", None)
+    if cw is not None:
+        cw(reset=True)  # the timed steps' exposed communication only
     t0 = time.perf_counter()
     loss = None
     for _ in range(steps):
         loss = engine.train_step(*batch)
     synchronize(engine.info)
     dt = time.perf_counter() - t0
-    t = torch.tensor([dt], dtype=torch.float64, device=engine.info.device)
+    from ..parallel.comm import control_device
+    t = torch.tensor([dt], dtype=torch.float64, device=control_device(engine.info.device))
     if dist.is_initialized():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return {"elapsed": float(t.item()), "loss": float(loss.item()) if loss is not None else float("nan")}
+    wait = cw() if cw is not None else None
+    return {"elapsed": float(t.item()), "loss": float(loss.item()) if loss is not None else float("nan"),
+            "comm_wait_ms": round(wait, 4) if wait is not None else None}

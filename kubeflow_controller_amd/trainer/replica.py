@@ -42,7 +42,7 @@ from typing import Optional
 import torch
 import torch.distributed as dist
 
-from .cluster import ClusterSpec, add_cluster_flags, parse_cluster
+from .cluster import ClusterSpec, add_cluster_flags, local_device, parse_cluster
 
 STEP_KEY = "kfa/global_step"
 DONE_KEY = "kfa/workers_done"
@@ -246,9 +246,9 @@ def run_ps_async(spec: ClusterSpec, args) -> int:
     model, _, _ = build(args, torch.device("cpu"))
     agg = _aggregate(spec, args)
     if transport == "device":
-        torch.cuda.set_device(0)
+        torch.cuda.set_device(local_device())
         server = DeviceAsyncPSServer(list(model.named_parameters()), W, P, spec.task_index, store,
-                                     torch.device("cuda", 0), lr=args.learning_rate, optimizer=args.optimizer,
+                                     torch.device("cuda", local_device()), lr=args.learning_rate, optimizer=args.optimizer,
                                      aggregate=agg, channels_last=model.__class__.__name__ == "ResNet")
     else:
         server = AsyncPSServer(list(model.named_parameters()), W, P, spec.task_index, lr=args.learning_rate,
@@ -272,11 +272,11 @@ def run_worker_async(spec: ClusterSpec, args) -> int:
     from ..parallel.async_ps import AsyncPSClient, DeviceAsyncPSClient
     W, P = spec.num_workers, len(spec.ps)
     use_gpu = _use_gpu(args)
-    device = torch.device("cuda", 0) if use_gpu else torch.device("cpu")
+    device = torch.device("cuda", local_device()) if use_gpu else torch.device("cpu")
     if not use_gpu and not os.environ.get("OMP_NUM_THREADS"):
         torch.set_num_threads(max(1, (os.cpu_count() or 1) // (W + P)))
     if use_gpu:
-        torch.cuda.set_device(0)
+        torch.cuda.set_device(local_device())
     store = _store(spec, spec.is_chief)
     dist.init_process_group("gloo", store=store, rank=spec.task_index, world_size=W + P, timeout=_pg_timeout(args))
     torch.manual_seed(args.seed)
@@ -397,12 +397,12 @@ def run_worker(spec: ClusterSpec, args) -> int:
     from .engine import DistInfo, Engine
 
     use_gpu = _use_gpu(args)
-    device = torch.device("cuda", 0) if use_gpu else torch.device("cpu")
+    device = torch.device("cuda", local_device()) if use_gpu else torch.device("cpu")
     if not use_gpu and not spec.is_local and not os.environ.get("OMP_NUM_THREADS"):
         # CPU replicas of one job share the node: don't oversubscribe the cores
         torch.set_num_threads(max(1, (os.cpu_count() or 1) // (spec.num_workers + len(spec.ps))))
     if use_gpu:
-        torch.cuda.set_device(0)
+        torch.cuda.set_device(local_device())
     world = 1 if spec.is_local else spec.num_workers
     rank = 0 if spec.is_local else spec.task_index
     if (args.sync_replicas and args.replicas_to_aggregate is not None and not spec.is_local
@@ -414,9 +414,10 @@ def run_worker(spec: ClusterSpec, args) -> int:
         if world > 1:
             os.environ.setdefault("KFA_CONV_OVERSUB", "2")  # see engine.init_distributed
         store = _store(spec, spec.is_chief)
-        backend = os.environ.get("KFA_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
-        dist.init_process_group(backend, store=store, rank=rank, world_size=world, timeout=_pg_timeout(args),
-                                **({"device_id": device} if backend == "nccl" else {}))
+        # GPU replicas: a control-only gloo group, gradients on the native RCCL layer
+        # (parallel/comm.py: one RCCL communicator per process); KFA_COMM=torch: nccl
+        from ..parallel.comm import init_default_group
+        init_default_group(rank, world, device, _pg_timeout(args), store=store)
     torch.manual_seed(args.seed)  # identical init everywhere (+ broadcast in the engine)
     num_ps = 0 if spec.is_local else len(spec.ps)
     args.num_ps = num_ps

@@ -294,3 +294,133 @@ def test_recv_any_serves_every_peer_in_per_peer_order(tmp_path):
         mine = [v for s, v in got if s == r]
         assert mine == [[r, 0, r * 10, 7], [r, 1, r * 10 + 1, 7]]
     assert got[0][0] == 2  # rank 1 started late
+
+
+def test_one_rccl_communicator_design_decisions(monkeypatch):
+    """GPU jobs on the native layer get a gloo default group (control scalars on the
+    CPU, no torch RCCL communicator); KFA_COMM=torch keeps nccl; a forced
+    KFA_DIST_BACKEND wins (and a forced gloo keeps torch.distributed for the traffic)."""
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    from kubeflow_controller_amd.parallel import comm as C
+    for v in ("KFA_COMM", "KFA_DIST_BACKEND"):
+        monkeypatch.delenv(v, raising=False)
+    assert C.dist_backend(use_gpu=True) == "gloo" and C.dist_backend(use_gpu=False) == "gloo"
+    monkeypatch.setenv("KFA_COMM", "torch")
+    assert C.dist_backend(use_gpu=True) == "nccl"
+    monkeypatch.setenv("KFA_DIST_BACKEND", "gloo")
+    assert C.dist_backend(use_gpu=True) == "gloo"
+    monkeypatch.delenv("KFA_COMM")
+    monkeypatch.delenv("KFA_DIST_BACKEND")
+    monkeypatch.setattr(dist, "is_initialized", lambda: True)
+    monkeypatch.setattr(dist, "get_backend", lambda *a: "gloo")
+    monkeypatch.setattr(C, "_CONTROL_ONLY", True)  # what init_default_group sets on a GPU job
+    assert C.comm_mode(torch.device("cuda", 0)) == "native"
+    assert C.control_device(torch.device("cuda", 0)) == torch.device("cpu")
+    monkeypatch.setattr(C, "_CONTROL_ONLY", False)  # KFA_DIST_BACKEND=gloo rehearsal
+    assert C.comm_mode(torch.device("cuda", 0)) == "torch"
+    monkeypatch.setattr(dist, "get_backend", lambda *a: "nccl")
+    assert C.control_device(torch.device("cuda", 0)) == torch.device("cuda", 0)
+    assert C.control_device(None) == torch.device("cpu")
+
+
+def _control_worker(rank, world, port, out):
+    sys.path.insert(0, ROOT)
+    import datetime
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    for v in ("KFA_COMM", "KFA_DIST_BACKEND"):
+        os.environ.pop(v, None)
+    from kubeflow_controller_amd.parallel import comm as C
+    from kubeflow_controller_amd.ops import conv, routes
+    # a GPU job's init (gloo needs no device: the "cuda" device only selects the layout)
+    be = C.init_default_group(rank, world, torch.device("cuda", 0), datetime.timedelta(seconds=60))
+    conv.set_lockstep(True)
+    res = {"backend": be, "default": dist.get_backend(), "mode": C.comm_mode(torch.device("cuda", 0)),
+           "ctl": str(C.control_device(torch.device("cuda", 0))),
+           # the in-step control collectives ride the CPU group: rank 0's pick wins everywhere
+           "agree": routes._agree_index(rank + 1, torch.device("cuda", 0)),
+           "agree_conv": conv._agree(rank == 0, torch.device("cuda", 0))}
+    torch.save(res, f"{out}.{rank}")
+    dist.destroy_process_group()
+
+
+def test_gpu_job_default_group_is_control_only_gloo(tmp_path):
+    """init_default_group on a GPU job: gloo default group (no torch RCCL
+    communicator is ever created while the native layer carries the traffic), the
+    native layer selected, control scalars (tuner agreement) on the CPU and
+    agreed from rank 0."""
+    out = str(tmp_path / "c")
+    mp.start_processes(_control_worker, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    for r in range(2):
+        res = torch.load(f"{out}.{r}", weights_only=True)
+        assert res["backend"] == "gloo" and res["default"] == "gloo", res
+        assert res["mode"] == "native" and res["ctl"] == "cpu", res
+        assert res["agree"] == 1 and res["agree_conv"] is True, res
+
+
+def test_parse_rccl_transport(tmp_path):
+    """RCCL's INIT/P2P log -> per-peer transport of this rank (bench config.comm)."""
+    sys.path.insert(0, ROOT)
+    from kubeflow_controller_amd.parallel.comm import parse_rccl_transport
+    log = tmp_path / "rccl.log"
+    log.write_text(
+        "host:1:1 [0] NCCL INFO Channel 00/0 : 0[0] -> 1[1] via P2P/IPC comm 0x1 nRanks 04\n"
+        "host:1:1 [0] NCCL INFO Channel 01/0 : 0[0] -> 1[1] via P2P/IPC comm 0x1 nRanks 04\n"
+        "host:1:1 [0] NCCL INFO Channel 00/0 : 3[3] -> 0[0] via SHM/direct/direct\n"
+        "host:1:1 [0] NCCL INFO Channel 00/0 : 1[1] -> 2[2] via P2P/IPC\n"
+        "host:1:1 [0] NCCL INFO Connected all rings\n")
+    t = parse_rccl_transport(str(log), 0)
+    assert t["via"] == {"P2P/IPC": 2, "SHM/direct/direct": 1}, t
+    assert t["peers"] == {"1": "P2P/IPC", "3": "SHM/direct/direct"}, t
+    assert parse_rccl_transport(str(tmp_path / "missing.log"), 0) == {"via": "unknown"}
+    assert parse_rccl_transport(None, 0) == {"via": "unknown"}
+
+
+def test_rank0_failure_is_published(monkeypatch):
+    """Rank 0 failing before it listens publishes ERR:<why> under the key, so the
+    other ranks fail at once instead of waiting out the store timeout."""
+    sys.path.insert(0, ROOT)
+    import datetime
+    import torch.distributed as dist
+    from kubeflow_controller_amd.parallel import comm as C
+    store = dist.HashStore()
+    store.set_timeout(datetime.timedelta(seconds=2))
+
+    def boom():
+        raise RuntimeError("comm library failed to build")
+    monkeypatch.setattr(C, "lib", boom)
+    with pytest.raises(RuntimeError, match="failed to build"):
+        C.Communicator.create(store, 0, 2, torch.device("cpu"), key="kfc/t0")
+    assert store.get("kfc/t0").decode().startswith("ERR:")
+    with pytest.raises(C.CommError, match="rank 0 could not open"):
+        C.Communicator.create(store, 1, 2, torch.device("cpu"), key="kfc/t0")
+
+
+def test_probe_catches_offset_and_order_errors():
+    """make_comm's bring-up probe checks a reduce-scatter and an all-gather of
+    rank-distinct values element by element (an all-reduce of ones cannot see a
+    wrong offset or rank order)."""
+    sys.path.insert(0, ROOT)
+    from kubeflow_controller_amd.parallel import comm as C
+
+    class Fake:  # a 2-rank job seen from rank 1, with the other rank's inputs simulated
+        def __init__(self, bug):
+            self.bug = bug
+
+        def reduce_scatter_tensor(self, out, inp, op="sum"):
+            n = out.numel()
+            base = torch.arange(2 * n, dtype=torch.float32)
+            tot = base * 1 + 0.0 + base * 2 + 1000.0   # rank 0's input + rank 1's
+            blk = 0 if self.bug == "offset" else 1     # rank 1 owns block 1
+            out.copy_(tot[blk * n:(blk + 1) * n])
+
+        def all_gather_into_tensor(self, out, inp):
+            n = inp.numel()
+            r0 = torch.full((n,), 1.0) + torch.arange(n, dtype=torch.float32)
+            parts = [inp, r0] if self.bug == "order" else [r0, inp]
+            out.copy_(torch.cat(parts))
+    dev = torch.device("cpu")
+    assert C._probe(Fake(None), dev, 2, 1) == ""
+    assert "reduce-scatter" in C._probe(Fake("offset"), dev, 2, 1)
+    assert "all-gather" in C._probe(Fake("order"), dev, 2, 1)

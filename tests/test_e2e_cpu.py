@@ -182,6 +182,42 @@ def test_gpu_binding_policy(tmp_path):
         n.shutdown()
 
 
+def test_gpu_binding_visible_mode(tmp_path):
+    """gpu_binding="visible": every node GPU stays visible (the device set bench.py
+    sees under torchrun) and each worker gets its own GPU as an ORDINAL
+    (KFA_LOCAL_DEVICE), which the replica runtime turns into its device, its
+    LOCAL_RANK and the physical index the async PS reports — the reference picks its
+    device out of a fully visible set (mnist_replica.py:125-129)."""
+    st = ObjectStore()
+    n = Node(st, kubelet=True, root_dir=str(tmp_path), num_gpus=4, resync=30, gpu_binding="visible").start()
+    try:
+        code = ("import os; from kubeflow_controller_amd.trainer.cluster import local_device, parse_cluster; "
+                "from kubeflow_controller_amd.parallel.async_ps import physical_gpu; "
+                "print('HIP=' + os.environ['HIP_VISIBLE_DEVICES'] + ' DEV=%d' % local_device() + "
+                "' LR=' + parse_cluster().torch_env()['LOCAL_RANK'] + ' PHYS=' + physical_gpu())")
+        cmd = [sys.executable, "-c", code]
+        st.create(_job("vis", [("PS", 1, cmd), ("Worker", 3, cmd)]))
+        wait_for_phase(st, "default", "vis", {"Succeeded"}, 60)
+        pods = st.list("Pod")
+        ws = [p for p in pods if p.metadata.labels["job_type"] == "Worker"]
+        assert sorted(p.status.gpus[0] for p in ws) == [0, 1, 2]
+        for p in ws:
+            g = p.status.gpus[0]
+            assert f"HIP=0,1,2,3 DEV={g} LR={g} PHYS={g}" in _logs(str(tmp_path), p), _logs(str(tmp_path), p)
+    finally:
+        n.shutdown()
+
+
+def test_local_device_isolated_default(monkeypatch):
+    from kubeflow_controller_amd.parallel.async_ps import physical_gpu
+    from kubeflow_controller_amd.trainer.cluster import local_device
+    monkeypatch.delenv("KFA_LOCAL_DEVICE", raising=False)
+    monkeypatch.setenv("KFA_GPUS", "5,2")  # isolated worker on GPU 5 seeing PS GPU 2
+    assert local_device() == 0 and physical_gpu() == "5"
+    monkeypatch.setenv("KFA_LOCAL_DEVICE", "bogus")
+    assert local_device() == 0
+
+
 @pytest.mark.slow
 def test_cli_standalone_controller_and_kfctl(tmp_path):
     url_file = tmp_path / "url"

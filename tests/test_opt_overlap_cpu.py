@@ -98,3 +98,26 @@ def test_direct_notification_counts_once():
         seen.clear()
         Direct.apply(x, w).sum().backward()
         assert [id(q) for q in seen].count(id(w)) == 1 and [id(q) for q in seen].count(id(x)) == 1, seen
+
+
+def test_bucket_overcount_raises():
+    """A gradient reported ready more often than its bucket counts (an undeclared
+    tied parameter delivered by two direct backwards) must not silently start the
+    bucket's collective / update early: the second notification after completion
+    raises."""
+    import pytest
+    from kubeflow_controller_amd.parallel import flat
+    from kubeflow_controller_amd.parallel.ddp import GradSync
+    model = torch.nn.Sequential(torch.nn.Linear(8, 8), torch.nn.Linear(8, 4))
+    groups = flat.split_params(model, None)
+    sync = GradSync(groups, bucket_mb=1.0)
+    done = []
+    sync.on_bucket_ready(done.append)
+    p = groups[0].params[0]
+    for g in groups:
+        for q in g.params:
+            flat.notify_grad_ready(q)
+    assert len(done) == len(sync.buckets)
+    with pytest.raises(RuntimeError, match="ready notifications"):
+        flat.notify_grad_ready(p)
+    assert sync.comm_wait_ms() is None  # world 1 / CPU: nothing timed

@@ -2,7 +2,9 @@
 (``Engine(opt_overlap=True)``, ``trainer/engine.py``) on the GPU: the HIP
 encoder / embedding / decoder backwards report a weight's gradient only after
 their last read of that weight, so the overlapped run ends with the one-pass
-step's weights.  A second one-pass engine bounds the run-to-run noise."""
+step's weights.  SGD (linear in the gradient: no noise amplification) is checked
+per tensor against a tight absolute bound; Adam by losses and an absolute cap on
+the share of weights that differ."""
 import copy
 
 import pytest
@@ -11,38 +13,92 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def test_overlapped_adam_matches_one_pass_bert():
-    from kubeflow_controller_amd.models.bert import BertConfig, BertForPreTraining, bert_loss, synthetic_mlm_batch
+def _tensor_update_errors(ref, other, init):
+    """Per parameter tensor: ||Δother - Δref|| / ||Δref|| of the fp32 masters'
+    updates since ``init`` (the list of the groups' initial fp32 buffers)."""
+    out = []
+    for gr, go, gi in zip(ref.groups, other.groups, init):
+        for k in range(len(gr.params)):
+            a, b = gr.param_range(k)
+            dr = gr.fp32[a:b].float() - gi[a:b]
+            do = go.fp32[a:b].float() - gi[a:b]
+            nr = float(dr.norm())
+            if nr > 0:
+                out.append(float((do - dr).norm()) / nr)
+    return out
+
+
+def _models(which, d):
+    if which == "bert":
+        from kubeflow_controller_amd.models.bert import BertConfig, BertForPreTraining, bert_loss, synthetic_mlm_batch
+        cfg = BertConfig(vocab_size=1024, hidden=256, layers=2, heads=4, intermediate=1024, max_position=128,
+                         hidden_dropout=0.0, attn_dropout=0.0)
+        torch.manual_seed(11)
+        base = BertForPreTraining(cfg)
+        batches = [tuple(t.to(d) if isinstance(t, torch.Tensor) else t
+                         for t in synthetic_mlm_batch(cfg, 8, 128, generator=torch.Generator().manual_seed(i)))
+                   for i in range(3)]
+        return base, bert_loss, batches, dict(channels_last=False, bucket_mb=0.5)
+    from kubeflow_controller_amd.models.resnet import ResNet
+    from kubeflow_controller_amd.ops.loss import cross_entropy
+    torch.manual_seed(11)
+    base = ResNet(layers=(1, 1, 1, 1), num_classes=10, width=64)
+    g = torch.Generator().manual_seed(3)
+    batches = [(torch.randn(8, 3, 64, 64, generator=g).to(d, torch.bfloat16).contiguous(memory_format=torch.channels_last),
+                torch.randint(0, 10, (8,), generator=g).to(d)) for _ in range(3)]
+    return base, (lambda m, x, y: cross_entropy(m(x), y)), batches, dict(channels_last=True, bucket_mb=0.25)
+
+
+@pytest.mark.parametrize("which", ["bert", "resnet"])
+def test_overlapped_sgd_matches_one_pass(which):
+    """SGD is linear in the gradient, so run-to-run noise (fp32 atomics summing in a
+    varying order) stays at rounding level instead of being amplified the way Adam's
+    first steps amplify a near-zero gradient's sign.  That allows a TIGHT absolute
+    bound: every parameter tensor's 3-step update in the overlapped run is within 2 %
+    (norm) of the one-pass run's.  An update that missed part of a bucket's gradient
+    (the round-5 bucket-count bug) moves whole tensors by O(100 %) of their update."""
     from kubeflow_controller_amd.trainer.engine import DistInfo, Engine
     d = torch.device("cuda")
-    cfg = BertConfig(vocab_size=1024, hidden=256, layers=2, heads=4, intermediate=1024, max_position=128)
-    torch.manual_seed(11)
-    base = BertForPreTraining(cfg)
-    batches = [tuple(t.to(d) if isinstance(t, torch.Tensor) else t
-                     for t in synthetic_mlm_batch(cfg, 8, 128, generator=torch.Generator().manual_seed(i)))
-               for i in range(3)]
+    base, loss, batches, kw = _models(which, d)
 
     def mk(ov):
-        return Engine(copy.deepcopy(base), bert_loss, optimizer="adam", lr=1e-3, compute_dtype=torch.bfloat16,
-                      channels_last=False, bucket_mb=0.5, dist_info=DistInfo(device=d), opt_overlap=ov)
-    ref, ctl, ovl = mk(False), mk(False), mk(True)
+        return Engine(copy.deepcopy(base), loss, optimizer="sgd", lr=0.05, momentum=0.9, weight_decay=0.0,
+                      compute_dtype=torch.bfloat16, dist_info=DistInfo(device=d), opt_overlap=ov, **kw)
+    ref, ovl = mk(False), mk(True)
     assert ovl.opt_overlap and len(ovl.sync.buckets) > 3
+    init = [g.fp32.float().clone() for g in ref.groups]
+    for e in (ref, ovl):
+        for b in batches:
+            e.train_step(*b)
+    torch.cuda.synchronize()
+    err = _tensor_update_errors(ref, ovl, init)
+    assert len(err) == sum(len(g.params) for g in ref.groups)
+    assert max(err) < 0.02, sorted(err)[-5:]
+
+
+def test_overlapped_adam_matches_one_pass_bert():
+    """Adam (what the overlap is for, BERT pre-training): losses agree and the share of
+    weights that differ is bounded by an ABSOLUTE cap of 2 % (a missed partial bucket
+    moved ~15 % of the weights; Adam's first steps turn run-to-run atomic-order noise
+    in near-zero gradients into +-lr moves, so this cannot be tight); the tight
+    per-tensor check is the SGD test above."""
+    from kubeflow_controller_amd.trainer.engine import DistInfo, Engine
+    d = torch.device("cuda")
+    base, loss, batches, kw = _models("bert", d)
+
+    def mk(ov):
+        return Engine(copy.deepcopy(base), loss, optimizer="adam", lr=1e-3, compute_dtype=torch.bfloat16,
+                      dist_info=DistInfo(device=d), opt_overlap=ov, **kw)
+    ref, ovl = mk(False), mk(True)
     losses = {}
-    for name, e in (("ref", ref), ("ctl", ctl), ("ovl", ovl)):
+    for name, e in (("ref", ref), ("ovl", ovl)):
         losses[name] = [float(e.train_step(*b)) for b in batches]
     torch.cuda.synchronize()
     assert ovl.opt.step_count == 3 and int(ovl.opt._t.item()) == 3
-
-    def frac(a, b):  # share of weights that moved apart by more than rounding
-        n = sum(g.fp32.numel() for g in a.groups)
-        return sum(int(((gb.fp32 - ga.fp32).abs() > 1e-5).sum()) for ga, gb in zip(a.groups, b.groups)) / n
-    # The one-pass runs already differ run to run: the embedding backward's fp32 atomics
-    # sum in a varying order, and Adam's first steps turn the sign of a near-zero gradient
-    # into a +-lr move, so a maximum difference cannot separate noise from a bug.  The
-    # share of weights that differ can: an update that missed part of a bucket's gradient
-    # moved whole tensors (19 of 41, ~15 % of the weights, before the bucket-count fix).
-    f_ctl, f_ovl = frac(ref, ctl), frac(ref, ovl)
-    assert f_ovl <= max(10 * f_ctl, 1e-3), (f_ovl, f_ctl, losses)
+    n = sum(g.fp32.numel() for g in ref.groups)
+    f_ovl = sum(int(((gb.fp32 - ga.fp32).abs() > 1e-5).sum()) for ga, gb in zip(ref.groups, ovl.groups)) / n
+    print(f"overlap adam: share of weights differing {f_ovl:.4%}")
+    assert f_ovl < 0.02, f_ovl
     for a, b in zip(losses["ref"], losses["ovl"]):
         assert abs(a - b) <= 1e-3 * max(1.0, abs(a)), losses
 

@@ -75,7 +75,8 @@ def test_routes_table_lookup_dump_and_summary(tmp_path, monkeypatch):
     from kubeflow_controller_amd.ops import routes
     tab = tmp_path / "routes_test.json"
     tab.write_text(json.dumps({"arch": "gfx950", "routes": {"proj|32768,2304,768": "ppp256",
-                                                            "conv_fwd|1,2,3": "igemm"}}))
+                                                            "conv_fwd|1,2,3": "igemm", "bn_apply|4": "sep",
+                                                            "dense_fwd|9": "hipblaslt"}}))
     monkeypatch.setattr(routes, "TABLE_PATH", str(tab))
     monkeypatch.setattr(routes, "MODE", "on")
     monkeypatch.setattr(routes, "_table", None)
@@ -84,10 +85,14 @@ def test_routes_table_lookup_dump_and_summary(tmp_path, monkeypatch):
     i = routes.decide("proj", (32768, 2304, 768), None, [("hipblaslt", boom), ("ppp192", boom), ("ppp256", boom)])
     assert i == 2
     assert routes.decide("conv_fwd", (1, 2, 3), None, [("igemm", boom), ("pp", boom)]) == 0
+    # the separate own BatchNorm apply ("sep") is an own kernel; hipBLASLt is the library
+    assert routes.decide("bn_apply", (4,), None, [("pro", boom), ("sep", boom)]) == 1
+    assert routes.decide("dense_fwd", (9,), None, [("hipblaslt", boom), ("ppw256", boom)]) == 0
     s = routes.summary()
-    assert s["from_table"] == 2 and s["timed"] == 0 and s["own"] == 2 and s["library"] == 0
+    assert s["from_table"] == 4 and s["timed"] == 0 and s["own"] == 3 and s["library"] == 1
     assert s["table"] == "routes_test.json" and len(s["table_sha"]) == 12
     out = tmp_path / "dumped.json"
     routes.dump(str(out))
     doc = json.loads(out.read_text())
-    assert doc["routes"] == {"conv_fwd|1,2,3": "igemm", "proj|32768,2304,768": "ppp256"}
+    assert doc["routes"] == {"conv_fwd|1,2,3": "igemm", "proj|32768,2304,768": "ppp256", "bn_apply|4": "sep",
+                             "dense_fwd|9": "hipblaslt"}
