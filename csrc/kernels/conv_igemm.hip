@@ -964,10 +964,17 @@ struct TDesc {
   int Cout, R, S, Cin, r0, dr, Rs, s0, ds, Ss, gx, gy;
 };
 
-__global__ void weight_transpose_multi(const TDesc* __restrict__ descs, const int* __restrict__ first, int n) {
-  __shared__ bf16_t tile[32][33];
+// 64 x 64 tiles, 256 threads: rows of 8 input channels (16 B) in, rows of 8 output
+// channels (16 B) out, the tile staged in LDS with a 2-element row pad (the column
+// reads of the write-out then spread over the banks).  The 32 x 32 / 2-byte form this
+// replaces moved 1.4 TB/s (BERT-base: 238 us per step for 85 M elements); partial
+// tiles and channel counts that are not multiples of 8 take the element-wise path.
+__global__ __launch_bounds__(256) void weight_transpose_multi(const TDesc* __restrict__ descs,
+                                                              const int* __restrict__ first, int n) {
+  constexpr int T = 64, P = T + 2;
+  __shared__ bf16_t tile[T * P];
   __shared__ int which;
-  if (threadIdx.x == 0 && threadIdx.y == 0) {
+  if (threadIdx.x == 0) {
     int lo = 0, hi = n - 1;  // last descriptor whose first block <= blockIdx.x
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
@@ -983,26 +990,54 @@ __global__ void weight_transpose_multi(const TDesc* __restrict__ descs, const in
   const int by = b % d.gy, tap = b / d.gy;
   const int ri = tap / d.Ss, si = tap - ri * d.Ss;
   const int r = d.r0 + d.dr * ri, s = d.s0 + d.ds * si;
-  const int co0 = by * 32, ci0 = bx * 32;
-  for (int y = threadIdx.y; y < 32; y += blockDim.y) {
-    const int co = co0 + y, ci = ci0 + threadIdx.x;
-    tile[y][threadIdx.x] = (co < d.Cout && ci < d.Cin) ? d.W[(((long)co * d.R + r) * d.S + s) * d.Cin + ci] : (bf16_t)0;
+  const int co0 = by * T, ci0 = bx * T;
+  const long ws = (long)d.R * d.S * d.Cin;        // W stride between output channels
+  const long ts = (long)d.Rs * d.Ss * d.Cout;     // Wt stride between input channels
+  const bf16_t* src = d.W + ((long)r * d.S + s) * d.Cin;
+  bf16_t* dst = d.Wt + ((long)ri * d.Ss + si) * d.Cout;
+  const bool vec = (d.Cin % 8 == 0) && (d.Cout % 8 == 0) && co0 + T <= d.Cout && ci0 + T <= d.Cin &&
+                   ((uintptr_t)d.W % 16 == 0) && ((uintptr_t)d.Wt % 16 == 0);
+  const int t = threadIdx.x;
+  if (vec) {
+#pragma unroll
+    for (int k = 0; k < 2; k++) {  // 64 rows x 8 chunks of 8 channels
+      const int q = t + k * 256, row = q >> 3, ch = (q & 7) * 8;
+      const uint4 v = *reinterpret_cast<const uint4*>(src + (co0 + row) * ws + ci0 + ch);
+      uint32_t* tp = reinterpret_cast<uint32_t*>(tile + row * P + ch);  // 4-B aligned: P and ch even
+      tp[0] = v.x; tp[1] = v.y; tp[2] = v.z; tp[3] = v.w;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      const int q = t + k * 256, ci = q >> 3, co = (q & 7) * 8;
+      uint32_t w[4];
+#pragma unroll
+      for (int e = 0; e < 4; e++)
+        w[e] = (uint32_t)tile[(co + 2 * e) * P + ci] | ((uint32_t)tile[(co + 2 * e + 1) * P + ci] << 16);
+      *reinterpret_cast<uint4*>(dst + (ci0 + ci) * ts + co0 + co) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    return;
+  }
+  for (int q = t; q < T * T; q += 256) {
+    const int row = q / T, ci = q % T;
+    tile[row * P + ci] = (co0 + row < d.Cout && ci0 + ci < d.Cin) ? src[(co0 + row) * ws + ci0 + ci] : (bf16_t)0;
   }
   __syncthreads();
-  for (int y = threadIdx.y; y < 32; y += blockDim.y) {
-    const int ci = ci0 + y, co = co0 + threadIdx.x;
-    if (ci < d.Cin && co < d.Cout) d.Wt[(((long)ci * d.Rs + ri) * d.Ss + si) * d.Cout + co] = tile[threadIdx.x][y];
+  for (int q = t; q < T * T; q += 256) {
+    const int ci = q / T, co = q % T;
+    if (ci0 + ci < d.Cin && co0 + co < d.Cout) dst[(ci0 + ci) * ts + co0 + co] = tile[co * P + ci];
   }
 }
 
 }  // namespace
 
-// descs: n x 14 ints-worth descriptors (TDesc, host-packed), first: n block offsets, total blocks
+// descs: n x 14 ints-worth descriptors (TDesc, host-packed; gx / gy = 64-wide tile counts
+// over Cin / Cout), first: n block offsets, total blocks
 KFA_API int kfa_tdesc_bytes() { return (int)sizeof(TDesc); }
 
 KFA_API int kfa_weight_transpose_multi(const void* descs, const int* first, int n, int total_blocks, hipStream_t st) {
   if (n <= 0 || total_blocks <= 0) return 0;
-  hipLaunchKernelGGL(weight_transpose_multi, dim3(total_blocks), dim3(32, 8), 0, st,
+  hipLaunchKernelGGL(weight_transpose_multi, dim3(total_blocks), dim3(256), 0, st,
                      reinterpret_cast<const TDesc*>(descs), first, n);
   return kfa_status();
 }

@@ -1104,6 +1104,335 @@ __global__ __launch_bounds__(512, 1) void gemm_ppw_kernel(PppArgs g) {
 #endif
 }
 
+// ---------------------------------------------------------------------------
+// gemm_ppw3_kernel: 256 x 192 tiles (N = 768: BERT-base's hidden size — at
+// M = 32768 that is 512 tiles, exactly two per CU, where 256-wide tiles leave 1.5)
+// on the wave-specialised persistent pipeline of gemm_ppw_kernel, with the
+// THREE-phase k-tile of gemm_ppp_kernel<192, ..., P3> (16 MFMAs per phase instead
+// of a 48-column wave tile's 16 / 8 / 8 / 16):
+//
+//   s0: A0 -> rows 0-63 x blocks 0, 1      (B0 read at the end of the previous k-tile)
+//   s1: A1 -> rows 64-127 x blocks 0, 1    (B0 fragments kept)
+//   s2: B1 -> rows 0-127 x block 2         (A0, A1 fragments kept); then B0 of k-tile u+1
+//
+// Group 0 (waves 0-3) issues every LDS-DMA: s0 A1(u+1) [4 per wave], s1 B1(u+1) [2:
+// piece 2 is the 64 rows of the wave column groups' third blocks], s2 A0 + B0 (u+2)
+// [8] — each piece DMA'd three phases before its read phase, into a buffer whose
+// previous piece was read >= 2 phases earlier; every phase leaves exactly the last
+// three phases' DMAs in flight: fixed vmcnt(14).  Group 1 (waves 4-7) issues no
+// DMA and stores all C: its own quadrants from registers, group 0's from the 32 KB
+// hand-off area (two 16 KB halves by phase parity, inline-asm ds ops so hipcc adds
+// no vmcnt(0) behind the DMAs in flight).
+//
+// Stores, per tile: rows 0-127 x blocks 0-1 are final after s0 / s1 of the tile's
+// LAST k-tile and are written in s1 / s2 of that k-tile; block 2 (final after s2)
+// in s2 of the next tile's first k-tile.  Only the block's final tile's block 2 —
+// a third of one tile — is written after the loop, where nothing overlaps it.
+template <bool NT>
+__global__ __launch_bounds__(512, 1) void gemm_ppw3_kernel(PppArgs g) {
+  constexpr int BN = 192, WN = 48, TM = 8, TN = 3;
+  constexpr int DW = 4;   // DMAs per full 16 KB piece per group-0 wave
+  constexpr int VMW = 14; // group-0 DMAs of three phases: A1 4 + B1 2 + A0/B0 8
+  __shared__ __attribute__((aligned(16))) char smem[2 * 4 * PIECE + 2 * HANDOFF];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const bool loader = wr == 0;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q8 = nwg >> 3, r8 = nwg & 7, x8 = bid & 7;
+  const int lc = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + (bid >> 3);
+  const int ntn = (g.N + BN - 1) / BN, ntm = (g.M + 255) / 256, ntiles = ntm * ntn;
+  const int nk = (g.K + BK - 1) / BK;
+  const int my_tiles = lc < ntiles ? (ntiles - 1 - lc) / nwg + 1 : 0;
+  const int J = my_tiles * nk;
+  if (J == 0) return;
+  constexpr int GM = 4;
+  auto tile_mn = [&](int i, int& m0, int& n0) __attribute__((always_inline)) {
+    const int wg = lc + i * nwg;
+    const int grp = wg / (GM * ntn), gm0 = grp * GM, gmn = min(GM, ntm - gm0), rem = wg - grp * GM * ntn;
+    m0 = (gm0 + rem % gmn) * 256;
+    n0 = (rem / gmn) * BN;
+  };
+  const __amdgpu_buffer_rsrc_t rA = rsrc(g.A, (unsigned)(((long)(g.M - 1) * g.lda + g.K) * 2));
+  const __amdgpu_buffer_rsrc_t rB = rsrc(g.B, (unsigned)(((long)(g.N - 1) * g.ldb + g.K) * 2));
+  const __amdgpu_buffer_rsrc_t rC = rsrc(g.C, g.c_bytes);
+  const int prow = wc * 8 + (lane >> 3);
+  const int lcx = (lane & 7) ^ ((prow >> 1) & 7);
+  int voff[4][DW];  // piece 2 uses entries 0-1 only (the compiler drops the rest)
+  // pieces: 0 = A rows {0-63, 128-191}, 3 = A rows {64-127, 192-255}, 1 = the first 32
+  // columns of each wave column group (128 rows), 2 = their third 16-column block (64 rows)
+  auto set_voff = [&](int p, int m0, int n0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < DW; j++) {
+      const int r = j * 32 + prow;
+      if (p == 0 || p == 3) {
+        const int m = m0 + (r >> 6) * 128 + (p == 3 ? 64 : 0) + (r & 63);
+        voff[p][j] = m < g.M ? (m * g.lda + lcx * 8) * 2 : (int)kOOB;
+      } else if (p == 1) {
+        const int n = n0 + (r >> 5) * WN + (r & 31);
+        voff[p][j] = n < g.N ? (n * g.ldb + lcx * 8) * 2 : (int)kOOB;
+      } else if (j < 2) {
+        const int n = n0 + (r >> 4) * WN + 32 + (r & 15);
+        voff[p][j] = n < g.N ? (n * g.ldb + lcx * 8) * 2 : (int)kOOB;
+      }
+    }
+  };
+  // issue side: pieces 3, 2 fetch k-tile u + 1 ("X"), pieces 0, 1 fetch u + 2 ("Y")
+  int xkt = 0, xti = 0, ykt = 0, yti = 0;
+  {
+    int m0, n0;
+    tile_mn(0, m0, n0);
+#pragma unroll
+    for (int p = 0; p < 4; p++) set_voff(p, m0, n0);
+  }
+  auto advance = [&](bool X) __attribute__((always_inline)) {
+    int& kt = X ? xkt : ykt;
+    int& ti = X ? xti : yti;
+    if (++kt == nk) {
+      kt = 0;
+      if (++ti < my_tiles) {
+        int m0, n0;
+        tile_mn(ti, m0, n0);
+        set_voff(X ? 2 : 0, m0, n0);
+        set_voff(X ? 3 : 1, m0, n0);
+      }
+    }
+  };
+  auto issue = [&](auto pc, int gk) __attribute__((always_inline)) {
+    constexpr int p = decltype(pc)::value;
+    constexpr bool X = (p == 2 || p == 3);
+    constexpr int nd = p == 2 ? 2 : DW;
+    if (!loader) return;
+    char* dst = smem + (gk & 1) * (4 * PIECE) + p * PIECE + wc * 8 * 128;
+    const __amdgpu_buffer_rsrc_t r = (p == 0 || p == 3) ? rA : rB;
+    const int kt = X ? xkt : ykt;
+    const int soff = kt * BK * 2;
+    const bool live = gk < J && kt * BK + lcx * 8 < g.K;
+#pragma unroll
+    for (int j = 0; j < nd; j++) dma16(r, dst + j * 32 * 128, live ? voff[p][j] : (int)kOOB, soff);
+  };
+  const int fr = lane & 15, fq = lane >> 4;
+  const int ro0 = fr * 128 + ((fq ^ (fr >> 1)) << 4), ro1 = fr * 128 + (((4 + fq) ^ (fr >> 1)) << 4);
+  floatx4 acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; i++)
+#pragma unroll
+    for (int j = 0; j < TM; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  short8 a0[4][2], a1[4][2], b0[2][2], b1[2];
+  const int cb = ((fq & 1) << 4) | ((fq >> 1) << 3);
+  typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+  // hand-off slot k (0..3) of phase parity hp: [wave column][k][lane] 16 B
+  auto ho_addr = [&](int hp, int k) __attribute__((always_inline)) {
+    return (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)(smem + 2 * 4 * PIECE + hp * HANDOFF) +
+           (unsigned)((wc * 4 + k) * 1024 + lane * 16);
+  };
+  // row half mh x blocks 0-1 of this wave's tile: 4 x 16 B per lane (8 consecutive columns
+  // per 16-row block after v_permlane16_swap), accumulators zeroed
+  auto pack01 = [&](int mh, uint4 (&v)[4]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int mi = 0; mi < 4; mi++) {
+      floatx4& x = acc[0][mh * 4 + mi];
+      floatx4& y = acc[1][mh * 4 + mi];
+      const unsigned x0 = cvt2(x[0], x[1]), x1 = cvt2(x[2], x[3]);
+      const unsigned y0 = cvt2(y[0], y[1]), y1 = cvt2(y[2], y[3]);
+      const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+      const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+      v[mi] = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+      x = floatx4{0.f, 0.f, 0.f, 0.f};
+      y = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  // block 2 (both row halves): 8 row blocks x 4 consecutive columns = 8 x 8 B per lane,
+  // two row blocks per 16-B slot
+  auto pack2b = [&](uint4 (&v)[4]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      floatx4& x = acc[2][2 * k];
+      floatx4& y = acc[2][2 * k + 1];
+      v[k] = make_uint4(cvt2(x[0], x[1]), cvt2(x[2], x[3]), cvt2(y[0], y[1]), cvt2(y[2], y[3]));
+      x = floatx4{0.f, 0.f, 0.f, 0.f};
+      y = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  using V4 = decltype(__builtin_amdgcn_raw_buffer_load_b128(rC, 0, 0, 0));
+  using V2 = decltype(__builtin_amdgcn_raw_buffer_load_b64(rC, 0, 0, 0));
+  auto store01 = [&](int grp, int mh, int m0, int n0, const uint4 (&v)[4]) __attribute__((always_inline)) {
+    const int n = n0 + wc * WN + cb;
+#pragma unroll
+    for (int mi = 0; mi < 4; mi++) {
+      const int m = m0 + grp * 128 + mh * 64 + mi * 16 + fr;
+      const unsigned off = (m < g.M && n < g.N) ? ((unsigned)m * (unsigned)g.ldc + (unsigned)n) * 2u : kOOB;
+      uint4 w = v[mi];
+      __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<V4*>(&w), rC, off, 0, NT ? 2 : 0);
+    }
+  };
+  auto store2b = [&](int grp, int m0, int n0, const uint4 (&v)[4]) __attribute__((always_inline)) {
+    const int n = n0 + wc * WN + 32 + fq * 4;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const int m = m0 + grp * 128 + (2 * k + h) * 16 + fr;
+        const unsigned off = (m < g.M && n < g.N) ? ((unsigned)m * (unsigned)g.ldc + (unsigned)n) * 2u : kOOB;
+        uint2 w = h ? make_uint2(v[k].z, v[k].w) : make_uint2(v[k].x, v[k].y);
+        __builtin_amdgcn_raw_buffer_store_b64(*reinterpret_cast<V2*>(&w), rC, off, 0, NT ? 2 : 0);
+      }
+  };
+  // a store phase: group 0 hands its part to group 1 through the hand-off half hp;
+  // group 1 stores its own part from registers, then group 0's from LDS.
+  // what: 0 / 1 = row half 0 / 1 x blocks 0-1, 2 = block 2
+  auto epi = [&](int what, int hp, int m0, int n0) __attribute__((always_inline)) {
+    uint4 v[4];
+    if (what == 2) pack2b(v);
+    else pack01(what, v);
+    if (loader) {
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const u32x4 w = {v[k].x, v[k].y, v[k].z, v[k].w};
+        asm volatile("ds_write_b128 %0, %1" ::"v"(ho_addr(hp, k)), "v"(w) : "memory");
+      }
+    } else {
+      // own part first (its registers are ready and then free), then the partner's
+      if (what == 2) store2b(1, m0, n0, v);
+      else store01(1, what, m0, n0, v);
+      u32x4 pw[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) asm volatile("ds_read_b128 %0, %1" : "=v"(pw[k]) : "v"(ho_addr(hp, k)) : "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(pw[0]), "+v"(pw[1]), "+v"(pw[2]), "+v"(pw[3]) :: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      uint4 pv[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) pv[k] = make_uint4(pw[k][0], pw[k][1], pw[k][2], pw[k][3]);
+      if (what == 2) store2b(0, m0, n0, pv);
+      else store01(0, what, m0, n0, pv);
+    }
+  };
+  auto mfma_blocks = [&](auto& bb, auto& aa, int mh, int nb0, auto nbc) __attribute__((always_inline)) {
+    constexpr int NBC = decltype(nbc)::value;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ks++)
+#pragma unroll
+      for (int ni = 0; ni < NBC; ni++)
+#pragma unroll
+        for (int mi = 0; mi < 4; mi++) {
+          short8 bv;
+          if constexpr (NBC == 1) bv = bb[ks];
+          else bv = bb[ni][ks];
+          acc[nb0 + ni][mh * 4 + mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bv, aa[mi][ks], acc[nb0 + ni][mh * 4 + mi], 0, 0, 0);
+        }
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto rd = [&](const char* p) -> short8 { return *reinterpret_cast<const short8*>(p); };
+  auto rd_b0 = [&](int u) __attribute__((always_inline)) {
+    const char* pb = smem + (u & 1) * (4 * PIECE) + PIECE + wc * 32 * 128;
+#pragma unroll
+    for (int ni = 0; ni < 2; ni++) {
+      b0[ni][0] = rd(pb + ni * 16 * 128 + ro0);
+      b0[ni][1] = rd(pb + ni * 16 * 128 + ro1);
+    }
+  };
+
+  // prologue: A0 B0 (k-tile 0), A1 (0), B1 (0), A0 B0 (1) — the steady state's
+  // "three phases in flight" picture right before s0 of k-tile 0
+  issue(std::integral_constant<int, 0>{}, 0);
+  issue(std::integral_constant<int, 1>{}, 0);
+  advance(false);
+  issue(std::integral_constant<int, 3>{}, 0);
+  issue(std::integral_constant<int, 2>{}, 0);
+  advance(true);
+  issue(std::integral_constant<int, 0>{}, 1);
+  issue(std::integral_constant<int, 1>{}, 1);
+  advance(false);
+  if (loader) vm_wait<VMW>();
+  asm volatile("s_barrier" ::: "memory");
+  if (wr) asm volatile("s_barrier" ::: "memory");
+  rd_b0(0);
+
+  int cm0, cn0, pm0 = 0, pn0 = 0;
+  tile_mn(0, cm0, cn0);
+  auto retire = [&](bool ho) __attribute__((always_inline)) {
+    if (loader) {
+      vm_wait<VMW>();
+      if (ho) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+  };
+  // MODE bit 0 (EPI): the tile's first k-tile (not the block's first tile) writes the
+  // previous tile's block 2 in s2; bit 1 (LAST): the tile's last k-tile writes its own
+  // rows 0-127 x blocks 0-1 in s1 / s2
+  auto ktile = [&](int u, auto mode) __attribute__((always_inline)) {
+    constexpr int MODE = decltype(mode)::value;
+    constexpr bool EPI = MODE & 1, LAST = MODE & 2;
+    const char* buf = smem + (u & 1) * (4 * PIECE);
+    {  // s0: A0 -> rows 0-63 x blocks 0, 1
+      const char* pa = buf + wr * 64 * 128;
+#pragma unroll
+      for (int mi = 0; mi < 4; mi++) {
+        a0[mi][0] = rd(pa + mi * 16 * 128 + ro0);
+        a0[mi][1] = rd(pa + mi * 16 * 128 + ro1);
+      }
+      issue(std::integral_constant<int, 3>{}, u + 1);
+      retire(false);
+      asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      mfma_blocks(b0, a0, 0, 0, std::integral_constant<int, 2>{});
+      asm volatile("s_barrier" ::: "memory");
+    }
+    {  // s1: A1 -> rows 64-127 x blocks 0, 1
+      const char* pa = buf + 3 * PIECE + wr * 64 * 128;
+#pragma unroll
+      for (int mi = 0; mi < 4; mi++) {
+        a1[mi][0] = rd(pa + mi * 16 * 128 + ro0);
+        a1[mi][1] = rd(pa + mi * 16 * 128 + ro1);
+      }
+      if constexpr (LAST) epi(0, 1, cm0, cn0);  // rows 0-63 x blocks 0-1: final since s0
+      issue(std::integral_constant<int, 2>{}, u + 1);
+      retire(LAST);
+      asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      mfma_blocks(b0, a1, 1, 0, std::integral_constant<int, 2>{});
+      asm volatile("s_barrier" ::: "memory");
+    }
+    {  // s2: B1 -> both row halves x block 2; then the next k-tile's B0
+      const char* pb = buf + 2 * PIECE + wc * 16 * 128;
+      b1[0] = rd(pb + ro0);
+      b1[1] = rd(pb + ro1);
+      if constexpr (EPI) epi(2, 0, pm0, pn0);   // the previous tile's block 2
+      if constexpr (LAST) epi(1, 0, cm0, cn0);  // rows 64-127 x blocks 0-1: final since s1
+      issue(std::integral_constant<int, 0>{}, u + 2);
+      issue(std::integral_constant<int, 1>{}, u + 2);
+      retire(EPI || LAST);
+      asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      mfma_blocks(b1, a0, 0, 2, std::integral_constant<int, 1>{});
+      mfma_blocks(b1, a1, 1, 2, std::integral_constant<int, 1>{});
+      rd_b0(u + 1);  // retired by this phase's vmcnt, published by its first barrier
+      asm volatile("s_barrier" ::: "memory");
+    }
+    advance(true);
+    advance(false);
+  };
+  static_assert(HANDOFF >= 4 * 4 * 1024, "hand-off half: 4 waves x 4 slots x 64 lanes x 16 B");
+
+  int u = 0;
+  for (int t = 0; t < my_tiles; t++) {
+    if (t > 0) {
+      pm0 = cm0;
+      pn0 = cn0;
+      tile_mn(t, cm0, cn0);
+    }
+    // nk >= 2 (K >= 128): the first and the last k-tile of a tile are different k-tiles
+    if (t > 0) ktile(u++, std::integral_constant<int, 1>{});
+    else ktile(u++, std::integral_constant<int, 0>{});
+    for (int k = 1; k < nk - 1; k++) ktile(u++, std::integral_constant<int, 0>{});
+    ktile(u++, std::integral_constant<int, 2>{});
+  }
+  if (!wr) asm volatile("s_barrier" ::: "memory");  // both groups at the same barrier count
+  {  // the block's last tile: block 2, every wave its own (group 0's DMAs are all issued)
+    uint4 v[4];
+    pack2b(v);
+    store2b(wr, cm0, cn0, v);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail's zero-fill DMAs land before the LDS is released
+}
+
 // out[c] (+)= sum over rows of part[r][c] (the DACT epilogue's column-sum bands):
 // block = 64 columns x 4 row lanes, grid = ceil(N / 64); fixed summation order.
 __global__ __launch_bounds__(256) void colpart_reduce(const float* __restrict__ part, int R, int N,
@@ -1256,6 +1585,14 @@ KFA_API int kfa_gemm_ppp(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int
   const PppArgs g{A, B, C, M, N, K, lda, ldb, ldc, (unsigned)cb, ws ? reinterpret_cast<float*>((char*)ws + 4096) : nullptr,
                   reinterpret_cast<int*>(ws), split, g_stagger};
   const dim3 gd(grid), bd(512);
+  if (probe == 11 || probe == 12) {  // wave-specialised stores, 256 x 192 three-phase tiles (gemm_ppw3_kernel)
+    const long t3 = (long)((M + 255) / 256) * ((N + 191) / 192);
+    const int gw = (int)(t3 < cus ? t3 : cus);
+    const PppArgs gp{A, B, C, M, N, K, lda, ldb, ldc, (unsigned)cb, nullptr, nullptr, 1, g_stagger};
+    if (probe == 11) hipLaunchKernelGGL((gemm_ppw3_kernel<false>), dim3(gw), dim3(512), 0, st, gp);
+    else hipLaunchKernelGGL((gemm_ppw3_kernel<true>), dim3(gw), dim3(512), 0, st, gp);
+    return kfa_status();
+  }
   if (probe == 9 || probe == 10) {  // wave-specialised stores (gemm_ppw_kernel): 256-wide, data-parallel tiles only
     const int gw = (int)(tiles < cus ? tiles : cus);
     const PppArgs gp{A, B, C, M, N, K, lda, ldb, ldc, (unsigned)cb, nullptr, nullptr, 1, g_stagger};

@@ -303,7 +303,7 @@ class _TransposeCache:
         tdesc = _lib.lib().kfa_tdesc_bytes()
         blob, first, total = bytearray(), [], 0
         for w, wt, (Co, R, S, Ci, r0, dr, Rs, s0, ds, Ss) in self.entries.values():
-            gx, gy = -(-Ci // 32), -(-Co // 32)
+            gx, gy = -(-Ci // 64), -(-Co // 64)  # weight_transpose_multi's 64 x 64 tiles
             rec = struct.pack("<QQ12i", w.data_ptr(), wt.data_ptr(), Co, R, S, Ci, r0, dr, Rs, s0, ds, Ss, gx, gy)
             blob += rec + bytes(tdesc - len(rec))
             first.append(total)

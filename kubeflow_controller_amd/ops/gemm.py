@@ -160,7 +160,9 @@ def gemm_ppp(a, b, *, out=None, blocks: int = 0, probe: int = 0, bn: int = 0, sp
     C written from the accumulators during the next tile's first k-tile.  K % 8 == 0, K >= 128
     (a partial last 64-deep k-tile reads zeros past K).
     ``blocks`` > 0 caps the persistent grid (tests: many tiles per block).  ``probe=1``:
-    timing probe with every C store dropped (C is left unwritten).  ``bn``: tile
+    timing probe with every C store dropped (C is left unwritten).  ``probe`` 9 / 10:
+    the wave-specialised 256 x 256 kernel (plain / non-temporal C stores); 11 / 12:
+    its 256 x 192 three-phase form (``gemm_ppw3_kernel``).  ``bn``: tile
     width 256 or 192 (0 = the kernel's pick: 192-wide tiles where N % 192 == 0 and
     256-wide ones would leave a partial last round, e.g. N = 768 at M = 32768).
     ``split``: the tiles past the grid's last full round are cut into k-ranges
@@ -316,6 +318,10 @@ def _ppp_candidates(a, b):
         c.append(("ppp256-split", lambda: gemm_ppp(a, b, bn=256)))
     if N % 192 == 0:
         c.append(("ppp192", lambda: gemm_ppp(a, b, bn=192)))
+        # wave-specialised 256 x 192 three-phase tiles (gemm_ppw3_kernel): N = 768 at
+        # M = 32768 is 512 tiles = exactly two per CU
+        c.append(("ppw192", lambda: gemm_ppp(a, b, probe=11, split=False)))
+        c.append(("ppw192-nt", lambda: gemm_ppp(a, b, probe=12, split=False)))
     return c
 
 

@@ -603,3 +603,30 @@ def test_resnet_block_lazy_bn2_fused_into_conv3(cin, mid, stride, monkeypatch):
         assert (u - v).abs().max().item() <= 3e-2 * max(1.0, v.abs().max().item())
     for C in (mid, 4 * mid):
         assert bn_slot_workspace(C, d).abs().max().item() == 0
+
+
+def test_batched_weight_transpose_matches_permute():
+    """The per-backward batched transpose (weight_transpose_multi, 64 x 64 vector tiles
+    with an element-wise path for partial tiles / odd channel counts) over a mix of
+    BERT dense weights, 3x3 conv weights with stride-2 tap subsets and odd shapes:
+    exact against torch's permute after the weights change."""
+    from kubeflow_controller_amd.ops.conv import _TransposeCache
+    torch.manual_seed(0)
+    d = torch.device("cuda")
+    shapes = [((3072, 768, 1, 1), (0, 1, 1, 0, 1, 1)), ((768, 2304, 1, 1), (0, 1, 1, 0, 1, 1)),
+              ((256, 128, 3, 3), (0, 1, 3, 0, 1, 3)), ((256, 128, 3, 3), (1, 2, 1, 0, 2, 2)),
+              ((100, 200, 1, 1), (0, 1, 1, 0, 1, 1)), ((10, 3, 3, 3), (0, 1, 3, 0, 1, 3)),
+              ((72, 136, 3, 3), (0, 2, 2, 1, 2, 1))]
+    ws = [torch.randn(*s, device=d).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+          for s, _ in shapes]
+    cache = _TransposeCache()
+    for w, (_, a) in zip(ws, shapes):
+        cache.get(w, *a)  # first use: the single-weight kernel; joins the batch after
+    for w in ws:
+        w.copy_(torch.randn_like(w))
+    cache.mark_stale()
+    for w, (shp, (r0, dr, Rs, s0, ds, Ss)) in zip(ws, shapes):
+        got = cache.get(w, r0, dr, Rs, s0, ds, Ss)  # refreshed by ONE batched launch
+        sub = w[:, :, r0::dr, s0::ds][:, :, :Rs, :Ss]          # [Co, Ci, Rs, Ss]
+        ref = sub.permute(1, 2, 3, 0).contiguous()              # [Ci, Rs, Ss, Co]
+        assert torch.equal(got.reshape(ref.shape), ref), shp

@@ -286,3 +286,28 @@ def test_ppw_gelu_backward_epilogue(M, N, K, with_bias, nt):
     db2 = torch.full((N,), 0.25, device=d)
     dz2 = bias_act_bwd(c.to(torch.bfloat16), z, bias, "gelu", db2)
     assert (dz.float() - dz2.float()).abs().max().item() <= 2e-2 * dz2.float().abs().max().item() + 1e-2
+
+
+@pytest.mark.parametrize("M,N,K,blocks", [
+    (256, 192, 128, 0),       # one tile: two k-tiles, the second LAST (2/3 of C in-loop), block 2 after
+    (512, 384, 128, 1),       # 4 tiles on one block, two k-tiles each: every k-tile EPI or LAST
+    (1000, 776, 192, 3),      # edge tiles in M and N (last tile 8 columns wide), uneven tile counts
+    (32768, 768, 768, 0),     # BERT out-projection / 768 x 768 dgrad: 512 tiles = two per CU
+    (32768, 768, 3072, 0),    # BERT FFN-down / FFN-up dgrad
+    (32768, 768, 2304, 0),    # BERT QKV dgrad
+    (2048, 1536, 2304, 5),    # long k-loop, many tiles per block
+    (300, 200, 128, 0),       # block 2 of the second tile column past N (8 columns of 192)
+    (1000, 776, 200, 0),      # K tail: a partial last k-tile of 8
+])
+@pytest.mark.parametrize("probe", [11, 12], ids=["ppw192", "ppw192_nt"])
+def test_gemm_ppw192_matches_fp32(M, N, K, blocks, probe):
+    """Wave-specialised 256 x 192 three-phase GEMM (gemm_ppw3_kernel): group 0 issues
+    every LDS-DMA piece (14 in flight), group 1 every C store; rows 0-127 x blocks 0-1
+    of a tile written during its own last k-tile, block 2 during the next tile's first."""
+    from kubeflow_controller_amd.ops import gemm as G
+    torch.manual_seed(M + N + K + 11)
+    a, b = _bf(M, K), _bf(N, K, s=0.05)
+    c = G.gemm_ppp(a, b, blocks=blocks, probe=probe, split=False)
+    _close(c, a.float() @ b.float().t(), 1e-2, f"ppw192 {M}x{N}x{K} blocks={blocks} probe={probe}")
+    c2 = G.gemm_ppp(a, b, blocks=blocks, probe=probe, split=False)
+    assert torch.equal(c, c2)
