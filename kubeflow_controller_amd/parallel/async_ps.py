@@ -18,7 +18,8 @@ progress independently — no collective, no lock-step:
   in place (owner-side apply: optimizer state lives only on the PS); the reply
   is ``[global_step, applied]`` (PS 0's counter is the job's global step);
 * ``PUSH_DEV`` → the same with the gradient already in the worker's device
-  mailbox (device transport, below);
+  mailbox (device transport, below); ``PUSH_SIG``: the mailbox copies are still
+  in flight and the PS's stream waits on the worker's event before reading it;
 * ``DONE``  → a worker finished; the PS exits when every worker has.
 
 Aggregation (``aggregate = N``, the ``SyncReplicasOptimizer`` semantics): a
@@ -51,6 +52,30 @@ loop (``kfc_recv_any``), where the per-pair message order stands in for the tags
   PS's GPU is not visible to this replica) that PS is served over the host
   transport instead, with a loud log line — the server speaks both.
 
+  Hand-offs ordered ON THE DEVICES instead of by host waits
+  (``KFA_PS_DEVICE_SIGNAL=1``, opt-in; the PS publishes its choice): each
+  worker records an interprocess HIP event (``hipIpcGetEventHandle``) after its
+  mailbox copies and the PS's stream waits on it before reading the mailbox;
+  the PS records its own interprocess event after every update and replies at
+  once, and the worker's stream waits on that event before its next pull (so it
+  reads the update) and before it rewrites the mailbox (so the update has read
+  it).  A PS that cannot see the worker's GPU (an isolated PS replica) cannot
+  wait on the worker's event: that worker host-waits its copies and sends
+  ``PUSH_DEV`` instead (every PS publishes the GPUs it sees).  The request /
+  reply headers stay on the host channel; the steady-state push / pull path has
+  no host synchronisation (``tests/test_async_ps_cpu_src.py`` checks the
+  sources).  Measured SLOWER, so not the default: BERT-base 2 workers + 1 PS on
+  one MI355X (``tools/async_rehearsal.py``) 3,377-3,643 ex/s with device
+  signalling vs 5,188-5,320 with host waits.  The host time it spends is
+  negligible (43 stream waits 1.3 ms, 3 event imports 0.17 s per run); the loss
+  is head-of-line blocking on the PS's one stream (an update queued behind
+  another worker's still-running mailbox copy) and workers' waits covering other
+  workers' updates — a host-waited header only reaches the PS once its data is
+  there.  ROCm's interprocess events also stop working after 31 records
+  (``tools/probe_ipc_event4.py``), hence the event chains below.
+  Default (``KFA_PS_DEVICE_SIGNAL`` unset / 0): host waits on recorded events
+  (the round-4 protocol).
+
 The synchronous collective modes (``--sync_replicas`` with N = W, or no PS) use
 RCCL reduce / reduce-scatter / all-gather on the GPUs instead
 (``parallel/ps.py``, ``parallel/ddp.py``).
@@ -69,7 +94,7 @@ import torch.distributed as dist
 from .comm import make_p2p
 from .ps import ps_assignment
 
-PULL, PUSH, DONE, PUSH_DEV = 1, 2, 3, 4
+PULL, PUSH, DONE, PUSH_DEV, PUSH_SIG = 1, 2, 3, 4, 5
 TAG_HDR, TAG_DATA, TAG_REPLY = 11, 12, 13
 ALIGN = 8  # = parallel/flat.py ALIGN: device-layout offsets match the worker's FlatGroups
 
@@ -134,13 +159,15 @@ class _Service:
 
     # transport hooks
     def _send_vars(self, src: int) -> None: ...
-    def _recv_grad(self, src: int, op: int) -> torch.Tensor: ...
+    def _recv_grad(self, src: int, op: int, seq: int = 0) -> torch.Tensor: ...
     def _apply(self, g: torch.Tensor, scale: float) -> None: ...
     def _acc_reset(self) -> None: ...
     def _acc_add(self, g: torch.Tensor) -> None: ...
     def _acc(self) -> torch.Tensor: ...
     def _reply(self, dst: int, applied: int) -> None:
-        self.p2p.send(torch.tensor([self.global_step, applied], dtype=torch.int64), dst, tag=TAG_REPLY)
+        # [global step, applied, this PS's update-event sequence number (0: no device signalling)]
+        self.p2p.send(torch.tensor([self.global_step, applied, getattr(self, "ps_seq", 0)], dtype=torch.int64), dst,
+                      tag=TAG_REPLY)
 
     def close(self) -> None:
         """Release the request channel (after :meth:`serve`)."""
@@ -149,7 +176,7 @@ class _Service:
     def serve(self, log: Optional[Callable[[str], None]] = None) -> int:
         """Run until every worker sent DONE; returns the number of pushes applied."""
         active = self.W
-        hdr = torch.zeros(2, dtype=torch.int64)
+        hdr = torch.zeros(3, dtype=torch.int64)  # [op, step tag, the pusher's mailbox-event sequence number]
         waiting: List[int] = []
         count = 0
         if self.aggregate:
@@ -168,11 +195,11 @@ class _Service:
 
         while active > 0:
             src = self.p2p.recv_any(hdr, tag=TAG_HDR)
-            op, tag = int(hdr[0]), int(hdr[1])
+            op, tag, seq = int(hdr[0]), int(hdr[1]), int(hdr[2])
             if op == PULL:
                 self._send_vars(src)
-            elif op in (PUSH, PUSH_DEV):
-                g = self._recv_grad(src, op)
+            elif op in (PUSH, PUSH_DEV, PUSH_SIG):
+                g = self._recv_grad(src, op, seq)
                 if not self.aggregate:
                     self._apply(g, 1.0)
                     self.applied_pushes += 1
@@ -236,7 +263,7 @@ class AsyncPSServer(_Service):
     def _send_vars(self, src: int) -> None:
         self.p2p.send(self.w, src, tag=TAG_DATA)
 
-    def _recv_grad(self, src: int, op: int) -> torch.Tensor:
+    def _recv_grad(self, src: int, op: int, seq: int = 0) -> torch.Tensor:
         if op != PUSH:
             raise RuntimeError(f"PS {self.idx}: host server got a device push from rank {src}")
         self.p2p.recv(self.grad, src, tag=TAG_DATA)
@@ -258,21 +285,23 @@ class _ClientSteps:
     def _init_steps(self, num_ps: int) -> None:
         self.tags = [0] * num_ps
         self.pushes_dropped = 0
-        self._hdr = torch.zeros(2, dtype=torch.int64)
-        self._reply = torch.zeros(2, dtype=torch.int64)
+        self._hdr = torch.zeros(3, dtype=torch.int64)
+        self._reply = torch.zeros(3, dtype=torch.int64)
+        self.ps_seq = [0] * num_ps  # each PS's update-event sequence number as last replied
 
     def close(self) -> None:
         """Release the request channel (after :meth:`done`)."""
         self.p2p.destroy()
 
-    def _header(self, rank: int, op: int, tag: int = 0) -> None:
-        self._hdr[0], self._hdr[1] = op, tag
+    def _header(self, rank: int, op: int, tag: int = 0, seq: int = 0) -> None:
+        self._hdr[0], self._hdr[1], self._hdr[2] = op, tag, seq
         self.p2p.send(self._hdr, rank, tag=TAG_HDR)
 
     def _await_reply(self, k: int, rank: int) -> int:
         self.p2p.recv(self._reply, rank, tag=TAG_REPLY)
         step, applied = int(self._reply[0]), int(self._reply[1])
         self.tags[k] = step
+        self.ps_seq[k] = int(self._reply[2])
         if not applied:
             self.pushes_dropped += 1
         return step
@@ -379,6 +408,88 @@ def _export(store, key: str, t: torch.Tensor) -> None:
     store.set(key, json.dumps(rec))
 
 
+def _export_event(store, key: str, ev: "torch.cuda.Event") -> None:
+    """Publish an interprocess HIP event (recorded at least once) as base64 text."""
+    store.set(key, base64.b64encode(bytes(ev.ipc_handle())).decode())
+
+
+def _import_event(store, key: str, device: int) -> "torch.cuda.Event":
+    """Open an event another process published with :func:`_export_event`;
+    ``device``: this process's ordinal of the exporter's GPU."""
+    return torch.cuda.Event.from_ipc_handle(torch.device("cuda", device), base64.b64decode(store.get(key)))
+
+
+class _EventChain:
+    """The producer side of a cross-process "done up to here" signal: an
+    interprocess HIP event per generation of ``G`` records, re-created and
+    published under ``key/<generation>`` when a generation is full.  ROCm's
+    interprocess event stops working after 31 records (every later
+    ``hipStreamWaitEvent`` on it fails with invalid argument, whatever the pacing:
+    ``tools/probe_ipc_event4.py``), so no event is recorded more than G = 16 times.
+    ``record`` returns the record's sequence number (1, 2, ...); the last
+    ``KEEP`` generations stay alive for consumers that open them late."""
+    G, KEEP = 16, 8
+
+    def __init__(self, store, key: str):
+        self.store, self.key, self.n = store, key, 0
+        self.gens: List[torch.cuda.Event] = []
+
+    def record(self, stream) -> int:
+        if self.n % self.G == 0:
+            ev = torch.cuda.Event(interprocess=True)
+            ev.record(stream)
+            _export_event(self.store, f"{self.key}/{self.n // self.G}", ev)
+            self.gens = (self.gens + [ev])[-self.KEEP:]
+        else:
+            self.gens[-1].record(stream)
+        self.n += 1
+        return self.n
+
+
+class _EventWaiter:
+    """The consumer side: order a stream after record ``seq`` of another process's
+    :class:`_EventChain` (a wait on that record's generation event waits for its
+    latest record, which is ``seq`` or a later one)."""
+
+    def __init__(self, store, key: str, device: int):
+        self.store, self.key, self.device = store, key, device
+        self.cache: Dict[int, torch.cuda.Event] = {}
+
+    STATS = {"imports": 0, "import_s": 0.0, "waits": 0, "wait_s": 0.0}  # host time (KFA_PS_SIGNAL_STATS=1)
+
+    def wait(self, stream, seq: int) -> None:
+        if seq <= 0:
+            return
+        import time
+        t0 = time.perf_counter()
+        gen = (seq - 1) // _EventChain.G
+        ev = self.cache.get(gen)
+        if ev is None:
+            ev = _import_event(self.store, f"{self.key}/{gen}", self.device)
+            self.cache = {g: e for g, e in self.cache.items() if g >= gen - 1}
+            self.cache[gen] = ev
+            self.STATS["imports"] += 1
+            self.STATS["import_s"] += time.perf_counter() - t0
+        t1 = time.perf_counter()
+        stream.wait_event(ev)
+        self.STATS["waits"] += 1
+        self.STATS["wait_s"] += time.perf_counter() - t1
+
+
+def _worker_key(rank: int, what: str) -> str:
+    return f"kfa/async_ps/worker/{rank}/{what}"
+
+
+def device_signal_enabled() -> bool:
+    return os.environ.get("KFA_PS_DEVICE_SIGNAL", "0") == "1"
+
+
+def _host_wait(ev: "torch.cuda.Event", stream) -> None:
+    """The KFA_PS_DEVICE_SIGNAL=0 protocol: record on ``stream`` and block the host."""
+    ev.record(stream)
+    ev.synchronize()
+
+
 def _import(store, key: str, device: Optional[int] = None) -> torch.Tensor:
     """Map a tensor another process of this job exported with :func:`_export`.
     ``device``: this process's ordinal of the exporter's GPU (the record holds the
@@ -465,6 +576,16 @@ class DeviceAsyncPSServer(_Service):
         store.set(_ipc_key(ps_index, "nonce"), str(nonce))
         store.set(_ipc_key(ps_index, "gpu"), physical_gpu())
         self._done = torch.cuda.Event()
+        # device-side hand-offs (module doc): this PS's "update recorded" event, and the
+        # workers' "mailbox written" events, opened at their first device push
+        self.signal = device_signal_enabled()
+        self._store = store
+        self._wev: Dict[int, _EventWaiter] = {}
+        self.ps_seq = 0
+        self._done_chain = _EventChain(store, _ipc_key(ps_index, "done")) if self.signal else None
+        store.set(_ipc_key(ps_index, "signal"), "1" if self.signal else "0")
+        store.set(_ipc_key(ps_index, "visible"),
+                  os.environ.get("KFA_GPUS") or os.environ.get("HIP_VISIBLE_DEVICES") or "")
         store.set(_ipc_key(ps_index, "ready"), "1")
         # after the buffers are published: the workers join the channel once they mapped them
         self.p2p = p2p if p2p is not None else make_p2p(store, group=group)
@@ -481,16 +602,33 @@ class DeviceAsyncPSServer(_Service):
             # TF AdamOptimizer form (eps outside the bias-corrected sqrt) with the fused HIP kernel
             _lib.call("kfa_adam_step", _lib.ptr(self.w), None, _lib.ptr(g), 0, _lib.ptr(self.m), _lib.ptr(self.v), n,
                       self.lr, b1, b2, self.eps / math.sqrt(bc2), 0.0, bc1, bc2, scale, None, _lib.stream())
-        # the reply below tells the pusher its mailbox may be rewritten and its next pull
-        # sees this update: host wait on THIS update's completion event (not the stream)
-        self._done.record(torch.cuda.current_stream(self.device))
-        self._done.synchronize()
+        self._after_update()
+
+    def _after_update(self) -> None:
+        """The reply that follows tells the pusher its mailbox may be rewritten and its
+        next pull sees this update: with device signalling the PS records its event
+        (the worker's stream waits on it) and replies at once; else a host wait on
+        THIS update's completion event (not the stream)."""
+        stream = torch.cuda.current_stream(self.device)
+        if self.signal:
+            self.ps_seq = self._done_chain.record(stream)  # replied to the pusher(s): they wait on it
+        else:
+            _host_wait(self._done, stream)
 
     def _send_vars(self, src: int) -> None:  # a host-transport client (IPC mapping failed on its side)
         self.stage.copy_(self.w)
         self.p2p.send(self.stage, src, tag=TAG_DATA)
 
-    def _recv_grad(self, src: int, op: int) -> torch.Tensor:
+    def _recv_grad(self, src: int, op: int, seq: int = 0) -> torch.Tensor:
+        if op == PUSH_SIG:  # the mailbox copies (record `seq` of the pusher's chain) are ordered first
+            w = self._wev.get(src)
+            if w is None:
+                dev, why = local_ordinal(self._store.get(_worker_key(src, "gpu")).decode())
+                if dev is None:
+                    raise RuntimeError(f"PS {self.idx}: PUSH_SIG from rank {src}, whose GPU I cannot see ({why})")
+                w = self._wev[src] = _EventWaiter(self._store, _worker_key(src, "copied"), dev)
+            w.wait(torch.cuda.current_stream(self.device), seq)
+            return self.mail[src]
         if op == PUSH_DEV:
             return self.mail[src]
         self.p2p.recv(self.stage, src, tag=TAG_DATA)
@@ -515,9 +653,8 @@ class DeviceAsyncPSServer(_Service):
 
     def _acc_add(self, g: torch.Tensor) -> None:
         self.acc.add_(g)
-        # the pusher may reuse its mailbox once replied to: wait for the add that read it
-        self._done.record(torch.cuda.current_stream(self.device))
-        self._done.synchronize()
+        # the pusher may reuse its mailbox once replied to: the add that read it is ordered first
+        self._after_update()
 
     def _acc(self) -> torch.Tensor:
         return self.acc
@@ -545,6 +682,8 @@ class DeviceAsyncPSClient(_ClientSteps):
         shapes = [(n, p.shape) for n, p in self.params]
         by_name = dict(self.params)
         self.plan = []
+        self.applied: List[Optional[_EventWaiter]] = []  # per PS: waits on its "update recorded" chain
+        self.sig: List[bool] = []  # per PS: it waits on this worker's "mailbox written" event (PUSH_SIG)
         self.transports: List[str] = []
         self.transport_desc: List[str] = []
         log = log or (lambda s: print(s, flush=True))
@@ -590,8 +729,19 @@ class DeviceAsyncPSClient(_ClientSteps):
                 w = mail = None
             stage = torch.empty(max(_round_up(total, ALIGN), ALIGN), dtype=torch.float32) \
                 if self.transports[-1] == "host" else None
+            applied, sig = None, False
+            if w is not None and store.get(_ipc_key(k, "signal")).decode() == "1":
+                applied = _EventWaiter(store, _ipc_key(k, "done"), dev)  # the PS's "update recorded" chain
+                vis = [v.strip() for v in store.get(_ipc_key(k, "visible")).decode().split(",") if v.strip()]
+                sig = not vis or physical_gpu() in vis  # the PS can open this worker's event
+            self.applied.append(applied)
+            self.sig.append(sig)
             self.plan.append((num_workers + k, groups, w, mail, stage))
         self._ev: Dict[torch.device, torch.cuda.Event] = {}
+        self._copied = None
+        if any(self.sig):  # this worker's "mailboxes written" chain, and its GPU (the PS opens the events there)
+            self._copied = _EventChain(store, _worker_key(rank, "copied"))
+            store.set(_worker_key(rank, "gpu"), physical_gpu())
         self._init_steps(num_ps)
         self.p2p = p2p if p2p is not None else make_p2p(store, group=group)
 
@@ -602,7 +752,8 @@ class DeviceAsyncPSClient(_ClientSteps):
 
     @torch.no_grad()
     def pull(self) -> None:
-        for rank, groups, w, _, stage in self.plan:
+        cur = torch.cuda.current_stream() if torch.cuda.is_available() else None
+        for k, (rank, groups, w, _, stage) in enumerate(self.plan):
             if not groups:
                 continue
             if stage is not None:
@@ -611,6 +762,8 @@ class DeviceAsyncPSClient(_ClientSteps):
                 src = stage
             else:
                 src = w
+                if self.applied[k] is not None:  # the PS's update last replied to this worker first
+                    self.applied[k].wait(cur, self.ps_seq[k])
             for g, start in groups:
                 g.data.copy_(src[start:start + g.numel])  # D2D (peer) copy + cast, or H2D
 
@@ -625,21 +778,23 @@ class DeviceAsyncPSClient(_ClientSteps):
         devs = set()
         for k, rank, groups, mail, stage in live:
             dst = stage if stage is not None else mail
+            if stage is None and self.applied[k] is not None:
+                # the PS's previous update (which read this mailbox) is ordered first
+                self.applied[k].wait(torch.cuda.current_stream(), self.ps_seq[k])
             for g, start in groups:
                 dst[start:start + g.numel].copy_(g.grad)
-            if stage is None:
+            if stage is None and not self.sig[k]:
                 devs |= {mail.device, groups[0][0].grad.device}
-        # the mailboxes are written before any header: one host wait on the copies' events
-        evs = []
+        seq = 0
+        if self._copied is not None:  # PUSH_SIG: the PS's stream waits on this record before it reads the mailbox
+            seq = self._copied.record(torch.cuda.current_stream())
+        # PUSH_DEV (signalling off, or the PS cannot see this GPU): the mailboxes are
+        # written before any header (host waits)
         for d in devs:
-            ev = self._ev.setdefault(d, torch.cuda.Event())
-            ev.record(torch.cuda.current_stream(d))
-            evs.append(ev)
-        for ev in evs:
-            ev.synchronize()
+            _host_wait(self._ev.setdefault(d, torch.cuda.Event()), torch.cuda.current_stream(d))
         for k, rank, groups, mail, stage in live:
             if stage is None:
-                self._header(rank, PUSH_DEV, self.tags[k])
+                self._header(rank, PUSH_SIG if self.sig[k] else PUSH_DEV, self.tags[k], seq if self.sig[k] else 0)
             else:
                 self._header(rank, PUSH, self.tags[k])
                 self.p2p.send(stage, rank, tag=TAG_DATA)
@@ -651,5 +806,7 @@ class DeviceAsyncPSClient(_ClientSteps):
         return step
 
     def done(self) -> None:
+        if os.environ.get("KFA_PS_SIGNAL_STATS") == "1":
+            print(f"[async ps] worker {self.rank} device-signal host time: {_EventWaiter.STATS}", flush=True)
         for rank, *_ in self.plan:
             self._header(rank, DONE)

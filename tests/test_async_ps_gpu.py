@@ -23,8 +23,9 @@ def _free_port():
     return p
 
 
-def _proc(rank, W, P, port, out, opt, agg):
+def _proc(rank, W, P, port, out, opt, agg, sig="1", nsteps=5):
     sys.path.insert(0, ROOT)
+    os.environ["KFA_PS_DEVICE_SIGNAL"] = sig
     import datetime
 
     import torch.distributed as dist
@@ -45,7 +46,7 @@ def _proc(rank, W, P, port, out, opt, agg):
         m = m.cuda()
         c = DeviceAsyncPSClient(list(m.named_parameters()), W, P, rank, store)
         steps = []
-        for _ in range(5):
+        for _ in range(nsteps):
             c.pull()
             c.zero_grad()
             for p in m.parameters():   # the grads are views of the client's flat buffers
@@ -59,25 +60,29 @@ def _proc(rank, W, P, port, out, opt, agg):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("opt,agg", [("sgd", 0), ("adam", 0), ("adam", 2)])
-def test_device_async_ps_matches_host_server(tmp_path, opt, agg):
+@pytest.mark.parametrize("sig", ["1", "0"], ids=["device_signal", "host_waits"])
+@pytest.mark.parametrize("opt,agg,nsteps", [("sgd", 0, 5), ("adam", 0, 5), ("adam", 2, 5), ("sgd", 0, 40)],
+                         ids=["sgd", "adam", "adam_agg2", "sgd_long"])
+def test_device_async_ps_matches_host_server(tmp_path, opt, agg, sig, nsteps):
     """Every push applied once (async) or every 2 averaged (sync replicas), the
     variables equal the host PS's TF-form update on the same gradients (Adam:
     fused HIP kernel vs AsyncPSServer._apply in fp32), and every client mapped
-    the PS memory (canary check passed: device transport, no host fallback)."""
+    the PS memory (canary check passed: device transport, no host fallback).
+    ``sgd_long``: 80 updates per PS, so the device-signalling event chains roll
+    over five generations (ROCm's interprocess events fail after 31 records)."""
     from kubeflow_controller_amd.parallel.async_ps import AsyncPSServer
     W, P = 2, 2
     out = str(tmp_path / "dps")
-    mp.start_processes(_proc, args=(W, P, _free_port(), out, opt, agg), nprocs=W + P, join=True,
+    mp.start_processes(_proc, args=(W, P, _free_port(), out, opt, agg, sig, nsteps), nprocs=W + P, join=True,
                        start_method="spawn")
     names = ["0.weight", "0.bias", "1.weight", "1.bias"]
-    updates = 5 if agg else 5 * W
+    updates = nsteps if agg else nsteps * W
     for k in range(P):
         ps = torch.load(f"{out}.ps{k}", weights_only=True)
-        assert sorted(ps["names"]) == sorted(names[k::P]) and ps["pushes"] == 5 * W and ps["step"] == updates
+        assert sorted(ps["names"]) == sorted(names[k::P]) and ps["pushes"] == nsteps * W and ps["step"] == updates
         for n, v in ps["vars"].items():
             if opt == "sgd":
-                want = torch.full_like(v, 0.5 - 0.25 * 5 * sum(range(1, W + 1)))
+                want = torch.full_like(v, 0.5 - 0.25 * nsteps * sum(range(1, W + 1)))
             else:  # constant gradient 1: the same update sequence whatever the arrival order
                 ref = AsyncPSServer([(n, torch.full((v.numel(),), 0.5))], 1, 1, 0, lr=0.25, optimizer="adam")
                 for _ in range(updates):
@@ -89,12 +94,12 @@ def test_device_async_ps_matches_host_server(tmp_path, opt, agg):
         assert got["transports"] == ["device"] * P
         if opt == "sgd":
             for n, t in got["final"].items():   # the last pull (after every push) sees the final PS values
-                assert t.min().item() >= 0.5 - 0.25 * 5 * sum(range(1, W + 1)) - 1e-5
+                assert t.min().item() >= 0.5 - 0.25 * nsteps * sum(range(1, W + 1)) - 1e-5
     steps = sorted(s for w in range(W) for s in torch.load(f"{out}.w{w}", weights_only=True)["steps"])
     if agg:
-        assert steps == sorted(list(range(1, 6)) * W)
+        assert steps == sorted(list(range(1, nsteps + 1)) * W)
     else:
-        assert steps == list(range(1, 5 * W + 1))
+        assert steps == list(range(1, nsteps * W + 1))
 
 
 def test_replica_async_bert_tiny_device_transport(tmp_path):
