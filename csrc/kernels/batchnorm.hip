@@ -62,6 +62,11 @@ __device__ __forceinline__ uint4 ld16(const bf16_t* p) {
 #ifndef KFA_BN_NT
 #define KFA_BN_NT 0
 #endif
+// rows per thread whose loads are issued together in the apply passes
+#ifndef KFA_BN_ROWS
+#define KFA_BN_ROWS 2
+#endif
+constexpr int kRows = KFA_BN_ROWS;
 // activation-sized outputs (y, dx, dres)
 __device__ __forceinline__ void st16(bf16_t* p, uint4 v) {
 #if KFA_BN_NT
@@ -284,13 +289,16 @@ __global__ __launch_bounds__(NT) void bn_apply(const bf16_t* __restrict__ x, con
       if (MB) mb[o >> 3] = (uint8_t)pos_bits(out);
     };
     long r = rb + r0;
-    for (; r + rpi < re; r += 2L * rpi) {
-      const long o0 = r * C + c0, o1 = (r + rpi) * C + c0;
-      const uint4 v0 = ld16(x + o0), v1 = ld16(x + o1);
-      uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;
-      if (RES) { q0 = ld16(res + o0); q1 = ld16(res + o1); }
-      one(v0, q0, o0);
-      one(v1, q1, o1);
+    for (; r + (kRows - 1L) * rpi < re; r += (long)kRows * rpi) {  // kRows rows' loads in flight
+      uint4 v[kRows], q[kRows];
+#pragma unroll
+      for (int i = 0; i < kRows; i++) {
+        const long o = (r + (long)i * rpi) * C + c0;
+        v[i] = ld16(x + o);
+        q[i] = RES ? ld16(res + o) : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < kRows; i++) one(v[i], q[i], (r + (long)i * rpi) * C + c0);
     }
     for (; r < re; r += rpi) {
       const long o = r * C + c0;
@@ -515,18 +523,22 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply(const bf16_t* __restrict__ dy
       st16(dx + o, pack8(out));
       if (DRES) st16(dres + o, pack8(dz));
     };
-    // two rows per iteration with all four (six) loads issued before either row is
-    // computed, as bn_apply: twice the bytes in flight per thread
+    // kRows rows per iteration with every load issued before any row is computed, as
+    // bn_apply: kRows times the bytes in flight per thread
     long r = rb + r0;
-    for (; r + rpi < re; r += 2L * rpi) {
-      const long o0 = r * C + c0, o1 = (r + rpi) * C + c0;
-      uint4 y0 = make_uint4(0, 0, 0, 0), y1 = y0;
-      if (MASK == 1) { y0 = ld16(y + o0); y1 = ld16(y + o1); }
-      const unsigned b0 = MASK == 3 ? (unsigned)mb[o0 >> 3] : 0u, b1 = MASK == 3 ? (unsigned)mb[o1 >> 3] : 0u;
-      const uint4 d0 = ld16(dy + o0), d1 = ld16(dy + o1);
-      const uint4 x0 = ld16(x + o0), x1 = ld16(x + o1);
-      one(o0, d0, x0, y0, b0);
-      one(o1, d1, x1, y1, b1);
+    for (; r + (kRows - 1L) * rpi < re; r += (long)kRows * rpi) {
+      uint4 yv[kRows], dv[kRows], xv[kRows];
+      unsigned bits[kRows];
+#pragma unroll
+      for (int i = 0; i < kRows; i++) {
+        const long o = (r + (long)i * rpi) * C + c0;
+        yv[i] = MASK == 1 ? ld16(y + o) : make_uint4(0, 0, 0, 0);
+        bits[i] = MASK == 3 ? (unsigned)mb[o >> 3] : 0u;
+        dv[i] = ld16(dy + o);
+        xv[i] = ld16(x + o);
+      }
+#pragma unroll
+      for (int i = 0; i < kRows; i++) one((r + (long)i * rpi) * C + c0, dv[i], xv[i], yv[i], bits[i]);
     }
     for (; r < re; r += rpi) {
       const long o = r * C + c0;

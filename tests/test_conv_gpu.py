@@ -131,7 +131,10 @@ def test_resnet_block_grads_igemm_vs_vendor():
                                              # a tail k-tile, edge tiles in both dims, a 1x1 conv's pixels
                                              (32768, 768, 768), (32768, 768, 3072), (12001, 512, 256),
                                              (9000, 768, 1280), (12544, 1024, 256),
-                                             (20000, 1024, 1680), (17000, 776, 1000)])  # edge tiles: N % 256 != 0
+                                             (20000, 1024, 1680), (17000, 776, 1000),  # edge tiles: N % 256 != 0
+                                             # small weights, hundreds of pixel splits: the reduce's
+                                             # 64 / 16 split-lanes per element
+                                             (200000, 64, 64), (60000, 128, 72)])
 def test_wgrad_dense_shapes(rows, out_f, in_f):
     """dW = dYᵀ·X through the wgrad kernel as a 1x1 conv over `rows` pixels."""
     from kubeflow_controller_amd.ops.conv import wgrad_into
