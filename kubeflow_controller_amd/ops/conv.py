@@ -177,7 +177,10 @@ def _igemm(args: list, stats_t=None, kind: str = "conv") -> None:
     the ping-pong kernel, from the table or timed once (statistics into a scratch
     slot buffer, so the real BatchNorm slots only see the real launch)."""
     N, K, C = args[16], args[10] * args[11] * args[7], args[7]
-    if PP == "auto" and N >= 64 and K > 0 and C % 64 == 0:
+    narrow = N <= 64 and args[_IG_VARIANT] in (1, 3)
+    # routed: every launch with whole 64-channel k-slices; the narrow tiles also for the
+    # multi-tap slices of the space-to-depth stem (C = 16), where only they apply
+    if PP == "auto" and N >= 64 and K > 0 and (C % 64 == 0 or narrow):
         from . import routes
         flags = tuple(int(args[i] is not None) for i in (3, _IG_STATS, 25, 31))
         key = tuple(args[4:23]) + flags
@@ -197,11 +200,16 @@ def _igemm(args: list, stats_t=None, kind: str = "conv") -> None:
         # every ping-pong form competes, even with part of its tile width empty: on the
         # 64-channel 3x3s the 512x128 tile (half empty) still beats the 128x64 one by 10 %
         # (profiles/r5_conv_pp_layers.md)
-        cands = [("igemm", run(args[_IG_VARIANT]), args[_IG_VARIANT]), ("pp", run(4), 4)]
-        if N <= 512:  # 512 x 128 ping-pong: the 64 / 128-channel layers and narrow N <= 512 grids
-            cands.append(("pp512", run(6), 6))
+        cands = [("igemm", run(args[_IG_VARIANT]), args[_IG_VARIANT])]
+        if C % 64 == 0:
+            cands.append(("pp", run(4), 4))
+            if N <= 512:  # 512 x 128 ping-pong: the 64 / 128-channel layers and narrow N <= 512 grids
+                cands.append(("pp512", run(6), 6))
         if args[_IG_VARIANT] == 2:  # the static rule chose the 8-wave 256x256 tile: the 128x128 one competes too
             cands.append(("igemm128", run(0), 0))
+        if narrow:  # narrow layers: the 128x64 and 256x64 tiles compete
+            other = 3 if args[_IG_VARIANT] == 1 else 1
+            cands.append(("igemm256x64" if other == 3 else "igemm128x64", run(other), other))
         i = routes.decide(kind, key, dev, [(n, f) for n, f, _ in cands])
         if i:
             args = list(args)

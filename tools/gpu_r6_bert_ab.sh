@@ -1,5 +1,6 @@
 #!/bin/bash
-# BERT-base A/B: committed routing table vs the round-5 copy (routes_gfx950_r5.json), interleaved
+# BERT-base A/B: committed routing table vs the round-5 copy (routes_gfx950_r5.json, recreate it first:
+#   git show ed33e07:kubeflow_controller_amd/ops/routes_gfx950.json > kubeflow_controller_amd/ops/routes_gfx950_r5.json), interleaved
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R; O=gpurun_out/r6bab; mkdir -p $O
 for i in 1 2 3; do
