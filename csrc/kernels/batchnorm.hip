@@ -67,6 +67,25 @@ __device__ __forceinline__ uint4 ld16(const bf16_t* p) {
 #define KFA_BN_ROWS 2
 #endif
 constexpr int kRows = KFA_BN_ROWS;
+
+// Block reduction of the per-thread channel sums (two accumulators x 8 channels per
+// thread): each thread writes two 16-B rows per accumulator, [accumulator][channel
+// half][thread][4] (lane-contiguous: conflict-free ds_write_b128; the earlier
+// [thread][8] rows put 8 lanes on every bank), regions 16 dwords past a multiple of 32
+// so the column reads (ds_read_b32: bank = dword mod 32 per 32-lane half) of the two
+// halves land on disjoint banks.
+constexpr int kRedStride = NT * 4 + 16;
+constexpr int kRedFloats = 4 * kRedStride;
+__device__ __forceinline__ void red_put(float* sh, int t, const float s1[8], const float s2[8]) {
+  *reinterpret_cast<float4*>(sh + 0 * kRedStride + t * 4) = make_float4(s1[0], s1[1], s1[2], s1[3]);
+  *reinterpret_cast<float4*>(sh + 1 * kRedStride + t * 4) = make_float4(s1[4], s1[5], s1[6], s1[7]);
+  *reinterpret_cast<float4*>(sh + 2 * kRedStride + t * 4) = make_float4(s2[0], s2[1], s2[2], s2[3]);
+  *reinterpret_cast<float4*>(sh + 3 * kRedStride + t * 4) = make_float4(s2[4], s2[5], s2[6], s2[7]);
+}
+// value j (channel j of its 8) of accumulator a written by thread tt
+__device__ __forceinline__ float red_get(const float* sh, int a, int tt, int j) {
+  return sh[(a * 2 + (j >> 2)) * kRedStride + tt * 4 + (j & 3)];
+}
 // activation-sized outputs (y, dx, dres)
 __device__ __forceinline__ void st16(bf16_t* p, uint4 v) {
 #if KFA_BN_NT
@@ -81,7 +100,7 @@ __device__ __forceinline__ void st16(bf16_t* p, uint4 v) {
 // block sums -> slot accumulators [kSlots][2][C] (shifted sum, shifted sum of squares)
 __global__ __launch_bounds__(NT) void bn_stats_partial(const bf16_t* __restrict__ x, float* __restrict__ part,
                                                         long M, int C, long chunk, int tpr, int rpi) {
-  __shared__ float sh[2][NT * 8];
+  __shared__ __attribute__((aligned(16))) float sh[kRedFloats];
   const int t = threadIdx.x;
   const int cg = t % tpr, r0 = t / tpr;
   const bool active = r0 < rpi;
@@ -120,8 +139,7 @@ __global__ __launch_bounds__(NT) void bn_stats_partial(const bf16_t* __restrict_
       }
     }
     if (active) {
-#pragma unroll
-      for (int j = 0; j < 8; j++) { sh[0][r0 * tpr * 8 + cg * 8 + j] = s1[j]; sh[1][r0 * tpr * 8 + cg * 8 + j] = s2[j]; }
+      red_put(sh, r0 * tpr + cg, s1, s2);
     }
     __syncthreads();
     const int width = tpr * 8;
@@ -129,7 +147,7 @@ __global__ __launch_bounds__(NT) void bn_stats_partial(const bf16_t* __restrict_
       const int a = idx / width, c = idx % width;
       if (g0 * 8 + c < C) {
         float acc = 0.f;
-        for (int rr = 0; rr < rpi; rr++) acc += sh[a][rr * width + c];
+        for (int rr = 0; rr < rpi; rr++) acc += red_get(sh, a, rr * tpr + (c >> 3), c & 7);
         __hip_atomic_fetch_add(&part[((long)(blockIdx.x % kSlots) * 2 + a) * C + g0 * 8 + c], acc,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
@@ -401,7 +419,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_partial(const bf16_t* __restrict__ 
                                                      const float* __restrict__ ss,
                                                      const float* __restrict__ mean, float* __restrict__ part, long M,
                                                      int C, long chunk, int tpr, int rpi) {
-  __shared__ float sh[2][NT * 8];
+  __shared__ __attribute__((aligned(16))) float sh[kRedFloats];
   const int t = threadIdx.x;
   const int cg = t % tpr, r0 = t / tpr;
   const bool active = r0 < rpi;
@@ -448,8 +466,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_partial(const bf16_t* __restrict__ 
       }
     }
     if (active) {
-#pragma unroll
-      for (int j = 0; j < 8; j++) { sh[0][r0 * tpr * 8 + cg * 8 + j] = s1[j]; sh[1][r0 * tpr * 8 + cg * 8 + j] = s2[j]; }
+      red_put(sh, r0 * tpr + cg, s1, s2);
     }
     __syncthreads();
     const int width = tpr * 8;
@@ -457,7 +474,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_partial(const bf16_t* __restrict__ 
       const int a = idx / width, c = idx % width;
       if (g0 * 8 + c < C) {
         float acc = 0.f;
-        for (int rr = 0; rr < rpi; rr++) acc += sh[a][rr * width + c];
+        for (int rr = 0; rr < rpi; rr++) acc += red_get(sh, a, rr * tpr + (c >> 3), c & 7);
         __hip_atomic_fetch_add(&part[((long)(blockIdx.x % kSlots) * 2 + a) * C + g0 * 8 + c], acc,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
@@ -562,7 +579,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_rstats(const bf16_t* __restri
                                                           bf16_t* __restrict__ dx, const bf16_t* __restrict__ r,
                                                           const float* __restrict__ rmean, float* __restrict__ rslots,
                                                           long M, int C, long chunk, int tpr, int rpi) {
-  __shared__ float sh[2][NT * 8];
+  __shared__ __attribute__((aligned(16))) float sh[kRedFloats];
   const int t = threadIdx.x;
   const int cg = t % tpr, r0 = t / tpr;
   const bool active = r0 < rpi;
@@ -614,8 +631,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_rstats(const bf16_t* __restri
       }
     }
     if (active) {
-#pragma unroll
-      for (int j = 0; j < 8; j++) { sh[0][r0 * tpr * 8 + cg * 8 + j] = s1[j]; sh[1][r0 * tpr * 8 + cg * 8 + j] = s2[j]; }
+      red_put(sh, r0 * tpr + cg, s1, s2);
     }
     __syncthreads();
     const int width = tpr * 8;
@@ -623,7 +639,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_rstats(const bf16_t* __restri
       const int a = idx / width, c = idx % width;
       if (g0 * 8 + c < C) {
         float acc = 0.f;
-        for (int rr = 0; rr < rpi; rr++) acc += sh[a][rr * width + c];
+        for (int rr = 0; rr < rpi; rr++) acc += red_get(sh, a, rr * tpr + (c >> 3), c & 7);
         __hip_atomic_fetch_add(&rslots[((long)(blockIdx.x % kSlots) * 2 + a) * C + g0 * 8 + c], acc,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }

@@ -138,6 +138,11 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ 
 // one row ahead leaves 8 waves x 1 row = ~36 KB of loads in flight per CU,
 // about half of what hides an HBM miss (MI355X_MICROARCH.md); two rows ahead
 // doubles it at +48 VGPRs (KFA_LN_BWD_DEEP).
+// floats per (wave, column half) region of ln_bwd_kernel's block reduction: H / 2 plus a
+// 16-dword shift (the column reads are ds_read_b32: bank = dword mod 32, so the two
+// halves land on disjoint banks), dropped at H = 4096 to stay within 64 KB of LDS
+__host__ __device__ __forceinline__ int ln_red_stride(int H) { return H / 2 + (H < 4096 ? 16 : 0); }
+
 template <int NV, bool TWO, int DEEP>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ dy2,
                                                      const bf16_t* __restrict__ xs,
@@ -148,7 +153,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
                                                      int H, long rows_per_block, uint32_t thresh, float dscale,
                                                      uint64_t seed) {
   static_assert(DEEP == 1 || DEEP == 2, "rows in flight");
-  extern __shared__ float red[];  // [4][H]
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [4 waves][2 halves][H / 2 + 32]
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const long r0 = (long)blockIdx.x * rows_per_block;
   const long r1 = min(rows, r0 + rows_per_block);
@@ -248,16 +253,23 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
   // block-reduce the three column accumulators
   auto reduce_out = [&](float (&acc)[NV][8], float* out) {
     if (!out) return;  // block-uniform
+    // [wave][column half][8-column group][4]: lane-contiguous 16-B writes (the earlier
+    // [wave][column] rows put 8 lanes on every bank), halves HS floats apart (see
+    // ln_red_stride: the two halves' column reads land on disjoint banks)
+    const int HS = ln_red_stride(H);
 #pragma unroll
     for (int j = 0; j < NV; j++) {
-      const int c = (j * 64 + lane) * 8;
-      if (c < H)
-#pragma unroll
-        for (int e = 0; e < 8; e++) red[w * H + c + e] = acc[j][e];
+      const int gi = j * 64 + lane;
+      if (gi * 8 < H) {
+        *reinterpret_cast<float4*>(red + (w * 2) * HS + gi * 4) = make_float4(acc[j][0], acc[j][1], acc[j][2], acc[j][3]);
+        *reinterpret_cast<float4*>(red + (w * 2 + 1) * HS + gi * 4) = make_float4(acc[j][4], acc[j][5], acc[j][6], acc[j][7]);
+      }
     }
     __syncthreads();
-    for (int c = threadIdx.x; c < H; c += 256)
-      atomicAdd(out + c, red[c] + red[H + c] + red[2 * H + c] + red[3 * H + c]);
+    for (int c = threadIdx.x; c < H; c += 256) {
+      const int o = ((c & 7) >> 2) * HS + (c >> 3) * 4 + (c & 3);
+      atomicAdd(out + c, red[o] + red[2 * HS + o] + red[4 * HS + o] + red[6 * HS + o]);
+    }
     __syncthreads();
   };
   reduce_out(ag, o_gamma);
@@ -336,7 +348,8 @@ __global__ __launch_bounds__(256) void bias_act_bwd_kernel(const bf16_t* __restr
                                                            long rows_per_block, uint32_t thresh, float dscale,
                                                            uint64_t seed, const float* __restrict__ gscale) {
   constexpr int RL = 256 / CL, W = CL * 8;
-  __shared__ float red[RL][W];
+  constexpr int RS = CL * 4 + 16;  // [row-lane][column half][column-lane][4], halves 16 banks apart (see ln_red_stride)
+  __shared__ __attribute__((aligned(16))) float red[RL * 2 * RS];
   const int cl = threadIdx.x % CL, rl = threadIdx.x / CL;
   const int c = blockIdx.x * W + cl * 8;
   const long r0 = (long)blockIdx.y * rows_per_block;
@@ -366,15 +379,16 @@ __global__ __launch_bounds__(256) void bias_act_bwd_kernel(const bf16_t* __restr
       for (int e = 0; e < 8; e++) acc[e] += d[e];
     }
   }
-#pragma unroll
-  for (int e = 0; e < 8; e++) red[rl][cl * 8 + e] = acc[e];
+  *reinterpret_cast<float4*>(red + (rl * 2) * RS + cl * 4) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+  *reinterpret_cast<float4*>(red + (rl * 2 + 1) * RS + cl * 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
   __syncthreads();
   if (dbias)
     for (int k = threadIdx.x; k < W; k += 256) {
       const int cc = blockIdx.x * W + k;
+      const int o = ((k & 7) >> 2) * RS + (k >> 3) * 4 + (k & 3);
       float sum = 0.f;
 #pragma unroll
-      for (int j = 0; j < RL; ++j) sum += red[j][k];
+      for (int j = 0; j < RL; ++j) sum += red[j * 2 * RS + o];
       if (cc < N) atomicAdd(dbias + cc, sum);
     }
 }
@@ -812,7 +826,7 @@ KFA_API int kfa_ln_bwd2(const void* dy, const void* dy2, const void* xs, const f
   const long rpb = (rows + nblk - 1) / nblk;
   const uint32_t th = drop_thresh(p);
   const float ds = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  const size_t lds = 4 * H * sizeof(float);
+  const size_t lds = 8 * (size_t)ln_red_stride(H) * sizeof(float);  // ln_bwd_kernel's reduction layout
   zero_if(dgamma, H, accumulate, s);
   zero_if(dbeta, H, accumulate, s);
   zero_if(dbias, H, accumulate, s);
