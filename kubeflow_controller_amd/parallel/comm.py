@@ -567,9 +567,11 @@ def default_store():
 
 
 def _probe(comm, device, world: int, rank: int) -> str:
-    """One reduce-scatter and one all-gather over rank-distinct values, checked
-    element by element: catches a wrong offset, order or dtype, not only a dead
-    communicator ("" = good)."""
+    """Every collective the training paths use — reduce-scatter, all-gather, fp32 and
+    bf16 all-reduce (sum, max), broadcast from the last rank, an uneven all-to-all —
+    over rank-distinct values, checked element by element: catches a wrong offset,
+    order, op or dtype, not only a dead communicator ("" = good).  Integers below
+    2^8 keep the bf16 sums exact."""
     n = 4 * world + 3  # per-rank block, odd
     base = torch.arange(n * world, dtype=torch.float32, device=device)
     inp = base * (rank + 1) + 1000.0 * rank
@@ -588,6 +590,35 @@ def _probe(comm, device, world: int, rank: int) -> str:
         torch.cuda.current_stream(device).synchronize()
     if not torch.equal(g, want):
         return f"probe all-gather mismatch on rank {rank}"
+    for dt in (torch.float32, torch.bfloat16):
+        a = (torch.arange(n, device=device) % 7 + rank + 1).to(dt)
+        comm.all_reduce(a, "sum")
+        want = (torch.arange(n, device=device) % 7 * world + sum(r + 1 for r in range(world))).to(dt)
+        if device.type == "cuda":
+            torch.cuda.current_stream(device).synchronize()
+        if not torch.equal(a, want):
+            return f"probe {dt} all-reduce mismatch on rank {rank}"
+    m = torch.arange(n, dtype=torch.float32, device=device) + 100.0 * rank
+    comm.all_reduce(m, "max")
+    b = torch.arange(n, dtype=torch.float32, device=device) * (rank + 2)
+    comm.broadcast(b, world - 1)
+    if device.type == "cuda":
+        torch.cuda.current_stream(device).synchronize()
+    if not torch.equal(m, torch.arange(n, dtype=torch.float32, device=device) + 100.0 * (world - 1)):
+        return f"probe all-reduce max mismatch on rank {rank}"
+    if not torch.equal(b, torch.arange(n, dtype=torch.float32, device=device) * (world + 1)):
+        return f"probe broadcast mismatch on rank {rank}"
+    # uneven all-to-all: rank r sends (r + p + 1) values r * 100 + p to rank p
+    ins = [r_ + p + 1 for r_ in [rank] for p in range(world)]
+    outs = [p + rank + 1 for p in range(world)]
+    src = torch.cat([torch.full((c,), float(rank * 100 + p), device=device) for p, c in enumerate(ins)])
+    dst = torch.empty(sum(outs), device=device)
+    comm.all_to_all_single(dst, src, outs, ins)
+    if device.type == "cuda":
+        torch.cuda.current_stream(device).synchronize()
+    want = torch.cat([torch.full((c,), float(p * 100 + rank), device=device) for p, c in enumerate(outs)])
+    if not torch.equal(dst, want):
+        return f"probe all-to-all mismatch on rank {rank}"
     return ""
 
 

@@ -398,9 +398,9 @@ def test_rank0_failure_is_published(monkeypatch):
 
 
 def test_probe_catches_offset_and_order_errors():
-    """make_comm's bring-up probe checks a reduce-scatter and an all-gather of
+    """make_comm's bring-up probe checks every collective the training paths use on
     rank-distinct values element by element (an all-reduce of ones cannot see a
-    wrong offset or rank order)."""
+    wrong offset, rank order or op code)."""
     sys.path.insert(0, ROOT)
     from kubeflow_controller_amd.parallel import comm as C
 
@@ -420,7 +420,29 @@ def test_probe_catches_offset_and_order_errors():
             r0 = torch.full((n,), 1.0) + torch.arange(n, dtype=torch.float32)
             parts = [inp, r0] if self.bug == "order" else [r0, inp]
             out.copy_(torch.cat(parts))
+
+        def all_reduce(self, t, op="sum"):
+            n = t.numel()
+            if op == "max":  # rank 0's probe values: arange
+                t.copy_(torch.maximum(t, torch.arange(n, dtype=t.dtype)))
+            elif self.bug == "op":  # a wrong op code: max where sum was asked
+                t.copy_(torch.maximum(t, (torch.arange(n) % 7 + 1).to(t.dtype)))
+            else:
+                t.add_((torch.arange(n) % 7 + 1).to(t.dtype))
+
+        def broadcast(self, t, src):
+            assert src == 1  # the last rank: this one
+            if self.bug == "bcast":  # the root's buffer overwritten by rank 0's
+                t.copy_(torch.arange(t.numel(), dtype=t.dtype) * 2)
+
+        def all_to_all_single(self, out, inp, out_splits, in_splits):
+            mine = inp[in_splits[0]:in_splits[0] + in_splits[1]]  # the block rank 1 keeps
+            peer = torch.full((out_splits[0],), 1.0)            # rank 0 sends 0 * 100 + 1
+            out.copy_(torch.cat([mine, peer] if self.bug == "a2a" else [peer, mine])[:out.numel()])
     dev = torch.device("cpu")
     assert C._probe(Fake(None), dev, 2, 1) == ""
     assert "reduce-scatter" in C._probe(Fake("offset"), dev, 2, 1)
     assert "all-gather" in C._probe(Fake("order"), dev, 2, 1)
+    assert "all-reduce" in C._probe(Fake("op"), dev, 2, 1)
+    assert "broadcast" in C._probe(Fake("bcast"), dev, 2, 1)
+    assert "all-to-all" in C._probe(Fake("a2a"), dev, 2, 1)

@@ -64,6 +64,14 @@ def test_rccl_world1_collectives(comm, dt):
     comm.barrier()
 
 
+def test_bringup_probe_passes_on_rccl(comm):
+    """make_comm's bring-up probe (every collective the training paths use, on
+    rank-distinct values) passes on the RCCL backend at world 1 — the probe itself
+    (its dtypes, stream syncs, all-to-all splits) runs on the device path it guards."""
+    from kubeflow_controller_amd.parallel.comm import _probe
+    assert _probe(comm, comm.device, 1, 0) == ""
+
+
 def test_rccl_async_event_handoff(comm):
     """async_op: the collective runs on the communicator's stream after the
     producer kernel; wait() orders the consumer after it without a host sync."""
