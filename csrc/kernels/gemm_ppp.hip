@@ -105,8 +105,9 @@ struct PppArgs {
   // many s_memrealtime ticks (10 ns) late, so half the CUs cross their tile
   // boundaries (and issue their C bursts) half a tile after the other half
   int stagger;
-  // GELU epilogue (gemm_ppp_kernel<256, ..., GELU = true>): C = z = A·Bᵀ + bias (the
-  // pre-activation the backward needs), Y = gelu(z); bias fp32 [N], N <= 8192
+  // activation epilogue (gemm_ppp_kernel<256, ..., ACT>): ACT 1: C = z = A·Bᵀ + bias (the
+  // pre-activation the backward needs), Y = gelu(z); ACT 2: C = relu(A·Bᵀ + bias);
+  // bias fp32 [N], N <= 8192
   bf16_t* Y;
   const float* bias;
   // GELU-backward epilogue (gemm_ppw_kernel<NT, DACT = true>): C = (A·Bᵀ) * gelu'(Zin + bias)
@@ -144,14 +145,17 @@ constexpr int kStoresPerPhase = 4;  // one 16-B store per 16-row block of a 64 x
 // B0 (u+2) — each piece DMA'd 3 phases (one k-tile) before its read phase and
 // only into a buffer whose previous piece was read >= 2 phases earlier; every
 // phase retires the DMAs of three phases ago: steady vmcnt(D = 7).
-// GELU (BN = 256, SMODE = 0, no split): the bias + GELU epilogue — each quadrant
-// store writes z = acc + bias to C and gelu(z) to Y (8 stores per phase instead of
-// 4, counted in the retire waits), the bias staged once in the 32 KB of LDS the
-// 128 KB ring leaves free — so the BERT FFN-up forward needs no bias / GELU pass.
-template <int BN = 256, bool NOST = false, int SMODE = 0, bool P3 = false, bool GELU = false>
+// ACT (BN = 256, SMODE = 0, no split): the bias + activation epilogue, the bias staged
+// once in the 32 KB of LDS the 128 KB ring leaves free.  ACT 1 (GELU): each quadrant
+// store writes z = acc + bias to C and gelu(z) to Y (8 stores per phase instead of 4,
+// counted in the retire waits) — the BERT FFN-up forward needs no bias / GELU pass.
+// ACT 2 (ReLU): C = relu(acc + bias) only, the plain 4 stores per phase — the ReLU
+// backward reads its mask from the output (y > 0 exactly where acc + bias > 0), so no
+// pre-activation is kept (the W&D MLP layers: no bias / ReLU pass, no z write).
+template <int BN = 256, bool NOST = false, int SMODE = 0, bool P3 = false, int ACT = 0>
 __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
   static_assert(BN == 256 || BN == 192, "tile width");
-  static_assert(!GELU || (BN == 256 && SMODE == 0 && !P3 && !NOST), "GELU epilogue: plain 256-wide schedule");
+  static_assert(!ACT || (BN == 256 && SMODE == 0 && !P3 && !NOST), "activation epilogue: plain 256-wide schedule");
   static_assert(!P3 || BN == 192, "three-phase k-tiles are the 192-wide schedule");
   static_assert(BN == 256 || !(SMODE & 2), "row pairs need two-block halves");
   constexpr int NB1 = BN == 256 ? 2 : 1;  // 16-column MFMA blocks in a wave's nh = 1 half
@@ -159,7 +163,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
   constexpr int TM = 8, TN = 2 + NB1;
   constexpr int D = 6 + NB1;              // DMAs per k-tile
   __shared__ __attribute__((aligned(16))) char smem[2 * 4 * PIECE];  // 128 KB: two k-tiles of four pieces
-  __shared__ __attribute__((aligned(16))) float sbias[GELU ? 8192 : 1];  // GELU: the bias vector (32 KB)
+  __shared__ __attribute__((aligned(16))) float sbias[ACT ? 8192 : 1];  // ACT: the bias vector (32 KB)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
@@ -191,8 +195,8 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
   const __amdgpu_buffer_rsrc_t rA = rsrc(g.A, (unsigned)(((long)(g.M - 1) * g.lda + g.K) * 2));
   const __amdgpu_buffer_rsrc_t rB = rsrc(g.B, (unsigned)(((long)(g.N - 1) * g.ldb + g.K) * 2));
   const __amdgpu_buffer_rsrc_t rC = rsrc(g.C, g.c_bytes);
-  const __amdgpu_buffer_rsrc_t rY = rsrc(GELU ? g.Y : g.C, GELU ? g.c_bytes : 0u);
-  if constexpr (GELU) {  // before any DMA is in flight: a plain load + LDS store + barrier
+  const __amdgpu_buffer_rsrc_t rY = rsrc(ACT == 1 ? g.Y : g.C, ACT == 1 ? g.c_bytes : 0u);
+  if constexpr (ACT != 0) {  // before any DMA is in flight: a plain load + LDS store + barrier
     for (int i = tid; i < 8192; i += 512) sbias[i] = i < g.N ? g.bias[i] : 0.f;
     __syncthreads();
   }
@@ -298,7 +302,29 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
     }
     const int n = n0 + wc * WN + nh * 32 + cb;
     const bool nok = n < g.N;
-    if constexpr (GELU) {
+    if constexpr (ACT == 2) {  // C = relu(acc + bias): the plain quadrant store of the activated value
+      const int nq = n0 + wc * WN + nh * 32 + fq * 4;
+      const float4 bx = *reinterpret_cast<const float4*>(sbias + nq);
+      const float4 by = *reinterpret_cast<const float4*>(sbias + nq + 16);
+#pragma unroll
+      for (int mi = 0; mi < 4; mi++) {
+        floatx4& x = acc[nh * 2][mh * 4 + mi];
+        floatx4& y = acc[nh * 2 + 1][mh * 4 + mi];
+        const unsigned x0 = cvt2(fmaxf(x[0] + bx.x, 0.f), fmaxf(x[1] + bx.y, 0.f));
+        const unsigned x1 = cvt2(fmaxf(x[2] + bx.z, 0.f), fmaxf(x[3] + bx.w, 0.f));
+        const unsigned y0 = cvt2(fmaxf(y[0] + by.x, 0.f), fmaxf(y[1] + by.y, 0.f));
+        const unsigned y1 = cvt2(fmaxf(y[2] + by.z, 0.f), fmaxf(y[3] + by.w, 0.f));
+        const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+        const int m = m0 + wr * 128 + mh * 64 + mi * 16 + fr;
+        const unsigned off = (m < g.M && nok) ? ((unsigned)m * (unsigned)g.ldc + (unsigned)n) * 2u : kOOB;
+        store16(rC, off, make_uint4(s0[0], s1[0], s0[1], s1[1]));
+        x = floatx4{0.f, 0.f, 0.f, 0.f};
+        y = floatx4{0.f, 0.f, 0.f, 0.f};
+      }
+      return;
+    }
+    if constexpr (ACT == 1) {
       // before the swap, x holds columns 4fq..4fq+3 of the quadrant's first 16-column
       // block, y the same of the second: their bias, then z = acc + bias -> C, gelu(z) -> Y
       const int nq = n0 + wc * WN + nh * 32 + fq * 4;
@@ -405,7 +431,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
       constexpr int s = decltype(sc)::value;
       // stores per phase: 4 each (quadrant per phase) or 8, 0, 8, 0 (row pairs)
       constexpr int RP = (SMODE & 2) ? 1 : 0;
-      constexpr int SPP = GELU ? 8 : 4;  // stores per quadrant phase (GELU: z and gelu(z))
+      constexpr int SPP = ACT == 1 ? 8 : 4;  // stores per quadrant phase (GELU: z and gelu(z))
       constexpr int upto = RP ? 8 * (s / 2 + 1) : SPP * (s + 1);          // phases 0..s
       constexpr int after = RP ? 8 * ((3 - s + (s % 2 == 0 ? 0 : 1)) / 2) : SPP * (3 - s);  // phases s+1..3
       constexpr int n = D + (EPI ? upto : 0) + (PEPI ? after : 0);
@@ -1534,7 +1560,26 @@ KFA_API int kfa_gemm_ppp_gelu(const bf16_t* A, const bf16_t* B, bf16_t* Z, bf16_
   const long cus = ppp_cus();
   const int grid = (int)(tiles < cus ? tiles : cus);
   const PppArgs g{A, B, Z, M, N, K, lda, ldb, ldc, (unsigned)cb, nullptr, nullptr, 1, g_stagger, Y, bias};
-  hipLaunchKernelGGL((gemm_ppp_kernel<256, false, 0, false, true>), dim3(grid), dim3(512), 0, st, g);
+  hipLaunchKernelGGL((gemm_ppp_kernel<256, false, 0, false, 1>), dim3(grid), dim3(512), 0, st, g);
+  return kfa_status();
+}
+
+// Y = relu(A · Bᵀ + bias) (bf16) on the persistent kernel with the bias + ReLU epilogue
+// (256-wide tiles, no split; the pre-activation is not written): same operand rules as
+// kfa_gemm_ppp_gelu.  Returns 0, -1 on unsupported operands.
+KFA_API int kfa_gemm_ppp_relu(const bf16_t* A, const bf16_t* B, bf16_t* Y, const float* bias, int M, int N, int K,
+                              int lda, int ldb, int ldc, hipStream_t st) {
+  if (M <= 0 || N <= 0) return 0;
+  if (K < 2 * BK || K % 8 || N % 8 || N > 8192 || lda % 8 || ldb % 8 || ldc % 8 || lda < K || ldb < K || ldc < N ||
+      !bias || !Y)
+    return -1;
+  const long cb = (long)M * ldc * 2;
+  if (cb >= (long)kOOB || (long)M * lda * 2 >= (long)kOOB || (long)N * ldb * 2 >= (long)kOOB) return -2;
+  const long tiles = (long)((M + 255) / 256) * ((N + 255) / 256);
+  const long cus = ppp_cus();
+  const int grid = (int)(tiles < cus ? tiles : cus);
+  const PppArgs g{A, B, Y, M, N, K, lda, ldb, ldc, (unsigned)cb, nullptr, nullptr, 1, g_stagger, nullptr, bias};
+  hipLaunchKernelGGL((gemm_ppp_kernel<256, false, 0, false, 2>), dim3(grid), dim3(512), 0, st, g);
   return kfa_status();
 }
 

@@ -36,6 +36,7 @@ _lib.register("kfa_gemm_ppp_ws_bytes", [I] * 5, restype=_lib.L)
 _lib.register("kfa_gemm_ppp_pick_bn", [I, I])
 _lib.register("kfa_gemm_skinny", [P, P, P, P] + [I] * 7 + [P, _lib.L, P])
 _lib.register("kfa_gemm_ppp_gelu", [P] * 5 + [I] * 6 + [P])
+_lib.register("kfa_gemm_ppp_relu", [P] * 4 + [I] * 6 + [P])
 _lib.register("kfa_gemm_ppw_dact", [P] * 7 + [I] * 8 + [P])
 _lib.register("kfa_gemm_ppw_dact_part_floats", [I, I], _lib.L)
 _lib.register("kfa_gemm_skinny_ws_bytes", [I] * 4, restype=_lib.L)
@@ -233,6 +234,20 @@ def gemm_ppp_gelu(a, b, bias):
     _lib.call("kfa_gemm_ppp_gelu", _lib.ptr(a), _lib.ptr(b), _lib.ptr(z), _lib.ptr(y), _lib.ptr(bias), M, N, K,
               a.stride(0), b.stride(0), N, _lib.stream())
     return y, z
+
+
+def gemm_ppp_relu(a, b, bias):
+    """``relu(a @ b.T + bias)`` (bf16) from ONE launch of the persistent GEMM with the
+    bias + ReLU epilogue (``gemm_ppp_kernel<..., ACT = 2>``): no bias / activation pass
+    and no pre-activation write — the backward takes the ReLU mask from the output."""
+    if not ppp_gelu_ok(a, b, bias):
+        raise ValueError(f"gemm_ppp_relu: unsupported operands {tuple(a.shape)} x {tuple(b.shape)}")
+    M, K = a.shape
+    N = b.shape[0]
+    y = torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
+    _lib.call("kfa_gemm_ppp_relu", _lib.ptr(a), _lib.ptr(b), _lib.ptr(y), _lib.ptr(bias), M, N, K,
+              a.stride(0), b.stride(0), N, _lib.stream())
+    return y
 
 
 def skinny_ok(a, b) -> bool:

@@ -293,6 +293,7 @@ class DenseFn(torch.autograd.Function):
         _gemm.mark_weights_stale()  # the dgrad's cached weight transposes refresh at the next backward
         mm = None  # plain GEMM of the unfused path (None: hipBLASLt)
         skinny = None  # split count of the split-K skinny GEMM with the bias fused (M <= 256, e.g. the ResNet FC)
+        relu_y = False  # the persistent GEMM with the bias + ReLU epilogue: y only, the backward masks by y > 0
         if fusable and _gemm.ROUTE_AUTO:
             # per shape, the fastest of: hipBLASLt + one bias/act pass, the MFMA GEMM with
             # the bias/act epilogue fused, the persistent MFMA GEMM + the bias/act pass,
@@ -303,6 +304,10 @@ class DenseFn(torch.autograd.Function):
             cands = ([("hipblaslt", lambda: ba(torch.mm(x2, weight.t()))),
                       ("gemm_nt-fused", lambda: _gemm.gemm_nt(x2, weight, bias=bias, act=act, want_z=has_act))]
                      + [(n, (lambda f: lambda: ba(f()))(f)) for n, f in own_pp])
+            nr = 0
+            if act == "relu" and own_pp and _gemm.ppp_gelu_ok(x2, weight, bias):
+                cands.append(("ppp256-relu", lambda: _gemm.gemm_ppp_relu(x2, weight, bias)))
+                nr = 1
             sk = _gemm.skinny_splits(x2, weight) if _gemm.skinny_ok(x2, weight) else []
             cands += [(n + "-bias", (lambda s: lambda: act_only(_gemm.gemm_skinny(x2, weight, bias, splits=s)))(s))
                       for n, s in sk]
@@ -312,8 +317,12 @@ class DenseFn(torch.autograd.Function):
             ns = len(cands) - len(sk)
             skinny = sk[i - ns][1] if i >= ns else None
             mm = own_pp[i - 2][1] if 2 <= i < 2 + len(own_pp) else None
+            relu_y = nr == 1 and i == 2 + len(own_pp)
         if fused:
             y, z = _gemm.gemm_nt(x2, weight, bias=bias, act=act, want_z=has_act)  # z includes the bias
+        elif relu_y:
+            y = _gemm.gemm_ppp_relu(x2, weight, bias)
+            z = y  # relu'(z + b) == (y > 0): the output stands in for the pre-activation
         elif skinny is not None:
             z = _gemm.gemm_skinny(x2, weight, bias, splits=skinny)  # z includes the bias
             y = bias_act_fwd(z, None, act, p, seed) if (has_act or p > 0) else z
@@ -322,7 +331,7 @@ class DenseFn(torch.autograd.Function):
             y = bias_act_fwd(z, bias, act, p, seed) if (bias is not None or has_act or p > 0) else z
         ctx.save_for_backward(x2, weight, z if has_act else None)
         ctx.bias = bias
-        ctx.cfg = (act, p, seed, shp, fused, fused or skinny is not None)
+        ctx.cfg = (act, p, seed, shp, fused, fused or skinny is not None or relu_y)
         return y.view(*shp[:-1], weight.shape[0])
 
     @staticmethod

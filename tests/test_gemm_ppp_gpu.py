@@ -257,6 +257,57 @@ def test_gemm_ppp_gelu_epilogue_matches_fp32(M, N, K):
     assert torch.equal(y, y2) and torch.equal(z, z2)
 
 
+@pytest.mark.parametrize("M,N,K", [
+    (65536, 512, 1024),    # W&D MLP layer 1: two tiles per CU
+    (65536, 1024, 1680),   # W&D layer 0: K % 64 != 0 (a partial last k-tile)
+    (1000, 776, 200),      # edge tiles in M and N, K tail
+    (300, 8192, 256),      # the widest bias the LDS stage holds
+])
+def test_gemm_ppp_relu_epilogue_matches_fp32(M, N, K):
+    """Persistent GEMM with the bias + ReLU epilogue (y only, the plain store count):
+    y = relu(A·Bᵀ + bias) vs fp32, run to run bit-identical."""
+    from kubeflow_controller_amd.ops import gemm as G
+    torch.manual_seed(M + N + K + 13)
+    a, b = _bf(M, K), _bf(N, K, s=0.05)
+    bias = torch.randn(N, device=D)
+    y = G.gemm_ppp_relu(a, b, bias)
+    _close(y, torch.relu(a.float() @ b.float().t() + bias), 1e-2, f"y {M}x{N}x{K}")
+    assert torch.equal(y, G.gemm_ppp_relu(a, b, bias))
+
+
+def test_dense_relu_epilogue_route_forward_backward(monkeypatch):
+    """The dense layer on the ReLU-epilogue route (forced): output, and the input / weight /
+    bias gradients (the backward masks by y > 0 instead of the pre-activation) vs fp32."""
+    from kubeflow_controller_amd.ops import gemm as G
+    from kubeflow_controller_amd.ops.transformer import dense
+    monkeypatch.setattr(G, "ROUTE_AUTO", True)
+    picked = []
+
+    def pick(kind, key, device, cands):  # the forward's ReLU-epilogue candidate; library elsewhere
+        names = [n for n, _ in cands]
+        if kind == "dense_fwd":
+            picked.append(names)
+            return names.index("ppp256-relu")
+        return 0
+    monkeypatch.setattr(G, "pick_fastest", pick)
+    torch.manual_seed(5)
+    M, N, K = 4096, 512, 1024
+    x = _bf(M, K).requires_grad_()
+    w = (torch.randn(N, K, device=D) * 0.03).to(torch.bfloat16).requires_grad_()
+    b = torch.randn(N, device=D).requires_grad_()
+    y = dense(x, w, b, act="relu")
+    dy = _bf(M, N)
+    y.backward(dy)
+    assert picked and "ppp256-relu" in picked[0]
+    xf, wf, bf = (t.detach().float().requires_grad_() for t in (x, w, b))
+    yr = torch.relu(xf @ wf.t() + bf)
+    yr.backward(dy.float())
+    _close(y, yr, 1e-2, "y")
+    _close(x.grad, xf.grad, 2e-2, "dx")
+    _close(w.grad, wf.grad, 2e-2, "dw")
+    _close(b.grad, bf.grad, 2e-2, "db")
+
+
 @pytest.mark.parametrize("M,N,K", [(4096, 3072, 768), (1000, 520, 136), (777, 256, 256), (2048, 1024, 512)])
 @pytest.mark.parametrize("with_bias", [True, False])
 @pytest.mark.parametrize("nt", [False, True])
