@@ -1,19 +1,15 @@
 #!/bin/bash
-# Same-box A/B/C/... of the ResNet-50 step over several environment settings,
-# interleaved (R rounds, default 2):
-#   gpurun -- bash tools/gpu_ab_multi.sh "BASE=1" "KFA_X=1" "KFA_Y=1 KFA_Z=0" ...
-# "BASE=1" (any unused variable) is the unmodified default.  One line per run:
-# <variant index> (<env>) <images/s> <ms/step>.  AB_CMD overrides the benchmark
-# (e.g. AB_CMD="tools/bench_model.py --model bert_base --batch 256 --seq 128").
+# Same-box ResNet-50 A/B over several environment settings, interleaved:
+#   gpurun -- bash tools/gpu_ab_multi.sh ROUNDS "KFA_X=0" "KFA_X=1 KFA_Y=2" ...   ("-" = no change)
 set -o pipefail
-cd ${GRAFT_REPO_ROOT:-.}; mkdir -p gpurun_out
-R=${AB_ROUNDS:-2}
-for i in $(seq 1 $R); do
-  v=0
+cd ${GRAFT_REPO_ROOT:-.}; mkdir -p gpurun_out/abm
+N=$1; shift
+for i in $(seq 1 $N); do
+  k=0
   for e in "$@"; do
-    r=$(env $e timeout -k 10 240 python -u ${AB_CMD:-bench.py} --steps 20 --warmup 5 2>gpurun_out/abm_$v.err | tail -1) \
-      || { tail -20 gpurun_out/abm_$v.err; exit 1; }
-    echo "$v ($e) $(echo "$r" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'])")"
-    v=$((v+1))
+    k=$((k+1)); [[ "$e" == "-" ]] && e="KFA_AB_NOP=1"
+    r=$(env $e timeout -k 10 300 python -u bench.py --steps 30 --warmup 5 2>gpurun_out/abm/$k.err | tail -1) \
+      || { tail -20 gpurun_out/abm/$k.err; exit 1; }
+    echo "$k ($e) $(echo "$r" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'])")"
   done
 done
