@@ -566,12 +566,12 @@ def default_store():
                              is_master=False)
 
 
-def _probe(comm, device, world: int, rank: int) -> str:
-    """Every collective the training paths use — reduce-scatter, all-gather, fp32 and
-    bf16 all-reduce (sum, max), broadcast from the last rank, an uneven all-to-all —
-    over rank-distinct values, checked element by element: catches a wrong offset,
-    order, op or dtype, not only a dead communicator ("" = good).  Integers below
-    2^8 keep the bf16 sums exact."""
+def _probe(comm, device, world: int, rank: int, a2a: bool = False) -> str:
+    """Every collective the data-parallel paths use — reduce-scatter, all-gather, fp32
+    and bf16 all-reduce (sum, max), broadcast from the last rank (``a2a``: also an uneven
+    all-to-all, the embedding exchange's) — over rank-distinct values, checked element by
+    element: catches a wrong offset, order, op or dtype, not only a dead communicator
+    ("" = good).  Integers below 2^8 keep the bf16 sums exact."""
     n = 4 * world + 3  # per-rank block, odd
     base = torch.arange(n * world, dtype=torch.float32, device=device)
     inp = base * (rank + 1) + 1000.0 * rank
@@ -608,17 +608,17 @@ def _probe(comm, device, world: int, rank: int) -> str:
         return f"probe all-reduce max mismatch on rank {rank}"
     if not torch.equal(b, torch.arange(n, dtype=torch.float32, device=device) * (world + 1)):
         return f"probe broadcast mismatch on rank {rank}"
-    # uneven all-to-all: rank r sends (r + p + 1) values r * 100 + p to rank p
-    ins = [r_ + p + 1 for r_ in [rank] for p in range(world)]
-    outs = [p + rank + 1 for p in range(world)]
-    src = torch.cat([torch.full((c,), float(rank * 100 + p), device=device) for p, c in enumerate(ins)])
-    dst = torch.empty(sum(outs), device=device)
-    comm.all_to_all_single(dst, src, outs, ins)
-    if device.type == "cuda":
-        torch.cuda.current_stream(device).synchronize()
-    want = torch.cat([torch.full((c,), float(p * 100 + rank), device=device) for p, c in enumerate(outs)])
-    if not torch.equal(dst, want):
-        return f"probe all-to-all mismatch on rank {rank}"
+    if a2a:  # uneven all-to-all: rank r sends (r + p + 1) values r * 100 + p to rank p
+        ins = [rank + p + 1 for p in range(world)]
+        outs = [p + rank + 1 for p in range(world)]
+        src = torch.cat([torch.full((c,), float(rank * 100 + p), device=device) for p, c in enumerate(ins)])
+        dst = torch.empty(sum(outs), device=device)
+        comm.all_to_all_single(dst, src, outs, ins)
+        if device.type == "cuda":
+            torch.cuda.current_stream(device).synchronize()
+        want = torch.cat([torch.full((c,), float(p * 100 + rank), device=device) for p, c in enumerate(outs)])
+        if not torch.equal(dst, want):
+            return f"probe all-to-all mismatch on rank {rank}"
     return ""
 
 
@@ -634,7 +634,7 @@ def make_comm(device: torch.device, process_group=None, store=None, mode: Option
     comm, err = None, ""
     try:
         comm = Communicator.create(store or default_store(), rank, world, device, timeout_s=t)
-        err = _probe(comm, device, world, rank)  # before any training traffic
+        err = _probe(comm, device, world, rank, a2a=os.environ.get("KFA_COMM_PROBE_A2A", "0") == "1")
         ok = not err
         if ok and comm.backend == "rccl":
             comm.transport  # noqa: B018 - read the log while the probe's connections are fresh

@@ -440,9 +440,10 @@ def test_probe_catches_offset_and_order_errors():
             peer = torch.full((out_splits[0],), 1.0)            # rank 0 sends 0 * 100 + 1
             out.copy_(torch.cat([mine, peer] if self.bug == "a2a" else [peer, mine])[:out.numel()])
     dev = torch.device("cpu")
-    assert C._probe(Fake(None), dev, 2, 1) == ""
+    assert C._probe(Fake(None), dev, 2, 1) == "" and C._probe(Fake(None), dev, 2, 1, a2a=True) == ""
     assert "reduce-scatter" in C._probe(Fake("offset"), dev, 2, 1)
     assert "all-gather" in C._probe(Fake("order"), dev, 2, 1)
     assert "all-reduce" in C._probe(Fake("op"), dev, 2, 1)
     assert "broadcast" in C._probe(Fake("bcast"), dev, 2, 1)
-    assert "all-to-all" in C._probe(Fake("a2a"), dev, 2, 1)
+    assert C._probe(Fake("a2a"), dev, 2, 1) == ""  # the all-to-all is probed on request only
+    assert "all-to-all" in C._probe(Fake("a2a"), dev, 2, 1, a2a=True)

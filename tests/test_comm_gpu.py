@@ -69,7 +69,7 @@ def test_bringup_probe_passes_on_rccl(comm):
     rank-distinct values) passes on the RCCL backend at world 1 — the probe itself
     (its dtypes, stream syncs, all-to-all splits) runs on the device path it guards."""
     from kubeflow_controller_amd.parallel.comm import _probe
-    assert _probe(comm, comm.device, 1, 0) == ""
+    assert _probe(comm, comm.device, 1, 0, a2a=True) == ""
 
 
 def test_rccl_async_event_handoff(comm):
