@@ -633,3 +633,39 @@ def test_batched_weight_transpose_matches_permute():
         sub = w[:, :, r0::dr, s0::ds][:, :, :Rs, :Ss]          # [Co, Ci, Rs, Ss]
         ref = sub.permute(1, 2, 3, 0).contiguous()              # [Ci, Rs, Ss, Co]
         assert torch.equal(got.reshape(ref.shape), ref), shp
+
+
+@pytest.mark.parametrize("want", ["igemm", "igemm256x64"])
+def test_narrow_conv_tiles_match_fp32(want, monkeypatch):
+    """The N = 64 launches on each narrow tile the router can pick — 128 x 64 ("igemm")
+    and 256 x 64 ("igemm256x64", conv_igemm_kernel<4,1,4,4>): a 64-channel 3x3 conv
+    forward / data / weight gradient, and the space-to-depth stem (C = 16 multi-tap
+    slices), vs fp32 PyTorch."""
+    import torch.nn.functional as F
+    from kubeflow_controller_amd.ops import routes
+    from kubeflow_controller_amd.ops.conv import Conv2d
+    seen = []
+
+    def decide(kind, key, dev, cands, margin=0.99, log=False):
+        names = [n for n, _ in cands]
+        seen.append(names)
+        return names.index(want) if want in names else 0
+    monkeypatch.setattr(routes, "decide", decide)
+    d = torch.device("cuda")
+    torch.manual_seed(6)
+    for cin, k, stride, pad, hw in [(64, 3, 1, 1, 28), (3, 7, 2, 3, 64)]:
+        conv = Conv2d(cin, 64, k, stride=stride, padding=pad).to(d)
+        conv.weight.data = conv.weight.data.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        x = torch.randn(2, cin, hw, hw, device=d).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        x.requires_grad_(cin != 3)
+        y = conv(x)
+        dy = torch.randn_like(y)
+        y.backward(dy)
+        xf = x.detach().float().requires_grad_(cin != 3)
+        wf = conv.weight.detach().float().requires_grad_()
+        yr = F.conv2d(xf, wf, None, stride, pad)
+        yr.backward(dy.float())
+        for name, a, r in [("y", y, yr), ("dw", conv.weight.grad, wf.grad)] + ([("dx", x.grad, xf.grad)] if cin != 3 else []):
+            err = (a.float() - r).abs().max().item()
+            assert err < 3e-2 * max(1.0, r.abs().max().item()), (cin, name, err)
+    assert any(want in n for n in seen), seen
