@@ -27,24 +27,28 @@ from ..ops import _lib
 from ..ops import transformer as T
 from ..parallel.embedding import ShardedEmbedding
 
-_lib.register("kfa_wd_input_fwd", [_lib.P, _lib.P, _lib.P, _lib.P, _lib.I, _lib.I, _lib.I, _lib.I, _lib.P])
+_lib.register("kfa_wd_input_fwd", [_lib.P] * 4 + [_lib.I] * 5 + [_lib.P])
 _lib.register("kfa_wd_input_bwd", [_lib.P, _lib.P, _lib.P, _lib.I, _lib.I, _lib.I, _lib.I, _lib.P])
 _lib.register("kfa_wd_head_blocks", [_lib.I])
-_lib.register("kfa_wd_head_fwd", [_lib.P] * 10 + [_lib.I] * 3 + [_lib.P])
-_lib.register("kfa_wd_head_bwd", [_lib.P] * 9 + [_lib.I] * 3 + [_lib.P])
+_lib.register("kfa_wd_head_fwd", [_lib.P] * 7 + [_lib.I] * 2 + [_lib.P] * 3 + [_lib.I] * 3 + [_lib.P])
+_lib.register("kfa_wd_head_bwd", [_lib.P] * 12 + [_lib.I] * 5 + [_lib.P])
 
 
 class _WDInputFn(torch.autograd.Function):
-    """(rows [B*F, E+8] bf16, dense_pad [B, Dp] fp32) -> (x [B, Dp+F*E] bf16, wide [B] fp32) in
+    """(rows [B*F, E+8] bf16, dense [B, Dn] fp32) -> (x [B, Dp+F*E] bf16, wide [B] fp32) in
     one HIP pass each way (``csrc/kernels/widedeep.hip``) — the slice / reshape / pad /
-    cat / cast chain and its autograd mirror were 16 % of the step."""
+    cat / cast chain and its autograd mirror were 16 % of the step.  The dense
+    features are zero-padded from Dn to ``Dp`` (default Dn) columns inside the kernel."""
 
     @staticmethod
-    def forward(ctx, rows, dense_pad, B, F, E):
-        Dp = dense_pad.shape[1]
+    def forward(ctx, rows, dense, B, F, E, Dp=None):
+        Dn = dense.shape[1]
+        Dp = Dn if Dp is None else Dp
+        if not (dense.dtype == torch.float32 and dense.is_contiguous() and Dn <= Dp and Dp % 8 == 0):
+            raise ValueError(f"_WDInputFn: dense {tuple(dense.shape)} {dense.dtype} for Dp={Dp}")
         x = torch.empty(B, Dp + F * E, dtype=torch.bfloat16, device=rows.device)
         wide = torch.empty(B, dtype=torch.float32, device=rows.device)
-        _lib.call("kfa_wd_input_fwd", _lib.ptr(rows), _lib.ptr(dense_pad), _lib.ptr(x), _lib.ptr(wide), B, F, E, Dp,
+        _lib.call("kfa_wd_input_fwd", _lib.ptr(rows), _lib.ptr(dense), _lib.ptr(x), _lib.ptr(wide), B, F, E, Dp, Dn,
                   _lib.stream())
         ctx.dims = (B, F, E, Dp)
         return x, wide
@@ -57,56 +61,96 @@ class _WDInputFn(torch.autograd.Function):
         dwide = (dwide if dwide is not None else torch.zeros(B, device=dx.device)).float().contiguous()
         drows = torch.empty(B * F, E + 8, dtype=torch.bfloat16, device=dx.device)
         _lib.call("kfa_wd_input_bwd", _lib.ptr(dx), _lib.ptr(dwide), _lib.ptr(drows), B, F, E, Dp, _lib.stream())
-        return drows, None, None, None, None
+        return drows, None, None, None, None, None
+
+
+def _head_weight(t: torch.Tensor, dt: torch.dtype) -> torch.Tensor:
+    """``t`` flattened as the head kernels read it: its own storage when it already is
+    ``dt``, contiguous and 16-B aligned (the flat-buffer views are), else a copy."""
+    t = t.detach().reshape(-1)
+    if t.dtype == dt and t.is_contiguous() and t.data_ptr() % 16 == 0:
+        return t
+    return t.to(dt).contiguous()
 
 
 class _WDHeadFn(torch.autograd.Function):
     """Output head + loss in one HIP pass each way (``csrc/kernels/widedeep.hip``):
-    ``z = x . out_w + out_b + wide + dpad . wide_dense``, mean sigmoid cross-entropy
+    ``z = x . out_w + out_b + wide + dense . wide_dense``, mean sigmoid cross-entropy
     against ``labels``.  Replaces two GEMV-shaped hipBLASLt calls per direction and
     the ATen loss / reduction chain.  Loss and every gradient reduce per-block
-    partials in a fixed order (deterministic)."""
+    partials in a fixed order (deterministic).
+
+    No glue kernels around it: ``out_w`` / ``wide_dense`` are read in their own dtype
+    (bf16 compute copies in the flat buffer, or fp32), ``labels`` as int64 or fp32,
+    ``dense`` raw ([B, Dn], Dn <= wide_dense.numel(): the pad columns are zeros), and
+    when the three head parameters live in flat gradient buffers the backward ADDS
+    their gradients there directly (``parallel/flat.py`` direct-gradient protocol) —
+    the fp32 -> bf16 casts and autograd's three accumulate kernels were ~0.04 ms of
+    the 2.1 ms W&D step (``profiles/r6_wide_deep_glue.md``)."""
 
     @staticmethod
-    def forward(ctx, x, out_w, out_b, wide, dpad, wide_dense, labels):
+    def forward(ctx, x, out_w, out_b, wide, dense, wide_dense, labels):
         B, H = x.shape
-        Dp = dpad.shape[1]
+        Dn, Dp = dense.shape[1], wide_dense.numel()
         dev = x.device
-        w = out_w.detach().float().reshape(-1).contiguous()
+        wbf = out_w.dtype == torch.bfloat16 and wide_dense.dtype == torch.bfloat16
+        wdt = torch.bfloat16 if wbf else torch.float32
+        w = _head_weight(out_w, wdt)
+        wd = _head_weight(wide_dense, wdt)
         ob = out_b.detach().float().reshape(-1).contiguous()
-        wd = wide_dense.detach().float().reshape(-1).contiguous()
-        y = labels.detach().float().reshape(-1).contiguous()
+        yint = labels.dtype == torch.int64
+        y = labels.detach().reshape(-1)
+        y = (y if (yint or y.dtype == torch.float32) else y.float()).contiguous()
         wide = wide.detach().float().contiguous()
+        dense = dense.detach().float().contiguous()
+        if Dn > Dp:
+            raise ValueError(f"_WDHeadFn: {Dn} dense features for {Dp} wide_dense weights")
         pmy = torch.empty(B, dtype=torch.float32, device=dev)
         part = torch.empty(_lib.lib().kfa_wd_head_blocks(B), dtype=torch.float32, device=dev)
         loss = torch.empty((), dtype=torch.float32, device=dev)
-        _lib.call("kfa_wd_head_fwd", _lib.ptr(x), _lib.ptr(w), _lib.ptr(ob), _lib.ptr(wide), _lib.ptr(dpad), _lib.ptr(wd),
-                  _lib.ptr(y), _lib.ptr(pmy), _lib.ptr(part), _lib.ptr(loss), B, H, Dp, _lib.stream())
-        ctx.save_for_backward(x, w, dpad, pmy)
-        ctx.meta = (out_w.shape, out_w.dtype, out_b.shape, out_b.dtype, wide_dense.shape, wide_dense.dtype)
+        _lib.call("kfa_wd_head_fwd", _lib.ptr(x), _lib.ptr(w), _lib.ptr(ob), _lib.ptr(wide), _lib.ptr(dense),
+                  _lib.ptr(wd), _lib.ptr(y), int(yint), int(wbf), _lib.ptr(pmy), _lib.ptr(part), _lib.ptr(loss), B, H,
+                  Dn, _lib.stream())
+        ctx.save_for_backward(x, w, dense, pmy)
+        ctx.params = (out_w, out_b, wide_dense)
+        ctx.meta = (Dp, wbf)
         return loss
 
     @staticmethod
     def backward(ctx, dloss):
-        x, w, dpad, pmy = ctx.saved_tensors
-        wshape, wdt, bshape, bdt, wdshape, wddt = ctx.meta
+        from ..parallel.flat import direct_grad_view, notify_grad_ready
+        x, w, dense, pmy = ctx.saved_tensors
+        out_w, out_b, wide_dense = ctx.params
+        Dp, wbf = ctx.meta
         B, H = x.shape
-        Dp = dpad.shape[1]
+        Dn = dense.shape[1]
         dl = dloss.detach().float().reshape(1).contiguous()
         dx = torch.empty_like(x)
         dwide = torch.empty(B, dtype=torch.float32, device=x.device)
         nb = _lib.lib().kfa_wd_head_blocks(B)
-        part = _lib.workspace(4 * nb * (H + Dp + 1), x.device, "wd_head_part")
-        grads = torch.empty(H + Dp + 1, dtype=torch.float32, device=x.device)
-        _lib.call("kfa_wd_head_bwd", _lib.ptr(x), _lib.ptr(w), _lib.ptr(dpad), _lib.ptr(pmy), _lib.ptr(dl), _lib.ptr(dx),
-                  _lib.ptr(dwide), _lib.ptr(part), _lib.ptr(grads), B, H, Dp, _lib.stream())
-        return (dx, grads[:H].view(wshape).to(wdt), grads[H + Dp:].view(bshape).to(bdt), dwide, None,
-                grads[H:H + Dp].view(wdshape).to(wddt), None)
+        part = _lib.workspace(4 * nb * (H + Dn + 1), x.device, "wd_head_part")
+        views = [direct_grad_view(p) for p in ctx.params]
+        wdt = torch.bfloat16 if wbf else torch.float32
+        direct = (all(v is not None and v.is_contiguous() for v in views)
+                  and views[0].dtype == wdt and views[2].dtype == wdt and views[1].dtype == torch.float32
+                  and views[0].numel() == H and views[2].numel() == Dp and views[1].numel() == 1
+                  and all(ctx.needs_input_grad[i] for i in (1, 2, 5)))
+        grads = None if direct else torch.empty(H + Dp + 1, dtype=torch.float32, device=x.device)
+        gw, gb, gwd = views if direct else (None, None, None)
+        _lib.call("kfa_wd_head_bwd", _lib.ptr(x), _lib.ptr(w), _lib.ptr(dense), _lib.ptr(pmy), _lib.ptr(dl),
+                  _lib.ptr(dx), _lib.ptr(dwide), _lib.ptr(part), _lib.ptr(grads), _lib.ptr(gw), _lib.ptr(gwd),
+                  _lib.ptr(gb), int(wbf), B, H, Dn, Dp, _lib.stream())
+        if direct:
+            for p in ctx.params:
+                notify_grad_ready(p)
+            return dx, None, None, dwide, None, None, None
+        return (dx, grads[:H].view(out_w.shape).to(out_w.dtype), grads[H + Dp:].view(out_b.shape).to(out_b.dtype),
+                dwide, None, grads[H:H + Dp].view(wide_dense.shape).to(wide_dense.dtype), None)
 
 
-def head_fusable(x: torch.Tensor, dpad: torch.Tensor) -> bool:
+def head_fusable(x: torch.Tensor, dense: torch.Tensor, dp: int) -> bool:
     return (FUSED_HEAD and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 2 and x.is_contiguous()
-            and x.shape[1] % 8 == 0 and x.shape[1] <= 512 and dpad.shape[1] <= 64 and x.data_ptr() % 16 == 0)
+            and x.shape[1] % 8 == 0 and x.shape[1] <= 512 and dense.shape[1] <= dp <= 64 and x.data_ptr() % 16 == 0)
 
 
 FUSED_HEAD = os.environ.get("KFA_WD_FUSED_HEAD", "1") != "0"  # csrc/kernels/widedeep.hip
@@ -175,15 +219,15 @@ class WideDeep(nn.Module):
         gids = (ids + self.offsets.view(1, nf)).reshape(-1)
         flat_rows = self.tables(gids, getattr(ids, "_kfa_plan", None))  # [B*nf, E+8]
         cdt = self.weights[0].dtype
-        dpad = F.pad(dense, (0, cfg.dense_pad - cfg.num_dense))
+        dense32 = dense.float().contiguous()  # (the fused kernels zero-pad it to dense_pad themselves)
         if (FUSED_INPUT and flat_rows.is_cuda and flat_rows.dtype == torch.bfloat16 and cdt == torch.bfloat16
                 and cfg.embed_dim % 8 == 0 and flat_rows.is_contiguous()):
-            x, wide = _WDInputFn.apply(flat_rows, dpad.float().contiguous(), B, nf, cfg.embed_dim)
+            x, wide = _WDInputFn.apply(flat_rows, dense32, B, nf, cfg.embed_dim, cfg.dense_pad)
         else:
             rows = flat_rows.view(B, nf, cfg.row_width)  # [B, nf, E+8]
             deep_emb = rows[:, :, :cfg.embed_dim].reshape(B, nf * cfg.embed_dim)
             wide = rows[:, :, cfg.embed_dim].float().sum(1)
-            x = torch.cat([dpad.to(rows.dtype), deep_emb], 1)
+            x = torch.cat([F.pad(dense, (0, cfg.dense_pad - cfg.num_dense)).to(rows.dtype), deep_emb], 1)
         if x.is_cuda:
             x = x.to(cdt)
             for w, b in zip(self.weights, self.biases):
@@ -192,9 +236,9 @@ class WideDeep(nn.Module):
             x = x.float()
             for w, b in zip(self.weights, self.biases):
                 x = torch.relu(x @ w.float().t() + b.float())
-        dpad32 = dpad.float().contiguous()
-        if head_fusable(x, dpad32):
-            return _WDHeadFn.apply(x, self.out_w, self.out_b, wide, dpad32, self.wide_dense, labels)
+        if head_fusable(x, dense32, cfg.dense_pad):
+            return _WDHeadFn.apply(x, self.out_w, self.out_b, wide, dense32, self.wide_dense, labels)
+        dpad = F.pad(dense, (0, cfg.dense_pad - cfg.num_dense))
         deep = (x @ self.out_w.to(x.dtype).t()).float().squeeze(1) + self.out_b.float()
         wide = wide + (dpad.float() @ self.wide_dense.float().t()).squeeze(1)
         return F.binary_cross_entropy_with_logits(deep + wide, labels.float())

@@ -84,3 +84,55 @@ def test_wd_head_matches_fp32_reference(B, H, Dp):
     loss2 = _WDHeadFn.apply(x, w, b, wide, dpad, wd, y)
     (loss2 * 3.0).backward()
     assert torch.equal(loss2, loss) and torch.equal(w.grad, g1[0]) and torch.equal(x.grad, g1[1])
+
+
+@pytest.mark.parametrize("B,H,Dn,Dp", [(65536, 256, 13, 16), (1000, 64, 5, 8)])
+def test_wd_head_flat_bf16_params_direct_grads(B, H, Dn, Dp):
+    """The training-time head: bf16 out_w / wide_dense and fp32 out_b living in flat
+    gradient buffers, raw [B, Dn] dense features (Dn < Dp, zero pad columns), int64
+    labels.  The backward ADDS the three parameter gradients into the flat buffers
+    (no casts, no autograd accumulate) and reports each parameter ready exactly once;
+    loss and gradients vs the fp32 PyTorch chain."""
+    from kubeflow_controller_amd.models.wide_deep import _WDHeadFn
+    from kubeflow_controller_amd.parallel.flat import FlatGroup, register_ready_hook
+    import torch.nn.functional as F
+    torch.manual_seed(B + Dn)
+    d = torch.device("cuda")
+    x = (torch.randn(B, H, device=d) * 0.5).to(torch.bfloat16).requires_grad_()
+    out_w = torch.nn.Parameter((torch.randn(1, H, device=d) * H ** -0.5).to(torch.bfloat16))
+    wide_dense = torch.nn.Parameter((torch.randn(1, Dp, device=d) * 0.1).to(torch.bfloat16))
+    out_b = torch.nn.Parameter(torch.randn(1, device=d))
+    gbf = FlatGroup([out_w, wide_dense])
+    g32 = FlatGroup([out_b])
+    prior = 0.25  # gradients already accumulated this step: the head must add to them
+    gbf.grad.fill_(prior)
+    g32.grad.fill_(prior)
+    seen = []
+    hooks = [register_ready_hook(p, lambda q: seen.append(id(q))) for p in (out_w, out_b, wide_dense)]
+    wide = torch.randn(B, device=d).requires_grad_()
+    dense = torch.randn(B, Dn, device=d)
+    y = (torch.rand(B, device=d) < 0.3).long()
+    loss = _WDHeadFn.apply(x, out_w, out_b, wide, dense, wide_dense, y)
+    (loss * 3.0).backward()
+    for h in hooks:
+        h.remove()
+    assert sorted(seen) == sorted(id(p) for p in (out_w, out_b, wide_dense))
+    xr = x.detach().float().requires_grad_()
+    wr = out_w.detach().float().requires_grad_()
+    wdr = wide_dense.detach().float().requires_grad_()
+    br = out_b.detach().clone().requires_grad_()
+    wider = wide.detach().clone().requires_grad_()
+    dpad = F.pad(dense, (0, Dp - Dn))
+    z = (xr @ wr.t()).squeeze(1) + br + wider + (dpad @ wdr.t()).squeeze(1)
+    ref = F.binary_cross_entropy_with_logits(z, y.float())
+    (ref * 3.0).backward()
+    torch.testing.assert_close(loss, ref, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=1e-6, rtol=1e-2)
+    torch.testing.assert_close(wide.grad, wider.grad, atol=1e-7, rtol=1e-5)
+    # the flat gradient views: prior + gradient, rounded once to bf16 (fp32 for out_b)
+    torch.testing.assert_close(out_w.grad.float(), (prior + wr.grad).to(torch.bfloat16).float(), atol=1e-3, rtol=1e-2)
+    torch.testing.assert_close(wide_dense.grad[:, :Dn].float(), (prior + wdr.grad[:, :Dn]).to(torch.bfloat16).float(),
+                               atol=1e-3, rtol=1e-2)
+    assert torch.all(wide_dense.grad[:, Dn:].float() == prior)  # pad columns: nothing added
+    torch.testing.assert_close(out_b.grad, prior + br.grad, atol=1e-6, rtol=1e-4)
+    assert out_w.grad.data_ptr() == gbf.grad.data_ptr() + gbf.offsets[0] * 2  # still the flat view
