@@ -115,6 +115,8 @@ struct PppArgs {
   // ([ceil(M / 64)][N] fp32, one row per 64-row quadrant band, each entry written once)
   const bf16_t* Zin;
   float* cpart;
+  // grouped-raster height in 256-row tiles (experiment knob kfa_gemm_ppp_set_gm; 0 = 4)
+  int gm;
 };
 
 __device__ __forceinline__ void ppp_stagger(int ticks, int lc) {
@@ -184,7 +186,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(PppArgs g) {
   const int skb = part * nk / ns, skl = (part + 1) * nk / ns - skb;  // the split unit's k-range
   const int J = ndp * nk + (has_split ? skl : 0);  // k-tiles this block runs, all tiles back to back
   if (J == 0) return;
-  constexpr int GM = 4;
+  const int GM = g.gm > 0 ? g.gm : 4;
   auto tile_mn = [&](int i, int& m0, int& n0) __attribute__((always_inline)) {
     const int wg = i < ndp ? lc + i * nwg : ndp * nwg + unit;
     const int grp = wg / (GM * ntn), gm0 = grp * GM, gmn = min(GM, ntm - gm0), rem = wg - grp * GM * ntn;
@@ -735,8 +737,14 @@ constexpr int HANDOFF = 16384;  // bytes per hand-off half: 4 waves x 64 rows x 
 // gelu'(z1 + b1) and the FFN-up bias gradient's column sums): group 1 loads the
 // quadrant's z (and the bias) one phase ahead of its store phase (its counter holds no
 // DMA), multiplies, stores dz and writes the quadrant band's column sums to cpart.
-template <bool NT, bool DACT = false>
+// FACT 2 (bias + ReLU forward epilogue, the W&D MLP layers): group 1 loads the bias of
+// the quadrant's 8 columns (the same for its own and its partner's quadrant) and stores
+// relu(c + bias) from the bf16 product — the library + bias/ReLU-pass rounding — so the
+// ReLU layers run on this schedule instead of gemm_ppp_kernel<..., ACT = 2>, whose C
+// stores share the DMA counter (W&D layer 1: 256.6 vs 215.9 us plain, tools/bench_wd_k1680.py).
+template <bool NT, bool DACT = false, int FACT = 0>
 __global__ __launch_bounds__(512, 1) void gemm_ppw_kernel(PppArgs g) {
+  static_assert(FACT == 0 || (FACT == 2 && !DACT), "forward epilogue: bias + ReLU, not with DACT");
   constexpr int BN = 256, WN = 64, TM = 8, TN = 4, NB1 = 2;
   constexpr int DW = 4;  // DMAs per piece per group-0 wave
   __shared__ __attribute__((aligned(16))) char smem[2 * 4 * PIECE + 2 * HANDOFF];
@@ -757,7 +765,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ppw_kernel(PppArgs g) {
   unsigned psum[kPwSeg] = {};
   unsigned long long plast_t = pw_now();
 #endif
-  constexpr int GM = 4;
+  const int GM = g.gm > 0 ? g.gm : 4;
   auto tile_mn = [&](int i, int& m0, int& n0) __attribute__((always_inline)) {
     const int wg = lc + i * nwg;
     const int grp = wg / (GM * ntn), gm0 = grp * GM, gmn = min(GM, ntm - gm0), rem = wg - grp * GM * ntn;
@@ -861,7 +869,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ppw_kernel(PppArgs g) {
     }
   };
   auto bload = [&](int nh, int n0) __attribute__((always_inline)) {
-    if constexpr (DACT) {
+    if constexpr (DACT || FACT) {
       const int n = n0 + wc * WN + nh * 32 + cb;
       if (g.bias && n < g.N) {
         const float4 x = *reinterpret_cast<const float4*>(g.bias + n), y = *reinterpret_cast<const float4*>(g.bias + n + 4);
@@ -890,6 +898,13 @@ __global__ __launch_bounds__(512, 1) void gemm_ppw_kernel(PppArgs g) {
           c[j] *= gelu_grad(z[j] + bq[j]);
           cs[j] += c[j];
         }
+        w = pack8(c);
+      }
+      if constexpr (FACT == 2) {  // y = relu(c + b)
+        float c[8];
+        unpack8(w, c);
+#pragma unroll
+        for (int j = 0; j < 8; j++) c[j] = fmaxf(c[j] + bq[j], 0.f);
         w = pack8(c);
       }
       __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<V*>(&w), rC, off, 0, NT ? 2 : 0);
@@ -943,6 +958,10 @@ __global__ __launch_bounds__(512, 1) void gemm_ppw_kernel(PppArgs g) {
         for (int mi = 0; mi < 4; mi++) pv[mi] = make_uint4(pw[mi][0], pw[mi][1], pw[mi][2], pw[mi][3]);
         store_v(0, mh, nh, pm0, pn0, pv);
         return;
+      }
+      if constexpr (FACT) {  // the quadrant columns' bias (group 1's counter holds no DMA: a plain wait)
+        bload(nh, pn0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       u32x4 pw[4];
 #pragma unroll
@@ -1111,6 +1130,10 @@ __global__ __launch_bounds__(512, 1) void gemm_ppw_kernel(PppArgs g) {
         bload(nh, cn0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
+      if constexpr (FACT) {
+        bload(nh, cn0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
       pack_q(mh, nh, v);
       store_v(wr, mh, nh, cm0, cn0, v);
     };
@@ -1172,7 +1195,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ppw3_kernel(PppArgs g) {
   const int my_tiles = lc < ntiles ? (ntiles - 1 - lc) / nwg + 1 : 0;
   const int J = my_tiles * nk;
   if (J == 0) return;
-  constexpr int GM = 4;
+  const int GM = g.gm > 0 ? g.gm : 4;
   auto tile_mn = [&](int i, int& m0, int& n0) __attribute__((always_inline)) {
     const int wg = lc + i * nwg;
     const int grp = wg / (GM * ntn), gm0 = grp * GM, gmn = min(GM, ntm - gm0), rem = wg - grp * GM * ntn;
@@ -1545,6 +1568,18 @@ KFA_API int kfa_gemm_ppp_set_stagger(int ticks) {
   return 0;
 }
 
+static int g_gm = 0;
+// experiment knob (tools/bench_wd_k1680.py): tile-raster group height (256-row tiles); 0 = 4
+KFA_API int kfa_gemm_ppp_set_gm(int gm) {
+  g_gm = gm < 0 ? 0 : gm;
+  return 0;
+}
+
+static inline PppArgs with_gm(PppArgs a) {
+  a.gm = g_gm;
+  return a;
+}
+
 // Z = A · Bᵀ + bias (bf16, the pre-activation), Y = gelu(Z) on the persistent kernel with
 // the bias + GELU epilogue (256-wide tiles, no split): K % 8 == 0, K >= 128, N % 8 == 0,
 // N <= 8192; Z and Y share ldc.  Returns 0, -1 on unsupported operands.
@@ -1560,7 +1595,7 @@ KFA_API int kfa_gemm_ppp_gelu(const bf16_t* A, const bf16_t* B, bf16_t* Z, bf16_
   const long cus = ppp_cus();
   const int grid = (int)(tiles < cus ? tiles : cus);
   const PppArgs g{A, B, Z, M, N, K, lda, ldb, ldc, (unsigned)cb, nullptr, nullptr, 1, g_stagger, Y, bias};
-  hipLaunchKernelGGL((gemm_ppp_kernel<256, false, 0, false, 1>), dim3(grid), dim3(512), 0, st, g);
+  hipLaunchKernelGGL((gemm_ppp_kernel<256, false, 0, false, 1>), dim3(grid), dim3(512), 0, st, with_gm(g));
   return kfa_status();
 }
 
@@ -1579,7 +1614,27 @@ KFA_API int kfa_gemm_ppp_relu(const bf16_t* A, const bf16_t* B, bf16_t* Y, const
   const long cus = ppp_cus();
   const int grid = (int)(tiles < cus ? tiles : cus);
   const PppArgs g{A, B, Y, M, N, K, lda, ldb, ldc, (unsigned)cb, nullptr, nullptr, 1, g_stagger, nullptr, bias};
-  hipLaunchKernelGGL((gemm_ppp_kernel<256, false, 0, false, 2>), dim3(grid), dim3(512), 0, st, g);
+  hipLaunchKernelGGL((gemm_ppp_kernel<256, false, 0, false, 2>), dim3(grid), dim3(512), 0, st, with_gm(g));
+  return kfa_status();
+}
+
+// Y = relu(A · Bᵀ + bias) (bf16) on the wave-specialised persistent kernel (gemm_ppw_kernel
+// <NT, false, 2>: the bias added to the bf16 product by the store waves); nt: non-temporal
+// stores.  Same operand rules as kfa_gemm_ppp_relu.  Returns 0, -1 on unsupported operands.
+KFA_API int kfa_gemm_ppw_relu(const bf16_t* A, const bf16_t* B, bf16_t* Y, const float* bias, int M, int N, int K,
+                              int lda, int ldb, int ldc, int nt, hipStream_t st) {
+  if (M <= 0 || N <= 0) return 0;
+  if (K < 2 * BK || K % 8 || N % 8 || lda % 8 || ldb % 8 || ldc % 8 || lda < K || ldb < K || ldc < N || !bias ||
+      !Y)
+    return -1;
+  const long cb = (long)M * ldc * 2;
+  if (cb >= (long)kOOB || (long)M * lda * 2 >= (long)kOOB || (long)N * ldb * 2 >= (long)kOOB) return -2;
+  const long tiles = (long)((M + 255) / 256) * ((N + 255) / 256);
+  const long cus = ppp_cus();
+  const int grid = (int)(tiles < cus ? tiles : cus);
+  const PppArgs g{A, B, Y, M, N, K, lda, ldb, ldc, (unsigned)cb, nullptr, nullptr, 1, g_stagger, nullptr, bias};
+  if (nt) hipLaunchKernelGGL((gemm_ppw_kernel<true, false, 2>), dim3(grid), dim3(512), 0, st, with_gm(g));
+  else hipLaunchKernelGGL((gemm_ppw_kernel<false, false, 2>), dim3(grid), dim3(512), 0, st, with_gm(g));
   return kfa_status();
 }
 
@@ -1604,8 +1659,8 @@ KFA_API int kfa_gemm_ppw_dact(const bf16_t* A, const bf16_t* B, bf16_t* C, const
   g.Zin = Zin;
   g.cpart = dbias ? cpart : nullptr;
   const int grid = (int)(tiles < cus ? tiles : cus);
-  if (nt) hipLaunchKernelGGL((gemm_ppw_kernel<true, true>), dim3(grid), dim3(512), 0, st, g);
-  else hipLaunchKernelGGL((gemm_ppw_kernel<false, true>), dim3(grid), dim3(512), 0, st, g);
+  if (nt) hipLaunchKernelGGL((gemm_ppw_kernel<true, true>), dim3(grid), dim3(512), 0, st, with_gm(g));
+  else hipLaunchKernelGGL((gemm_ppw_kernel<false, true>), dim3(grid), dim3(512), 0, st, with_gm(g));
   if (dbias)
     hipLaunchKernelGGL(colpart_reduce, dim3((N + 63) / 64), dim3(256), 0, st, cpart, (M + 63) / 64, N, dbias,
                        accumulate);
@@ -1634,34 +1689,34 @@ KFA_API int kfa_gemm_ppp(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int
     const long t3 = (long)((M + 255) / 256) * ((N + 191) / 192);
     const int gw = (int)(t3 < cus ? t3 : cus);
     const PppArgs gp{A, B, C, M, N, K, lda, ldb, ldc, (unsigned)cb, nullptr, nullptr, 1, g_stagger};
-    if (probe == 11) hipLaunchKernelGGL((gemm_ppw3_kernel<false>), dim3(gw), dim3(512), 0, st, gp);
-    else hipLaunchKernelGGL((gemm_ppw3_kernel<true>), dim3(gw), dim3(512), 0, st, gp);
+    if (probe == 11) hipLaunchKernelGGL((gemm_ppw3_kernel<false>), dim3(gw), dim3(512), 0, st, with_gm(gp));
+    else hipLaunchKernelGGL((gemm_ppw3_kernel<true>), dim3(gw), dim3(512), 0, st, with_gm(gp));
     return kfa_status();
   }
   if (probe == 9 || probe == 10) {  // wave-specialised stores (gemm_ppw_kernel): 256-wide, data-parallel tiles only
     const int gw = (int)(tiles < cus ? tiles : cus);
     const PppArgs gp{A, B, C, M, N, K, lda, ldb, ldc, (unsigned)cb, nullptr, nullptr, 1, g_stagger};
-    if (probe == 9) hipLaunchKernelGGL((gemm_ppw_kernel<false>), dim3(gw), dim3(512), 0, st, gp);
-    else hipLaunchKernelGGL((gemm_ppw_kernel<true>), dim3(gw), dim3(512), 0, st, gp);
+    if (probe == 9) hipLaunchKernelGGL((gemm_ppw_kernel<false>), dim3(gw), dim3(512), 0, st, with_gm(gp));
+    else hipLaunchKernelGGL((gemm_ppw_kernel<true>), dim3(gw), dim3(512), 0, st, with_gm(gp));
     return kfa_status();
   }
   if (bn == 192) {  // three-phase k-tiles (P3); probe 7 / 8: the four-phase schedule (with / without stores)
-    if (probe == 1 || probe == 6) hipLaunchKernelGGL((gemm_ppp_kernel<192, true, 0, true>), gd, bd, 0, st, g);
-    else if (probe == 7) hipLaunchKernelGGL((gemm_ppp_kernel<192, false>), gd, bd, 0, st, g);
-    else if (probe == 8) hipLaunchKernelGGL((gemm_ppp_kernel<192, true>), gd, bd, 0, st, g);
-    else if (probe == 2) hipLaunchKernelGGL((gemm_ppp_kernel<192, false, 1>), gd, bd, 0, st, g);
-    else hipLaunchKernelGGL((gemm_ppp_kernel<192, false, 0, true>), gd, bd, 0, st, g);
+    if (probe == 1 || probe == 6) hipLaunchKernelGGL((gemm_ppp_kernel<192, true, 0, true>), gd, bd, 0, st, with_gm(g));
+    else if (probe == 7) hipLaunchKernelGGL((gemm_ppp_kernel<192, false>), gd, bd, 0, st, with_gm(g));
+    else if (probe == 8) hipLaunchKernelGGL((gemm_ppp_kernel<192, true>), gd, bd, 0, st, with_gm(g));
+    else if (probe == 2) hipLaunchKernelGGL((gemm_ppp_kernel<192, false, 1>), gd, bd, 0, st, with_gm(g));
+    else hipLaunchKernelGGL((gemm_ppp_kernel<192, false, 0, true>), gd, bd, 0, st, with_gm(g));
     return kfa_status();
   }
   if (probe == 1)  // timing probe: no C stores
-    hipLaunchKernelGGL((gemm_ppp_kernel<256, true>), gd, bd, 0, st, g);
+    hipLaunchKernelGGL((gemm_ppp_kernel<256, true>), gd, bd, 0, st, with_gm(g));
   else if (probe == 2)  // store-policy experiments: nt / row pairs / both
-    hipLaunchKernelGGL((gemm_ppp_kernel<256, false, 1>), gd, bd, 0, st, g);
+    hipLaunchKernelGGL((gemm_ppp_kernel<256, false, 1>), gd, bd, 0, st, with_gm(g));
   else if (probe == 3)
-    hipLaunchKernelGGL((gemm_ppp_kernel<256, false, 2>), gd, bd, 0, st, g);
+    hipLaunchKernelGGL((gemm_ppp_kernel<256, false, 2>), gd, bd, 0, st, with_gm(g));
   else if (probe == 4)
-    hipLaunchKernelGGL((gemm_ppp_kernel<256, false, 3>), gd, bd, 0, st, g);
+    hipLaunchKernelGGL((gemm_ppp_kernel<256, false, 3>), gd, bd, 0, st, with_gm(g));
   else
-    hipLaunchKernelGGL((gemm_ppp_kernel<256, false>), gd, bd, 0, st, g);
+    hipLaunchKernelGGL((gemm_ppp_kernel<256, false>), gd, bd, 0, st, with_gm(g));
   return kfa_status();
 }

@@ -37,6 +37,7 @@ _lib.register("kfa_gemm_ppp_pick_bn", [I, I])
 _lib.register("kfa_gemm_skinny", [P, P, P, P] + [I] * 7 + [P, _lib.L, P])
 _lib.register("kfa_gemm_ppp_gelu", [P] * 5 + [I] * 6 + [P])
 _lib.register("kfa_gemm_ppp_relu", [P] * 4 + [I] * 6 + [P])
+_lib.register("kfa_gemm_ppw_relu", [P] * 4 + [I] * 7 + [P])
 _lib.register("kfa_gemm_ppw_dact", [P] * 7 + [I] * 8 + [P])
 _lib.register("kfa_gemm_ppw_dact_part_floats", [I, I], _lib.L)
 _lib.register("kfa_gemm_skinny_ws_bytes", [I] * 4, restype=_lib.L)
@@ -247,6 +248,21 @@ def gemm_ppp_relu(a, b, bias):
     y = torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
     _lib.call("kfa_gemm_ppp_relu", _lib.ptr(a), _lib.ptr(b), _lib.ptr(y), _lib.ptr(bias), M, N, K,
               a.stride(0), b.stride(0), N, _lib.stream())
+    return y
+
+
+def gemm_ppw_relu(a, b, bias, nt: bool = False):
+    """``relu(a @ b.T + bias)`` (bf16) from ONE launch of the wave-specialised persistent
+    GEMM (``gemm_ppw_kernel<NT, false, 2>``): the store waves add the bias to the bf16
+    product and clamp — the C stores stay off the DMA waves' counter, as in the plain
+    ``ppw256`` variant (``nt``: non-temporal stores)."""
+    if not ppp_gelu_ok(a, b, bias) or bias.data_ptr() % 16:
+        raise ValueError(f"gemm_ppw_relu: unsupported operands {tuple(a.shape)} x {tuple(b.shape)}")
+    M, K = a.shape
+    N = b.shape[0]
+    y = torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
+    _lib.call("kfa_gemm_ppw_relu", _lib.ptr(a), _lib.ptr(b), _lib.ptr(y), _lib.ptr(bias), M, N, K,
+              a.stride(0), b.stride(0), N, int(nt), _lib.stream())
     return y
 
 

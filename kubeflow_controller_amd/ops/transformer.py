@@ -304,10 +304,12 @@ class DenseFn(torch.autograd.Function):
             cands = ([("hipblaslt", lambda: ba(torch.mm(x2, weight.t()))),
                       ("gemm_nt-fused", lambda: _gemm.gemm_nt(x2, weight, bias=bias, act=act, want_z=has_act))]
                      + [(n, (lambda f: lambda: ba(f()))(f)) for n, f in own_pp])
-            nr = 0
+            relu_fns = []  # bias + ReLU epilogue variants: y only, the backward masks by y > 0
             if act == "relu" and own_pp and _gemm.ppp_gelu_ok(x2, weight, bias):
-                cands.append(("ppp256-relu", lambda: _gemm.gemm_ppp_relu(x2, weight, bias)))
-                nr = 1
+                relu_fns = [("ppp256-relu", lambda: _gemm.gemm_ppp_relu(x2, weight, bias)),
+                            ("ppw256-relu", lambda: _gemm.gemm_ppw_relu(x2, weight, bias)),
+                            ("ppw256-nt-relu", lambda: _gemm.gemm_ppw_relu(x2, weight, bias, nt=True))]
+                cands += relu_fns
             sk = _gemm.skinny_splits(x2, weight) if _gemm.skinny_ok(x2, weight) else []
             cands += [(n + "-bias", (lambda s: lambda: act_only(_gemm.gemm_skinny(x2, weight, bias, splits=s)))(s))
                       for n, s in sk]
@@ -317,11 +319,12 @@ class DenseFn(torch.autograd.Function):
             ns = len(cands) - len(sk)
             skinny = sk[i - ns][1] if i >= ns else None
             mm = own_pp[i - 2][1] if 2 <= i < 2 + len(own_pp) else None
-            relu_y = nr == 1 and i == 2 + len(own_pp)
+            r0 = 2 + len(own_pp)
+            relu_y = relu_fns[i - r0][1] if r0 <= i < r0 + len(relu_fns) else False
         if fused:
             y, z = _gemm.gemm_nt(x2, weight, bias=bias, act=act, want_z=has_act)  # z includes the bias
         elif relu_y:
-            y = _gemm.gemm_ppp_relu(x2, weight, bias)
+            y = relu_y()
             z = y  # relu'(z + b) == (y > 0): the output stands in for the pre-activation
         elif skinny is not None:
             z = _gemm.gemm_skinny(x2, weight, bias, splits=skinny)  # z includes the bias
@@ -331,7 +334,7 @@ class DenseFn(torch.autograd.Function):
             y = bias_act_fwd(z, bias, act, p, seed) if (bias is not None or has_act or p > 0) else z
         ctx.save_for_backward(x2, weight, z if has_act else None)
         ctx.bias = bias
-        ctx.cfg = (act, p, seed, shp, fused, fused or skinny is not None or relu_y)
+        ctx.cfg = (act, p, seed, shp, fused, fused or skinny is not None or bool(relu_y))
         return y.view(*shp[:-1], weight.shape[0])
 
     @staticmethod

@@ -275,19 +275,42 @@ def test_gemm_ppp_relu_epilogue_matches_fp32(M, N, K):
     assert torch.equal(y, G.gemm_ppp_relu(a, b, bias))
 
 
-def test_dense_relu_epilogue_route_forward_backward(monkeypatch):
+@pytest.mark.parametrize("M,N,K", [
+    (65536, 1024, 1680),   # W&D layer 0: four tiles per CU, K % 64 != 0
+    (65536, 256, 512),     # W&D layer 2: one tile column
+    (1000, 776, 200),      # edge tiles in M and N, K tail
+])
+@pytest.mark.parametrize("nt", [False, True])
+def test_gemm_ppw_relu_epilogue_matches_fp32(M, N, K, nt):
+    """Wave-specialised persistent GEMM with the bias + ReLU store epilogue
+    (gemm_ppw_kernel<NT, false, 2>): y = relu(bf16(A·Bᵀ) + bias) vs fp32, equal to the
+    plain ppw GEMM + the bias/ReLU pass (the same bf16 product), run to run bit-identical."""
+    from kubeflow_controller_amd.ops import gemm as G
+    torch.manual_seed(M + N + K + 17)
+    a, b = _bf(M, K), _bf(N, K, s=0.05)
+    bias = torch.randn(N, device=D)
+    y = G.gemm_ppw_relu(a, b, bias, nt=nt)
+    _close(y, torch.relu(a.float() @ b.float().t() + bias), 1e-2, f"y {M}x{N}x{K}")
+    ref = torch.relu(G.gemm_ppp(a, b, probe=10 if nt else 9, split=False).float() + bias).to(torch.bfloat16)
+    assert torch.equal(y, ref)
+    assert torch.equal(y, G.gemm_ppw_relu(a, b, bias, nt=nt))
+
+
+@pytest.mark.parametrize("route", ["ppp256-relu", "ppw256-relu", "ppw256-nt-relu"])
+def test_dense_relu_epilogue_route_forward_backward(monkeypatch, route):
     """The dense layer on the ReLU-epilogue route (forced): output, and the input / weight /
     bias gradients (the backward masks by y > 0 instead of the pre-activation) vs fp32."""
     from kubeflow_controller_amd.ops import gemm as G
     from kubeflow_controller_amd.ops.transformer import dense
     monkeypatch.setattr(G, "ROUTE_AUTO", True)
     picked = []
+    forced = [route]
 
     def pick(kind, key, device, cands):  # the forward's ReLU-epilogue candidate; library elsewhere
         names = [n for n, _ in cands]
         if kind == "dense_fwd":
             picked.append(names)
-            return names.index("ppp256-relu")
+            return names.index(forced[0])
         return 0
     monkeypatch.setattr(G, "pick_fastest", pick)
     torch.manual_seed(5)
@@ -298,7 +321,20 @@ def test_dense_relu_epilogue_route_forward_backward(monkeypatch):
     y = dense(x, w, b, act="relu")
     dy = _bf(M, N)
     y.backward(dy)
-    assert picked and "ppp256-relu" in picked[0]
+    assert picked and route in picked[0]
+    if route.startswith("ppw"):
+        # the store epilogue adds the bias to the bf16 product, as the plain ppw GEMM + the
+        # bias/ReLU pass does: bit-equal to that route, forward and backward (vs fp32 the
+        # mask differs where z rounds across 0, as for every library + pass route)
+        forced[0] = route[:-len("-relu")]
+        xc, wc, bc = (t.detach().clone().requires_grad_() for t in (x, w, b))
+        yc = dense(xc, wc, bc, act="relu")
+        yc.backward(dy)
+        assert torch.equal(y, yc) and torch.equal(x.grad, xc.grad)
+        assert torch.equal(w.grad, wc.grad)
+        # the bias column sums: same values, the per-block partial sums may land in another order
+        torch.testing.assert_close(b.grad, bc.grad, rtol=1e-5, atol=1e-4)
+        return
     xf, wf, bf = (t.detach().float().requires_grad_() for t in (x, w, b))
     yr = torch.relu(xf @ wf.t() + bf)
     yr.backward(dy.float())
