@@ -29,6 +29,7 @@ from ..parallel.embedding import ShardedEmbedding
 
 _lib.register("kfa_wd_input_fwd", [_lib.P] * 4 + [_lib.I] * 5 + [_lib.P])
 _lib.register("kfa_wd_input_bwd", [_lib.P, _lib.P, _lib.P, _lib.I, _lib.I, _lib.I, _lib.I, _lib.P])
+_lib.register("kfa_wd_gather_fwd", [_lib.P] * 5 + [_lib.I] * 5 + [_lib.P])
 _lib.register("kfa_wd_head_blocks", [_lib.I])
 _lib.register("kfa_wd_head_fwd", [_lib.P] * 7 + [_lib.I] * 2 + [_lib.P] * 3 + [_lib.I] * 3 + [_lib.P])
 _lib.register("kfa_wd_head_bwd", [_lib.P] * 12 + [_lib.I] * 5 + [_lib.P])
@@ -62,6 +63,53 @@ class _WDInputFn(torch.autograd.Function):
         drows = torch.empty(B * F, E + 8, dtype=torch.bfloat16, device=dx.device)
         _lib.call("kfa_wd_input_bwd", _lib.ptr(dx), _lib.ptr(dwide), _lib.ptr(drows), B, F, E, Dp, _lib.stream())
         return drows, None, None, None, None, None
+
+
+class _WDLookupInputFn(torch.autograd.Function):
+    """World-1 lookup + input assembly in one HIP pass (``kfa_wd_gather_fwd``): x rows are
+    gathered straight from the fp32 table (bf16-rounded, as the lookup's output) next to
+    the zero-padded dense features, wide sums alongside — bit-equal to
+    ``ShardedEmbedding`` + :class:`_WDInputFn` without their [B*F, E+8] bf16 rows
+    (written once, read once: ~0.13 ms of the 2.0 ms step).  The backward builds the
+    rows' gradient (``kfa_wd_input_bwd``) and hands it to the table's own sparse
+    optimizer, exactly as the lookup's backward does (``parallel/embedding.py``)."""
+
+    @staticmethod
+    def forward(ctx, gids, weight, emb, dense, B, F, E, Dp):
+        Dn = dense.shape[1]
+        emb._check_table()
+        x = torch.empty(B, Dp + F * E, dtype=torch.bfloat16, device=dense.device)
+        wide = torch.empty(B, dtype=torch.float32, device=dense.device)
+        # the id sort of the sparse update needs no gradient: start it now, beside the dense layers
+        ctx.prep = emb.prepare_sparse(gids) if ctx.needs_input_grad[1] else None
+        _lib.call("kfa_wd_gather_fwd", _lib.ptr(gids), _lib.ptr(weight), _lib.ptr(dense), _lib.ptr(x), _lib.ptr(wide),
+                  B, F, E, Dp, Dn, _lib.stream())
+        ctx.save_for_backward(gids)
+        ctx.emb = emb
+        ctx.dims = (B, F, E, Dp)
+        return x, wide
+
+    @staticmethod
+    def backward(ctx, dx, dwide):
+        (gids,) = ctx.saved_tensors
+        B, F, E, Dp = ctx.dims
+        dx = (dx if dx is not None else torch.zeros(B, Dp + F * E, dtype=torch.bfloat16,
+                                                    device=gids.device)).to(torch.bfloat16).contiguous()
+        dwide = (dwide if dwide is not None else torch.zeros(B, device=gids.device)).float().contiguous()
+        drows = torch.empty(B * F, E + 8, dtype=torch.bfloat16, device=gids.device)
+        _lib.call("kfa_wd_input_bwd", _lib.ptr(dx), _lib.ptr(dwide), _lib.ptr(drows), B, F, E, Dp, _lib.stream())
+        ctx.emb.apply_sparse(gids, drows, prep=ctx.prep)
+        ctx.prep = None
+        return None, None, None, None, None, None, None, None
+
+
+def lookup_fusable(emb: ShardedEmbedding, gids: torch.Tensor, E: int) -> bool:
+    """:class:`_WDLookupInputFn` applies: one rank holds every row (world 1), the fp32
+    table on the GPU with 16-B aligned (E + 8)-wide rows, int64 ids."""
+    w = emb.weight
+    return (FUSED_INPUT and FUSED_LOOKUP and emb.world == 1 and emb.owners == 1 and w.is_cuda
+            and w.dtype == torch.float32 and w.is_contiguous() and emb.dim == E + 8 and E % 8 == 0
+            and w.data_ptr() % 16 == 0 and gids.dtype == torch.int64 and gids.is_contiguous())
 
 
 def _head_weight(t: torch.Tensor, dt: torch.dtype) -> torch.Tensor:
@@ -155,6 +203,7 @@ def head_fusable(x: torch.Tensor, dense: torch.Tensor, dp: int) -> bool:
 
 FUSED_HEAD = os.environ.get("KFA_WD_FUSED_HEAD", "1") != "0"  # csrc/kernels/widedeep.hip
 FUSED_INPUT = os.environ.get("KFA_WD_FUSED_INPUT", "1") != "0"  # csrc/kernels/widedeep.hip
+FUSED_LOOKUP = os.environ.get("KFA_WD_FUSED_LOOKUP", "1") != "0"  # world 1: gather straight into x
 CRITEO_LIKE = (4_000_000,) * 4 + (1_000_000,) * 6 + (100_000,) * 8 + (10_000,) * 8
 
 
@@ -213,21 +262,30 @@ class WideDeep(nn.Module):
         self.out_b = nn.Parameter(torch.zeros(1))
         self.wide_dense = nn.Parameter(torch.zeros(1, cfg.dense_pad))
 
+    def _assemble(self, flat_rows, dense, dense32, B, nf, cdt):
+        """Looked-up rows [B*nf, E+8] (+ dense) -> (MLP input x, wide sums)."""
+        cfg = self.cfg
+        if (FUSED_INPUT and flat_rows.is_cuda and flat_rows.dtype == torch.bfloat16 and cdt == torch.bfloat16
+                and cfg.embed_dim % 8 == 0 and flat_rows.is_contiguous()):
+            return _WDInputFn.apply(flat_rows, dense32, B, nf, cfg.embed_dim, cfg.dense_pad)
+        rows = flat_rows.view(B, nf, cfg.row_width)  # [B, nf, E+8]
+        deep_emb = rows[:, :, :cfg.embed_dim].reshape(B, nf * cfg.embed_dim)
+        wide = rows[:, :, cfg.embed_dim].float().sum(1)
+        x = torch.cat([F.pad(dense, (0, cfg.dense_pad - cfg.num_dense)).to(rows.dtype), deep_emb], 1)
+        return x, wide
+
     def forward(self, dense: torch.Tensor, ids: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
         cfg = self.cfg
         B, nf = ids.shape
         gids = (ids + self.offsets.view(1, nf)).reshape(-1)
-        flat_rows = self.tables(gids, getattr(ids, "_kfa_plan", None))  # [B*nf, E+8]
         cdt = self.weights[0].dtype
         dense32 = dense.float().contiguous()  # (the fused kernels zero-pad it to dense_pad themselves)
-        if (FUSED_INPUT and flat_rows.is_cuda and flat_rows.dtype == torch.bfloat16 and cdt == torch.bfloat16
-                and cfg.embed_dim % 8 == 0 and flat_rows.is_contiguous()):
-            x, wide = _WDInputFn.apply(flat_rows, dense32, B, nf, cfg.embed_dim, cfg.dense_pad)
+        if cdt == torch.bfloat16 and lookup_fusable(self.tables, gids, cfg.embed_dim):
+            # world 1: the lookup gathers straight into the MLP input
+            x, wide = _WDLookupInputFn.apply(gids, self.tables.weight, self.tables, dense32, B, nf, cfg.embed_dim,
+                                             cfg.dense_pad)
         else:
-            rows = flat_rows.view(B, nf, cfg.row_width)  # [B, nf, E+8]
-            deep_emb = rows[:, :, :cfg.embed_dim].reshape(B, nf * cfg.embed_dim)
-            wide = rows[:, :, cfg.embed_dim].float().sum(1)
-            x = torch.cat([F.pad(dense, (0, cfg.dense_pad - cfg.num_dense)).to(rows.dtype), deep_emb], 1)
+            x, wide = self._assemble(self.tables(gids, getattr(ids, "_kfa_plan", None)), dense, dense32, B, nf, cdt)
         if x.is_cuda:
             x = x.to(cdt)
             for w, b in zip(self.weights, self.biases):

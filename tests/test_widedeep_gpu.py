@@ -136,3 +136,47 @@ def test_wd_head_flat_bf16_params_direct_grads(B, H, Dn, Dp):
     assert torch.all(wide_dense.grad[:, Dn:].float() == prior)  # pad columns: nothing added
     torch.testing.assert_close(out_b.grad, prior + br.grad, atol=1e-6, rtol=1e-4)
     assert out_w.grad.data_ptr() == gbf.grad.data_ptr() + gbf.offsets[0] * 2  # still the flat view
+
+
+def test_wd_fused_lookup_matches_lookup_then_assembly(monkeypatch):
+    """World 1: the table gather straight into the MLP input (kfa_wd_gather_fwd) vs the
+    lookup kernel + the assembly kernel — the same loss, and the table's sparse optimizer
+    receives bit-identical ids and row gradients either way (the update itself is the
+    same segment-reduce Adam call; its fp32 segment sums are not order-deterministic)."""
+    import copy
+    from kubeflow_controller_amd.models import wide_deep as WD
+    from kubeflow_controller_amd.parallel.embedding import ShardedEmbedding
+    d = torch.device("cuda")
+    cfg = WD.WideDeepConfig(cardinalities=(5000, 300, 40, 7) * 3, embed_dim=32, mlp=(64, 32))
+    torch.manual_seed(0)
+    base = WD.WideDeep(cfg, device=d).to(d)
+    for p in base.weights:
+        p.data = p.data.to(torch.bfloat16)
+    g = torch.Generator().manual_seed(3)
+    dense, ids, labels = WD.synthetic_batch(cfg, 3000, g, d)
+    orig_asm, orig_apply = WD.WideDeep._assemble, ShardedEmbedding.apply_sparse
+    seen = {}
+
+    def spy_asm(self, *a, **k):  # the lookup + assembly pair ran
+        seen["unfused"] = True
+        return orig_asm(self, *a, **k)
+
+    def spy_apply(self, local, grad, prep=None):
+        seen["sparse"] = (local.clone(), grad.clone())
+        return orig_apply(self, local, grad, prep=prep)
+    monkeypatch.setattr(WD.WideDeep, "_assemble", spy_asm)
+    monkeypatch.setattr(ShardedEmbedding, "apply_sparse", spy_apply)
+    out = {}
+    for fused in (True, False):
+        monkeypatch.setattr(WD, "FUSED_LOOKUP", fused)
+        m = copy.deepcopy(base)
+        gids = (ids + m.offsets.view(1, -1)).reshape(-1)
+        assert WD.lookup_fusable(m.tables, gids, cfg.embed_dim) is fused
+        seen.clear()
+        loss = m(dense, ids, labels)
+        loss.backward()
+        torch.cuda.synchronize()
+        assert seen.get("unfused", False) is (not fused) and "sparse" in seen
+        out[fused] = (float(loss.detach()),) + seen["sparse"]
+    assert out[True][0] == out[False][0]
+    assert torch.equal(out[True][1], out[False][1]) and torch.equal(out[True][2], out[False][2])
