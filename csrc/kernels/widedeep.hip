@@ -303,6 +303,19 @@ int head_blocks(int B) {
   return b < 256 ? b : 256;
 }
 
+// the forward keeps one partial float per block: up to 2048 blocks (8 per CU), so each
+// half-wave walks 4 rows at B = 65536 instead of 32 — its x rows come from HBM when the
+// producing GEMM stored them non-temporally, and 256 blocks left that latency exposed
+int head_fwd_blocks(int B) {
+  static int cap = -1;  // KFA_WD_HEAD_FWD_BLOCKS: A/B knob (256 = the backward's grid)
+  if (cap < 0) {
+    const char* e = getenv("KFA_WD_HEAD_FWD_BLOCKS");
+    cap = (e && atoi(e) > 0) ? atoi(e) : 2048;
+  }
+  const int b = (B + kHeadRowsPerBlock - 1) / kHeadRowsPerBlock;
+  return b < cap ? b : cap;
+}
+
 int blocks_for(long n) {
   const long b = (n + 255) / 256;
   return (int)(b < 8192 ? (b < 1 ? 1 : b) : 8192);
@@ -322,15 +335,16 @@ KFA_API int kfa_wd_input_fwd(const bf16_t* rows, const float* dense, bf16_t* x, 
 
 // blocks of the head kernels for B rows (the partial buffers hold this many rows)
 KFA_API int kfa_wd_head_blocks(int B) { return head_blocks(B); }
+KFA_API int kfa_wd_head_fwd_blocks(int B) { return head_fwd_blocks(B); }
 
 // H % 8 == 0, H <= 512, Dn <= 64; x / dx 16-B aligned rows, w 16-B aligned; wbf: w / wd
 // are bf16 (else fp32); y: B labels, int64 (yint) or fp32; dense: [B][Dn] fp32; part:
-// head_blocks(B) floats; loss: one float (written); pmy: B floats (written, for the backward)
+// head_fwd_blocks(B) floats; loss: one float (written); pmy: B floats (written, for the backward)
 KFA_API int kfa_wd_head_fwd(const bf16_t* x, const void* w, const float* ob, const float* wide, const float* dense,
                             const void* wd, const void* y, int yint, int wbf, float* pmy, float* part, float* loss,
                             int B, int H, int Dn, hipStream_t st) {
   if (B <= 0 || H % 8 || H > 8 * 32 * kHeadMaxPieces || Dn < 0 || Dn > kHeadMaxDp) return -1;
-  const int nb = head_blocks(B);
+  const int nb = head_fwd_blocks(B);
   if (wbf)
     hipLaunchKernelGGL(wd_head_fwd<true>, dim3(nb), dim3(256), 0, st, x, w, ob, wide, dense, wd, y, yint, pmy, part, B,
                        H, Dn);

@@ -31,6 +31,7 @@ _lib.register("kfa_wd_input_fwd", [_lib.P] * 4 + [_lib.I] * 5 + [_lib.P])
 _lib.register("kfa_wd_input_bwd", [_lib.P, _lib.P, _lib.P, _lib.I, _lib.I, _lib.I, _lib.I, _lib.P])
 _lib.register("kfa_wd_gather_fwd", [_lib.P] * 5 + [_lib.I] * 5 + [_lib.P])
 _lib.register("kfa_wd_head_blocks", [_lib.I])
+_lib.register("kfa_wd_head_fwd_blocks", [_lib.I])
 _lib.register("kfa_wd_head_fwd", [_lib.P] * 7 + [_lib.I] * 2 + [_lib.P] * 3 + [_lib.I] * 3 + [_lib.P])
 _lib.register("kfa_wd_head_bwd", [_lib.P] * 12 + [_lib.I] * 5 + [_lib.P])
 
@@ -154,7 +155,7 @@ class _WDHeadFn(torch.autograd.Function):
         if Dn > Dp:
             raise ValueError(f"_WDHeadFn: {Dn} dense features for {Dp} wide_dense weights")
         pmy = torch.empty(B, dtype=torch.float32, device=dev)
-        part = torch.empty(_lib.lib().kfa_wd_head_blocks(B), dtype=torch.float32, device=dev)
+        part = torch.empty(_lib.lib().kfa_wd_head_fwd_blocks(B), dtype=torch.float32, device=dev)
         loss = torch.empty((), dtype=torch.float32, device=dev)
         _lib.call("kfa_wd_head_fwd", _lib.ptr(x), _lib.ptr(w), _lib.ptr(ob), _lib.ptr(wide), _lib.ptr(dense),
                   _lib.ptr(wd), _lib.ptr(y), int(yint), int(wbf), _lib.ptr(pmy), _lib.ptr(part), _lib.ptr(loss), B, H,
