@@ -296,11 +296,17 @@ __global__ __launch_bounds__(256) void wd_head_reduce(const float* __restrict__ 
   }
 }
 
-// blocks of the head kernels: 8 rows per block-iteration, at most 256 blocks (the
-// backward's partial rows: 256 x (H + Dp + 1) floats)
+// blocks of the head backward: 8 rows per block-iteration, at most 512 blocks (the partial
+// rows: 512 x (H + Dp + 1) floats; 256 / 512 / 1024 measured 34.79-34.97 / 35.00-35.03 /
+// 35.03 M ex/s on W&D, tools/gpu_r6_wdheadb.sh)
 int head_blocks(int B) {
+  static int cap = -1;  // KFA_WD_HEAD_BWD_BLOCKS: A/B knob
+  if (cap < 0) {
+    const char* e = getenv("KFA_WD_HEAD_BWD_BLOCKS");
+    cap = (e && atoi(e) > 0) ? atoi(e) : 512;
+  }
   const int b = (B + kHeadRowsPerBlock - 1) / kHeadRowsPerBlock;
-  return b < 256 ? b : 256;
+  return b < cap ? b : cap;
 }
 
 // the forward keeps one partial float per block: up to 2048 blocks (8 per CU), so each
