@@ -904,11 +904,18 @@ static int bias_act_bwd_launch(const void* dy, const void* x, const float* b, vo
   const float ds = p > 0.f ? 1.f / (1.f - p) : 1.f;
   zero_if(dbias, N, accumulate, s);
   static const int cl16 = [] { const char* e = getenv("KFA_BIAS_ACT_CL16"); return e ? atoi(e) : 1; }();
+  // KFA_BIAS_ACT_RPB: minimum rows per block of the CL = 16 form (A/B override).  Default 64
+  // (4 rows per thread) on wide N; 256 when N <= 512 (two to four column blocks), where
+  // reaching 2048 blocks left each thread 4 rows and the block reduction + atomics
+  // dominated: W&D 34.99-35.03 -> 35.49-35.67 M ex/s, BERT (N >= 768) 10,114-10,135 with
+  // 64 vs 10,081-10,092 with 256 everywhere (tools/gpu_r6_barpb.sh)
+  static const long rpb_env = [] { const char* e = getenv("KFA_BIAS_ACT_RPB"); return e && atol(e) > 0 ? atol(e) : 0L; }();
   if (N >= 128 && cl16) {
-    // >= 2048 blocks, >= 4 rows per thread; the dbias atomics stay at <= max(chunks, 256) per column
+    // >= 2048 blocks, >= min_rpb / 16 rows per thread; the dbias atomics stay at <= max(chunks, 256) per column
     const long bx = (N + 127) / 128;
+    const long min_rpb = rpb_env > 0 ? rpb_env : (bx <= 4 ? 256L : 64L);
     const long want = std::max(chunks, (2048 + bx - 1) / bx);
-    const long ch = std::max(1L, std::min(want, (rows + 63) / 64));
+    const long ch = std::max(1L, std::min(want, (rows + min_rpb - 1) / min_rpb));
     const long rp = (rows + ch - 1) / ch;
     hipLaunchKernelGGL(bias_act_bwd_kernel<16>, dim3((unsigned)bx, (unsigned)ch), dim3(256), 0, s,
                        (const bf16_t*)dy, (const bf16_t*)x, b, (bf16_t*)dx, dbias, rows, N, act, rp, th, ds,
