@@ -36,6 +36,16 @@ struct OptP {
   float lr, b1, b2, eps, wd, c1, c2, gscale;
 };
 
+// Where seg_apply_kernel reads entry r's gradient row: g [n][D] bf16 (dx == nullptr), or
+// (the Wide&Deep lookup, r = b * F + f) straight from the MLP input gradient dx [B][XW]
+// bf16 — row r's first E columns at dx[b][Dp + f E ...] — then bf16(dwide[b]) and zeros:
+// the [n][E + 8] rows kfa_wd_input_bwd would materialise, without the HBM round trip.
+struct WdSrc {
+  const bf16_t* dx;
+  const float* dwide;
+  int F, E, Dp, XW;
+};
+
 __global__ __launch_bounds__(256) void seg_prep_kernel(const long* __restrict__ ids, unsigned* __restrict__ keys,
                                                        int* __restrict__ pos, int n) {
   for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
@@ -104,7 +114,7 @@ __global__ __launch_bounds__(256) void seg_apply_kernel(const unsigned* __restri
                                                         const bf16_t* __restrict__ g, const int* __restrict__ segbeg,
                                                         float* __restrict__ slots, float* __restrict__ w,
                                                         float* __restrict__ m, float* __restrict__ v, int n, int D,
-                                                        OptP p) {
+                                                        OptP p, WdSrc ws) {
   extern __shared__ float rows[];   // [CH][D + 4] fp32 (row padding spreads the lanes' LDS banks)
   __shared__ int sstart[CH + 1];
   __shared__ unsigned skey[CH];
@@ -115,9 +125,20 @@ __global__ __launch_bounds__(256) void seg_apply_kernel(const unsigned* __restri
   const int V = D >> 3, RS = D + 4;
   for (int it = t; it < cnt * V; it += 256) {
     const int e = it / V, vv = it - e * V;
-    const uint4 q = *reinterpret_cast<const uint4*>(g + (long)pos[c0 + e] * D + vv * 8);
     float f[8];
-    unpack8(q, f);
+    if (ws.dx == nullptr) {
+      const uint4 q = *reinterpret_cast<const uint4*>(g + (long)pos[c0 + e] * D + vv * 8);
+      unpack8(q, f);
+    } else {
+      const int r = pos[c0 + e], b = r / ws.F, fi = r - b * ws.F;
+      if (vv * 8 < ws.E) {
+        unpack8(*reinterpret_cast<const uint4*>(ws.dx + (long)b * ws.XW + ws.Dp + fi * ws.E + vv * 8), f);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) f[i] = 0.f;
+        if (vv * 8 == ws.E) f[0] = bf2f(f2bf(ws.dwide[b]));
+      }
+    }
     float4* dst = reinterpret_cast<float4*>(rows + e * RS + vv * 8);
     dst[0] = make_float4(f[0], f[1], f[2], f[3]);
     dst[1] = make_float4(f[4], f[5], f[6], f[7]);
@@ -245,6 +266,29 @@ bool bad_args(long n, int nbits, long ws_bytes) {
 }
 }  // namespace
 
+namespace {
+int seg_apply_launch(const void* g, WdSrc src, long n, int D, int nbits, const void* ws, float* slots, float* w,
+                     float* m, float* v, int opt, float lr, float b1, float b2, float eps, float wd, float c1, float c2,
+                     float gscale, hipStream_t s) {
+  const int ni = (int)n;
+  const int nch = (ni + CH - 1) / CH;
+  WsLayout L = layout(const_cast<void*>(ws), n, nbits);
+  const OptP op{lr, b1, b2, eps, wd, c1, c2, gscale};
+  const size_t lds = (size_t)CH * (D + 4) * sizeof(float);
+  const int gh = min(16384, (nch + 3) / 4);
+  if (opt == 0) {
+    hipLaunchKernelGGL(seg_apply_kernel<0>, dim3(nch), dim3(256), lds, s, L.keys, L.pos, (const bf16_t*)g, L.segbeg,
+                       slots, w, m, v, ni, D, op, src);
+    hipLaunchKernelGGL(seg_fixup_kernel<0>, dim3(gh), dim3(256), 0, s, L.keys, L.lh, slots, w, m, v, ni, nch, D, op);
+  } else {
+    hipLaunchKernelGGL(seg_apply_kernel<1>, dim3(nch), dim3(256), lds, s, L.keys, L.pos, (const bf16_t*)g, L.segbeg,
+                       slots, w, m, v, ni, D, op, src);
+    hipLaunchKernelGGL(seg_fixup_kernel<1>, dim3(gh), dim3(256), 0, s, L.keys, L.lh, slots, w, m, v, ni, nch, D, op);
+  }
+  return kfa_status();
+}
+}  // namespace
+
 // Gradient-independent half: sort the ids and find the segment structure into ws
 // (it only needs the ids, so the caller may run it on a side stream as soon as the
 // forward lookup has its ids, overlapped with the dense layers).
@@ -277,22 +321,22 @@ KFA_API int kfa_seg_apply(const void* g, long n, int D, int nbits, const void* w
                           float c1, float c2, float gscale, hipStream_t s) {
   if (n <= 0) return 0;
   if (bad_args(n, nbits, ws_bytes) || D % 8 != 0 || D > MAXD) return (int)hipErrorInvalidValue;
-  const int ni = (int)n;
-  const int nch = (ni + CH - 1) / CH;
-  WsLayout L = layout(const_cast<void*>(ws), n, nbits);
-  const OptP op{lr, b1, b2, eps, wd, c1, c2, gscale};
-  const size_t lds = (size_t)CH * (D + 4) * sizeof(float);
-  const int gh = min(16384, (nch + 3) / 4);
-  if (opt == 0) {
-    hipLaunchKernelGGL(seg_apply_kernel<0>, dim3(nch), dim3(256), lds, s, L.keys, L.pos, (const bf16_t*)g, L.segbeg,
-                       slots, w, m, v, ni, D, op);
-    hipLaunchKernelGGL(seg_fixup_kernel<0>, dim3(gh), dim3(256), 0, s, L.keys, L.lh, slots, w, m, v, ni, nch, D, op);
-  } else {
-    hipLaunchKernelGGL(seg_apply_kernel<1>, dim3(nch), dim3(256), lds, s, L.keys, L.pos, (const bf16_t*)g, L.segbeg,
-                       slots, w, m, v, ni, D, op);
-    hipLaunchKernelGGL(seg_fixup_kernel<1>, dim3(gh), dim3(256), 0, s, L.keys, L.lh, slots, w, m, v, ni, nch, D, op);
-  }
-  return kfa_status();
+  return seg_apply_launch(g, WdSrc{nullptr, nullptr, 1, 0, 0, 0}, n, D, nbits, ws, slots, w, m, v, opt, lr, b1, b2,
+                          eps, wd, c1, c2, gscale, s);
+}
+
+// kfa_seg_apply with the gradient rows read from the Wide&Deep MLP input gradient
+// (see WdSrc): dx [n / F][XW] bf16 (16-B aligned rows), dwide [n / F] fp32; D == E + 8.
+KFA_API int kfa_seg_apply_wd(const void* dx, const float* dwide, int F, int E, int Dp, int XW, long n, int D,
+                             int nbits, const void* ws, long ws_bytes, float* slots, float* w, float* m, float* v,
+                             int opt, float lr, float b1, float b2, float eps, float wd, float c1, float c2,
+                             float gscale, hipStream_t s) {
+  if (n <= 0) return 0;
+  if (bad_args(n, nbits, ws_bytes) || D % 8 != 0 || D > MAXD || D != E + 8 || E % 8 || F <= 0 || n % F ||
+      Dp % 8 || XW % 8 || Dp + F * E > XW || !dx || !dwide)
+    return (int)hipErrorInvalidValue;
+  return seg_apply_launch(nullptr, WdSrc{(const bf16_t*)dx, dwide, F, E, Dp, XW}, n, D, nbits, ws, slots, w, m, v, opt,
+                          lr, b1, b2, eps, wd, c1, c2, gscale, s);
 }
 
 // both halves on one stream

@@ -71,9 +71,10 @@ class _WDLookupInputFn(torch.autograd.Function):
     gathered straight from the fp32 table (bf16-rounded, as the lookup's output) next to
     the zero-padded dense features, wide sums alongside — bit-equal to
     ``ShardedEmbedding`` + :class:`_WDInputFn` without their [B*F, E+8] bf16 rows
-    (written once, read once: ~0.13 ms of the 2.0 ms step).  The backward builds the
-    rows' gradient (``kfa_wd_input_bwd``) and hands it to the table's own sparse
-    optimizer, exactly as the lookup's backward does (``parallel/embedding.py``)."""
+    (written once, read once: ~0.13 ms of the 2.0 ms step).  The backward hands the
+    rows' gradient to the table's own sparse optimizer as the lookup's backward does
+    (``parallel/embedding.py``) — read in place out of dx / dwide by the segment update
+    (``kfa_seg_apply_wd``), or materialised by ``kfa_wd_input_bwd`` where that path is off."""
 
     @staticmethod
     def forward(ctx, gids, weight, emb, dense, B, F, E, Dp):
@@ -97,9 +98,14 @@ class _WDLookupInputFn(torch.autograd.Function):
         dx = (dx if dx is not None else torch.zeros(B, Dp + F * E, dtype=torch.bfloat16,
                                                     device=gids.device)).to(torch.bfloat16).contiguous()
         dwide = (dwide if dwide is not None else torch.zeros(B, device=gids.device)).float().contiguous()
-        drows = torch.empty(B * F, E + 8, dtype=torch.bfloat16, device=gids.device)
-        _lib.call("kfa_wd_input_bwd", _lib.ptr(dx), _lib.ptr(dwide), _lib.ptr(drows), B, F, E, Dp, _lib.stream())
-        ctx.emb.apply_sparse(gids, drows, prep=ctx.prep)
+        emb = ctx.emb
+        if FUSED_LOOKUP_BWD and emb.can_apply_wd(gids, ctx.prep):
+            # the segment update reads each row's gradient straight out of dx / dwide
+            emb.apply_sparse(gids, None, prep=ctx.prep, wd_src=(dx, dwide, F, E, Dp))
+        else:
+            drows = torch.empty(B * F, E + 8, dtype=torch.bfloat16, device=gids.device)
+            _lib.call("kfa_wd_input_bwd", _lib.ptr(dx), _lib.ptr(dwide), _lib.ptr(drows), B, F, E, Dp, _lib.stream())
+            emb.apply_sparse(gids, drows, prep=ctx.prep)
         ctx.prep = None
         return None, None, None, None, None, None, None, None
 
@@ -205,6 +211,8 @@ def head_fusable(x: torch.Tensor, dense: torch.Tensor, dp: int) -> bool:
 FUSED_HEAD = os.environ.get("KFA_WD_FUSED_HEAD", "1") != "0"  # csrc/kernels/widedeep.hip
 FUSED_INPUT = os.environ.get("KFA_WD_FUSED_INPUT", "1") != "0"  # csrc/kernels/widedeep.hip
 FUSED_LOOKUP = os.environ.get("KFA_WD_FUSED_LOOKUP", "1") != "0"  # world 1: gather straight into x
+# ... and its backward: the table's segment update reads the row gradients out of dx
+FUSED_LOOKUP_BWD = os.environ.get("KFA_WD_FUSED_LOOKUP_BWD", "1") != "0"
 CRITEO_LIKE = (4_000_000,) * 4 + (1_000_000,) * 6 + (100_000,) * 8 + (10_000,) * 8
 
 

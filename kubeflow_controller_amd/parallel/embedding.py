@@ -53,6 +53,7 @@ _lib.register("kfa_seg_ws_bytes", [_L, _I], restype=_L)
 _lib.register("kfa_seg_sparse_apply", [_P, _P, _L, _I, _I, _P, _L, _P, _P, _P, _P, _I] + [_F] * 8 + [_P])
 _lib.register("kfa_seg_prepare", [_P, _L, _I, _P, _L, _P])
 _lib.register("kfa_seg_apply", [_P, _L, _I, _I, _P, _L, _P, _P, _P, _P, _I] + [_F] * 8 + [_P])
+_lib.register("kfa_seg_apply_wd", [_P, _P, _I, _I, _I, _I, _L, _I, _I, _P, _L, _P, _P, _P, _P, _I] + [_F] * 8 + [_P])
 
 _SIDE = {}
 
@@ -261,8 +262,17 @@ class ShardedEmbedding(nn.Module):
         local.record_stream(side)
         return ws, nbits, done
 
+    def can_apply_wd(self, local: torch.Tensor, prep) -> bool:
+        """:meth:`apply_sparse` can read the row gradients straight from a Wide&Deep MLP
+        input gradient (``wd_src``): the GPU segment path with a prepared sort."""
+        return prep is not None and self.weight.is_cuda and _segment_path(local.numel(), self.dim)
+
     @torch.no_grad()
-    def apply_sparse(self, local: torch.Tensor, g: torch.Tensor, prep=None) -> None:
+    def apply_sparse(self, local: torch.Tensor, g: Optional[torch.Tensor], prep=None, wd_src=None) -> None:
+        """Owner-side sparse update of the rows ``local`` with gradients ``g`` ([n, dim]).
+        ``wd_src = (dx, dwide, F, E, Dp)`` (only where :meth:`can_apply_wd`): the row
+        gradients are read in place from the Wide&Deep MLP input gradient (row b*F + f =
+        [dx[b, Dp + f E : + E] | dwide[b] | 0 ...], ``kfa_seg_apply_wd``) — no [n, dim] copy."""
         self.t += 1
         if local.numel() == 0:
             return
@@ -273,10 +283,27 @@ class ShardedEmbedding(nn.Module):
         self._check_table()
         n, D = local.numel(), self.dim
         st = _lib.stream()
-        g16 = g.to(torch.bfloat16).contiguous()
         adam = self.optimizer == "adam"
         c1 = 1.0 / (1.0 - b1 ** self.t) if adam else 1.0
         c2 = 1.0 / (1.0 - b2 ** self.t) if adam else 1.0
+        if wd_src is not None:
+            if not self.can_apply_wd(local, prep):
+                raise ValueError("apply_sparse: wd_src needs the prepared GPU segment path (can_apply_wd)")
+            dx, dwide, F, E, Dp = wd_src
+            if not (dx.dtype == torch.bfloat16 and dx.is_contiguous() and dx.dim() == 2 and dx.data_ptr() % 16 == 0
+                    and dx.shape[0] * F == n and dwide.dtype == torch.float32 and dwide.is_contiguous()
+                    and dwide.numel() == dx.shape[0] and D == E + 8 and Dp + F * E <= dx.shape[1]):
+                raise ValueError(f"apply_sparse: bad wd_src {tuple(dx.shape)} for {n} rows of {D}")
+            ws, nbits, done = prep
+            torch.cuda.current_stream().wait_event(done)
+            slots = _lib.workspace(_lib.lib().kfa_seg_slot_floats(n, D) * 4, self.weight.device,
+                                   f"seg_sparse_slots{id(self)}").view(torch.float32)
+            _lib.call("kfa_seg_apply_wd", _lib.ptr(dx), _lib.ptr(dwide), F, E, Dp, dx.shape[1], n, D, nbits,
+                      _lib.ptr(ws), ws.numel(), _lib.ptr(slots), _lib.ptr(self.weight), _lib.ptr(self.exp_avg),
+                      _lib.ptr(self.exp_avg_sq), 0 if adam else 1, self.lr, b1, b2, self.eps, self.wd, c1, c2,
+                      self.grad_scale, st)
+            return
+        g16 = g.to(torch.bfloat16).contiguous()
         if prep is not None and _segment_path(n, D):
             ws, nbits, done = prep
             torch.cuda.current_stream().wait_event(done)

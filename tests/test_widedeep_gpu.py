@@ -161,9 +161,15 @@ def test_wd_fused_lookup_matches_lookup_then_assembly(monkeypatch):
         seen["unfused"] = True
         return orig_asm(self, *a, **k)
 
-    def spy_apply(self, local, grad, prep=None):
-        seen["sparse"] = (local.clone(), grad.clone())
-        return orig_apply(self, local, grad, prep=prep)
+    def spy_apply(self, local, grad, prep=None, wd_src=None):
+        if wd_src is not None:  # the rows the segment update reads out of dx / dwide, materialised
+            dx, dwide, F, E, Dp = wd_src
+            nb = dx.shape[0]
+            tail = torch.zeros(nb * F, 8, dtype=torch.bfloat16, device=dx.device)
+            tail[:, 0] = dwide.to(torch.bfloat16).repeat_interleave(F)
+            grad_eq = torch.cat([dx[:, Dp:Dp + F * E].reshape(nb * F, E), tail], 1)
+        seen["sparse"] = (local.clone(), (grad if wd_src is None else grad_eq).clone())
+        return orig_apply(self, local, grad, prep=prep, wd_src=wd_src)
     monkeypatch.setattr(WD.WideDeep, "_assemble", spy_asm)
     monkeypatch.setattr(ShardedEmbedding, "apply_sparse", spy_apply)
     out = {}
@@ -180,3 +186,32 @@ def test_wd_fused_lookup_matches_lookup_then_assembly(monkeypatch):
         out[fused] = (float(loss.detach()),) + seen["sparse"]
     assert out[True][0] == out[False][0]
     assert torch.equal(out[True][1], out[False][1]) and torch.equal(out[True][2], out[False][2])
+
+
+def test_seg_apply_reads_wd_gradient_in_place():
+    """kfa_seg_apply_wd (the table's segment Adam reading each row's gradient straight out
+    of the MLP input gradient dx / dwide) vs kfa_seg_apply on the materialised rows
+    (kfa_wd_input_bwd): the same table, moments and step afterwards."""
+    import copy
+    from kubeflow_controller_amd.models.wide_deep import _lib as L
+    from kubeflow_controller_amd.parallel.embedding import ShardedEmbedding
+    d = torch.device("cuda")
+    torch.manual_seed(7)
+    B, F, E, Dp = 4000, 13, 32, 16
+    emb = ShardedEmbedding(20000, E + 8, lr=1e-2, device=d)
+    ids = (torch.rand(B * F, device=d) ** 3 * 20000).long().clamp_(0, 19999)   # hot rows, long segments
+    dx = torch.randn(B, Dp + F * E, device=d).to(torch.bfloat16)
+    dwide = torch.randn(B, device=d)
+    e2 = copy.deepcopy(emb)
+    prep = emb.prepare_sparse(ids)
+    assert emb.can_apply_wd(ids, prep)
+    emb.apply_sparse(ids, None, prep=prep, wd_src=(dx, dwide, F, E, Dp))
+    drows = torch.empty(B * F, E + 8, dtype=torch.bfloat16, device=d)
+    L.call("kfa_wd_input_bwd", L.ptr(dx), L.ptr(dwide), L.ptr(drows), B, F, E, Dp, L.stream())
+    e2.apply_sparse(ids, drows, prep=e2.prepare_sparse(ids))
+    torch.cuda.synchronize()
+    assert emb.t == e2.t == 1
+    # chunk-crossing segments meet in fp32 atomics: equal up to summation order
+    torch.testing.assert_close(emb.weight, e2.weight, atol=1e-6, rtol=0)
+    torch.testing.assert_close(emb.exp_avg, e2.exp_avg, atol=1e-6, rtol=1e-5)
+    torch.testing.assert_close(emb.exp_avg_sq, e2.exp_avg_sq, atol=1e-8, rtol=1e-4)
