@@ -46,10 +46,12 @@ struct WdSrc {
   int F, E, Dp, XW;
 };
 
-__global__ __launch_bounds__(256) void seg_prep_kernel(const long* __restrict__ ids, unsigned* __restrict__ keys,
-                                                       int* __restrict__ pos, int n) {
+// keys = ids (+ offs[i % F]: per-feature table offsets, so a caller holding [B][F]
+// per-table ids needs no separate global-row pass), pos = identity
+__global__ __launch_bounds__(256) void seg_prep_kernel(const long* __restrict__ ids, const long* __restrict__ offs,
+                                                       int F, unsigned* __restrict__ keys, int* __restrict__ pos, int n) {
   for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-    keys[i] = (unsigned)ids[i];
+    keys[i] = (unsigned)(ids[i] + (offs ? offs[i % F] : 0));
     pos[i] = i;
   }
 }
@@ -292,14 +294,29 @@ int seg_apply_launch(const void* g, WdSrc src, long n, int D, int nbits, const v
 // Gradient-independent half: sort the ids and find the segment structure into ws
 // (it only needs the ids, so the caller may run it on a side stream as soon as the
 // forward lookup has its ids, overlapped with the dense layers).
+static int seg_prepare(const long* ids, const long* offs, int F, long n, int nbits, void* ws, long ws_bytes,
+                       hipStream_t s);
+
 KFA_API int kfa_seg_prepare(const long* ids, long n, int nbits, void* ws, long ws_bytes, hipStream_t s) {
+  return seg_prepare(ids, nullptr, 1, n, nbits, ws, ws_bytes, s);
+}
+
+// the same for ids [n / F][F] of F tables stored back to back: row = ids[i] + offs[i % F]
+KFA_API int kfa_seg_prepare_off(const long* ids, const long* offs, int F, long n, int nbits, void* ws, long ws_bytes,
+                                hipStream_t s) {
+  if (F <= 0 || !offs || (n > 0 && n % F)) return (int)hipErrorInvalidValue;
+  return seg_prepare(ids, offs, F, n, nbits, ws, ws_bytes, s);
+}
+
+static int seg_prepare(const long* ids, const long* offs, int F, long n, int nbits, void* ws, long ws_bytes,
+                       hipStream_t s) {
   if (n <= 0) return 0;
   if (bad_args(n, nbits, ws_bytes)) return (int)hipErrorInvalidValue;
   const int ni = (int)n;
   const int nch = (ni + CH - 1) / CH;
   WsLayout L = layout(ws, n, nbits);
   const int gp = min(16384, (ni + 255) / 256);
-  hipLaunchKernelGGL(seg_prep_kernel, dim3(gp), dim3(256), 0, s, ids, L.keys_in, L.pos_in, ni);
+  hipLaunchKernelGGL(seg_prep_kernel, dim3(gp), dim3(256), 0, s, ids, offs, F, L.keys_in, L.pos_in, ni);
   int e = kfa_radix::sort_pairs(L.keys_in, L.pos_in, L.keys, L.pos, ni, nbits, L.hist, s);
   if (e) return e;
   const int gh = min(16384, (nch + 3) / 4);

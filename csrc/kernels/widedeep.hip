@@ -49,7 +49,8 @@ __global__ __launch_bounds__(256) void wd_input_fwd(const bf16_t* __restrict__ r
 // gid[b*F + f] (rounded to bf16, as the lookup's bf16 output would be); wide[b] = the
 // sum over f of bf16(table[gid][E]) in f order — bit-equal to kfa_embed_fwd +
 // kfa_wd_input_fwd without the [B*F, E+8] bf16 rows round trip through HBM.
-__global__ __launch_bounds__(256) void wd_gather_fwd(const long* __restrict__ gid, const float* __restrict__ table,
+__global__ __launch_bounds__(256) void wd_gather_fwd(const long* __restrict__ gid, const long* __restrict__ offs,
+                                                     const float* __restrict__ table,
                                                      const float* __restrict__ dense, bf16_t* __restrict__ x,
                                                      float* __restrict__ wide, int B, int F, int E, int Dp, int Dn) {
   const int RW = E + 8;
@@ -63,7 +64,7 @@ __global__ __launch_bounds__(256) void wd_gather_fwd(const long* __restrict__ gi
       for (int k = 0; k < 8; k++) f8[k] = j * 8 + k < Dn ? dense[(long)b * Dn + j * 8 + k] : 0.f;
     } else {
       const int e = (j - Dp / 8) * 8, f = e / E, k = e - f * E;
-      const float* src = table + gid[(long)b * F + f] * RW + k;
+      const float* src = table + (gid[(long)b * F + f] + (offs ? offs[f] : 0)) * RW + k;
       const float4 a = *reinterpret_cast<const float4*>(src), c = *reinterpret_cast<const float4*>(src + 4);
       f8[0] = a.x; f8[1] = a.y; f8[2] = a.z; f8[3] = a.w; f8[4] = c.x; f8[5] = c.y; f8[6] = c.z; f8[7] = c.w;
     }
@@ -71,7 +72,7 @@ __global__ __launch_bounds__(256) void wd_gather_fwd(const long* __restrict__ gi
   }
   for (long b = (long)blockIdx.x * blockDim.x + threadIdx.x; b < B; b += (long)gridDim.x * blockDim.x) {
     float s = 0.f;
-    for (int f = 0; f < F; f++) s += bf2f(f2bf(table[gid[b * F + f] * RW + E]));
+    for (int f = 0; f < F; f++) s += bf2f(f2bf(table[(gid[b * F + f] + (offs ? offs[f] : 0)) * RW + E]));
     wide[b] = s;
   }
 }
@@ -383,13 +384,14 @@ KFA_API int kfa_wd_head_bwd(const bf16_t* x, const void* w, const float* dense, 
   return kfa_status();
 }
 
-// table: fp32 [rows][E + 8] (16-B aligned rows: E % 8 == 0), gid: B*F int64 rows of it;
-// dense [B][Dn] fp32, Dn <= Dp, Dp % 8 == 0; x 16-B aligned
-KFA_API int kfa_wd_gather_fwd(const long* gid, const float* table, const float* dense, bf16_t* x, float* wide, int B,
-                              int F, int E, int Dp, int Dn, hipStream_t st) {
+// table: fp32 [rows][E + 8] (16-B aligned rows: E % 8 == 0), gid: B*F int64 rows of it
+// (+ offs[f], nullable: per-feature table offsets for per-table ids); dense [B][Dn] fp32,
+// Dn <= Dp, Dp % 8 == 0; x 16-B aligned
+KFA_API int kfa_wd_gather_fwd(const long* gid, const long* offs, const float* table, const float* dense, bf16_t* x,
+                              float* wide, int B, int F, int E, int Dp, int Dn, hipStream_t st) {
   if (E % 8 || Dp % 8 || B <= 0 || Dn < 0 || Dn > Dp) return -1;
-  hipLaunchKernelGGL(wd_gather_fwd, dim3(blocks_for((long)B * ((Dp + F * E) / 8))), dim3(256), 0, st, gid, table,
-                     dense, x, wide, B, F, E, Dp, Dn);
+  hipLaunchKernelGGL(wd_gather_fwd, dim3(blocks_for((long)B * ((Dp + F * E) / 8))), dim3(256), 0, st, gid, offs,
+                     table, dense, x, wide, B, F, E, Dp, Dn);
   return kfa_status();
 }
 

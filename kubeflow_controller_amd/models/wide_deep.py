@@ -29,7 +29,7 @@ from ..parallel.embedding import ShardedEmbedding
 
 _lib.register("kfa_wd_input_fwd", [_lib.P] * 4 + [_lib.I] * 5 + [_lib.P])
 _lib.register("kfa_wd_input_bwd", [_lib.P, _lib.P, _lib.P, _lib.I, _lib.I, _lib.I, _lib.I, _lib.P])
-_lib.register("kfa_wd_gather_fwd", [_lib.P] * 5 + [_lib.I] * 5 + [_lib.P])
+_lib.register("kfa_wd_gather_fwd", [_lib.P] * 6 + [_lib.I] * 5 + [_lib.P])
 _lib.register("kfa_wd_head_blocks", [_lib.I])
 _lib.register("kfa_wd_head_fwd_blocks", [_lib.I])
 _lib.register("kfa_wd_head_fwd", [_lib.P] * 7 + [_lib.I] * 2 + [_lib.P] * 3 + [_lib.I] * 3 + [_lib.P])
@@ -77,24 +77,26 @@ class _WDLookupInputFn(torch.autograd.Function):
     (``kfa_seg_apply_wd``), or materialised by ``kfa_wd_input_bwd`` where that path is off."""
 
     @staticmethod
-    def forward(ctx, gids, weight, emb, dense, B, F, E, Dp):
+    def forward(ctx, ids, offsets, weight, emb, dense, B, F, E, Dp):
+        # ids: [B*F] per-table ids; table row = ids[b*F + f] + offsets[f] (added in the kernels)
         Dn = dense.shape[1]
         emb._check_table()
         x = torch.empty(B, Dp + F * E, dtype=torch.bfloat16, device=dense.device)
         wide = torch.empty(B, dtype=torch.float32, device=dense.device)
         # the id sort of the sparse update needs no gradient: start it now, beside the dense layers
-        ctx.prep = emb.prepare_sparse(gids) if ctx.needs_input_grad[1] else None
-        _lib.call("kfa_wd_gather_fwd", _lib.ptr(gids), _lib.ptr(weight), _lib.ptr(dense), _lib.ptr(x), _lib.ptr(wide),
-                  B, F, E, Dp, Dn, _lib.stream())
-        ctx.save_for_backward(gids)
+        ctx.prep = emb.prepare_sparse(ids, offsets=offsets, F=F) if ctx.needs_input_grad[2] else None
+        _lib.call("kfa_wd_gather_fwd", _lib.ptr(ids), _lib.ptr(offsets), _lib.ptr(weight), _lib.ptr(dense), _lib.ptr(x),
+                  _lib.ptr(wide), B, F, E, Dp, Dn, _lib.stream())
+        ctx.save_for_backward(ids, offsets)
         ctx.emb = emb
         ctx.dims = (B, F, E, Dp)
         return x, wide
 
     @staticmethod
     def backward(ctx, dx, dwide):
-        (gids,) = ctx.saved_tensors
+        ids, offsets = ctx.saved_tensors
         B, F, E, Dp = ctx.dims
+        gids = ids
         dx = (dx if dx is not None else torch.zeros(B, Dp + F * E, dtype=torch.bfloat16,
                                                     device=gids.device)).to(torch.bfloat16).contiguous()
         dwide = (dwide if dwide is not None else torch.zeros(B, device=gids.device)).float().contiguous()
@@ -105,9 +107,11 @@ class _WDLookupInputFn(torch.autograd.Function):
         else:
             drows = torch.empty(B * F, E + 8, dtype=torch.bfloat16, device=gids.device)
             _lib.call("kfa_wd_input_bwd", _lib.ptr(dx), _lib.ptr(dwide), _lib.ptr(drows), B, F, E, Dp, _lib.stream())
-            emb.apply_sparse(gids, drows, prep=ctx.prep)
+            # (the prepared sort already holds the global rows; without one, form them here)
+            rows = ids if ctx.prep is not None else (ids.view(B, F) + offsets.view(1, F)).reshape(-1)
+            emb.apply_sparse(rows, drows, prep=ctx.prep)
         ctx.prep = None
-        return None, None, None, None, None, None, None, None
+        return None, None, None, None, None, None, None, None, None
 
 
 def lookup_fusable(emb: ShardedEmbedding, gids: torch.Tensor, E: int) -> bool:
@@ -286,14 +290,16 @@ class WideDeep(nn.Module):
     def forward(self, dense: torch.Tensor, ids: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
         cfg = self.cfg
         B, nf = ids.shape
-        gids = (ids + self.offsets.view(1, nf)).reshape(-1)
         cdt = self.weights[0].dtype
         dense32 = dense.float().contiguous()  # (the fused kernels zero-pad it to dense_pad themselves)
-        if cdt == torch.bfloat16 and lookup_fusable(self.tables, gids, cfg.embed_dim):
-            # world 1: the lookup gathers straight into the MLP input
-            x, wide = _WDLookupInputFn.apply(gids, self.tables.weight, self.tables, dense32, B, nf, cfg.embed_dim,
-                                             cfg.dense_pad)
+        flat_ids = ids.reshape(-1)
+        if cdt == torch.bfloat16 and self.offsets.is_cuda and lookup_fusable(self.tables, flat_ids, cfg.embed_dim):
+            # world 1: the lookup gathers straight into the MLP input (global row = id + the
+            # table's offset, added inside the gather and the sort's key pass)
+            x, wide = _WDLookupInputFn.apply(flat_ids, self.offsets, self.tables.weight, self.tables, dense32, B, nf,
+                                             cfg.embed_dim, cfg.dense_pad)
         else:
+            gids = (ids + self.offsets.view(1, nf)).reshape(-1)
             x, wide = self._assemble(self.tables(gids, getattr(ids, "_kfa_plan", None)), dense, dense32, B, nf, cdt)
         if x.is_cuda:
             x = x.to(cdt)

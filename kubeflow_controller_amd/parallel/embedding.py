@@ -52,6 +52,7 @@ _lib.register("kfa_seg_slot_floats", [_L, _I], restype=_L)
 _lib.register("kfa_seg_ws_bytes", [_L, _I], restype=_L)
 _lib.register("kfa_seg_sparse_apply", [_P, _P, _L, _I, _I, _P, _L, _P, _P, _P, _P, _I] + [_F] * 8 + [_P])
 _lib.register("kfa_seg_prepare", [_P, _L, _I, _P, _L, _P])
+_lib.register("kfa_seg_prepare_off", [_P, _P, _I, _L, _I, _P, _L, _P])
 _lib.register("kfa_seg_apply", [_P, _L, _I, _I, _P, _L, _P, _P, _P, _P, _I] + [_F] * 8 + [_P])
 _lib.register("kfa_seg_apply_wd", [_P, _P, _I, _I, _I, _I, _L, _I, _I, _P, _L, _P, _P, _P, _P, _I] + [_F] * 8 + [_P])
 
@@ -240,12 +241,14 @@ class ShardedEmbedding(nn.Module):
         return max(1, (self.local_rows - 1).bit_length())
 
     @torch.no_grad()
-    def prepare_sparse(self, local: torch.Tensor):
+    def prepare_sparse(self, local: torch.Tensor, offsets: Optional[torch.Tensor] = None, F: int = 1):
         """Gradient-independent half of the segment update (radix sort of the ids,
         segment heads) launched on a side stream right after the forward lookup,
         so it runs under the dense layers instead of inside backward.  Returns the
         handle :meth:`apply_sparse` consumes, or None (CPU, atomic path,
-        ``KFA_SPARSE_OVERLAP=0``)."""
+        ``KFA_SPARSE_OVERLAP=0``).  ``offsets`` (int64 [F]): ``local`` holds per-table ids of
+        F tables stored back to back, row = local[i] + offsets[i % F] (added by the sort's
+        key pass, no separate global-row tensor)."""
         n = local.numel()
         if (not self.weight.is_cuda or n == 0 or not _segment_path(n, self.dim)
                 or os.environ.get("KFA_SPARSE_OVERLAP", "1") == "0"):
@@ -255,7 +258,14 @@ class ShardedEmbedding(nn.Module):
         main = torch.cuda.current_stream(local.device)
         side = _side_stream(local.device)
         side.wait_stream(main)
-        _lib.call("kfa_seg_prepare", _lib.ptr(local), n, nbits, _lib.ptr(ws), ws.numel(), side.cuda_stream)
+        if offsets is not None:
+            if not (offsets.dtype == torch.int64 and offsets.is_contiguous() and offsets.numel() == F and n % F == 0):
+                raise ValueError(f"prepare_sparse: offsets {tuple(offsets.shape)} for {n} ids of {F} tables")
+            _lib.call("kfa_seg_prepare_off", _lib.ptr(local), _lib.ptr(offsets), F, n, nbits, _lib.ptr(ws), ws.numel(),
+                      side.cuda_stream)
+            offsets.record_stream(side)
+        else:
+            _lib.call("kfa_seg_prepare", _lib.ptr(local), n, nbits, _lib.ptr(ws), ws.numel(), side.cuda_stream)
         done = torch.cuda.Event()
         done.record(side)
         ws.record_stream(side)

@@ -183,15 +183,19 @@ def test_wd_fused_lookup_matches_lookup_then_assembly(monkeypatch):
         loss.backward()
         torch.cuda.synchronize()
         assert seen.get("unfused", False) is (not fused) and "sparse" in seen
-        out[fused] = (float(loss.detach()),) + seen["sparse"]
+        local, grad = seen["sparse"]
+        if fused:  # per-table ids (the sort adds the table offsets itself): as global rows
+            local = (local.view(-1, len(cfg.cardinalities)) + m.offsets.view(1, -1)).reshape(-1)
+        out[fused] = (float(loss.detach()), local, grad)
     assert out[True][0] == out[False][0]
     assert torch.equal(out[True][1], out[False][1]) and torch.equal(out[True][2], out[False][2])
 
 
 def test_seg_apply_reads_wd_gradient_in_place():
     """kfa_seg_apply_wd (the table's segment Adam reading each row's gradient straight out
-    of the MLP input gradient dx / dwide) vs kfa_seg_apply on the materialised rows
-    (kfa_wd_input_bwd): the same table, moments and step afterwards."""
+    of the MLP input gradient dx / dwide, on a sort whose key pass added the per-table
+    offsets: kfa_seg_prepare_off) vs kfa_seg_apply on the materialised rows
+    (kfa_wd_input_bwd) sorted by global row: the same table, moments and step afterwards."""
     import copy
     from kubeflow_controller_amd.models.wide_deep import _lib as L
     from kubeflow_controller_amd.parallel.embedding import ShardedEmbedding
@@ -199,16 +203,19 @@ def test_seg_apply_reads_wd_gradient_in_place():
     torch.manual_seed(7)
     B, F, E, Dp = 4000, 13, 32, 16
     emb = ShardedEmbedding(20000, E + 8, lr=1e-2, device=d)
-    ids = (torch.rand(B * F, device=d) ** 3 * 20000).long().clamp_(0, 19999)   # hot rows, long segments
+    # per-table ids of 13 tables of 1500 rows (hot rows, long segments); global row = id + offset
+    ids = (torch.rand(B * F, device=d) ** 3 * 1500).long().clamp_(0, 1499)
+    offs = torch.arange(F, device=d, dtype=torch.int64) * 1500
+    gids = (ids.view(B, F) + offs.view(1, F)).reshape(-1)
     dx = torch.randn(B, Dp + F * E, device=d).to(torch.bfloat16)
     dwide = torch.randn(B, device=d)
     e2 = copy.deepcopy(emb)
-    prep = emb.prepare_sparse(ids)
+    prep = emb.prepare_sparse(ids, offsets=offs, F=F)   # the sort's key pass adds the offsets
     assert emb.can_apply_wd(ids, prep)
     emb.apply_sparse(ids, None, prep=prep, wd_src=(dx, dwide, F, E, Dp))
     drows = torch.empty(B * F, E + 8, dtype=torch.bfloat16, device=d)
     L.call("kfa_wd_input_bwd", L.ptr(dx), L.ptr(dwide), L.ptr(drows), B, F, E, Dp, L.stream())
-    e2.apply_sparse(ids, drows, prep=e2.prepare_sparse(ids))
+    e2.apply_sparse(gids, drows, prep=e2.prepare_sparse(gids))
     torch.cuda.synchronize()
     assert emb.t == e2.t == 1
     # chunk-crossing segments meet in fp32 atomics: equal up to summation order
