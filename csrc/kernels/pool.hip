@@ -97,9 +97,13 @@ __global__ __launch_bounds__(256) void maxpool_bwd(const bf16_t* __restrict__ dy
 // loads of a thread, leaving the pool latency-bound at 2-3 TB/s.  Out-of-range
 // taps load a clamped (valid) address and are masked afterwards.
 // BN: x is the PRE-BatchNorm tensor; every window element is first mapped to
-// the bf16 value the BN + ReLU apply pass would have written,
-// bf16(relu(fma(x, scale[c], shift[c]))) (ss = [scale | shift]), so the stem's
-// BN output is never materialised (its backward recomputes the mask from x).
+// relu(fma(x, scale[c], shift[c])) (ss = [scale | shift]) in fp32 and the max is
+// rounded to bf16 once: rounding is monotone, so the output equals the max of the
+// bf16 values the BN + ReLU apply pass would have written (only the argmax among
+// taps that round to the same bf16 value can differ), and fmaxf(., 0) already maps
+// NaN to 0, so the NaN-propagating compare is dropped — 5 VALU ops per element and
+// tap instead of 11 (the stem pool is VALU-bound).  The stem's BN output is never
+// materialised (its backward recomputes the mask from x).
 template <bool BN>
 __global__ __launch_bounds__(256) void maxpool3s2_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
                                                       uint8_t* __restrict__ idx, int N, int H, int W, int C, int Ho,
@@ -142,11 +146,11 @@ __global__ __launch_bounds__(256) void maxpool3s2_fwd(const bf16_t* __restrict__
     unpack8(in[pos], f);
     if (BN) {
 #pragma unroll
-      for (int j = 0; j < 8; j++) f[j] = bf2f(f2bf(fmaxf(fmaf(f[j], sc[j], sf[j]), 0.f)));
+      for (int j = 0; j < 8; j++) f[j] = fmaxf(fmaf(f[j], sc[j], sf[j]), 0.f);
     }
 #pragma unroll
     for (int j = 0; j < 8; j++)
-      if (f[j] > best[j] || (f[j] != f[j] && best[j] == best[j])) { best[j] = f[j]; bi[j] = pos; }
+      if (f[j] > best[j] || (!BN && f[j] != f[j] && best[j] == best[j])) { best[j] = f[j]; bi[j] = pos; }
   }
   const long o = (long)v * 8;  // output NHWC offset == vector index * 8
   *reinterpret_cast<uint4*>(y + o) = pack8(best);
@@ -208,17 +212,17 @@ __global__ __launch_bounds__(256) void maxpool3s2_fwd2(const bf16_t* __restrict_
       unpack8(in[q], f);
       if (BN) {
 #pragma unroll
-        for (int j = 0; j < 8; j++) f[j] = bf2f(f2bf(fmaxf(fmaf(f[j], sc[j], sf[j]), 0.f)));
+        for (int j = 0; j < 8; j++) f[j] = fmaxf(fmaf(f[j], sc[j], sf[j]), 0.f);
       }
       if (kw < 3) {  // output ow0: window columns 0..2, tap index kh * 3 + kw
 #pragma unroll
         for (int j = 0; j < 8; j++)
-          if (f[j] > best0[j] || (f[j] != f[j] && best0[j] == best0[j])) { best0[j] = f[j]; bi0[j] = kh * 3 + kw; }
+          if (f[j] > best0[j] || (!BN && f[j] != f[j] && best0[j] == best0[j])) { best0[j] = f[j]; bi0[j] = kh * 3 + kw; }
       }
       if (kw >= 2) {  // output ow0 + 1: window columns 2..4
 #pragma unroll
         for (int j = 0; j < 8; j++)
-          if (f[j] > best1[j] || (f[j] != f[j] && best1[j] == best1[j])) { best1[j] = f[j]; bi1[j] = kh * 3 + kw - 2; }
+          if (f[j] > best1[j] || (!BN && f[j] != f[j] && best1[j] == best1[j])) { best1[j] = f[j]; bi1[j] = kh * 3 + kw - 2; }
       }
     }
   const long o0 = ((((long)n * Ho + oh) * Wo) + ow0) * C + cg * 8;
