@@ -1,5 +1,6 @@
 #!/bin/bash
 # segment Adam gather-store bank order (KFA_SEG_SWZ 1 = swizzled halves, 0 = plain): tests + W&D A/B
+# (the swizzle and its knob were reverted after this A/B: docs/kernels.md; kept as the record of the run)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R; O=gpurun_out/r6segswz; mkdir -p $O
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_widedeep_gpu.py > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
