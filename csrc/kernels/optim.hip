@@ -101,9 +101,11 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ w, bf16_t
 
 // t += 1; bc = (1 - b1^t, 1 - b2^t): the per-step scalars of Adam kept on the
 // device, so a captured step needs no host value that changes per step
-__global__ void adam_bc_kernel(int* __restrict__ t, float* __restrict__ bc, float b1, float b2) {
+// seed >= 0 (an eager step): the host's step count replaces the device one first — the
+// re-seed that used to be a separate fill launch; seed < 0 (graph replay): t advances
+__global__ void adam_bc_kernel(int* __restrict__ t, float* __restrict__ bc, float b1, float b2, int seed) {
   if (threadIdx.x == 0 && blockIdx.x == 0) {
-    const int s = t[0] + 1;
+    const int s = (seed >= 0 ? seed : t[0]) + 1;
     t[0] = s;
     bc[0] = 1.f - powf(b1, (float)s);
     bc[1] = 1.f - powf(b2, (float)s);
@@ -174,7 +176,13 @@ KFA_API int kfa_adam_step(float* w, bf16_t* wb, const void* g, int g_is_bf16, fl
 }
 
 KFA_API int kfa_adam_bc(int* t, float* bc, float b1, float b2, hipStream_t s) {
-  hipLaunchKernelGGL(adam_bc_kernel, dim3(1), dim3(64), 0, s, t, bc, b1, b2);
+  hipLaunchKernelGGL(adam_bc_kernel, dim3(1), dim3(64), 0, s, t, bc, b1, b2, -1);
+  return kfa_status();
+}
+
+// the same, the device count first set to `seed` when seed >= 0 (eager steps, resumes)
+KFA_API int kfa_adam_bc_seed(int* t, float* bc, float b1, float b2, int seed, hipStream_t s) {
+  hipLaunchKernelGGL(adam_bc_kernel, dim3(1), dim3(64), 0, s, t, bc, b1, b2, seed);
   return kfa_status();
 }
 

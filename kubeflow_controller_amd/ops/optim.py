@@ -22,6 +22,7 @@ P, L, I, F = _lib.P, _lib.L, _lib.I, _lib.F
 _lib.register("kfa_sgd_step", [P, P, P, I, P, L, F, F, F, F, I, F, I, P])
 _lib.register("kfa_adam_step", [P, P, P, I, P, P, L, F, F, F, F, F, F, F, F, P, P])
 _lib.register("kfa_adam_bc", [P, P, F, F, P])
+_lib.register("kfa_adam_bc_seed", [P, P, F, F, I, P])
 _lib.register("kfa_f32_to_bf16", [P, P, L, P])
 _lib.register("kfa_sumsq", [P, I, L, P, P])
 
@@ -159,9 +160,11 @@ class FusedAdam(_FusedBase):
         """Open one optimizer step whose updates are issued per range (``update``):
         the step count and the bias corrections advance once, here."""
         if self._t is not None:
-            if not torch.cuda.is_current_stream_capturing():
-                self._t.fill_(self.step_count)  # eager steps (and resumes) re-seed the device count
-            _lib.call("kfa_adam_bc", _lib.ptr(self._t), _lib.ptr(self._bc), self.b1, self.b2, _lib.stream())
+            # eager steps (and resumes) re-seed the device count inside the same launch; a
+            # captured step advances it on the device (graph replay)
+            seed = -1 if torch.cuda.is_current_stream_capturing() else self.step_count
+            _lib.call("kfa_adam_bc_seed", _lib.ptr(self._t), _lib.ptr(self._bc), self.b1, self.b2, seed,
+                      _lib.stream())
         self.step_count += 1
 
     @torch.no_grad()
